@@ -1,0 +1,391 @@
+// extern "C" implementation of include/mi_engine.h.  Every entry point
+// catches exceptions and reports them through mi_last_error().
+#include "engine.h"
+
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+using namespace mi;
+
+struct mi_model { Model impl; };
+struct mi_ctx { std::unique_ptr<Ctx> impl; };
+
+#define MI_TRY(fail) catch (const std::exception& e) { set_last_error(e.what()); return fail; } \
+                     catch (...) { set_last_error("unknown error"); return fail; }
+
+extern "C" {
+
+const char* mi_last_error(void) { return last_error(); }
+
+mi_model* mi_model_load_from_memory(const void* data, size_t size, const mi_model_params* params) {
+    try {
+        set_last_error("");
+        mi_model_params p{0, 0, 0, 0};
+        if (params) p = *params;
+        if (p.cpu_only) throw Error("cpu_only: the CPU path is the reference's ggml backend, not this engine");
+        auto* m = new mi_model();
+        try {
+            m->impl.load(static_cast<const uint8_t*>(data), size, p);
+        } catch (...) {
+            delete m;
+            throw;
+        }
+        return m;
+    }
+    MI_TRY(nullptr)
+}
+
+mi_model* mi_model_load(const char* path, const mi_model_params* params) {
+    try {
+        if (!path) throw Error("null path");
+        const int fd = ::open(path, O_RDONLY);
+        if (fd < 0) throw Error(std::string("cannot open ") + path);
+        struct stat st;
+        if (fstat(fd, &st) != 0) { ::close(fd); throw Error("fstat failed"); }
+        const size_t size = (size_t)st.st_size;
+        void* map = mmap(nullptr, size, PROT_READ, MAP_PRIVATE, fd, 0);
+        ::close(fd);
+        if (map == MAP_FAILED) throw Error(std::string("mmap failed for ") + path);
+        mi_model* m = mi_model_load_from_memory(map, size, params);
+        munmap(map, size);
+        return m;
+    }
+    MI_TRY(nullptr)
+}
+
+void mi_model_free(mi_model* model) { delete model; }
+
+int32_t mi_model_n_vocab(const mi_model* m) { return m ? m->impl.hp.n_vocab : -1; }
+int32_t mi_model_n_ctx_train(const mi_model* m) { return m ? m->impl.hp.n_ctx_train : -1; }
+int32_t mi_model_n_embd(const mi_model* m) { return m ? m->impl.hp.n_embd : -1; }
+int32_t mi_model_n_layer(const mi_model* m) { return m ? m->impl.hp.n_layer : -1; }
+int32_t mi_model_n_head(const mi_model* m) { return m ? m->impl.hp.n_head : -1; }
+int32_t mi_model_n_head_kv(const mi_model* m) { return m ? m->impl.hp.n_head_kv : -1; }
+int32_t mi_model_n_ff(const mi_model* m) { return m ? m->impl.hp.n_ff : -1; }
+int32_t mi_model_n_expert(const mi_model* m) { return m ? m->impl.hp.n_expert : -1; }
+int32_t mi_model_token_bos(const mi_model* m) { return m ? m->impl.bos : -1; }
+int32_t mi_model_token_eos(const mi_model* m) { return m ? m->impl.eos : -1; }
+int32_t mi_model_add_bos(const mi_model* m) { return m ? (m->impl.add_bos ? 1 : 0) : -1; }
+
+int32_t mi_model_token_is_eog(const mi_model* m, int32_t token) {
+    if (!m) return -1;
+    return (token == m->impl.eos || (m->impl.eot >= 0 && token == m->impl.eot)) ? 1 : 0;
+}
+
+int32_t mi_model_token_text(const mi_model* m, int32_t token, char* buf, int32_t size) {
+    if (!m || token < 0 || token >= (int)m->impl.tokens.size()) { set_last_error("token out of range"); return -1; }
+    const std::string& s = m->impl.tokens[token];
+    if (buf && size > 0) {
+        const int n = std::min<int>((int)s.size(), size - 1);
+        std::memcpy(buf, s.data(), n);
+        buf[n] = 0;
+    }
+    return (int32_t)s.size();
+}
+
+int32_t mi_model_meta_str(const mi_model* m, const char* key, char* buf, int32_t size) {
+    if (!m || !key) return -1;
+    const GgufValue* v = m->impl.gguf.get(key);
+    if (!v) return -1;
+    std::string s = v->type == 8 ? v->s : (v->type == 6 || v->type == 12) ? std::to_string(v->f) : std::to_string(v->i);
+    if (buf && size > 0) {
+        const int n = std::min<int>((int)s.size(), size - 1);
+        std::memcpy(buf, s.data(), n);
+        buf[n] = 0;
+    }
+    return (int32_t)s.size();
+}
+
+int64_t mi_model_weight_bytes(const mi_model* m) { return m ? m->impl.weight_bytes : -1; }
+
+int32_t mi_model_arena(const mi_model* m, void** dev_ptr, size_t* bytes) {
+    if (!m) return -1;
+    if (dev_ptr) *dev_ptr = m->impl.arena;
+    if (bytes) *bytes = m->impl.arena_bytes;
+    return 0;
+}
+
+int32_t mi_model_type_histogram(const mi_model* m, int64_t* out, int32_t n) {
+    if (!m || !out) return -1;
+    const int k = std::min(n, 32);
+    for (int i = 0; i < k; ++i) out[i] = m->impl.type_bytes[i];
+    return k;
+}
+
+mi_ctx* mi_ctx_create(mi_model* model, uint32_t n_ctx, uint32_t n_batch, uint32_t n_ubatch) {
+    try {
+        if (!model) throw Error("null model");
+        auto* c = new mi_ctx();
+        try {
+            c->impl.reset(new Ctx(&model->impl, n_ctx, n_batch, n_ubatch));
+        } catch (...) {
+            delete c;
+            throw;
+        }
+        return c;
+    }
+    MI_TRY(nullptr)
+}
+
+void mi_ctx_free(mi_ctx* ctx) { delete ctx; }
+uint32_t mi_n_ctx(const mi_ctx* c) { return c ? c->impl->n_ctx : 0; }
+uint32_t mi_n_batch(const mi_ctx* c) { return c ? c->impl->n_batch : 0; }
+
+int32_t mi_decode(mi_ctx* c, const int32_t* tokens, int32_t n, int32_t out_mode) {
+    try {
+        if (!c || !tokens) throw Error("null argument");
+        if (out_mode != MI_OUT_LAST) throw Error("decode: only MI_OUT_LAST is implemented");
+        return c->impl->decode(tokens, n);
+    }
+    MI_TRY(-1)
+}
+
+int32_t mi_topk(mi_ctx* c, int32_t row, int32_t k, int32_t* ids, float* logits) {
+    try {
+        if (!c || !ids || !logits) throw Error("null argument");
+        if (row != -1 && row != 0) throw Error("topk: only the last output row is kept");
+        return c->impl->topk(k, ids, logits);
+    }
+    MI_TRY(-1)
+}
+
+int32_t mi_gather(mi_ctx* c, int32_t row, const int32_t* ids, int32_t n, float* out) {
+    try {
+        if (!c || (n > 0 && (!ids || !out))) throw Error("null argument");
+        if (row != -1 && row != 0) throw Error("gather: only the last output row is kept");
+        return c->impl->gather(ids, n, out);
+    }
+    MI_TRY(-1)
+}
+
+const float* mi_logits(mi_ctx* c, int32_t row) {
+    try {
+        if (!c) throw Error("null ctx");
+        if (row != -1 && row != 0) throw Error("logits: only the last output row is kept");
+        return c->impl->logits_host();
+    }
+    MI_TRY(nullptr)
+}
+
+void mi_synchronize(mi_ctx* c) {
+    try { if (c) c->impl->sync(); } catch (const std::exception& e) { set_last_error(e.what()); }
+}
+
+void mi_kv_clear(mi_ctx* c) { if (c) c->impl->kv_clear(); }
+
+int32_t mi_kv_seq_rm(mi_ctx* c, int32_t p0, int32_t p1) {
+    try { if (!c) throw Error("null ctx"); return c->impl->kv_seq_rm(p0, p1); }
+    MI_TRY(-1)
+}
+int32_t mi_kv_seq_add(mi_ctx* c, int32_t p0, int32_t p1, int32_t delta) {
+    try { if (!c) throw Error("null ctx"); return c->impl->kv_seq_shift(p0, p1, delta, 0); }
+    MI_TRY(-1)
+}
+int32_t mi_kv_seq_div(mi_ctx* c, int32_t p0, int32_t p1, int32_t d) {
+    try {
+        if (!c) throw Error("null ctx");
+        if (d <= 0) throw Error("seq_div: divisor must be positive");
+        return c->impl->kv_seq_shift(p0, p1, 0, d);
+    }
+    MI_TRY(-1)
+}
+int32_t mi_kv_pos_max(const mi_ctx* c) { return c ? c->impl->pos_max : -1; }
+int32_t mi_kv_n_cells(const mi_ctx* c) { return c ? c->impl->n_cells : -1; }
+
+size_t mi_state_size(mi_ctx* c) { return c ? c->impl->state_size() : 0; }
+size_t mi_state_get(mi_ctx* c, uint8_t* dst, size_t size) {
+    try { if (!c || !dst) throw Error("null argument"); return c->impl->state_get(dst, size); }
+    MI_TRY(0)
+}
+size_t mi_state_set(mi_ctx* c, const uint8_t* src, size_t size) {
+    try { if (!c || !src) throw Error("null argument"); return c->impl->state_set(src, size); }
+    MI_TRY(0)
+}
+
+int32_t mi_prof_enable(mi_ctx* c, int32_t layer) {
+    if (!c) return -1;
+    if (layer >= c->impl->m->hp.n_layer) layer = c->impl->m->hp.n_layer - 1;
+    if (c->impl->prof_layer != layer) {
+        c->impl->prof_layer = layer < 0 ? -1 : layer;
+        c->impl->invalidate_graphs();
+    }
+    return 0;
+}
+int32_t mi_prof_read(mi_ctx* c, float* us, int32_t n) {
+    try { if (!c || !us) throw Error("null argument"); return c->impl->prof_read(us, n); }
+    MI_TRY(-1)
+}
+int64_t mi_prof_ffn_bytes(const mi_ctx* c) { return c ? c->impl->ffn_bytes() : -1; }
+
+}  // extern "C"
+
+// ------------------------------------------------------------- op level ---
+namespace {
+struct DevBuf {
+    void* p = nullptr;
+    explicit DevBuf(size_t n) { MI_HIP(hipMalloc(&p, n ? n : 16)); }
+    ~DevBuf() { if (p) hipFree(p); }
+    template <class T> T* as() { return static_cast<T*>(p); }
+};
+
+// Upload GGUF blocks and repack them into planes; returns the QMat view.
+QMat upload_qmat(int type, const void* raw, int rows, int K, std::vector<std::unique_ptr<DevBuf>>& keep) {
+    if (!is_quant(type)) throw Error("op: unsupported quant type");
+    if (K % 256) throw Error("op: K must be a multiple of 256");
+    const size_t nbytes = (size_t)rows * (K / block_elems(type)) * block_bytes(type);
+    auto staging = std::make_unique<DevBuf>(nbytes);
+    MI_HIP(hipMemcpy(staging->p, raw, nbytes, hipMemcpyHostToDevice));
+    QMat m{};
+    m.type = type;
+    m.rows = rows;
+    m.K = K;
+    m.nb = K / 256;
+    uint8_t* planes[4] = {nullptr, nullptr, nullptr, nullptr};
+    for (int k = 0; k < plane_count(type); ++k) {
+        keep.push_back(std::make_unique<DevBuf>((size_t)rows * m.nb * plane_sb_bytes(type, k)));
+        planes[k] = keep.back()->as<uint8_t>();
+        m.p[k] = planes[k];
+    }
+    launch_repack(staging->as<uint8_t>(), type, rows, K, planes, nullptr);
+    MI_HIP(hipDeviceSynchronize());
+    return m;
+}
+
+GemvParams single_gemv(const QMat& m, const float* x, float* y) {
+    GemvParams p;
+    std::memset(&p, 0, sizeof(p));
+    p.pro = PRO_PLAIN;
+    p.nslots = 1;
+    p.x[0] = x;
+    p.K = m.K;
+    p.nseg = 1;
+    p.seg[0].A = m;
+    p.seg[0].pair = PAIR_ADJ;
+    p.seg[0].epi = EPI_STORE;
+    p.seg[0].units = (m.rows + 1) / 2;
+    p.seg[0].expA = p.seg[0].expB = -1;
+    p.seg[0].out = y;
+    p.total_units = p.seg[0].units;
+    p.need_q8k = m.type != T_Q8_0;
+    p.need_q80 = m.type == T_Q8_0;
+    return p;
+}
+
+void ensure_attrs(int device) {
+    static std::vector<int> done(64, 0);
+    if (device >= 0 && device < 64 && !done[device]) {
+        init_kernel_attributes();
+        done[device] = 1;
+    }
+}
+}  // namespace
+
+extern "C" {
+
+int32_t mi_op_gemv(int32_t device, int32_t type, const void* raw, int32_t rows, int32_t K, const float* x, float* y) {
+    try {
+        MI_HIP(hipSetDevice(device));
+        ensure_attrs(device);
+        std::vector<std::unique_ptr<DevBuf>> keep;
+        const QMat m = upload_qmat(type, raw, rows, K, keep);
+        DevBuf dx(K * sizeof(float)), dy(rows * sizeof(float));
+        MI_HIP(hipMemcpy(dx.p, x, K * sizeof(float), hipMemcpyHostToDevice));
+        launch_gemv(single_gemv(m, dx.as<float>(), dy.as<float>()), ROLE_GENERIC, 0, nullptr);
+        MI_HIP(hipDeviceSynchronize());
+        MI_HIP(hipMemcpy(y, dy.p, rows * sizeof(float), hipMemcpyDeviceToHost));
+        return 0;
+    }
+    MI_TRY(-1)
+}
+
+int32_t mi_op_gemv_bench(int32_t device, int32_t type, const void* raw, int32_t rows, int32_t K, int32_t iters,
+                         float* median_us) {
+    try {
+        MI_HIP(hipSetDevice(device));
+        ensure_attrs(device);
+        std::vector<std::unique_ptr<DevBuf>> keep;
+        const QMat m = upload_qmat(type, raw, rows, K, keep);
+        DevBuf dx(K * sizeof(float)), dy(rows * sizeof(float));
+        std::vector<float> hx(K, 0.5f);
+        MI_HIP(hipMemcpy(dx.p, hx.data(), K * sizeof(float), hipMemcpyHostToDevice));
+        const GemvParams p = single_gemv(m, dx.as<float>(), dy.as<float>());
+        hipEvent_t a, b;
+        MI_HIP(hipEventCreate(&a));
+        MI_HIP(hipEventCreate(&b));
+        std::vector<float> t;
+        for (int i = 0; i < 10; ++i) launch_gemv(p, ROLE_GENERIC, 0, nullptr);
+        for (int i = 0; i < iters; ++i) {
+            MI_HIP(hipEventRecord(a, nullptr));
+            launch_gemv(p, ROLE_GENERIC, 0, nullptr);
+            MI_HIP(hipEventRecord(b, nullptr));
+            MI_HIP(hipEventSynchronize(b));
+            float ms = 0;
+            MI_HIP(hipEventElapsedTime(&ms, a, b));
+            t.push_back(ms * 1000.0f);
+        }
+        hipEventDestroy(a);
+        hipEventDestroy(b);
+        std::sort(t.begin(), t.end());
+        *median_us = t.empty() ? 0.0f : t[t.size() / 2];
+        return 0;
+    }
+    MI_TRY(-1)
+}
+
+int32_t mi_op_dequant(int32_t device, int32_t type, const void* raw, int32_t rows, int32_t K, float* out) {
+    try {
+        MI_HIP(hipSetDevice(device));
+        std::vector<std::unique_ptr<DevBuf>> keep;
+        const QMat m = upload_qmat(type, raw, rows, K, keep);
+        DevBuf d((size_t)rows * K * sizeof(float));
+        launch_dequant_rows(m, 0, rows, d.as<float>(), nullptr);
+        MI_HIP(hipDeviceSynchronize());
+        MI_HIP(hipMemcpy(out, d.p, (size_t)rows * K * sizeof(float), hipMemcpyDeviceToHost));
+        return 0;
+    }
+    MI_TRY(-1)
+}
+
+int32_t mi_op_quantize_q8_K(int32_t device, const float* x, int32_t K, int8_t* qs, float* d, int32_t* bsums) {
+    try {
+        if (K % 256) throw Error("K must be a multiple of 256");
+        MI_HIP(hipSetDevice(device));
+        const int nb = K / 256;
+        DevBuf dx(K * sizeof(float)), dq(K), dd(nb * sizeof(float)), db(nb * 16 * sizeof(int));
+        MI_HIP(hipMemcpy(dx.p, x, K * sizeof(float), hipMemcpyHostToDevice));
+        launch_quantize_q8k(dx.as<float>(), K, dq.as<int8_t>(), dd.as<float>(), db.as<int>(), nullptr);
+        MI_HIP(hipDeviceSynchronize());
+        MI_HIP(hipMemcpy(qs, dq.p, K, hipMemcpyDeviceToHost));
+        MI_HIP(hipMemcpy(d, dd.p, nb * sizeof(float), hipMemcpyDeviceToHost));
+        MI_HIP(hipMemcpy(bsums, db.p, nb * 16 * sizeof(int), hipMemcpyDeviceToHost));
+        return 0;
+    }
+    MI_TRY(-1)
+}
+
+int32_t mi_op_topk(int32_t device, const float* logits, int32_t n, int32_t k, int32_t* ids, float* vals) {
+    try {
+        if (k < 0 || k > TOPK_MAX) throw Error("k must be in [0, 64]");
+        MI_HIP(hipSetDevice(device));
+        DevBuf dl(n * sizeof(float)), dc(TOPK_GROUPS * TOPK_MAX * 8), di(TOPK_MAX * 4), dv(TOPK_MAX * 4);
+        MI_HIP(hipMemcpy(dl.p, logits, n * sizeof(float), hipMemcpyHostToDevice));
+        TopkParams tp{dl.as<float>(), n, dc.as<unsigned long long>(), di.as<int>(), dv.as<float>()};
+        launch_topk(tp, nullptr);
+        MI_HIP(hipDeviceSynchronize());
+        std::vector<int> hi(TOPK_MAX);
+        std::vector<float> hv(TOPK_MAX);
+        MI_HIP(hipMemcpy(hi.data(), di.p, TOPK_MAX * 4, hipMemcpyDeviceToHost));
+        MI_HIP(hipMemcpy(hv.data(), dv.p, TOPK_MAX * 4, hipMemcpyDeviceToHost));
+        for (int i = 0; i < k; ++i) { ids[i] = hi[i]; vals[i] = hv[i]; }
+        return k;
+    }
+    MI_TRY(-1)
+}
+
+}  // extern "C"

@@ -1,0 +1,869 @@
+// Engine host code: GGUF parsing, weight residency and the batch-1 decode
+// schedule captured into HIP graphs.
+//
+// Reference anchors (the llama.h functions this replaces):
+//   llama_model_load_from_file  /root/reference/inference/code/llama/Model.cpp:52
+//   llama_init_from_model       /root/reference/inference/code/llama/Instance.cpp:36
+//   llama_decode                /root/reference/inference/code/llama/Session.cpp:388
+//   llama_get_logits_ith        /root/reference/inference/code/llama/Session.cpp:24
+//   llama_kv_self_*             /root/reference/inference/code/llama/Session.cpp:53,341-361
+//   llama_state_*               /root/reference/inference/code/llama/Session.cpp:291-304
+#include "engine.h"
+
+#include <algorithm>
+#include <climits>
+#include <cmath>
+#include <cstring>
+
+namespace mi {
+
+static thread_local std::string g_last_error;
+void set_last_error(const std::string& s) { g_last_error = s; }
+const char* last_error() { return g_last_error.c_str(); }
+
+// ================================================================== GGUF ===
+namespace {
+struct Reader {
+    const uint8_t* p;
+    size_t n, pos = 0;
+    void need(size_t k) {
+        if (pos + k > n) throw Error("GGUF: truncated header");
+    }
+    template <class T> T rd() {
+        need(sizeof(T));
+        T v;
+        std::memcpy(&v, p + pos, sizeof(T));
+        pos += sizeof(T);
+        return v;
+    }
+    std::string str() {
+        const uint64_t len = rd<uint64_t>();
+        need(len);
+        std::string s(reinterpret_cast<const char*>(p + pos), len);
+        pos += len;
+        return s;
+    }
+};
+
+enum { G_U8 = 0, G_I8, G_U16, G_I16, G_U32, G_I32, G_F32, G_BOOL, G_STR, G_ARR, G_U64, G_I64, G_F64 };
+
+double read_num(Reader& r, int t, bool* is_float) {
+    *is_float = false;
+    switch (t) {
+    case G_U8: return r.rd<uint8_t>();
+    case G_I8: return r.rd<int8_t>();
+    case G_U16: return r.rd<uint16_t>();
+    case G_I16: return r.rd<int16_t>();
+    case G_U32: return r.rd<uint32_t>();
+    case G_I32: return r.rd<int32_t>();
+    case G_F32: *is_float = true; return r.rd<float>();
+    case G_BOOL: return r.rd<uint8_t>();
+    case G_U64: return (double)r.rd<uint64_t>();
+    case G_I64: return (double)r.rd<int64_t>();
+    case G_F64: *is_float = true; return r.rd<double>();
+    default: throw Error("GGUF: bad value type");
+    }
+}
+}  // namespace
+
+void Gguf::parse(const uint8_t* data, size_t size) {
+    Reader r{data, size};
+    if (size < 24 || std::memcmp(data, "GGUF", 4) != 0) throw Error("not a GGUF file");
+    r.pos = 4;
+    const uint32_t ver = r.rd<uint32_t>();
+    if (ver != 2 && ver != 3) throw Error("unsupported GGUF version " + std::to_string(ver));
+    const uint64_t nt = r.rd<uint64_t>(), nkv = r.rd<uint64_t>();
+    for (uint64_t i = 0; i < nkv; ++i) {
+        std::string key = r.str();
+        GgufValue v;
+        v.type = (int)r.rd<uint32_t>();
+        if (v.type == G_STR) {
+            v.s = r.str();
+        } else if (v.type == G_ARR) {
+            v.arr_type = (int)r.rd<uint32_t>();
+            v.arr_n = (long long)r.rd<uint64_t>();
+            if (v.arr_type == G_STR) {
+                v.arr_s.reserve(v.arr_n);
+                for (long long k = 0; k < v.arr_n; ++k) v.arr_s.push_back(r.str());
+            } else {
+                v.arr_num.reserve(v.arr_n);
+                bool fl;
+                for (long long k = 0; k < v.arr_n; ++k) v.arr_num.push_back(read_num(r, v.arr_type, &fl));
+            }
+        } else {
+            bool fl;
+            const double d = read_num(r, v.type, &fl);
+            v.f = d;
+            v.i = (long long)d;
+        }
+        kv.emplace(std::move(key), std::move(v));
+    }
+    for (uint64_t i = 0; i < nt; ++i) {
+        GgufTensor t;
+        t.name = r.str();
+        t.n_dims = (int)r.rd<uint32_t>();
+        if (t.n_dims < 1 || t.n_dims > 4) throw Error("GGUF: bad n_dims for " + t.name);
+        long long n = 1;
+        for (int d = 0; d < t.n_dims; ++d) { t.ne[d] = (long long)r.rd<uint64_t>(); n *= t.ne[d]; }
+        t.type = (int)r.rd<uint32_t>();
+        t.offset = r.rd<uint64_t>();
+        const int be = block_elems(t.type), bb = block_bytes(t.type);
+        if (bb == 0) {
+            t.nbytes = 0;   // unsupported type: only an error if the tensor is used
+        } else {
+            if (n % be) throw Error("GGUF: tensor " + t.name + " not a whole number of blocks");
+            t.nbytes = (size_t)(n / be) * bb;
+        }
+        tensors.push_back(t);
+    }
+    const long long align = get_int("general.alignment", 32);
+    data_offset = (r.pos + align - 1) / align * align;
+}
+
+long long Gguf::get_int(const std::string& k, long long def) const {
+    const GgufValue* v = get(k);
+    return (v && v->type != G_STR && v->type != G_ARR) ? v->i : def;
+}
+double Gguf::get_float(const std::string& k, double def) const {
+    const GgufValue* v = get(k);
+    return (v && v->type != G_STR && v->type != G_ARR) ? v->f : def;
+}
+std::string Gguf::get_str(const std::string& k, const std::string& def) const {
+    const GgufValue* v = get(k);
+    return (v && v->type == G_STR) ? v->s : def;
+}
+const GgufTensor* Gguf::tensor(const std::string& name) const {
+    for (const auto& t : tensors)
+        if (t.name == name) return &t;
+    return nullptr;
+}
+
+// ================================================================= model ===
+Model::~Model() {
+    if (arena) {
+        hipSetDevice(device);
+        hipFree(arena);
+    }
+}
+
+const QMat* Model::find_qmat(const std::string&) const { return nullptr; }
+
+namespace {
+size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
+
+struct Planned {
+    const GgufTensor* t;
+    size_t off[4];     // arena offsets of the planes (quant) or of the raw copy (p0)
+    long long rows;    // rows across all experts
+    int K;
+    int experts;
+};
+}  // namespace
+
+void Model::load(const uint8_t* data, size_t size, const mi_model_params& p) {
+    device = p.device_ordinal;
+    vocab_only = p.vocab_only != 0;
+    gguf.parse(data, size);
+    const std::string arch = gguf.get_str("general.architecture", "");
+    if (arch != "llama")
+        throw Error("unsupported architecture '" + arch + "' (this backend serves the llama graph)");
+    auto key = [&](const char* k) { return arch + "." + k; };
+    hp.n_embd = (int)gguf.get_int(key("embedding_length"), 0);
+    hp.n_layer = (int)gguf.get_int(key("block_count"), 0);
+    hp.n_ff = (int)gguf.get_int(key("feed_forward_length"), 0);
+    hp.n_head = (int)gguf.get_int(key("attention.head_count"), 0);
+    hp.n_head_kv = (int)gguf.get_int(key("attention.head_count_kv"), hp.n_head);
+    hp.n_ctx_train = (int)gguf.get_int(key("context_length"), 2048);
+    hp.eps = (float)gguf.get_float(key("attention.layer_norm_rms_epsilon"), 1e-5);
+    hp.rope_base = (float)gguf.get_float(key("rope.freq_base"), 10000.0);
+    const double fs = gguf.get_float(key("rope.scale_linear"), 0.0);
+    hp.freq_scale = fs > 0.0 ? (float)(1.0 / fs) : 1.0f;
+    hp.n_expert = (int)gguf.get_int(key("expert_count"), 0);
+    hp.n_expert_used = (int)gguf.get_int(key("expert_used_count"), 0);
+    if (hp.n_embd <= 0 || hp.n_layer <= 0 || hp.n_head <= 0) throw Error("GGUF: missing llama hparams");
+    hp.head_dim = hp.n_embd / hp.n_head;
+    hp.n_rot = (int)gguf.get_int(key("rope.dimension_count"), hp.head_dim);
+
+    if (const GgufValue* tv = gguf.get("tokenizer.ggml.tokens")) tokens = tv->arr_s;
+    if (const GgufValue* tt = gguf.get("tokenizer.ggml.token_type"))
+        for (double d : tt->arr_num) token_type.push_back((int)d);
+    hp.n_vocab = (int)tokens.size();
+    if (const GgufTensor* te = gguf.tensor("token_embd.weight")) hp.n_vocab = (int)te->ne[1];
+    bos = (int)gguf.get_int("tokenizer.ggml.bos_token_id", 1);
+    eos = (int)gguf.get_int("tokenizer.ggml.eos_token_id", 2);
+    eot = (int)gguf.get_int("tokenizer.ggml.eot_token_id", -1);
+    add_bos = gguf.get_int("tokenizer.ggml.add_bos_token", 1) != 0;
+    if (vocab_only) return;
+    if (p.cpu_only) throw Error("cpu_only models are served by the CPU reference path, not this engine");
+
+    // ---- plan the arena ----
+    std::vector<Planned> plan;
+    size_t off = 0;
+    auto add = [&](const std::string& name, bool required, int experts) -> int {
+        const GgufTensor* t = gguf.tensor(name);
+        if (!t) {
+            if (required) throw Error("GGUF: missing tensor " + name);
+            return -1;
+        }
+        Planned pl{};
+        pl.t = t;
+        pl.K = (int)t->ne[0];
+        pl.experts = experts;
+        pl.rows = t->ne[1] * (t->n_dims > 2 ? t->ne[2] : 1);
+        if (is_quant(t->type)) {
+            if (pl.K % 256) throw Error("tensor " + name + ": K not a multiple of 256");
+            const long long nsb = pl.rows * (pl.K / 256);
+            for (int k = 0; k < plane_count(t->type); ++k) {
+                pl.off[k] = off;
+                off = align256(off + (size_t)nsb * plane_sb_bytes(t->type, k));
+            }
+        } else if (t->type == T_F32 || t->type == T_F16) {
+            pl.off[0] = off;
+            off = align256(off + t->nbytes);
+        } else {
+            throw Error("tensor " + name + ": unsupported ggml type " + std::to_string(t->type));
+        }
+        plan.push_back(pl);
+        return (int)plan.size() - 1;
+    };
+    struct LayerIdx { int an, fn, q, k, v, o, g, u, d, r; };
+    const int i_te = add("token_embd.weight", true, 1);
+    const int i_on = add("output_norm.weight", true, 1);
+    int i_out = add("output.weight", false, 1);
+    const int i_rf = add("rope_freqs.weight", false, 1);
+    std::vector<LayerIdx> li(hp.n_layer);
+    const int E = hp.n_expert > 0 ? hp.n_expert : 1;
+    for (int l = 0; l < hp.n_layer; ++l) {
+        const std::string b = "blk." + std::to_string(l) + ".";
+        LayerIdx& x = li[l];
+        x.an = add(b + "attn_norm.weight", true, 1);
+        x.fn = add(b + "ffn_norm.weight", true, 1);
+        x.q = add(b + "attn_q.weight", true, 1);
+        x.k = add(b + "attn_k.weight", true, 1);
+        x.v = add(b + "attn_v.weight", true, 1);
+        x.o = add(b + "attn_output.weight", true, 1);
+        if (hp.n_expert > 0) {
+            x.r = add(b + "ffn_gate_inp.weight", true, 1);
+            x.g = add(b + "ffn_gate_exps.weight", true, E);
+            x.u = add(b + "ffn_up_exps.weight", true, E);
+            x.d = add(b + "ffn_down_exps.weight", true, E);
+        } else {
+            x.r = -1;
+            x.g = add(b + "ffn_gate.weight", true, 1);
+            x.u = add(b + "ffn_up.weight", true, 1);
+            x.d = add(b + "ffn_down.weight", true, 1);
+        }
+    }
+    if (hp.n_expert > 0 && hp.n_expert_used != 2)
+        throw Error("MoE: this build serves top-2 routing (expert_used_count=2)");
+    arena_bytes = off;
+    for (const auto& pl : plan) {
+        if (pl.t->name != "token_embd.weight") weight_bytes += (long long)pl.t->nbytes;
+        if (pl.t->type >= 0 && pl.t->type < 32) type_bytes[pl.t->type] += (long long)pl.t->nbytes;
+    }
+    if (i_out < 0) weight_bytes += (long long)plan[i_te].t->nbytes;   // tied output head
+
+    MI_HIP(hipSetDevice(device));
+    MI_HIP(hipMalloc(&arena, arena_bytes));
+
+    // ---- upload + repack ----
+    if (!p.no_upload) {
+        size_t max_raw = 0;
+        for (const auto& pl : plan)
+            if (is_quant(pl.t->type)) max_raw = std::max(max_raw, pl.t->nbytes);
+        uint8_t* staging = nullptr;
+        if (max_raw) MI_HIP(hipMalloc(&staging, max_raw));
+        for (const auto& pl : plan) {
+            const size_t src = gguf.data_offset + pl.t->offset;
+            if (src + pl.t->nbytes > size) {
+                if (staging) hipFree(staging);
+                throw Error("GGUF: tensor data of " + pl.t->name + " beyond the end of the image");
+            }
+            if (is_quant(pl.t->type)) {
+                MI_HIP(hipMemcpy(staging, data + src, pl.t->nbytes, hipMemcpyHostToDevice));
+                uint8_t* planes[4] = {arena + pl.off[0], arena + pl.off[1], arena + pl.off[2], arena + pl.off[3]};
+                launch_repack(staging, pl.t->type, pl.rows, pl.K, planes, nullptr);
+            } else {
+                MI_HIP(hipMemcpy(arena + pl.off[0], data + src, pl.t->nbytes, hipMemcpyHostToDevice));
+            }
+        }
+        MI_HIP(hipDeviceSynchronize());
+        if (staging) hipFree(staging);
+    }
+
+    // ---- device views ----
+    auto qm = [&](int idx) -> QMat {
+        QMat m{};
+        const Planned& pl = plan[idx];
+        m.type = pl.t->type;
+        m.K = pl.K;
+        m.nb = pl.K / 256;
+        m.rows = (int)(pl.rows / pl.experts);
+        if (is_quant(m.type)) {
+            for (int k = 0; k < plane_count(m.type); ++k) {
+                m.p[k] = arena + pl.off[k];
+                m.expert_stride[k] = (long long)m.rows * m.nb * plane_sb_bytes(m.type, k);
+            }
+        } else {
+            m.p[0] = arena + pl.off[0];
+        }
+        return m;
+    };
+    auto f32p = [&](int idx) -> float* {
+        if (idx < 0) return nullptr;
+        if (plan[idx].t->type != T_F32) throw Error("tensor " + plan[idx].t->name + " must be F32");
+        return reinterpret_cast<float*>(arena + plan[idx].off[0]);
+    };
+    tok_embd = qm(i_te);
+    output = i_out >= 0 ? qm(i_out) : qm(i_te);
+    if (!is_quant(output.type)) throw Error("output head must be a quantised tensor in this build");
+    output_norm = f32p(i_on);
+    rope_freqs = f32p(i_rf);
+    layers.resize(hp.n_layer);
+    for (int l = 0; l < hp.n_layer; ++l) {
+        Layer& L = layers[l];
+        const LayerIdx& x = li[l];
+        L.attn_norm = f32p(x.an);
+        L.ffn_norm = f32p(x.fn);
+        L.wq = qm(x.q); L.wk = qm(x.k); L.wv = qm(x.v); L.wo = qm(x.o);
+        L.gate = qm(x.g); L.up = qm(x.u); L.down = qm(x.d);
+        L.router = f32p(x.r);
+        for (const QMat* m : {&L.wq, &L.wk, &L.wv, &L.wo, &L.gate, &L.up, &L.down})
+            if (!is_quant(m->type)) throw Error("layer weights must be quantised (Q4_K/Q5_K/Q6_K/Q8_0)");
+    }
+}
+
+// =============================================================== context ===
+namespace {
+std::vector<int> g_attr_done(64, 0);
+
+void seg_init(GemvSeg& s) {
+    std::memset(&s, 0, sizeof(s));
+    s.expA = s.expB = -1;
+}
+void params_finish(GemvParams& p) {
+    int u = 0;
+    p.need_q8k = p.need_q80 = 0;
+    for (int i = 0; i < p.nseg; ++i) {
+        p.seg[i].unit0 = u;
+        u += p.seg[i].units;
+        for (const QMat* m : {&p.seg[i].A, &p.seg[i].B}) {
+            if (!m->p[0]) continue;
+            if (m->type == T_Q8_0) p.need_q80 = 1; else p.need_q8k = 1;
+        }
+    }
+    p.total_units = u;
+}
+}  // namespace
+
+Ctx::Ctx(Model* model, uint32_t nctx, uint32_t nbatch, uint32_t nubatch) : m(model) {
+    if (m->vocab_only) throw Error("cannot create a context on a vocab-only model");
+    device = m->device;
+    MI_HIP(hipSetDevice(device));
+    n_ctx = nctx ? nctx : (uint32_t)m->hp.n_ctx_train;
+    n_batch = std::min(nbatch ? nbatch : 2048u, n_ctx);   // "may be silently truncated to ctxSize"
+    n_ubatch = nubatch ? std::min(nubatch, n_batch) : n_batch;
+    const HParams& hp = m->hp;
+    kv_dim = hp.n_head_kv * hp.head_dim;
+    if ((size_t)n_ctx * 4 + 8192 > 160 * 1024) throw Error("n_ctx too large for this build's attention kernel");
+    if (device < (int)g_attr_done.size() && !g_attr_done[device]) {
+        init_kernel_attributes();
+        g_attr_done[device] = 1;
+    }
+    MI_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    const size_t kvb = (size_t)hp.n_layer * n_ctx * kv_dim * sizeof(__half);
+    MI_HIP(hipMalloc(&kcache, kvb));
+    MI_HIP(hipMalloc(&vcache, kvb));
+    MI_HIP(hipMemset(kcache, 0, kvb));
+    MI_HIP(hipMemset(vcache, 0, kvb));
+    MI_HIP(hipMalloc(&cell_pos, n_ctx * sizeof(int)));
+    MI_HIP(hipMemset(cell_pos, 0, n_ctx * sizeof(int)));
+    MI_HIP(hipMalloc(&tokpos, 4 * sizeof(int)));
+    MI_HIP(hipMemset(tokpos, 0, 4 * sizeof(int)));
+    const int big = std::max(hp.n_embd, hp.n_ff);
+    MI_HIP(hipMalloc(&x, hp.n_embd * sizeof(float)));
+    MI_HIP(hipMalloc(&q, hp.n_embd * sizeof(float)));
+    MI_HIP(hipMalloc(&attn, hp.n_embd * sizeof(float)));
+    MI_HIP(hipMalloc(&h, big * sizeof(float)));
+    MI_HIP(hipMalloc(&h2, big * sizeof(float)));
+    MI_HIP(hipMalloc(&logits, (size_t)hp.n_vocab * sizeof(float)));
+    MI_HIP(hipMalloc(&cand, TOPK_GROUPS * TOPK_MAX * sizeof(unsigned long long)));
+    MI_HIP(hipMalloc(&topk_ids, TOPK_MAX * sizeof(int)));
+    MI_HIP(hipMalloc(&topk_vals, TOPK_MAX * sizeof(float)));
+    MI_HIP(hipMalloc(&sel, 64 * sizeof(int)));
+    MI_HIP(hipMalloc(&selw, 64 * sizeof(float)));
+    MI_HIP(hipMemset(sel, 0, 64 * sizeof(int)));
+    MI_HIP(hipMemset(selw, 0, 64 * sizeof(float)));
+    MI_HIP(hipMalloc(&gather_ids, 4096 * sizeof(int)));
+    MI_HIP(hipMalloc(&gather_out, 4096 * sizeof(float)));
+    MI_HIP(hipMalloc(&cell_delta, n_ctx * sizeof(int)));
+    MI_HIP(hipMalloc(&move_src, n_ctx * sizeof(int)));
+    MI_HIP(hipHostMalloc(&h_tokpos, kTokRing * 4 * sizeof(int)));
+    MI_HIP(hipHostMalloc(&h_topk_ids, TOPK_MAX * sizeof(int)));
+    MI_HIP(hipHostMalloc(&h_topk_vals, TOPK_MAX * sizeof(float)));
+    MI_HIP(hipHostMalloc(&h_logits, (size_t)hp.n_vocab * sizeof(float)));
+    MI_HIP(hipHostMalloc(&h_gather, 4096 * sizeof(float)));
+    h_cell_pos.assign(n_ctx, 0);
+}
+
+Ctx::~Ctx() {
+    hipSetDevice(device);
+    if (stream) hipStreamSynchronize(stream);
+    invalidate_graphs();
+    for (auto e : prof_ev) if (e) hipEventDestroy(e);
+    for (void* p : {(void*)kcache, (void*)vcache, (void*)kv_scratch, (void*)cell_pos, (void*)tokpos, (void*)x,
+                    (void*)q, (void*)attn, (void*)h, (void*)h2, (void*)logits, (void*)cand, (void*)topk_ids,
+                    (void*)topk_vals, (void*)sel, (void*)selw, (void*)gather_ids, (void*)gather_out,
+                    (void*)cell_delta, (void*)move_src})
+        if (p) hipFree(p);
+    for (void* p : {(void*)h_tokpos, (void*)h_topk_ids, (void*)h_topk_vals, (void*)h_logits, (void*)h_gather})
+        if (p) hipHostFree(p);
+    if (stream) hipStreamDestroy(stream);
+}
+
+void Ctx::invalidate_graphs() {
+    if (g_full) hipGraphExecDestroy(g_full);
+    if (g_nolog) hipGraphExecDestroy(g_nolog);
+    for (auto& g : g_seg) {
+        if (g) hipGraphExecDestroy(g);
+        g = nullptr;
+    }
+    g_full = g_nolog = nullptr;
+}
+
+long long Ctx::ffn_bytes() const {
+    const Layer& L = m->layers[0];
+    auto mb = [](const QMat& q) { return (long long)q.rows * q.nb * ((long long)block_bytes(q.type) * 256 / block_elems(q.type)); };
+    const HParams& hp = m->hp;
+    const long long w = hp.n_expert > 0 ? 2 * (mb(L.gate) + mb(L.up)) : mb(L.gate) + mb(L.up);
+    const long long act = (long long)hp.n_embd * 4 * 2 + (long long)hp.n_ff * 4 * (hp.n_expert > 0 ? 2 : 1);
+    return w + act;   // weights + x and norm weight read + h written
+}
+
+// One decode step for the token in tokpos (batch 1): the llm_build_llama graph.
+// With seg_filter >= 0 only the ops of that profiling segment are enqueued
+// (0: up to layer prof_layer's FFN gate/up, 1: that launch, 2: the rest).
+void Ctx::enqueue_step(bool with_logits) {
+    const HParams& hp = m->hp;
+    int seg = 0;
+    auto on = [&]() { return seg_filter < 0 || seg_filter == seg; };
+    EmbedParams ep{m->tok_embd, tokpos, x, hp.n_embd};
+    if (on()) launch_embed(ep, stream);
+    const float theta_scale = std::pow(hp.rope_base, -2.0f / (float)hp.n_rot);
+    const float kq_scale = 1.0f / std::sqrt((float)hp.head_dim);
+    for (int l = 0; l < hp.n_layer; ++l) {
+        const Layer& L = m->layers[l];
+        __half* kl = kcache + (size_t)l * n_ctx * kv_dim;
+        __half* vl = vcache + (size_t)l * n_ctx * kv_dim;
+        GemvParams base;
+        std::memset(&base, 0, sizeof(base));
+        base.tokpos = tokpos;
+        base.cell_pos = cell_pos;
+        base.head_dim = hp.head_dim;
+        base.kv_dim = kv_dim;
+        base.sel = sel;
+        base.selw = selw;
+        base.eps = hp.eps;
+        base.nslots = 1;
+        // ---- Q/K/V projections + RoPE + KV append ----
+        {
+            GemvParams p = base;
+            p.pro = PRO_RMSNORM;
+            p.x[0] = x;
+            p.norm_w = L.attn_norm;
+            p.K = hp.n_embd;
+            p.theta_scale = theta_scale;
+            p.freq_scale = hp.freq_scale;
+            p.n_rot = hp.n_rot;
+            p.freq_factors = m->rope_freqs;
+            p.kcache = kl;
+            p.vcache = vl;
+            p.nseg = 3;
+            const QMat* mats[3] = {&L.wq, &L.wk, &L.wv};
+            const int epis[3] = {EPI_ROPE_Q, EPI_ROPE_K, EPI_V};
+            for (int i = 0; i < 3; ++i) {
+                seg_init(p.seg[i]);
+                p.seg[i].A = *mats[i];
+                p.seg[i].pair = PAIR_ADJ;
+                p.seg[i].epi = epis[i];
+                p.seg[i].units = (mats[i]->rows + 1) / 2;
+                p.seg[i].out = q;
+            }
+            params_finish(p);
+            if (on()) launch_gemv(p, ROLE_QKV, 0, stream);
+        }
+        // ---- attention ----
+        {
+            AttnParams a{q, kl, vl, tokpos, cell_pos, attn, hp.n_head, hp.n_head_kv, hp.head_dim, kv_dim,
+                         (int)n_ctx, kq_scale};
+            if (on()) launch_attn(a, stream);
+        }
+        // ---- output projection + residual ----
+        {
+            GemvParams p = base;
+            p.pro = PRO_PLAIN;
+            p.x[0] = attn;
+            p.K = hp.n_embd;
+            p.nseg = 1;
+            seg_init(p.seg[0]);
+            p.seg[0].A = L.wo;
+            p.seg[0].pair = PAIR_ADJ;
+            p.seg[0].epi = EPI_ADD;
+            p.seg[0].units = (L.wo.rows + 1) / 2;
+            p.seg[0].out = x;
+            p.seg[0].resid = x;
+            params_finish(p);
+            if (on()) launch_gemv(p, ROLE_WO, 0, stream);
+        }
+        if (hp.n_expert > 0) {
+            RouterParams rp{x, L.ffn_norm, hp.eps, L.router, hp.n_embd, hp.n_expert, hp.n_expert_used, sel, selw};
+            if (on()) launch_router(rp, stream);
+        }
+        // ---- FFN gate/up + SwiGLU ----
+        {
+            GemvParams p = base;
+            p.pro = PRO_RMSNORM;
+            p.x[0] = x;
+            p.norm_w = L.ffn_norm;
+            p.K = hp.n_embd;
+            const int nsl = hp.n_expert > 0 ? 2 : 1;
+            p.nseg = nsl;
+            for (int k = 0; k < nsl; ++k) {
+                seg_init(p.seg[k]);
+                p.seg[k].A = L.gate;
+                p.seg[k].B = L.up;
+                p.seg[k].pair = PAIR_AB;
+                p.seg[k].epi = EPI_SWIGLU;
+                p.seg[k].units = L.gate.rows;
+                p.seg[k].out = k == 0 ? h : h2;
+                if (hp.n_expert > 0) p.seg[k].expA = p.seg[k].expB = k;
+            }
+            params_finish(p);
+            if (l == prof_layer) seg = 1;
+            if (on()) launch_gemv(p, ROLE_FFN_UP, 0, stream);
+            if (l == prof_layer) seg = 2;
+        }
+        // ---- FFN down + residual ----
+        {
+            GemvParams p = base;
+            p.pro = PRO_PLAIN;
+            p.x[0] = h;
+            p.K = hp.n_ff;
+            p.nseg = 1;
+            seg_init(p.seg[0]);
+            if (hp.n_expert > 0) {
+                p.nslots = 2;
+                p.x[1] = h2;
+                p.seg[0].A = L.down;
+                p.seg[0].B = L.down;
+                p.seg[0].pair = PAIR_AB;
+                p.seg[0].epi = EPI_MOE_DOWN;
+                p.seg[0].units = L.down.rows;
+                p.seg[0].actA = 0;
+                p.seg[0].actB = 1;
+                p.seg[0].expA = 0;
+                p.seg[0].expB = 1;
+            } else {
+                p.seg[0].A = L.down;
+                p.seg[0].pair = PAIR_ADJ;
+                p.seg[0].epi = EPI_ADD;
+                p.seg[0].units = (L.down.rows + 1) / 2;
+            }
+            p.seg[0].out = x;
+            p.seg[0].resid = x;
+            params_finish(p);
+            if (on()) launch_gemv(p, ROLE_FFN_DOWN, 0, stream);
+        }
+    }
+    if (with_logits && on()) {
+        GemvParams p;
+        std::memset(&p, 0, sizeof(p));
+        p.pro = PRO_RMSNORM;
+        p.nslots = 1;
+        p.x[0] = x;
+        p.norm_w = m->output_norm;
+        p.eps = hp.eps;
+        p.K = hp.n_embd;
+        p.tokpos = tokpos;
+        p.nseg = 1;
+        seg_init(p.seg[0]);
+        p.seg[0].A = m->output;
+        p.seg[0].pair = PAIR_ADJ;
+        p.seg[0].epi = EPI_STORE;
+        p.seg[0].units = (m->output.rows + 1) / 2;
+        p.seg[0].out = logits;
+        params_finish(p);
+        launch_gemv(p, ROLE_OUTPUT, 0, stream);
+        TopkParams tp{logits, hp.n_vocab, cand, topk_ids, topk_vals};
+        launch_topk(tp, stream);
+        MI_HIP(hipMemcpyAsync(h_topk_ids, topk_ids, TOPK_MAX * sizeof(int), hipMemcpyDeviceToHost, stream));
+        MI_HIP(hipMemcpyAsync(h_topk_vals, topk_vals, TOPK_MAX * sizeof(float), hipMemcpyDeviceToHost, stream));
+    }
+}
+
+hipGraphExec_t Ctx::build_graph(bool with_logits, int seg) {
+    hipGraph_t g = nullptr;
+    seg_filter = seg;
+    MI_HIP(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
+    try {
+        enqueue_step(with_logits);
+    } catch (...) {
+        seg_filter = -1;
+        hipStreamEndCapture(stream, &g);
+        if (g) hipGraphDestroy(g);
+        throw;
+    }
+    seg_filter = -1;
+    MI_HIP(hipStreamEndCapture(stream, &g));
+    hipGraphExec_t ex = nullptr;
+    MI_HIP(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+    MI_HIP(hipGraphDestroy(g));
+    return ex;
+}
+
+int Ctx::decode(const int32_t* tokens, int n) {
+    MI_HIP(hipSetDevice(device));
+    if (n <= 0) throw Error("decode: empty batch");
+    for (int i = 0; i < n; ++i)
+        if (tokens[i] < 0 || tokens[i] >= m->hp.n_vocab) throw Error("decode: token id out of range");
+    if (n_cells + n > (int)n_ctx) return 1;   // no KV slot (llama_decode returns 1)
+    for (int i = 0; i < n; ++i) {
+        const bool last = i == n - 1;
+        const int pos = pos_max + 1, cell = n_cells;
+        const long long slot = tok_slot++ % kTokRing;
+        if (slot == 0 && tok_slot > 1) MI_HIP(hipStreamSynchronize(stream));
+        int* hp = h_tokpos + slot * 4;
+        hp[0] = tokens[i];
+        hp[1] = pos;
+        hp[2] = cell;
+        hp[3] = 0;
+        MI_HIP(hipMemcpyAsync(tokpos, hp, 4 * sizeof(int), hipMemcpyHostToDevice, stream));
+        if (last && prof_layer >= 0 && prof_layer < m->hp.n_layer) {
+            for (int k = 0; k < 3; ++k)
+                if (!g_seg[k]) g_seg[k] = build_graph(true, k);
+            for (int k = 0; k < 2; ++k)
+                if (!prof_ev[k]) MI_HIP(hipEventCreate(&prof_ev[k]));
+            MI_HIP(hipGraphLaunch(g_seg[0], stream));
+            MI_HIP(hipEventRecord(prof_ev[0], stream));
+            MI_HIP(hipGraphLaunch(g_seg[1], stream));
+            MI_HIP(hipEventRecord(prof_ev[1], stream));
+            MI_HIP(hipGraphLaunch(g_seg[2], stream));
+            prof_pending = true;
+        } else {
+            hipGraphExec_t& g = last ? g_full : g_nolog;
+            if (!g) g = build_graph(last, -1);
+            MI_HIP(hipGraphLaunch(g, stream));
+        }
+        h_cell_pos[cell] = pos;
+        n_cells++;
+        pos_max = pos;
+    }
+    logits_valid = true;
+    return 0;
+}
+
+void Ctx::sync() {
+    MI_HIP(hipSetDevice(device));
+    MI_HIP(hipStreamSynchronize(stream));
+}
+
+int Ctx::topk(int k, int32_t* ids, float* vals) {
+    if (!logits_valid) throw Error("no logits: decode a token first");
+    if (k < 0 || k > TOPK_MAX) throw Error("topk: k must be in [0, 64]");
+    sync();
+    for (int i = 0; i < k; ++i) {
+        ids[i] = h_topk_ids[i];
+        vals[i] = h_topk_vals[i];
+    }
+    return k;
+}
+
+int Ctx::gather(const int32_t* ids, int n, float* out) {
+    if (!logits_valid) throw Error("no logits: decode a token first");
+    if (n < 0 || n > 4096) throw Error("gather: n must be in [0, 4096]");
+    for (int i = 0; i < n; ++i)
+        if (ids[i] < 0 || ids[i] >= m->hp.n_vocab) throw Error("gather: id out of range");
+    if (n == 0) return 0;
+    MI_HIP(hipSetDevice(device));
+    MI_HIP(hipMemcpyAsync(gather_ids, ids, n * sizeof(int), hipMemcpyHostToDevice, stream));
+    launch_gather(logits, gather_ids, n, gather_out, stream);
+    MI_HIP(hipMemcpyAsync(h_gather, gather_out, n * sizeof(float), hipMemcpyDeviceToHost, stream));
+    sync();
+    std::memcpy(out, h_gather, n * sizeof(float));
+    return n;
+}
+
+const float* Ctx::logits_host() {
+    if (!logits_valid) throw Error("no logits: decode a token first");
+    MI_HIP(hipSetDevice(device));
+    MI_HIP(hipMemcpyAsync(h_logits, logits, (size_t)m->hp.n_vocab * sizeof(float), hipMemcpyDeviceToHost, stream));
+    sync();
+    return h_logits;
+}
+
+void Ctx::kv_clear() {
+    n_cells = 0;
+    pos_max = -1;
+}
+
+// Remove cells with pos in [p0, p1); the survivors keep their order and are
+// compacted to the front of the cache.
+int Ctx::kv_seq_rm(int p0, int p1) {
+    if (p0 < 0) p0 = 0;
+    if (p1 < 0) p1 = INT_MAX;
+    std::vector<int> keep;
+    keep.reserve(n_cells);
+    for (int c = 0; c < n_cells; ++c)
+        if (h_cell_pos[c] < p0 || h_cell_pos[c] >= p1) keep.push_back(c);
+    bool prefix = true;
+    for (int j = 0; j < (int)keep.size(); ++j)
+        if (keep[j] != j) { prefix = false; break; }
+    if (!prefix) {
+        MI_HIP(hipSetDevice(device));
+        const HParams& hp = m->hp;
+        if (!kv_scratch) MI_HIP(hipMalloc(&kv_scratch, (size_t)hp.n_layer * n_ctx * kv_dim * sizeof(__half)));
+        MI_HIP(hipMemcpyAsync(move_src, keep.data(), keep.size() * sizeof(int), hipMemcpyHostToDevice, stream));
+        launch_kv_move(kcache, hp.n_layer, n_ctx, kv_dim, move_src, (int)keep.size(), kv_scratch, stream);
+        launch_kv_move(vcache, hp.n_layer, n_ctx, kv_dim, move_src, (int)keep.size(), kv_scratch, stream);
+        std::vector<int> np(keep.size());
+        for (size_t j = 0; j < keep.size(); ++j) np[j] = h_cell_pos[keep[j]];
+        for (size_t j = 0; j < keep.size(); ++j) h_cell_pos[j] = np[j];
+        MI_HIP(hipMemcpyAsync(cell_pos, h_cell_pos.data(), keep.size() * sizeof(int), hipMemcpyHostToDevice, stream));
+        sync();
+    }
+    n_cells = (int)keep.size();
+    pos_max = -1;
+    for (int c = 0; c < n_cells; ++c) pos_max = std::max(pos_max, h_cell_pos[c]);
+    return 0;
+}
+
+// seq_add (div == 0: pos += delta) / seq_div (pos /= div) over [p0, p1):
+// positions change and cached K is re-rotated by the delta (K-shift).
+int Ctx::kv_seq_shift(int p0, int p1, int delta, int div) {
+    if (p0 < 0) p0 = 0;
+    if (p1 < 0) p1 = INT_MAX;
+    if (p0 == p1) return 0;
+    if (div == 0 && delta == 0) return 0;
+    if (div == 1) return 0;
+    std::vector<int> dlt(n_cells, 0);
+    bool any = false, neg = false;
+    for (int c = 0; c < n_cells; ++c) {
+        const int ps = h_cell_pos[c];
+        if (ps >= p0 && ps < p1) {
+            const int np = div ? ps / div : ps + delta;
+            dlt[c] = np - ps;
+            h_cell_pos[c] = np;
+            any = any || dlt[c] != 0;
+            neg = neg || np < 0;
+        }
+    }
+    if (any) {
+        MI_HIP(hipSetDevice(device));
+        const HParams& hp = m->hp;
+        MI_HIP(hipMemcpyAsync(cell_delta, dlt.data(), n_cells * sizeof(int), hipMemcpyHostToDevice, stream));
+        KvShiftParams kp{kcache, hp.n_layer, (int)n_ctx, kv_dim, hp.head_dim, hp.n_rot, cell_delta, n_cells,
+                         std::pow(hp.rope_base, -2.0f / (float)hp.n_rot), hp.freq_scale, m->rope_freqs};
+        launch_kv_shift(kp, stream);
+        MI_HIP(hipMemcpyAsync(cell_pos, h_cell_pos.data(), n_cells * sizeof(int), hipMemcpyHostToDevice, stream));
+        sync();
+    }
+    if (neg) return kv_seq_rm(INT_MIN, 0);   // cells shifted below 0 are removed (llama.cpp semantics)
+    pos_max = -1;
+    for (int c = 0; c < n_cells; ++c) pos_max = std::max(pos_max, h_cell_pos[c]);
+    return 0;
+}
+
+// ---- state: header | cell positions | K rows | V rows | last logits ----
+namespace {
+struct StateHdr {
+    char magic[8];
+    int32_t version, n_layer, kv_dim, n_vocab, n_cells, pos_max, logits_valid, pad;
+};
+}  // namespace
+
+size_t Ctx::state_size() const {
+    const HParams& hp = m->hp;
+    return sizeof(StateHdr) + (size_t)n_cells * sizeof(int) +
+           2 * (size_t)hp.n_layer * n_cells * kv_dim * sizeof(__half) + (size_t)hp.n_vocab * sizeof(float);
+}
+
+size_t Ctx::state_get(uint8_t* dst, size_t size) {
+    const size_t need = state_size();
+    if (size < need) throw Error("state_get: buffer too small");
+    const HParams& hp = m->hp;
+    StateHdr hd{};
+    std::memcpy(hd.magic, "MISTATE1", 8);
+    hd.version = 1;
+    hd.n_layer = hp.n_layer;
+    hd.kv_dim = kv_dim;
+    hd.n_vocab = hp.n_vocab;
+    hd.n_cells = n_cells;
+    hd.pos_max = pos_max;
+    hd.logits_valid = logits_valid ? 1 : 0;
+    uint8_t* o = dst;
+    std::memcpy(o, &hd, sizeof(hd));
+    o += sizeof(hd);
+    std::memcpy(o, h_cell_pos.data(), n_cells * sizeof(int));
+    o += n_cells * sizeof(int);
+    MI_HIP(hipSetDevice(device));
+    sync();
+    const size_t row = (size_t)n_cells * kv_dim * sizeof(__half);
+    for (__half* cache : {kcache, vcache})
+        for (int l = 0; l < hp.n_layer; ++l) {
+            if (row) MI_HIP(hipMemcpy(o, cache + (size_t)l * n_ctx * kv_dim, row, hipMemcpyDeviceToHost));
+            o += row;
+        }
+    if (logits_valid) MI_HIP(hipMemcpy(o, logits, (size_t)hp.n_vocab * sizeof(float), hipMemcpyDeviceToHost));
+    else std::memset(o, 0, (size_t)hp.n_vocab * sizeof(float));
+    return need;
+}
+
+size_t Ctx::state_set(const uint8_t* src, size_t size) {
+    const HParams& hp = m->hp;
+    StateHdr hd;
+    if (size < sizeof(hd)) throw Error("state_set: truncated state");
+    std::memcpy(&hd, src, sizeof(hd));
+    if (std::memcmp(hd.magic, "MISTATE1", 8) != 0 || hd.n_layer != hp.n_layer || hd.kv_dim != kv_dim ||
+        hd.n_vocab != hp.n_vocab)
+        throw Error("state_set: state does not match this model");
+    if (hd.n_cells < 0 || hd.n_cells > (int)n_ctx) throw Error("state_set: too many cells for this context");
+    const size_t need = sizeof(hd) + (size_t)hd.n_cells * sizeof(int) +
+                        2 * (size_t)hp.n_layer * hd.n_cells * kv_dim * sizeof(__half) + (size_t)hp.n_vocab * sizeof(float);
+    if (size < need) throw Error("state_set: truncated state");
+    const uint8_t* s = src + sizeof(hd);
+    n_cells = hd.n_cells;
+    pos_max = hd.pos_max;
+    std::memcpy(h_cell_pos.data(), s, n_cells * sizeof(int));
+    s += n_cells * sizeof(int);
+    MI_HIP(hipSetDevice(device));
+    sync();
+    if (n_cells) MI_HIP(hipMemcpy(cell_pos, h_cell_pos.data(), n_cells * sizeof(int), hipMemcpyHostToDevice));
+    const size_t row = (size_t)n_cells * kv_dim * sizeof(__half);
+    for (__half* cache : {kcache, vcache})
+        for (int l = 0; l < hp.n_layer; ++l) {
+            if (row) MI_HIP(hipMemcpy(cache + (size_t)l * n_ctx * kv_dim, s, row, hipMemcpyHostToDevice));
+            s += row;
+        }
+    logits_valid = hd.logits_valid != 0;
+    if (logits_valid) {
+        MI_HIP(hipMemcpy(logits, s, (size_t)hp.n_vocab * sizeof(float), hipMemcpyHostToDevice));
+        TopkParams tp{logits, hp.n_vocab, cand, topk_ids, topk_vals};
+        launch_topk(tp, stream);
+        MI_HIP(hipMemcpyAsync(h_topk_ids, topk_ids, TOPK_MAX * sizeof(int), hipMemcpyDeviceToHost, stream));
+        MI_HIP(hipMemcpyAsync(h_topk_vals, topk_vals, TOPK_MAX * sizeof(float), hipMemcpyDeviceToHost, stream));
+        sync();
+    }
+    return need;
+}
+
+int Ctx::prof_read(float* us, int n) {
+    if (!prof_pending || n < 1) return 0;
+    sync();
+    float ms = 0.0f;
+    MI_HIP(hipEventElapsedTime(&ms, prof_ev[0], prof_ev[1]));
+    us[0] = ms * 1000.0f;
+    prof_pending = false;
+    return 1;
+}
+
+}  // namespace mi

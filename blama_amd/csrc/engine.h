@@ -1,0 +1,165 @@
+// Engine internals: GGUF parsing, the device-resident model and the decode
+// context.  The public surface is the C ABI in include/mi_engine.h.
+#pragma once
+#include "common.h"
+#include "kernels.h"
+#include "mi_engine.h"
+
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+namespace mi {
+
+// ---------------------------------------------------------------- GGUF ----
+struct GgufValue {
+    int type = -1;                // gguf_type
+    long long i = 0;
+    double f = 0.0;
+    std::string s;
+    int arr_type = -1;
+    long long arr_n = 0;
+    std::vector<std::string> arr_s;
+    std::vector<double> arr_num;
+};
+
+struct GgufTensor {
+    std::string name;
+    int type = 0;
+    int n_dims = 0;
+    long long ne[4] = {1, 1, 1, 1};
+    unsigned long long offset = 0;   // within the data section
+    size_t nbytes = 0;
+};
+
+struct Gguf {
+    std::map<std::string, GgufValue> kv;
+    std::vector<GgufTensor> tensors;
+    size_t data_offset = 0;          // start of the data section in the file
+    // parse the header (metadata + tensor infos) from a memory image
+    void parse(const uint8_t* data, size_t size);
+    const GgufValue* get(const std::string& k) const {
+        auto it = kv.find(k);
+        return it == kv.end() ? nullptr : &it->second;
+    }
+    long long get_int(const std::string& k, long long def) const;
+    double get_float(const std::string& k, double def) const;
+    std::string get_str(const std::string& k, const std::string& def) const;
+    const GgufTensor* tensor(const std::string& name) const;
+};
+
+// --------------------------------------------------------------- model ----
+struct HParams {
+    int n_vocab = 0, n_embd = 0, n_layer = 0, n_head = 0, n_head_kv = 0, n_ff = 0, n_ctx_train = 0;
+    int n_rot = 0, head_dim = 0, n_expert = 0, n_expert_used = 0;
+    float eps = 1e-5f, rope_base = 10000.0f, freq_scale = 1.0f;
+};
+
+struct Layer {
+    float* attn_norm = nullptr;
+    float* ffn_norm = nullptr;
+    QMat wq{}, wk{}, wv{}, wo{};
+    QMat gate{}, up{}, down{};          // dense FFN, or the *_exps tensors for MoE
+    float* router = nullptr;            // ffn_gate_inp (F32) for MoE
+};
+
+struct Model {
+    HParams hp;
+    Gguf gguf;
+    std::vector<std::string> tokens;
+    std::vector<int> token_type;
+    int bos = -1, eos = -1, eot = -1;
+    bool add_bos = true;
+    int device = 0;
+    bool vocab_only = false;
+
+    uint8_t* arena = nullptr;
+    size_t arena_bytes = 0;
+    long long weight_bytes = 0;         // GGUF bytes streamed per token (all but tok_embd)
+    long long type_bytes[32] = {0};
+
+    QMat tok_embd{};
+    QMat output{};
+    float* output_norm = nullptr;
+    float* rope_freqs = nullptr;
+    std::vector<Layer> layers;
+
+    ~Model();
+    // data: the GGUF image (header at least; tensor data unless no_upload/vocab_only)
+    void load(const uint8_t* data, size_t size, const mi_model_params& p);
+    const QMat* find_qmat(const std::string& name) const;
+};
+
+// ------------------------------------------------------------- context ----
+struct Ctx {
+    Model* m = nullptr;
+    int device = 0;
+    uint32_t n_ctx = 0, n_batch = 0, n_ubatch = 0;
+    int kv_dim = 0;
+    hipStream_t stream = nullptr;
+
+    // device buffers
+    __half* kcache = nullptr;           // [n_layer][n_ctx][kv_dim]
+    __half* vcache = nullptr;
+    __half* kv_scratch = nullptr;       // compaction scratch (allocated lazily)
+    int* cell_pos = nullptr;            // [n_ctx]
+    int* tokpos = nullptr;              // {token, pos, cell, 0}
+    float *x = nullptr, *q = nullptr, *attn = nullptr, *h = nullptr, *h2 = nullptr, *logits = nullptr;
+    unsigned long long* cand = nullptr;
+    int* topk_ids = nullptr;
+    float* topk_vals = nullptr;
+    int* sel = nullptr;
+    float* selw = nullptr;
+    int* gather_ids = nullptr;
+    float* gather_out = nullptr;
+    int* cell_delta = nullptr;
+    int* move_src = nullptr;
+
+    // pinned host buffers
+    int* h_tokpos = nullptr;            // ring of kTokRing x 4 ints
+    int* h_topk_ids = nullptr;
+    float* h_topk_vals = nullptr;
+    float* h_logits = nullptr;
+    float* h_gather = nullptr;
+    long long tok_slot = 0;
+
+    // host mirror of the cache cells
+    std::vector<int> h_cell_pos;
+    int n_cells = 0;
+    int pos_max = -1;
+    bool logits_valid = false;
+
+    // decode graphs (with / without the output head).  With profiling on, the
+    // full step is split in three graphs around one layer's FFN gate/up GEMV so
+    // that plain HIP events on the stream bracket exactly that launch.
+    hipGraphExec_t g_full = nullptr, g_nolog = nullptr;
+    hipGraphExec_t g_seg[3] = {nullptr, nullptr, nullptr};
+    int prof_layer = -1;
+    hipEvent_t prof_ev[2] = {nullptr, nullptr};
+    bool prof_pending = false;
+    int seg_filter = -1;                // -1: enqueue everything; else only ops of this segment
+
+    static constexpr int kTokRing = 8192;
+
+    Ctx(Model* model, uint32_t n_ctx, uint32_t n_batch, uint32_t n_ubatch);
+    ~Ctx();
+    void enqueue_step(bool with_logits);
+    hipGraphExec_t build_graph(bool with_logits, int seg);
+    void invalidate_graphs();
+    int decode(const int32_t* tokens, int n);
+    void sync();
+    int topk(int k, int32_t* ids, float* vals);
+    int gather(const int32_t* ids, int n, float* out);
+    const float* logits_host();
+    void kv_clear();
+    int kv_seq_rm(int p0, int p1);
+    int kv_seq_shift(int p0, int p1, int delta, int div);
+    size_t state_size() const;
+    size_t state_get(uint8_t* dst, size_t size);
+    size_t state_set(const uint8_t* src, size_t size);
+    int prof_read(float* us, int n);
+    long long ffn_bytes() const;
+};
+
+}  // namespace mi

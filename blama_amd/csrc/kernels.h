@@ -1,0 +1,138 @@
+// Kernel parameter blocks and host-side launchers (implemented in kernels.hip).
+#pragma once
+#include "common.h"
+
+namespace mi {
+
+// ---- fused quantised GEMV ------------------------------------------------
+// One launch computes several "segments".  A segment is a list of units; a
+// unit is a PAIR of output rows computed by one wave (so RoPE pairs and the
+// SwiGLU gate/up pair are available together in the epilogue):
+//   PAIR_ADJ: rows (2u, 2u+1) of A          PAIR_AB: row u of A and row u of B
+enum Pair { PAIR_ADJ = 0, PAIR_AB = 1 };
+enum Epi {
+    EPI_STORE = 0,    // out[r] = y
+    EPI_ADD = 1,      // out[r] = y + resid[r]            (residual add, llm_build_llama)
+    EPI_ROPE_Q = 2,   // rope(pair) -> out (f32)
+    EPI_ROPE_K = 3,   // rope(pair) -> f16 K cache row of this token's cell
+    EPI_V = 4,        // -> f16 V cache row of this token's cell
+    EPI_SWIGLU = 5,   // out[u] = silu(yA) * yB            (LLM_FFN_SILU + LLM_FFN_PAR)
+    EPI_MOE_DOWN = 6, // out[u] = (yA*wA + yB*wB) + resid[u] (build_moe_ffn aggregation)
+};
+enum Pro { PRO_PLAIN = 0, PRO_RMSNORM = 1 };
+
+struct GemvSeg {
+    QMat A, B;
+    int pair, epi;
+    int units, unit0;     // unit count, first global unit index
+    int actA, actB;       // activation slot feeding A / B rows
+    int expA, expB;       // MoE: slot in sel[] choosing the expert (-1: dense)
+    float* out;
+    const float* resid;
+};
+
+constexpr int GEMV_MAX_SEG = 4;
+constexpr int GEMV_THREADS = 512;
+
+struct GemvParams {
+    GemvSeg seg[GEMV_MAX_SEG];
+    int nseg, total_units;
+    // prologue: activation slots are built in LDS by every workgroup
+    int pro;                  // PRO_RMSNORM applies to slot 0 only
+    int nslots;               // 1 or 2
+    const float* x[2];
+    const float* norm_w;
+    float eps;
+    int K;                    // activation length (multiple of 256)
+    int need_q8k, need_q80;   // which activation formats the segments consume
+    // RoPE / KV cache (decode)
+    const int* tokpos;        // {token, pos, cell}
+    int* cell_pos;            // cell -> position (written by the K epilogue)
+    float theta_scale, freq_scale;
+    int n_rot, head_dim;
+    const float* freq_factors;
+    __half* kcache;           // this layer's K cache [n_ctx][kv_dim]
+    __half* vcache;
+    int kv_dim;
+    // MoE routing results
+    const int* sel;
+    const float* selw;
+};
+
+enum GemvRole { ROLE_QKV = 0, ROLE_WO = 1, ROLE_FFN_UP = 2, ROLE_FFN_DOWN = 3, ROLE_OUTPUT = 4, ROLE_GENERIC = 5 };
+size_t gemv_smem_bytes(const GemvParams& p);
+void launch_gemv(const GemvParams& p, int role, int grid, hipStream_t s);
+void init_kernel_attributes();   // once per device, before any graph capture
+int gemv_default_grid(const GemvParams& p);
+
+// ---- token embedding: get_rows(tok_embd, token) with ggml dequantisation ----
+struct EmbedParams {
+    QMat E;                    // quant planes, or E.p[0] = raw f32/f16 rows
+    const int* tokpos;
+    float* out;
+    int n_embd;
+};
+void launch_embed(const EmbedParams& p, hipStream_t s);
+
+// ---- attention over the f16 cache (KQ -> soft_max -> KQV, ggml CPU semantics) ----
+struct AttnParams {
+    const float* q;            // [n_head*hd] (roped)
+    const __half* kcache;      // [n_ctx][kv_dim]
+    const __half* vcache;
+    const int* tokpos;
+    const int* cell_pos;
+    float* out;                // [n_head*hd]
+    int n_head, n_head_kv, head_dim, kv_dim, n_ctx;
+    float scale;
+};
+void launch_attn(const AttnParams& p, hipStream_t s);
+
+// ---- top-k over logits (sorted by logit desc, id asc), k <= 64 ----
+constexpr int TOPK_MAX = 64;
+constexpr int TOPK_GROUPS = 64;
+struct TopkParams {
+    const float* logits;
+    int n;
+    unsigned long long* cand;  // [TOPK_GROUPS*TOPK_MAX]
+    int* ids;                  // [TOPK_MAX]
+    float* vals;
+};
+void launch_topk(const TopkParams& p, hipStream_t s);
+
+// ---- gather logits at ids ----
+void launch_gather(const float* logits, const int* ids, int n, float* out, hipStream_t s);
+
+// ---- MoE router: softmax gating + top-k + weight normalisation ----
+struct RouterParams {
+    const float* x;            // residual stream (pre-norm)
+    const float* norm_w;
+    float eps;
+    const float* w;            // F32 [n_expert][n_embd]
+    int n_embd, n_expert, n_used;
+    int* sel;
+    float* selw;
+};
+void launch_router(const RouterParams& p, hipStream_t s);
+
+// ---- load-time repack of GGUF blocks into planes ----
+void launch_repack(const uint8_t* raw, int type, long long rows, int K, uint8_t* const planes[4],
+                   hipStream_t s);
+
+// ---- KV cache maintenance (context shift / self-extend K re-rotation) ----
+struct KvShiftParams {
+    __half* kcache;            // all layers [n_layer][n_ctx][kv_dim]
+    int n_layer, n_ctx, kv_dim, head_dim, n_rot;
+    const int* cell_delta;     // per cell position delta (0 = untouched)
+    int n_cells;
+    float theta_scale, freq_scale;
+    const float* freq_factors;
+};
+void launch_kv_shift(const KvShiftParams& p, hipStream_t s);
+void launch_kv_move(__half* cache, int n_layer, int n_ctx, int kv_dim, const int* src_cell,
+                    int n_dst, __half* scratch, hipStream_t s);
+
+// ---- single-op entry points used by the op-level parity tests ----
+void launch_dequant_rows(const QMat& m, int row0, int nrows, float* out, hipStream_t s);
+void launch_quantize_q8k(const float* x, int K, int8_t* q, float* d, int* bsums, hipStream_t s);
+
+}  // namespace mi

@@ -1,0 +1,325 @@
+"""ctypes binding of the C ABI in include/mi_engine.h.
+
+This is the Python-side view of the drop-in boundary (the same entry points a
+cgo/JNI/ctypes binding in a host application would declare).  It loads the
+in-tree ``blama_amd/libmi_engine.so`` and fails loudly if it is missing: there
+is no CPU fallback anywhere in the product path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmi_engine.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "mi_engine.h")
+
+_lib = None
+
+
+class EngineError(RuntimeError):
+    pass
+
+
+class ModelParams(C.Structure):
+    _fields_ = [("device_ordinal", C.c_int32), ("cpu_only", C.c_int32),
+                ("vocab_only", C.c_int32), ("no_upload", C.c_int32)]
+
+
+_P = C.c_void_p
+_SIGS = {
+    "mi_last_error": (C.c_char_p, []),
+    "mi_model_load": (_P, [C.c_char_p, C.POINTER(ModelParams)]),
+    "mi_model_load_from_memory": (_P, [_P, C.c_size_t, C.POINTER(ModelParams)]),
+    "mi_model_free": (None, [_P]),
+    "mi_model_n_vocab": (C.c_int32, [_P]),
+    "mi_model_n_ctx_train": (C.c_int32, [_P]),
+    "mi_model_n_embd": (C.c_int32, [_P]),
+    "mi_model_n_layer": (C.c_int32, [_P]),
+    "mi_model_n_head": (C.c_int32, [_P]),
+    "mi_model_n_head_kv": (C.c_int32, [_P]),
+    "mi_model_n_ff": (C.c_int32, [_P]),
+    "mi_model_n_expert": (C.c_int32, [_P]),
+    "mi_model_token_bos": (C.c_int32, [_P]),
+    "mi_model_token_eos": (C.c_int32, [_P]),
+    "mi_model_add_bos": (C.c_int32, [_P]),
+    "mi_model_token_is_eog": (C.c_int32, [_P, C.c_int32]),
+    "mi_model_token_text": (C.c_int32, [_P, C.c_int32, C.c_char_p, C.c_int32]),
+    "mi_model_meta_str": (C.c_int32, [_P, C.c_char_p, C.c_char_p, C.c_int32]),
+    "mi_model_weight_bytes": (C.c_int64, [_P]),
+    "mi_model_arena": (C.c_int32, [_P, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]),
+    "mi_model_type_histogram": (C.c_int32, [_P, C.POINTER(C.c_int64), C.c_int32]),
+    "mi_ctx_create": (_P, [_P, C.c_uint32, C.c_uint32, C.c_uint32]),
+    "mi_ctx_free": (None, [_P]),
+    "mi_n_ctx": (C.c_uint32, [_P]),
+    "mi_n_batch": (C.c_uint32, [_P]),
+    "mi_decode": (C.c_int32, [_P, C.POINTER(C.c_int32), C.c_int32, C.c_int32]),
+    "mi_topk": (C.c_int32, [_P, C.c_int32, C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_float)]),
+    "mi_gather": (C.c_int32, [_P, C.c_int32, C.POINTER(C.c_int32), C.c_int32, C.POINTER(C.c_float)]),
+    "mi_logits": (C.POINTER(C.c_float), [_P, C.c_int32]),
+    "mi_synchronize": (None, [_P]),
+    "mi_kv_clear": (None, [_P]),
+    "mi_kv_seq_rm": (C.c_int32, [_P, C.c_int32, C.c_int32]),
+    "mi_kv_seq_add": (C.c_int32, [_P, C.c_int32, C.c_int32, C.c_int32]),
+    "mi_kv_seq_div": (C.c_int32, [_P, C.c_int32, C.c_int32, C.c_int32]),
+    "mi_kv_pos_max": (C.c_int32, [_P]),
+    "mi_kv_n_cells": (C.c_int32, [_P]),
+    "mi_state_size": (C.c_size_t, [_P]),
+    "mi_state_get": (C.c_size_t, [_P, _P, C.c_size_t]),
+    "mi_state_set": (C.c_size_t, [_P, _P, C.c_size_t]),
+    "mi_prof_enable": (C.c_int32, [_P, C.c_int32]),
+    "mi_prof_read": (C.c_int32, [_P, C.POINTER(C.c_float), C.c_int32]),
+    "mi_prof_ffn_bytes": (C.c_int64, [_P]),
+    "mi_op_gemv": (C.c_int32, [C.c_int32, C.c_int32, _P, C.c_int32, C.c_int32, _P, _P]),
+    "mi_op_dequant": (C.c_int32, [C.c_int32, C.c_int32, _P, C.c_int32, C.c_int32, _P]),
+    "mi_op_quantize_q8_K": (C.c_int32, [C.c_int32, _P, C.c_int32, _P, _P, _P]),
+    "mi_op_topk": (C.c_int32, [C.c_int32, _P, C.c_int32, C.c_int32, _P, _P]),
+    "mi_op_gemv_bench": (C.c_int32, [C.c_int32, C.c_int32, _P, C.c_int32, C.c_int32, C.c_int32,
+                                     C.POINTER(C.c_float)]),
+}
+
+
+def header_symbols(path: str = HEADER_PATH) -> list[str]:
+    """Names of the functions include/mi_engine.h declares."""
+    txt = open(path).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(mi_[A-Za-z0-9_]+)\s*\(", txt)))
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise EngineError(f"{LIB_PATH} is missing: run __graft_entry__.build() (no CPU fallback exists)")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def last_error() -> str:
+    return (lib().mi_last_error() or b"").decode()
+
+
+def _check(rc, what):
+    if rc is None or (isinstance(rc, int) and rc < 0):
+        raise EngineError(f"{what}: {last_error()}")
+    return rc
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+class Model:
+    """Owns an mi_model (llama_model_load_from_file + llama_model_free)."""
+
+    def __init__(self, source, device: int = 0, vocab_only: bool = False, no_upload: bool = False):
+        L = lib()
+        p = ModelParams(device, 0, int(vocab_only), int(no_upload))
+        if isinstance(source, (str, os.PathLike)):
+            h = L.mi_model_load(os.fspath(source).encode(), C.byref(p))
+        else:
+            if isinstance(source, (bytes, bytearray, memoryview)):
+                buf = np.frombuffer(source, np.uint8)
+            else:
+                buf = np.ascontiguousarray(source, dtype=np.uint8)
+            h = L.mi_model_load_from_memory(_ptr(buf), buf.size, C.byref(p))
+        if not h:
+            raise EngineError(f"model load failed: {last_error()}")
+        self.h = h
+        self.n_vocab = L.mi_model_n_vocab(h)
+        self.n_embd = L.mi_model_n_embd(h)
+        self.n_layer = L.mi_model_n_layer(h)
+        self.n_ctx_train = L.mi_model_n_ctx_train(h)
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().mi_model_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def weight_bytes(self) -> int:
+        return lib().mi_model_weight_bytes(self.h)
+
+    def arena(self):
+        p = C.c_void_p()
+        n = C.c_size_t()
+        _check(lib().mi_model_arena(self.h, C.byref(p), C.byref(n)), "arena")
+        return p.value, n.value
+
+    def type_histogram(self) -> dict:
+        a = (C.c_int64 * 32)()
+        lib().mi_model_type_histogram(self.h, a, 32)
+        return {i: int(a[i]) for i in range(32) if a[i]}
+
+    def token_text(self, tok: int) -> str:
+        n = lib().mi_model_token_text(self.h, tok, None, 0)
+        _check(n, "token_text")
+        b = C.create_string_buffer(n + 1)
+        lib().mi_model_token_text(self.h, tok, b, n + 1)
+        return b.raw[:n].decode("utf-8", errors="replace")
+
+    @property
+    def bos(self):
+        return lib().mi_model_token_bos(self.h)
+
+    @property
+    def eos(self):
+        return lib().mi_model_token_eos(self.h)
+
+    def is_eog(self, tok: int) -> bool:
+        return lib().mi_model_token_is_eog(self.h, tok) == 1
+
+
+class Context:
+    """Owns an mi_ctx (llama_init_from_model + llama_free)."""
+
+    def __init__(self, model: Model, n_ctx: int = 0, n_batch: int = 2048, n_ubatch: int = 512):
+        h = lib().mi_ctx_create(model.h, n_ctx, n_batch, n_ubatch)
+        if not h:
+            raise EngineError(f"context creation failed: {last_error()}")
+        self.h = h
+        self.model = model
+        self.n_ctx = lib().mi_n_ctx(h)
+        self.n_batch = lib().mi_n_batch(h)
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().mi_ctx_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def decode(self, tokens) -> int:
+        t = np.ascontiguousarray(tokens, dtype=np.int32)
+        rc = lib().mi_decode(self.h, t.ctypes.data_as(C.POINTER(C.c_int32)), t.size, 0)
+        _check(rc, "decode")
+        return rc
+
+    def topk(self, k: int = 10):
+        ids = np.empty(k, np.int32)
+        vals = np.empty(k, np.float32)
+        _check(lib().mi_topk(self.h, -1, k, ids.ctypes.data_as(C.POINTER(C.c_int32)),
+                             vals.ctypes.data_as(C.POINTER(C.c_float))), "topk")
+        return ids, vals
+
+    def gather(self, ids):
+        ids = np.ascontiguousarray(ids, dtype=np.int32)
+        out = np.empty(ids.size, np.float32)
+        _check(lib().mi_gather(self.h, -1, ids.ctypes.data_as(C.POINTER(C.c_int32)), ids.size,
+                               out.ctypes.data_as(C.POINTER(C.c_float))), "gather")
+        return out
+
+    def logits(self) -> np.ndarray:
+        p = lib().mi_logits(self.h, -1)
+        if not p:
+            raise EngineError(f"logits: {last_error()}")
+        return np.ctypeslib.as_array(p, shape=(self.model.n_vocab,)).copy()
+
+    def synchronize(self):
+        lib().mi_synchronize(self.h)
+
+    def kv_clear(self):
+        lib().mi_kv_clear(self.h)
+
+    def kv_seq_rm(self, p0, p1):
+        return _check(lib().mi_kv_seq_rm(self.h, p0, p1), "kv_seq_rm")
+
+    def kv_seq_add(self, p0, p1, delta):
+        return _check(lib().mi_kv_seq_add(self.h, p0, p1, delta), "kv_seq_add")
+
+    def kv_seq_div(self, p0, p1, d):
+        return _check(lib().mi_kv_seq_div(self.h, p0, p1, d), "kv_seq_div")
+
+    @property
+    def pos_max(self):
+        return lib().mi_kv_pos_max(self.h)
+
+    @property
+    def n_cells(self):
+        return lib().mi_kv_n_cells(self.h)
+
+    def state_get(self) -> bytes:
+        n = lib().mi_state_size(self.h)
+        buf = np.empty(n, np.uint8)
+        got = lib().mi_state_get(self.h, _ptr(buf), n)
+        if got != n:
+            raise EngineError(f"state_get: {last_error()}")
+        return buf.tobytes()
+
+    def state_set(self, data: bytes):
+        buf = np.frombuffer(data, np.uint8).copy()
+        got = lib().mi_state_set(self.h, _ptr(buf), buf.size)
+        if got == 0:
+            raise EngineError(f"state_set: {last_error()}")
+
+    def prof_enable(self, stride: int):
+        lib().mi_prof_enable(self.h, stride)
+
+    def prof_read(self, n: int = 64) -> np.ndarray:
+        a = np.zeros(n, np.float32)
+        k = _check(lib().mi_prof_read(self.h, a.ctypes.data_as(C.POINTER(C.c_float)), n), "prof_read")
+        return a[:k]
+
+    @property
+    def ffn_bytes(self) -> int:
+        return lib().mi_prof_ffn_bytes(self.h)
+
+
+# ---- op-level entry points (parity tests / micro-benchmarks) ----
+
+def op_gemv(type_: int, raw: np.ndarray, rows: int, K: int, x: np.ndarray, device: int = 0) -> np.ndarray:
+    raw = np.ascontiguousarray(raw, np.uint8)
+    x = np.ascontiguousarray(x, np.float32)
+    y = np.empty(rows, np.float32)
+    _check(lib().mi_op_gemv(device, type_, _ptr(raw), rows, K, _ptr(x), _ptr(y)), "op_gemv")
+    return y
+
+
+def op_gemv_bench(type_: int, raw: np.ndarray, rows: int, K: int, iters: int = 100, device: int = 0) -> float:
+    raw = np.ascontiguousarray(raw, np.uint8)
+    us = C.c_float()
+    _check(lib().mi_op_gemv_bench(device, type_, _ptr(raw), rows, K, iters, C.byref(us)), "op_gemv_bench")
+    return us.value
+
+
+def op_dequant(type_: int, raw: np.ndarray, rows: int, K: int, device: int = 0) -> np.ndarray:
+    raw = np.ascontiguousarray(raw, np.uint8)
+    out = np.empty(rows * K, np.float32)
+    _check(lib().mi_op_dequant(device, type_, _ptr(raw), rows, K, _ptr(out)), "op_dequant")
+    return out
+
+
+def op_quantize_q8_K(x: np.ndarray, device: int = 0):
+    x = np.ascontiguousarray(x, np.float32)
+    K = x.size
+    qs = np.empty(K, np.int8)
+    d = np.empty(K // 256, np.float32)
+    bs = np.empty((K // 256) * 16, np.int32)
+    _check(lib().mi_op_quantize_q8_K(device, _ptr(x), K, _ptr(qs), _ptr(d), _ptr(bs)), "op_quantize_q8_K")
+    return qs, d, bs
+
+
+def op_topk(logits: np.ndarray, k: int, device: int = 0):
+    logits = np.ascontiguousarray(logits, np.float32)
+    ids = np.empty(k, np.int32)
+    vals = np.empty(k, np.float32)
+    _check(lib().mi_op_topk(device, _ptr(logits), logits.size, k, _ptr(ids), _ptr(vals)), "op_topk")
+    return ids, vals

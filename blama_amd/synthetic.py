@@ -1,0 +1,251 @@
+"""Synthetic LLaMA-family GGUF images for the BASELINE.json configs.
+
+No checkpoint can be downloaded here, so tests and the
+bench use GGUF images with the *exact* tensor names, shapes and per-tensor
+quant types of the named models, filled with seeded random -- but valid and
+realistically scaled -- quant blocks.
+
+Per-tensor type rules follow llama.cpp b5187 ``llama_tensor_get_type``
+(src/llama-quant.cpp) as summarised in SURVEY.md §8 "Q4_K_M tensor mix":
+Q4_K_M -> output Q6_K; attn_v / ffn_down Q6_K where use_more_bits(i, n);
+everything else Q4_K; 8-expert models bump attn_k/attn_v to Q8_0 and
+attn_output to Q5_K (Q4_K_M) ; norms F32.
+"""
+from __future__ import annotations
+
+import hashlib
+from dataclasses import dataclass, replace
+
+import numpy as np
+
+from . import gguf
+
+F32, F16, Q8_0, Q4_K, Q5_K, Q6_K = 0, 1, 8, 12, 13, 14
+
+
+@dataclass(frozen=True)
+class LlamaConfig:
+    name: str
+    n_vocab: int
+    n_embd: int
+    n_layer: int
+    n_head: int
+    n_head_kv: int
+    n_ff: int
+    n_ctx_train: int
+    rope_base: float
+    eps: float
+    ftype: str            # "Q4_K_M", "Q5_K_M", "Q6_K", "Q8_0", "Q4_K"...
+    n_expert: int = 0
+    n_expert_used: int = 0
+
+    @property
+    def head_dim(self):
+        return self.n_embd // self.n_head
+
+
+CONFIGS = {
+    # BASELINE.json configs[0..4]
+    "tinyllama-1.1b-q8_0": LlamaConfig("TinyLlama-1.1B", 32000, 2048, 22, 32, 4, 5632, 2048,
+                                        10000.0, 1e-5, "Q8_0"),
+    "llama2-7b-q4_k_m": LlamaConfig("Llama-2-7B", 32000, 4096, 32, 32, 32, 11008, 4096,
+                                     10000.0, 1e-5, "Q4_K_M"),
+    "llama3-8b-q6_k": LlamaConfig("Llama-3-8B", 128256, 4096, 32, 32, 8, 14336, 8192,
+                                   500000.0, 1e-5, "Q6_K"),
+    "mixtral-8x7b-q5_k_m": LlamaConfig("Mixtral-8x7B", 32000, 4096, 32, 32, 8, 14336, 32768,
+                                        1e6, 1e-5, "Q5_K_M", n_expert=8, n_expert_used=2),
+    # small shapes for parity tests (same code paths, seconds on the CPU oracle)
+    "tiny-q4_k_m": LlamaConfig("tiny", 512, 256, 4, 4, 2, 512, 256, 10000.0, 1e-5, "Q4_K_M"),
+    "tiny-q5_k_m": LlamaConfig("tiny", 512, 256, 2, 4, 2, 512, 256, 10000.0, 1e-5, "Q5_K_M"),
+    "tiny-q6_k": LlamaConfig("tiny", 640, 256, 2, 4, 1, 768, 256, 500000.0, 1e-5, "Q6_K"),
+    "tiny-q8_0": LlamaConfig("tiny", 384, 256, 2, 8, 4, 768, 256, 10000.0, 1e-6, "Q8_0"),
+    "tiny1-q4_k_m": LlamaConfig("tiny1", 512, 256, 1, 4, 2, 512, 256, 10000.0, 1e-5, "Q4_K_M"),
+    "tiny-moe-q5_k_m": LlamaConfig("tiny-moe", 512, 256, 2, 4, 2, 512, 256, 1e6, 1e-5,
+                                    "Q5_K_M", n_expert=4, n_expert_used=2),
+}
+
+
+def use_more_bits(i: int, n: int) -> bool:
+    # llama-quant.cpp use_more_bits
+    return i < n // 8 or i >= 7 * n // 8 or (i - n // 8) % 3 == 2
+
+
+def tensor_types(cfg: LlamaConfig) -> dict:
+    """name -> ggml type for every weight (the Q*_K_M mixes of llama_tensor_get_type)."""
+    base = {"Q4_K_M": Q4_K, "Q5_K_M": Q5_K, "Q6_K": Q6_K, "Q8_0": Q8_0, "Q4_K": Q4_K,
+            "Q5_K": Q5_K}[cfg.ftype]
+    mixed = cfg.ftype in ("Q4_K_M", "Q5_K_M")
+    t = {"token_embd.weight": base, "output_norm.weight": F32,
+         "output.weight": Q8_0 if base == Q8_0 else Q6_K}
+    n = cfg.n_layer
+    for i in range(n):
+        p = f"blk.{i}."
+        t[p + "attn_norm.weight"] = F32
+        t[p + "ffn_norm.weight"] = F32
+        t[p + "attn_q.weight"] = base
+        t[p + "attn_k.weight"] = base
+        t[p + "attn_v.weight"] = base
+        t[p + "attn_output.weight"] = base
+        if mixed and use_more_bits(i, n):
+            t[p + "attn_v.weight"] = Q6_K
+        if cfg.n_expert == 8 and base != Q8_0:
+            t[p + "attn_k.weight"] = Q8_0
+            t[p + "attn_v.weight"] = Q8_0
+            if cfg.ftype == "Q4_K_M":
+                t[p + "attn_output.weight"] = Q5_K
+        down = Q6_K if (mixed and use_more_bits(i, n)) else base
+        if cfg.n_expert:
+            t[p + "ffn_gate_inp.weight"] = F32
+            t[p + "ffn_gate_exps.weight"] = base
+            t[p + "ffn_up_exps.weight"] = base
+            t[p + "ffn_down_exps.weight"] = down
+        else:
+            t[p + "ffn_gate.weight"] = base
+            t[p + "ffn_up.weight"] = base
+            t[p + "ffn_down.weight"] = down
+    return t
+
+
+def tensor_shapes(cfg: LlamaConfig) -> dict:
+    """name -> ggml ne shape (ne0 = input dim K)."""
+    d, kv = cfg.n_embd, cfg.n_head_kv * cfg.head_dim
+    s = {"token_embd.weight": (d, cfg.n_vocab), "output_norm.weight": (d,),
+         "output.weight": (d, cfg.n_vocab)}
+    for i in range(cfg.n_layer):
+        p = f"blk.{i}."
+        s[p + "attn_norm.weight"] = (d,)
+        s[p + "ffn_norm.weight"] = (d,)
+        s[p + "attn_q.weight"] = (d, d)
+        s[p + "attn_k.weight"] = (d, kv)
+        s[p + "attn_v.weight"] = (d, kv)
+        s[p + "attn_output.weight"] = (d, d)
+        if cfg.n_expert:
+            s[p + "ffn_gate_inp.weight"] = (d, cfg.n_expert)
+            s[p + "ffn_gate_exps.weight"] = (d, cfg.n_ff, cfg.n_expert)
+            s[p + "ffn_up_exps.weight"] = (d, cfg.n_ff, cfg.n_expert)
+            s[p + "ffn_down_exps.weight"] = (cfg.n_ff, d, cfg.n_expert)
+        else:
+            s[p + "ffn_gate.weight"] = (d, cfg.n_ff)
+            s[p + "ffn_up.weight"] = (d, cfg.n_ff)
+            s[p + "ffn_down.weight"] = (cfg.n_ff, d)
+    return s
+
+
+def _rng(seed: int, name: str):
+    h = hashlib.sha256(f"{seed}:{name}".encode()).digest()
+    return np.random.default_rng(int.from_bytes(h[:8], "little"))
+
+
+def _pack_scales_k4(sc: np.ndarray, m: np.ndarray) -> np.ndarray:
+    """Inverse of get_scale_min_k4 (the packing of quantize_row_q4_K_ref)."""
+    nb = sc.shape[0]
+    s = np.zeros((nb, 12), np.uint8)
+    for j in range(4):
+        s[:, j] = sc[:, j]
+        s[:, j + 4] = m[:, j]
+    for j in range(4, 8):
+        s[:, j + 4] = (sc[:, j] & 0xF) | ((m[:, j] & 0xF) << 4)
+        s[:, j - 4] |= (sc[:, j] >> 4) << 6
+        s[:, j] |= (m[:, j] >> 4) << 6
+    return s
+
+
+def fill_quant(view: np.ndarray, t: int, rng, std: float = 0.03):
+    """Fill a tensor's bytes with valid random blocks whose dequantised values
+    are roughly zero-mean with standard deviation ``std``."""
+    be, bb = gguf.GGML_BLOCK[t]
+    if t == F32:
+        v = view.view(np.float32)
+        v[:] = rng.standard_normal(v.size, dtype=np.float32) * np.float32(std)
+        return
+    if t == F16:
+        v = view.view(np.float16)
+        v[:] = (rng.standard_normal(v.size, dtype=np.float32) * np.float32(std)).astype(np.float16)
+        return
+    nb = view.size // bb
+    bl = view.reshape(nb, bb)
+    CH = 1 << 16   # blocks per chunk (bounded temporaries)
+    for a in range(0, nb, CH):
+        b = bl[a:a + CH]
+        n = b.shape[0]
+        b[:] = rng.integers(0, 256, size=b.shape, dtype=np.uint8)
+        if t in (Q4_K, Q5_K):
+            qmax = 15 if t == Q4_K else 31
+            sc = rng.integers(24, 64, size=(n, 8), dtype=np.int32)
+            d = (std / (40.0 * (qmax + 1) / np.sqrt(12.0))) * rng.uniform(0.8, 1.2, n)
+            ratio = 16.0 if t == Q4_K else 32.0      # dmin = d*ratio
+            dmin = d * ratio
+            m = np.clip(np.rint(sc * (qmax / 2.0) / ratio), 0, 63).astype(np.int32)
+            b[:, 0:2] = d.astype(np.float16).view(np.uint8).reshape(n, 2)
+            b[:, 2:4] = dmin.astype(np.float16).view(np.uint8).reshape(n, 2)
+            b[:, 4:16] = _pack_scales_k4(sc.astype(np.uint8), m.astype(np.uint8))
+        elif t == Q6_K:
+            sc = rng.integers(16, 48, size=(n, 16), dtype=np.int32)
+            sgn = rng.integers(0, 2, size=(n, 16), dtype=np.int32) * 2 - 1
+            b[:, 192:208] = (sc * sgn).astype(np.int8).view(np.uint8)
+            d = (std / (32.0 * 64 / np.sqrt(12.0))) * rng.uniform(0.8, 1.2, n)
+            b[:, 208:210] = d.astype(np.float16).view(np.uint8).reshape(n, 2)
+        elif t == Q8_0:
+            d = (std / (256 / np.sqrt(12.0))) * rng.uniform(0.8, 1.2, n)
+            b[:, 0:2] = d.astype(np.float16).view(np.uint8).reshape(n, 2)
+        else:
+            raise NotImplementedError(t)
+
+
+def vocab_tokens(n_vocab: int):
+    toks = ["<unk>", "<s>", "</s>"] + ["<0x%02X>" % i for i in range(256)]
+    toks += ["▁t%d" % i for i in range(n_vocab - len(toks))]
+    return toks[:n_vocab]
+
+
+def build_gguf(cfg: LlamaConfig, seed: int = 0) -> np.ndarray:
+    """The whole synthetic GGUF file as one uint8 array."""
+    w = gguf.GGUFWriter()
+    arch = "llama"
+    w.add_str("general.architecture", arch)
+    w.add_str("general.name", f"synthetic {cfg.name} {cfg.ftype}")
+    w.add_u32("general.file_type", {"Q8_0": 7, "Q4_K_M": 15, "Q5_K_M": 17, "Q6_K": 18,
+                                    "Q4_K": 15, "Q5_K": 17}[cfg.ftype])
+    w.add_u32(f"{arch}.context_length", cfg.n_ctx_train)
+    w.add_u32(f"{arch}.embedding_length", cfg.n_embd)
+    w.add_u32(f"{arch}.block_count", cfg.n_layer)
+    w.add_u32(f"{arch}.feed_forward_length", cfg.n_ff)
+    w.add_u32(f"{arch}.attention.head_count", cfg.n_head)
+    w.add_u32(f"{arch}.attention.head_count_kv", cfg.n_head_kv)
+    w.add_f32(f"{arch}.attention.layer_norm_rms_epsilon", cfg.eps)
+    w.add_f32(f"{arch}.rope.freq_base", cfg.rope_base)
+    w.add_u32(f"{arch}.rope.dimension_count", cfg.head_dim)
+    w.add_u32(f"{arch}.vocab_size", cfg.n_vocab)
+    if cfg.n_expert:
+        w.add_u32(f"{arch}.expert_count", cfg.n_expert)
+        w.add_u32(f"{arch}.expert_used_count", cfg.n_expert_used)
+    w.add_str("tokenizer.ggml.model", "llama")
+    toks = vocab_tokens(cfg.n_vocab)
+    w.add_array("tokenizer.ggml.tokens", gguf.T_STRING, toks)
+    w.add_array("tokenizer.ggml.scores", gguf.T_FLOAT32, [-float(i) for i in range(len(toks))])
+    ttype = [2, 3, 3] + [6] * 256 + [1] * (len(toks) - 259)
+    w.add_array("tokenizer.ggml.token_type", gguf.T_INT32, ttype[:len(toks)])
+    w.add_u32("tokenizer.ggml.bos_token_id", 1)
+    w.add_u32("tokenizer.ggml.eos_token_id", 2)
+    w.add_u32("tokenizer.ggml.unknown_token_id", 0)
+    w.add_bool("tokenizer.ggml.add_bos_token", True)
+    types = tensor_types(cfg)
+    shapes = tensor_shapes(cfg)
+    for name in types:
+        w.add_tensor(name, types[name], shapes[name])
+
+    def fill(name, t, shape, view):
+        rng = _rng(seed, name)
+        if name.endswith("norm.weight"):
+            v = view.view(np.float32)
+            v[:] = rng.uniform(0.8, 1.2, v.size).astype(np.float32)
+        elif name.endswith("ffn_gate_inp.weight"):
+            fill_quant(view, t, rng, std=0.05)
+        else:
+            fill_quant(view, t, rng)
+
+    return w.to_bytes(fill=fill)
+
+
+def small_config(name: str, **kw) -> LlamaConfig:
+    return replace(CONFIGS[name], **kw)

@@ -1,0 +1,138 @@
+/* mi_engine.h -- C ABI of the MI355X-native quantized-inference engine.
+ *
+ * This is the drop-in boundary for Blama's hot path.  Blama's inference layer
+ * (bl::llama, /root/reference/inference/code/llama) binds the llama.cpp C API
+ * (llama.h, llama.cpp tag b5187); the entry points below replace the hot-path
+ * subset of it.  Each declaration cites the reference call
+ * site whose llama.h function it replaces.
+ *
+ * Conventions: plain C types only; functions returning pointers return NULL on
+ * error and functions returning int32_t return a negative value on error, with
+ * the message available from mi_last_error() (thread-local).  mi_decode keeps
+ * llama_decode's convention: 0 = ok, 1 = no KV space, < 0 = error
+ * (checked "!= 0" at Session.cpp:388).  One context is used by one thread at a
+ * time (Server.cpp:36); a model may back several contexts.
+ */
+#ifndef MI_ENGINE_H
+#define MI_ENGINE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct mi_model mi_model;
+typedef struct mi_ctx mi_ctx;
+
+typedef struct mi_model_params {
+    int32_t device_ordinal; /* HIP device; Model.cpp:18-21 binds the first GPU */
+    int32_t cpu_only;       /* Model::Params::gpu=false -- not served here: returns NULL */
+    int32_t vocab_only;     /* Model::Params::vocabOnly: parse metadata/vocab, no weights */
+    int32_t no_upload;      /* allocate the weight arena but leave it unfilled (replica
+                               that receives the weights by RCCL broadcast) */
+} mi_model_params;
+
+/* Last error message of this thread ("" if none). */
+const char* mi_last_error(void);
+
+/* ---- model: replaces llama_model_load_from_file / llama_model_free
+ *      (Model.cpp:52, Model.hpp:55) ---- */
+mi_model* mi_model_load(const char* gguf_path, const mi_model_params* params);
+/* Same, from a GGUF image in host memory (with no_upload/vocab_only only the
+ * header -- metadata and tensor infos -- needs to be present). */
+mi_model* mi_model_load_from_memory(const void* data, size_t size, const mi_model_params* params);
+void mi_model_free(mi_model* model);
+
+/* hparams / vocab queries: llama_vocab_n_tokens (Session.cpp:27),
+ * llama_model_n_ctx_train (Model.cpp:41), llama_vocab_bos/eos (Instance.cpp:91-92),
+ * llama_vocab_get_add_bos (Model.cpp:45), llama_model_meta_val_str (Model.cpp:57) */
+int32_t mi_model_n_vocab(const mi_model* model);
+int32_t mi_model_n_ctx_train(const mi_model* model);
+int32_t mi_model_n_embd(const mi_model* model);
+int32_t mi_model_n_layer(const mi_model* model);
+int32_t mi_model_n_head(const mi_model* model);
+int32_t mi_model_n_head_kv(const mi_model* model);
+int32_t mi_model_n_ff(const mi_model* model);
+int32_t mi_model_n_expert(const mi_model* model);
+int32_t mi_model_token_bos(const mi_model* model);
+int32_t mi_model_token_eos(const mi_model* model);
+int32_t mi_model_add_bos(const mi_model* model);
+int32_t mi_model_token_is_eog(const mi_model* model, int32_t token);
+/* Text of a vocabulary entry (raw GGUF piece); returns its length or < 0. */
+int32_t mi_model_token_text(const mi_model* model, int32_t token, char* buf, int32_t size);
+int32_t mi_model_meta_str(const mi_model* model, const char* key, char* buf, int32_t size);
+/* Bytes of quantised weights a decode step streams (all tensors but tok_embd). */
+int64_t mi_model_weight_bytes(const mi_model* model);
+/* The device weight arena (one allocation) -- for the replica broadcast. */
+int32_t mi_model_arena(const mi_model* model, void** dev_ptr, size_t* bytes);
+/* Per ggml type id (0..31): bytes of weights of that type (the GGUF's byte histogram). */
+int32_t mi_model_type_histogram(const mi_model* model, int64_t* bytes_by_type, int32_t n);
+
+/* ---- context: replaces llama_init_from_model / llama_free (Instance.cpp:36);
+ *      n_ctx 0 = training context (Instance.hpp:22) ---- */
+mi_ctx* mi_ctx_create(mi_model* model, uint32_t n_ctx, uint32_t n_batch, uint32_t n_ubatch);
+void mi_ctx_free(mi_ctx* ctx);
+uint32_t mi_n_ctx(const mi_ctx* ctx);     /* llama_n_ctx   (Session.cpp:57,72,162,322) */
+uint32_t mi_n_batch(const mi_ctx* ctx);   /* llama_n_batch (Session.cpp:381) */
+
+/* llama_decode(llama_batch_get_one(tokens, n)) (Session.cpp:388, Instance.cpp:115):
+ * tokens take positions pos_max+1...; asynchronous on the context's stream.
+ * out_mode 0 = logits of the last token only (llama_batch_get_one). */
+#define MI_OUT_LAST 0
+int32_t mi_decode(mi_ctx* ctx, const int32_t* tokens, int32_t n, int32_t out_mode);
+
+/* Top-k of the last output row, sorted by logit descending then id ascending;
+ * k <= 64.  Replaces fillLogits + std::sort + first 10 (Session.cpp:246-261) and
+ * feeds the sampler chain's top_k(40) stage (Sampler.cpp:15-97).  Synchronises. */
+int32_t mi_topk(mi_ctx* ctx, int32_t row, int32_t k, int32_t* ids, float* logits);
+/* Logits of the last output row at the given ids (Session.cpp:263-282).  Synchronises. */
+int32_t mi_gather(mi_ctx* ctx, int32_t row, const int32_t* ids, int32_t n, float* out);
+/* Full-vocabulary escape hatch: llama_get_logits_ith(ctx, -1) (Session.cpp:24,
+ * Sampler.cpp:111).  Context-owned; valid until the next decode.  Synchronises. */
+const float* mi_logits(mi_ctx* ctx, int32_t row);
+void mi_synchronize(mi_ctx* ctx);         /* llama_synchronize (Session.cpp:54) */
+
+/* KV cache (single sequence): llama_kv_self_clear (Session.cpp:53),
+ * llama_kv_self_seq_rm / seq_add / seq_div (Session.cpp:341-342, 359-361).
+ * p1 < 0 means "to the end". */
+void mi_kv_clear(mi_ctx* ctx);
+int32_t mi_kv_seq_rm(mi_ctx* ctx, int32_t p0, int32_t p1);
+int32_t mi_kv_seq_add(mi_ctx* ctx, int32_t p0, int32_t p1, int32_t delta);
+int32_t mi_kv_seq_div(mi_ctx* ctx, int32_t p0, int32_t p1, int32_t d);
+int32_t mi_kv_pos_max(const mi_ctx* ctx); /* -1 when empty */
+int32_t mi_kv_n_cells(const mi_ctx* ctx);
+
+/* State save/restore: llama_state_get_size / get_data / set_data (Session.cpp:291-304). */
+size_t mi_state_size(mi_ctx* ctx);
+size_t mi_state_get(mi_ctx* ctx, uint8_t* dst, size_t size);
+size_t mi_state_set(mi_ctx* ctx, const uint8_t* src, size_t size);
+
+/* ---- measurement: HIP events on the context's stream bracketing the FFN
+ * gate/up GEMV launch of `layer` in every output-producing decode step (the
+ * step's graph is split in three around it); layer < 0 disables.
+ * mi_prof_read returns 1 and that launch's duration (microseconds) once per
+ * timed step, 0 if no step was timed since the last read. ---- */
+int32_t mi_prof_enable(mi_ctx* ctx, int32_t layer);
+int32_t mi_prof_read(mi_ctx* ctx, float* us, int32_t n);
+/* Algorithmic HBM bytes of one FFN gate/up launch (weights + activation in/out). */
+int64_t mi_prof_ffn_bytes(const mi_ctx* ctx);
+
+/* ---- op-level entry points (host buffers in/out) used by the parity tests ----
+ * raw_blocks: GGUF-layout blocks of a rows x K matrix of ggml type `type`. */
+int32_t mi_op_gemv(int32_t device, int32_t type, const void* raw_blocks, int32_t rows, int32_t K,
+                   const float* x, float* y);
+int32_t mi_op_dequant(int32_t device, int32_t type, const void* raw_blocks, int32_t rows, int32_t K,
+                      float* out);
+int32_t mi_op_quantize_q8_K(int32_t device, const float* x, int32_t K, int8_t* qs, float* d,
+                            int32_t* bsums);
+int32_t mi_op_topk(int32_t device, const float* logits, int32_t n, int32_t k, int32_t* ids, float* vals);
+/* Median device time (us) of `iters` launches of the GEMV above (micro-benchmark). */
+int32_t mi_op_gemv_bench(int32_t device, int32_t type, const void* raw_blocks, int32_t rows, int32_t K,
+                         int32_t iters, float* median_us);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MI_ENGINE_H */

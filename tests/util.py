@@ -1,0 +1,50 @@
+"""Shared test helpers: seeded random quant matrices and synthetic models."""
+import numpy as np
+
+import ggml_ref as R
+from blama_amd import gguf, synthetic
+
+QTYPES = [R.Q4_K, R.Q5_K, R.Q6_K, R.Q8_0]
+
+
+def rand_matrix(t: int, rows: int, K: int, seed: int = 0, std: float = 0.03) -> np.ndarray:
+    buf = np.empty(R.row_bytes(t, K) * rows, np.uint8)
+    synthetic.fill_quant(buf, t, np.random.default_rng(seed), std=std)
+    return buf
+
+
+def rand_x(K: int, seed: int = 1, scale: float = 1.0) -> np.ndarray:
+    return (np.random.default_rng(seed).standard_normal(K) * scale).astype(np.float32)
+
+
+def oracle_from_gguf(buf, n_ctx: int = 0) -> R.LlamaOracle:
+    rd = gguf.GGUFReader(buf)
+    kv = rd.kv
+    a = kv["general.architecture"]
+    n_embd = int(kv[f"{a}.embedding_length"])
+    n_head = int(kv[f"{a}.attention.head_count"])
+    te = rd.tensors["token_embd.weight"]
+    hp = R.HParams(
+        n_vocab=int(te.shape[1]), n_embd=n_embd, n_layer=int(kv[f"{a}.block_count"]),
+        n_head=n_head, n_head_kv=int(kv.get(f"{a}.attention.head_count_kv", n_head)),
+        n_ff=int(kv[f"{a}.feed_forward_length"]), n_ctx_train=int(kv[f"{a}.context_length"]),
+        eps=float(kv[f"{a}.attention.layer_norm_rms_epsilon"]),
+        rope_base=float(kv.get(f"{a}.rope.freq_base", 10000.0)),
+        n_rot=int(kv.get(f"{a}.rope.dimension_count", n_embd // n_head)),
+        n_expert=int(kv.get(f"{a}.expert_count", 0)), n_expert_used=int(kv.get(f"{a}.expert_used_count", 0)))
+    tens = {k: R.Tensor(v.type, v.shape, v.data) for k, v in rd.tensors.items()}
+    return R.LlamaOracle(hp, tens, n_ctx=n_ctx)
+
+
+def parse_state(st: bytes, n_layer: int, kv_dim: int):
+    """Split an mi_state_get() blob: (cell_pos, K[n_layer][n_cells][kv_dim], V[...])."""
+    import struct
+    st = np.frombuffer(st, np.uint8)
+    h = struct.unpack("8s8i", st[:40].tobytes())
+    nc = h[5]
+    pos = np.frombuffer(st[40:40 + nc * 4].tobytes(), np.int32)
+    off = 40 + nc * 4
+    n = n_layer * nc * kv_dim * 2
+    k = np.frombuffer(st[off:off + n].tobytes(), np.float16).reshape(n_layer, nc, kv_dim)
+    v = np.frombuffer(st[off + n:off + 2 * n].tobytes(), np.float16).reshape(n_layer, nc, kv_dim)
+    return pos, k, v
