@@ -248,7 +248,8 @@ QMat upload_qmat(int type, const void* raw, int rows, int K, std::vector<std::un
     m.nb = K / 256;
     uint8_t* planes[4] = {nullptr, nullptr, nullptr, nullptr};
     for (int k = 0; k < plane_count(type); ++k) {
-        keep.push_back(std::make_unique<DevBuf>((size_t)rows * m.nb * plane_sb_bytes(type, k)));
+        keep.push_back(std::make_unique<DevBuf>((size_t)(rows * m.nb + kPlanePadSb) * plane_sb_bytes(type, k)));
+        MI_HIP(hipMemset(keep.back()->p, 0, (size_t)(rows * m.nb + kPlanePadSb) * plane_sb_bytes(type, k)));
         planes[k] = keep.back()->as<uint8_t>();
         m.p[k] = planes[k];
     }
@@ -310,17 +311,32 @@ int32_t mi_op_gemv_bench(int32_t device, int32_t type, const void* raw, int32_t 
         MI_HIP(hipSetDevice(device));
         ensure_attrs(device);
         std::vector<std::unique_ptr<DevBuf>> keep;
-        const QMat m = upload_qmat(type, raw, rows, K, keep);
+        const QMat m0 = upload_qmat(type, raw, rows, K, keep);
+        // enough copies that consecutive launches stream from HBM, not the 256 MiB Infinity Cache
+        size_t mbytes = 0;
+        for (int k = 0; k < plane_count(type); ++k)
+            mbytes += (size_t)(rows * m0.nb + kPlanePadSb) * plane_sb_bytes(type, k);
+        const int copies = (int)std::min<size_t>(64, std::max<size_t>(1, (768ull << 20) / mbytes + 1));
+        std::vector<QMat> mats(copies, m0);
+        for (int c = 1; c < copies; ++c)
+            for (int k = 0; k < plane_count(type); ++k) {
+                const size_t n = (size_t)(rows * m0.nb + kPlanePadSb) * plane_sb_bytes(type, k);
+                keep.push_back(std::make_unique<DevBuf>(n));
+                MI_HIP(hipMemcpy(keep.back()->p, m0.p[k], n, hipMemcpyDeviceToDevice));
+                mats[c].p[k] = keep.back()->as<uint8_t>();
+            }
         DevBuf dx(K * sizeof(float)), dy(rows * sizeof(float));
-        std::vector<float> hx(K, 0.5f);
+        std::vector<float> hx(K);
+        for (int i = 0; i < K; ++i) hx[i] = 0.5f + 0.001f * (float)(i % 97);
         MI_HIP(hipMemcpy(dx.p, hx.data(), K * sizeof(float), hipMemcpyHostToDevice));
-        const GemvParams p = single_gemv(m, dx.as<float>(), dy.as<float>());
         hipEvent_t a, b;
         MI_HIP(hipEventCreate(&a));
         MI_HIP(hipEventCreate(&b));
         std::vector<float> t;
-        for (int i = 0; i < 10; ++i) launch_gemv(p, ROLE_GENERIC, 0, nullptr);
+        for (int i = 0; i < copies + 2; ++i)
+            launch_gemv(single_gemv(mats[i % copies], dx.as<float>(), dy.as<float>()), ROLE_GENERIC, 0, nullptr);
         for (int i = 0; i < iters; ++i) {
+            const GemvParams p = single_gemv(mats[i % copies], dx.as<float>(), dy.as<float>());
             MI_HIP(hipEventRecord(a, nullptr));
             launch_gemv(p, ROLE_GENERIC, 0, nullptr);
             MI_HIP(hipEventRecord(b, nullptr));

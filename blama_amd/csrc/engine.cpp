@@ -214,8 +214,8 @@ void Model::load(const uint8_t* data, size_t size, const mi_model_params& p) {
             if (pl.K % 256) throw Error("tensor " + name + ": K not a multiple of 256");
             const long long nsb = pl.rows * (pl.K / 256);
             for (int k = 0; k < plane_count(t->type); ++k) {
-                pl.off[k] = off;
-                off = align256(off + (size_t)nsb * plane_sb_bytes(t->type, k));
+                pl.off[k] = off;   // + 8 superblocks of tail padding read by idle GEMV lanes
+                off = align256(off + (size_t)(nsb + kPlanePadSb) * plane_sb_bytes(t->type, k));
             }
         } else if (t->type == T_F32 || t->type == T_F16) {
             pl.off[0] = off;
@@ -478,19 +478,28 @@ void Ctx::enqueue_step(bool with_logits) {
             p.freq_factors = m->rope_freqs;
             p.kcache = kl;
             p.vcache = vl;
-            p.nseg = 3;
+            // one launch per distinct quant type (Q4_K_M mixes Q6_K attn_v into some layers)
             const QMat* mats[3] = {&L.wq, &L.wk, &L.wv};
             const int epis[3] = {EPI_ROPE_Q, EPI_ROPE_K, EPI_V};
-            for (int i = 0; i < 3; ++i) {
-                seg_init(p.seg[i]);
-                p.seg[i].A = *mats[i];
-                p.seg[i].pair = PAIR_ADJ;
-                p.seg[i].epi = epis[i];
-                p.seg[i].units = (mats[i]->rows + 1) / 2;
-                p.seg[i].out = q;
+            bool done[3] = {false, false, false};
+            for (int a = 0; a < 3; ++a) {
+                if (done[a]) continue;
+                GemvParams pl = p;
+                pl.nseg = 0;
+                for (int i = a; i < 3; ++i) {
+                    if (done[i] || mats[i]->type != mats[a]->type) continue;
+                    GemvSeg& sg = pl.seg[pl.nseg++];
+                    seg_init(sg);
+                    sg.A = *mats[i];
+                    sg.pair = PAIR_ADJ;
+                    sg.epi = epis[i];
+                    sg.units = (mats[i]->rows + 1) / 2;
+                    sg.out = q;
+                    done[i] = true;
+                }
+                params_finish(pl);
+                if (on()) launch_gemv(pl, ROLE_QKV, 0, stream);
             }
-            params_finish(p);
-            if (on()) launch_gemv(p, ROLE_QKV, 0, stream);
         }
         // ---- attention ----
         {

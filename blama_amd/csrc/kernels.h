@@ -32,7 +32,7 @@ struct GemvSeg {
 };
 
 constexpr int GEMV_MAX_SEG = 4;
-constexpr int GEMV_THREADS = 512;
+constexpr int GEMV_THREADS = 1024;   // one workgroup per CU (16 waves)
 
 struct GemvParams {
     GemvSeg seg[GEMV_MAX_SEG];
@@ -57,6 +57,7 @@ struct GemvParams {
     // MoE routing results
     const int* sel;
     const float* selw;
+    int upw;                  // units per workgroup (set by launch_gemv)
 };
 
 enum GemvRole { ROLE_QKV = 0, ROLE_WO = 1, ROLE_FFN_UP = 2, ROLE_FFN_DOWN = 3, ROLE_OUTPUT = 4, ROLE_GENERIC = 5 };

@@ -11,6 +11,7 @@
 // where ggml rounds twice.
 #include "kernels.h"
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 
 namespace mi {
 
@@ -30,6 +31,20 @@ __device__ __forceinline__ float wave_sum(float v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
 }
+// Full-wave sum through DPP (row_shr 1/2/4/8, row_bcast 15/31): the total
+// lands in lane 63.  Fixed combination order -> deterministic.
+#define MI_DPP(v, ctrl, rmask) \
+    __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), ctrl, rmask, 0xf, false))
+__device__ __forceinline__ float wave_sum63(float v) {
+    v += MI_DPP(v, 0x111, 0xf);   // row_shr:1
+    v += MI_DPP(v, 0x112, 0xf);   // row_shr:2
+    v += MI_DPP(v, 0x114, 0xf);   // row_shr:4
+    v += MI_DPP(v, 0x118, 0xf);   // row_shr:8  -> lane 15 of each row holds the row sum
+    v += MI_DPP(v, 0x142, 0xa);   // row_bcast:15 -> rows 1,3 add lane 15 of rows 0,2
+    v += MI_DPP(v, 0x143, 0xc);   // row_bcast:31 -> rows 2,3 add lane 31
+    return v;                     // lane 63 = total
+}
+#undef MI_DPP
 __device__ __forceinline__ double wave_sum_d(double v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -144,21 +159,38 @@ __device__ __forceinline__ Act act_view(const char* smem, const ActLayout& L, in
 // quant plane (plus its side planes) and returns its fp32 partial.
 // ---------------------------------------------------------------------------
 template <int T> struct Kq;
+template <int T> struct PlaneBytes;   // bytes per superblock of each plane (common.h plane_sb_bytes)
+template <> struct PlaneBytes<T_Q4_K> { static constexpr int b[4] = {128, 16, 0, 0}; };
+template <> struct PlaneBytes<T_Q5_K> { static constexpr int b[4] = {128, 32, 16, 0}; };
+template <> struct PlaneBytes<T_Q6_K> { static constexpr int b[4] = {128, 64, 16, 2}; };
+template <> struct PlaneBytes<T_Q8_0> { static constexpr int b[4] = {256, 16, 0, 0}; };
 
 template <> struct Kq<T_Q4_K> {
     static constexpr int LPS = 8;
     struct Ld { u32x4 qs, hdr; };
-    __device__ static Ld load(const uint8_t* const* p, long long sbi, int j) {
+    // rp: plane pointers at the start of the row (wave-uniform); sb = s*8 + sbl
+    __device__ static Ld load(const uint8_t* const* rp, int sb, int j) {
         Ld l;
-        l.qs = ldg16(p[0] + sbi * 128 + j * 16);
-        l.hdr = ldg16(p[1] + sbi * 16);
+        l.qs = ldg16(rp[0] + sb * 128 + j * 16);
+        l.hdr = ldg16(rp[1] + sb * 16);
         return l;
     }
-    __device__ static float dot(const Ld& l, const Act& a, int sb, int j) {
+    // the activation slice lane (sb, j) needs -- identical for every row
+    struct AR { i32x4 alo, ahi; int bs_lo, bs_hi; float dx; };
+    __device__ static AR act(const Act& a, int sb, int j) {
         const int g = j >> 1, half = j & 1;
         const int8_t* ab = a.q8k + sb * 256 + 64 * g + 16 * half;
-        const i32x4 alo = *reinterpret_cast<const i32x4*>(ab);
-        const i32x4 ahi = *reinterpret_cast<const i32x4*>(ab + 32);
+        AR r;
+        r.alo = *reinterpret_cast<const i32x4*>(ab);
+        r.ahi = *reinterpret_cast<const i32x4*>(ab + 32);
+        r.bs_lo = a.bsum[sb * 16 + 4 * g + half];
+        r.bs_hi = a.bsum[sb * 16 + 4 * g + 2 + half];
+        r.dx = a.dk[sb];
+        return r;
+    }
+    __device__ static float dot(const Ld& l, const AR& r, int j) {
+        const int g = j >> 1;
+        const i32x4 alo = r.alo, ahi = r.ahi;
         int dlo = 0, dhi = 0;
         dlo = dot4(l.qs.x & 0x0F0F0F0F, alo.x, dlo);
         dlo = dot4(l.qs.y & 0x0F0F0F0F, alo.y, dlo);
@@ -174,11 +206,9 @@ template <> struct Kq<T_Q4_K> {
         const unsigned SC = g < 2 ? (Y & 0x3F3Fu) : ((W & 0x0F0Fu) | ((Y >> 2) & 0x3030u));
         const unsigned MM = g < 2 ? (Z & 0x3F3Fu) : (((W >> 4) & 0x0F0Fu) | ((Z >> 2) & 0x3030u));
         const int S = (int)(SC & 0xFF) * dlo + (int)((SC >> 8) & 0xFF) * dhi;
-        const int* bs = a.bsum + sb * 16 + 4 * g + half;
-        const int M = (int)(MM & 0xFF) * bs[0] + (int)((MM >> 8) & 0xFF) * bs[2];
-        const float dx = a.dk[sb];
-        const float d = h2f(l.hdr.x) * dx;
-        const float dm = h2f(l.hdr.x >> 16) * dx;
+        const int M = (int)(MM & 0xFF) * r.bs_lo + (int)((MM >> 8) & 0xFF) * r.bs_hi;
+        const float d = h2f(l.hdr.x) * r.dx;
+        const float dm = h2f(l.hdr.x >> 16) * r.dx;
         return d * (float)S - dm * (float)M;
     }
 };
@@ -186,18 +216,18 @@ template <> struct Kq<T_Q4_K> {
 template <> struct Kq<T_Q5_K> {
     static constexpr int LPS = 8;
     struct Ld { u32x4 qs, qh, hdr; };
-    __device__ static Ld load(const uint8_t* const* p, long long sbi, int j) {
+    __device__ static Ld load(const uint8_t* const* rp, int sb, int j) {
         Ld l;
-        l.qs = ldg16(p[0] + sbi * 128 + j * 16);
-        l.qh = ldg16(p[1] + sbi * 32 + (j & 1) * 16);
-        l.hdr = ldg16(p[2] + sbi * 16);
+        l.qs = ldg16(rp[0] + sb * 128 + j * 16);
+        l.qh = ldg16(rp[1] + sb * 32 + (j & 1) * 16);
+        l.hdr = ldg16(rp[2] + sb * 16);
         return l;
     }
-    __device__ static float dot(const Ld& l, const Act& a, int sb, int j) {
-        const int g = j >> 1, half = j & 1;
-        const int8_t* ab = a.q8k + sb * 256 + 64 * g + 16 * half;
-        const i32x4 alo = *reinterpret_cast<const i32x4*>(ab);
-        const i32x4 ahi = *reinterpret_cast<const i32x4*>(ab + 32);
+    using AR = Kq<T_Q4_K>::AR;
+    __device__ static AR act(const Act& a, int sb, int j) { return Kq<T_Q4_K>::act(a, sb, j); }
+    __device__ static float dot(const Ld& l, const AR& r, int j) {
+        const int g = j >> 1;
+        const i32x4 alo = r.alo, ahi = r.ahi;
         const unsigned s0 = 2 * g, s1 = 2 * g + 1;
         int dlo = 0, dhi = 0;
 #define Q5L(c) ((l.qs.c & 0x0F0F0F0Fu) | (((l.qh.c >> s0) & 0x01010101u) << 4))
@@ -217,11 +247,9 @@ template <> struct Kq<T_Q5_K> {
         const unsigned SC = g < 2 ? (Y & 0x3F3Fu) : ((W & 0x0F0Fu) | ((Y >> 2) & 0x3030u));
         const unsigned MM = g < 2 ? (Z & 0x3F3Fu) : (((W >> 4) & 0x0F0Fu) | ((Z >> 2) & 0x3030u));
         const int S = (int)(SC & 0xFF) * dlo + (int)((SC >> 8) & 0xFF) * dhi;
-        const int* bs = a.bsum + sb * 16 + 4 * g + half;
-        const int M = (int)(MM & 0xFF) * bs[0] + (int)((MM >> 8) & 0xFF) * bs[2];
-        const float dx = a.dk[sb];
-        const float d = h2f(l.hdr.x) * dx;
-        const float dm = h2f(l.hdr.x >> 16) * dx;
+        const int M = (int)(MM & 0xFF) * r.bs_lo + (int)((MM >> 8) & 0xFF) * r.bs_hi;
+        const float d = h2f(l.hdr.x) * r.dx;
+        const float dm = h2f(l.hdr.x >> 16) * r.dx;
         return d * (float)S - dm * (float)M;
     }
 };
@@ -229,25 +257,37 @@ template <> struct Kq<T_Q5_K> {
 template <> struct Kq<T_Q6_K> {
     static constexpr int LPS = 8;
     struct Ld { u32x4 ql, qh; unsigned sc0, sc1, d; };
-    __device__ static Ld load(const uint8_t* const* p, long long sbi, int j) {
+    __device__ static Ld load(const uint8_t* const* rp, int sb, int j) {
         Ld l;
         const int h = j >> 2, half = j & 1;
-        l.ql = ldg16(p[0] + sbi * 128 + j * 16);
-        l.qh = ldg16(p[1] + sbi * 64 + 32 * h + 16 * half);
+        l.ql = ldg16(rp[0] + sb * 128 + j * 16);
+        l.qh = ldg16(rp[1] + sb * 64 + 32 * h + 16 * half);
         // scales 8h..8h+7: is_lo = 8h+2hq+half lives in word 0, is_hi = is_lo+4 in word 1
-        const unsigned* scw = reinterpret_cast<const unsigned*>(p[2] + sbi * 16) + 2 * h;
-        l.sc0 = __builtin_nontemporal_load(scw);
-        l.sc1 = __builtin_nontemporal_load(scw + 1);
-        l.d = __builtin_nontemporal_load(reinterpret_cast<const unsigned short*>(p[3] + sbi * 2));
+        typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+        const u32x2 sc = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(rp[2] + sb * 16) + h);
+        l.sc0 = sc.x;
+        l.sc1 = sc.y;
+        l.d = __builtin_nontemporal_load(reinterpret_cast<const unsigned short*>(rp[3] + sb * 2));
         return l;
     }
-    __device__ static float dot(const Ld& l, const Act& a, int sb, int j) {
+    struct AR { i32x4 alo, ahi; int bs_lo, bs_hi; float dx; };
+    __device__ static AR act(const Act& a, int sb, int j) {
         const int h = j >> 2, hq = (j >> 1) & 1, half = j & 1;
-        const unsigned sh = hq * 2;
         const int e_lo = 128 * h + 32 * hq + 16 * half;
         const int8_t* ab = a.q8k + sb * 256 + e_lo;
-        const i32x4 alo = *reinterpret_cast<const i32x4*>(ab);
-        const i32x4 ahi = *reinterpret_cast<const i32x4*>(ab + 64);
+        const int is_lo = 8 * h + 2 * hq + half;
+        AR r;
+        r.alo = *reinterpret_cast<const i32x4*>(ab);
+        r.ahi = *reinterpret_cast<const i32x4*>(ab + 64);
+        r.bs_lo = a.bsum[sb * 16 + is_lo];
+        r.bs_hi = a.bsum[sb * 16 + is_lo + 4];
+        r.dx = a.dk[sb];
+        return r;
+    }
+    __device__ static float dot(const Ld& l, const AR& r, int j) {
+        const int hq = (j >> 1) & 1, half = j & 1;
+        const unsigned sh = hq * 2;
+        const i32x4 alo = r.alo, ahi = r.ahi;
         int dlo = 0, dhi = 0;
 #define Q6L(c) ((l.ql.c & 0x0F0F0F0Fu) | (((l.qh.c >> sh) & 0x03030303u) << 4))
 #define Q6H(c) (((l.ql.c >> 4) & 0x0F0F0F0Fu) | (((l.qh.c >> (sh + 4)) & 0x03030303u) << 4))
@@ -265,108 +305,91 @@ template <> struct Kq<T_Q6_K> {
         const int bsh = 8 * (2 * hq + half);
         const int sc_lo = (int)(signed char)((l.sc0 >> bsh) & 0xFF);
         const int sc_hi = (int)(signed char)((l.sc1 >> bsh) & 0xFF);
-        const int is_lo = 8 * h + 2 * hq + half;
-        const int* bs = a.bsum + sb * 16;
-        const int S = sc_lo * (dlo - 32 * bs[is_lo]) + sc_hi * (dhi - 32 * bs[is_lo + 4]);
-        const float d = h2f(l.d) * a.dk[sb];
+        const int S = sc_lo * (dlo - 32 * r.bs_lo) + sc_hi * (dhi - 32 * r.bs_hi);
+        const float d = h2f(l.d) * r.dx;
         return d * (float)S;
     }
 };
 
 template <> struct Kq<T_Q8_0> {
-    static constexpr int LPS = 16;
-    struct Ld { u32x4 qs; unsigned d; };
-    __device__ static Ld load(const uint8_t* const* p, long long sbi, int c) {
+    static constexpr int LPS = 8;          // lane j owns block j (32 weights) of the superblock
+    struct Ld { u32x4 q0, q1; unsigned d; };
+    __device__ static Ld load(const uint8_t* const* rp, int sb, int j) {
         Ld l;
-        l.qs = ldg16(p[0] + sbi * 256 + c * 16);
-        l.d = __builtin_nontemporal_load(reinterpret_cast<const unsigned short*>(p[1] + sbi * 16 + (c >> 1) * 2));
+        l.q0 = ldg16(rp[0] + sb * 256 + j * 32);
+        l.q1 = ldg16(rp[0] + sb * 256 + j * 32 + 16);
+        l.d = __builtin_nontemporal_load(reinterpret_cast<const unsigned short*>(rp[1] + sb * 16 + j * 2));
         return l;
     }
-    __device__ static float dot(const Ld& l, const Act& a, int sb, int c) {
-        const i32x4 av = *reinterpret_cast<const i32x4*>(a.q80 + sb * 256 + c * 16);
+    struct AR { i32x4 a0, a1; float d0; };
+    __device__ static AR act(const Act& a, int sb, int j) {
+        const int8_t* ab = a.q80 + sb * 256 + j * 32;
+        AR r;
+        r.a0 = *reinterpret_cast<const i32x4*>(ab);
+        r.a1 = *reinterpret_cast<const i32x4*>(ab + 16);
+        r.d0 = a.d0[sb * 8 + j];
+        return r;
+    }
+    __device__ static float dot(const Ld& l, const AR& r, int j) {
+        const i32x4 a0 = r.a0, a1 = r.a1;
         int s = 0;
-        s = dot4((int)l.qs.x, av.x, s);
-        s = dot4((int)l.qs.y, av.y, s);
-        s = dot4((int)l.qs.z, av.z, s);
-        s = dot4((int)l.qs.w, av.w, s);
-        const float d = h2f(l.d) * a.d0[sb * 8 + (c >> 1)];
+        s = dot4((int)l.q0.x, a0.x, s);
+        s = dot4((int)l.q0.y, a0.y, s);
+        s = dot4((int)l.q0.z, a0.z, s);
+        s = dot4((int)l.q0.w, a0.w, s);
+        s = dot4((int)l.q1.x, a1.x, s);
+        s = dot4((int)l.q1.y, a1.y, s);
+        s = dot4((int)l.q1.z, a1.z, s);
+        s = dot4((int)l.q1.w, a1.w, s);
+        const float d = h2f(l.d) * r.d0;   // fp16(x.d) * fp16(y.d), then * sumi
         return d * (float)s;
     }
 };
 
-// Two rows (A row ra, B row rb) against their activations; one wave.
-template <int T>
-__device__ __forceinline__ void unit_rows(const uint8_t* const* pa, long long ra, const uint8_t* const* pb,
-                                          long long rb, bool hasB, int nb, const Act& aA, const Act& aB,
-                                          int lane, float& yA, float& yB) {
-    using K = Kq<T>;
-    constexpr int LPS = K::LPS;
-    constexpr int SPS = 64 / LPS;
-    const int sbl = lane / LPS, j = lane % LPS;
-    const int steps = (nb + SPS - 1) / SPS;
-    float accA = 0.0f, accB = 0.0f;
-    int s = 0;
-    for (; s + 1 < steps; s += 2) {
-        const int sb0 = s * SPS + sbl, sb1 = sb0 + SPS;
-        const bool v1 = sb1 < nb;
-        typename K::Ld a0 = K::load(pa, ra * nb + sb0, j), a1, b0, b1;
-        if (v1) a1 = K::load(pa, ra * nb + sb1, j);
-        if (hasB) {
-            b0 = K::load(pb, rb * nb + sb0, j);
-            if (v1) b1 = K::load(pb, rb * nb + sb1, j);
-        }
-        accA += K::dot(a0, aA, sb0, j);
-        if (v1) accA += K::dot(a1, aA, sb1, j);
-        if (hasB) {
-            accB += K::dot(b0, aB, sb0, j);
-            if (v1) accB += K::dot(b1, aB, sb1, j);
-        }
-    }
-    if (s < steps) {
-        const int sb0 = s * SPS + sbl;
-        if (sb0 < nb) {
-            typename K::Ld a0 = K::load(pa, ra * nb + sb0, j), b0;
-            if (hasB) b0 = K::load(pb, rb * nb + sb0, j);
-            accA += K::dot(a0, aA, sb0, j);
-            if (hasB) accB += K::dot(b0, aB, sb0, j);
-        }
-    }
-    yA = wave_sum(accA);
-    yB = hasB ? wave_sum(accB) : 0.0f;
-}
-
 // ---------------------------------------------------------------------------
-// The fused GEMV kernel
+// The fused GEMV kernel, specialised per quant type T.
+//
+// Work decomposition: a unit is a pair of output rows (see kernels.h); a wave
+// owns units gw, gw + W, gw + 2W, ... (W = waves in the grid).  A unit is
+// streamed in "chunks" (one step of SPS superblocks for both rows), and the
+// wave keeps D chunks in flight in a register ring: while chunk q is being
+// reduced against the LDS activations, chunks q+1 .. q+D-1 are loading.  The
+// first D-1 chunks are issued before the prologue so that the weight stream
+// starts while the activations are normalised and quantised.
 // ---------------------------------------------------------------------------
-__global__ void attn_kernel(const AttnParams P);
-
 struct SmemPlan {
     ActLayout L;
-    int act_bytes, rope_off, red_off, total;
+    int act_bytes, rope_off, red_off, resid_off, total;
 };
-__host__ __device__ inline SmemPlan smem_plan(int K, int nslots, int need_q8k, int need_q80, int n_rot) {
+// resid_rows: residual values staged per workgroup (its contiguous unit range)
+__host__ __device__ inline SmemPlan smem_plan(int K, int nslots, int need_q8k, int need_q80, int n_rot,
+                                              int resid_rows) {
     SmemPlan P;
     P.L = act_layout(K, need_q8k, need_q80);
     P.act_bytes = P.L.slot_bytes * nslots;
     P.rope_off = P.act_bytes;
     P.red_off = P.rope_off + ((n_rot / 2) * 8 + 15) / 16 * 16;
-    P.total = P.red_off + 32 * 8;
+    P.resid_off = P.red_off + 32 * 8;
+    P.total = P.resid_off + ((resid_rows * 4 + 15) / 16) * 16;
     return P;
 }
+__host__ __device__ inline int resid_rows_per_wg(const GemvParams&) { return 0; }
 
 __device__ __forceinline__ float silu_f(float x) { return x / (1.0f + expf(-x)); }
 
-__device__ __forceinline__ void gemv_body(const GemvParams& P) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nwaves = blockDim.x >> 6;
-    const SmemPlan SP = smem_plan(P.K, P.nslots, P.need_q8k, P.need_q80, P.n_rot);
+// Prologue (every workgroup, redundantly): RMSNorm of slot 0 if requested,
+// quantisation of the activation slots into LDS, residual rows of this
+// workgroup's unit range, and the RoPE cos/sin table of this token.
+__device__ __forceinline__ void gemv_prologue(const GemvParams& P, char* smem, const SmemPlan& SP, int pos) {
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int nwaves = blockDim.x >> 6;
     const ActLayout& L = SP.L;
     double* red = reinterpret_cast<double*>(smem + SP.red_off);
-
-    // ---- prologue: RMSNorm (ggml_compute_forward_rms_norm_f32: double sum) and
-    //      activation quantisation into LDS, redundantly per workgroup ----
+    if (P.pro < 0) return;   // debug: skip the prologue (timing ablation only)
     float scale = 1.0f;
     if (P.pro == PRO_RMSNORM) {
+        // ggml_compute_forward_rms_norm_f32: sum of float squares in double
         double s = 0.0;
         const float4* x4 = reinterpret_cast<const float4*>(P.x[0]);
         for (int i = tid; i < P.K / 4; i += blockDim.x) {
@@ -389,7 +412,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams& P) {
         const float4* x4 = reinterpret_cast<const float4*>(P.x[slot]);
         const bool norm = slot == 0 && P.pro == PRO_RMSNORM;
         for (int blk = wave; blk < L.nb; blk += nwaves) {
-            float4 xv = x4[blk * 64 + lane];
+            const float4 xv = x4[blk * 64 + lane];
             float v[4] = {xv.x, xv.y, xv.z, xv.w};
             if (norm) {
                 const float4 w = reinterpret_cast<const float4*>(P.norm_w)[blk * 64 + lane];
@@ -407,10 +430,17 @@ __device__ __forceinline__ void gemv_body(const GemvParams& P) {
                                 reinterpret_cast<float*>(base + L.d0) + blk * 8);
         }
     }
+    // residual rows of this workgroup (in-place residual add: x[r] = W.a + x[r])
+    const int rrows = resid_rows_per_wg(P);
+    if (rrows > 0) {
+        float* rs = reinterpret_cast<float*>(smem + SP.resid_off);
+        const long long r0 = (long long)blockIdx.x * rrows;
+        const long long nrow = P.seg[0].pair == PAIR_ADJ ? P.seg[0].A.rows : P.seg[0].units;
+        for (int i = tid; i < rrows; i += blockDim.x) rs[i] = (r0 + i < nrow) ? P.seg[0].resid[r0 + i] : 0.0f;
+    }
     // RoPE cache for this token's position (ggml_rope_cache_init, ext_factor 0, mscale 1)
-    float* rope = reinterpret_cast<float*>(smem + SP.rope_off);
     if (P.n_rot > 0 && wave == 0) {
-        const int pos = P.tokpos[1];
+        float* rope = reinterpret_cast<float*>(smem + SP.rope_off);
         for (int i = lane; i < P.n_rot / 2; i += 64) {
             float theta = (float)pos;
             for (int k = 0; k < i; ++k) theta = theta * P.theta_scale;
@@ -420,138 +450,331 @@ __device__ __forceinline__ void gemv_body(const GemvParams& P) {
             rope[2 * i + 1] = sinf(th);
         }
     }
-    __syncthreads();
+}
 
-    // ---- main loop: every wave takes units grid-strided ----
-    const int total_waves = gridDim.x * nwaves;
-    for (int u = blockIdx.x * nwaves + wave; u < P.total_units; u += total_waves) {
-        int si = 0;
-        while (si + 1 < P.nseg && u >= P.seg[si + 1].unit0) ++si;
-        const GemvSeg& S = P.seg[si];
-        const int lu = u - S.unit0;
-        long long ra, rb;
-        bool hasB;
-        if (S.pair == PAIR_ADJ) { ra = 2LL * lu; rb = ra + 1; hasB = rb < S.A.rows; }
-        else { ra = rb = lu; hasB = true; }
+struct UnitRef {
+    int si;           // segment
+    int lu;           // unit within segment
+    long long ra, rb; // rows
+    bool hasB;
+};
+
+__device__ __forceinline__ UnitRef unit_ref(const GemvParams& P, int u) {
+    UnitRef c;
+    int si = 0;
+    while (si + 1 < P.nseg && u >= P.seg[si + 1].unit0) ++si;
+    c.si = si;
+    c.lu = u - P.seg[si].unit0;
+    if (P.seg[si].pair == PAIR_ADJ) {
+        c.ra = 2LL * c.lu;
+        c.rb = c.ra + 1;
+        c.hasB = c.rb < P.seg[si].A.rows;
+    } else {
+        c.ra = c.rb = c.lu;
+        c.hasB = true;
+    }
+    return c;
+}
+
+// rva / rvb: residual values of rows A / B (loaded with the unit's weights)
+__device__ __forceinline__ void gemv_epilogue(const GemvParams& P, const UnitRef& c, const float* rope,
+                                              float rva, float rvb, float wa, float wb,
+                                              int pos, int cell, float yA, float yB) {
+    const GemvSeg& S = P.seg[c.si];
+    const long long ra = c.ra, rb = c.rb;
+    switch (S.epi) {
+    case EPI_STORE:
+        S.out[ra] = yA;
+        if (c.hasB) S.out[rb] = yB;
+        break;
+    case EPI_ADD:
+        S.out[ra] = yA + rva;
+        if (c.hasB) S.out[rb] = yB + rvb;
+        break;
+    case EPI_ROPE_Q:
+    case EPI_ROPE_K: {
+        const int i0 = (int)(ra % P.head_dim);   // even
+        float o0 = yA, o1 = yB;
+        if (i0 < P.n_rot) {
+            const float cs = rope[i0], sn = rope[i0 + 1];
+            o0 = yA * cs - yB * sn;
+            o1 = yA * sn + yB * cs;
+        }
+        if (S.epi == EPI_ROPE_Q) {
+            S.out[ra] = o0;
+            S.out[rb] = o1;
+        } else {
+            __half* kr = P.kcache + (long long)cell * P.kv_dim;
+            kr[ra] = __float2half_rn(o0);
+            kr[rb] = __float2half_rn(o1);
+            if (c.lu == 0) P.cell_pos[cell] = pos;
+        }
+        break;
+    }
+    case EPI_V: {
+        __half* vr = P.vcache + (long long)cell * P.kv_dim;
+        vr[ra] = __float2half_rn(yA);
+        if (c.hasB) vr[rb] = __float2half_rn(yB);
+        break;
+    }
+    case EPI_SWIGLU:
+        S.out[c.lu] = silu_f(yA) * yB;
+        break;
+    case EPI_MOE_DOWN:
+        S.out[c.lu] = (yA * wa + yB * wb) + rva;
+        break;
+    default: break;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// The fused GEMV kernel, specialised per quant type T and per NS = superblock
+// steps per row (ceil(K/256/8)).  A wave computes one unit (two rows) at a
+// time: all NS x 2 row loads are issued together (8 lanes per superblock, one
+// aligned 16-byte load of the main plane per lane), the next unit's loads are
+// issued as soon as the current unit's dot products are done, so they overlap
+// the DPP reduction and the epilogue.  The first unit's loads are issued
+// before the prologue.  Latency is hidden by occupancy (256-thread workgroups,
+// 2 rows x NS loads in flight per wave).
+// ---------------------------------------------------------------------------
+// ---------------------------------------------------------------------------
+// The fused GEMV kernel, specialised per quant type T, per NSW (superblock
+// steps streamed by one wave per row, <= 2) and per KS (waves of the workgroup
+// that split one row pair's K range; KS*NSW*8 >= K/256).
+//
+// * Each wave keeps, for its NSW steps, the activation slice its lanes need in
+//   registers (it is the same for every row), loaded from LDS once after the
+//   prologue; the inner loop touches no LDS.
+// * A unit (row pair) is loaded with all NSW x 2 row loads issued together
+//   (8 lanes per superblock, aligned 16-B loads), the first unit before the
+//   prologue so the weight stream starts while activations are quantised.
+// * KS > 1: the KS waves' partial sums are combined through LDS in fixed
+//   order (deterministic) by the group's first wave, which runs the epilogue.
+// ---------------------------------------------------------------------------
+template <int T, int NSW, int KS, int DUAL, int ROLE>
+__global__ __launch_bounds__(GEMV_THREADS) void gemv_t(const GemvParams P) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    using K = Kq<T>;
+    static_assert(K::LPS == 8, "8 lanes per superblock");
+    constexpr int NW = GEMV_THREADS / 64;
+    constexpr int NGRP = NW / KS;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform -> SGPRs
+    const int grp = wave / KS, wk = wave % KS;
+    const int sbl = lane >> 3, j = lane & 7;
+    const SmemPlan SP = smem_plan(P.K, P.nslots, P.need_q8k, P.need_q80, P.n_rot, resid_rows_per_wg(P));
+    const int nb = P.K >> 8;
+    const int ns = (nb + 7) >> 3;
+    // token position / cache cell and MoE routing results, read once
+    int pos = 0, cell = 0;
+    if (P.tokpos) {
+        pos = __builtin_amdgcn_readfirstlane(P.tokpos[1]);
+        cell = __builtin_amdgcn_readfirstlane(P.tokpos[2]);
+    }
+    int e0 = 0, e1 = 0;
+    float w0 = 0.0f, w1 = 0.0f;
+    if (P.sel) {
+        e0 = __builtin_amdgcn_readfirstlane(P.sel[0]);
+        e1 = __builtin_amdgcn_readfirstlane(P.sel[1]);
+        w0 = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(P.selw[0])));
+        w1 = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(P.selw[1])));
+    }
+    // groups of KS waves sweep the units grid-strided, so neighbouring groups
+    // (in and across workgroups) stream neighbouring rows at the same time
+    const int G_total = gridDim.x * NGRP;
+    const int g0 = blockIdx.x * NGRP + grp;
+    const int n_iter = (P.total_units + G_total - 1) / G_total;   // same for every wave of the workgroup
+
+    typename K::Ld la[NSW], lb[NSW];
+    float rva = 0.0f, rvb = 0.0f;
+    const uint8_t* ra_p[4];
+    const uint8_t* rb_p[4];
+    auto rows_of = [&](const UnitRef& c) {
+        const GemvSeg& S = P.seg[c.si];
         const QMat& MB = S.pair == PAIR_ADJ ? S.A : S.B;
-        const int ea = S.expA >= 0 ? P.sel[S.expA] : 0;
-        const int eb = S.expB >= 0 ? P.sel[S.expB] : 0;
-        const uint8_t* pa[4];
-        const uint8_t* pb[4];
+        const long long ea = S.expA == 0 ? e0 : S.expA == 1 ? e1 : 0;
+        const long long eb = S.expB == 0 ? e0 : S.expB == 1 ? e1 : 0;
+        const long long rb = c.hasB ? c.rb : c.ra;   // odd tail: re-read row A, result unused
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            pa[i] = S.A.p[i] + (long long)ea * S.A.expert_stride[i];
-            pb[i] = MB.p[i] + (long long)eb * MB.expert_stride[i];
+            ra_p[i] = S.A.p[i] + ea * S.A.expert_stride[i] + c.ra * nb * PlaneBytes<T>::b[i];
+            rb_p[i] = MB.p[i] + eb * MB.expert_stride[i] + rb * nb * PlaneBytes<T>::b[i];
         }
-        const Act aA = act_view(smem, L, S.actA);
-        const Act aB = act_view(smem, L, S.pair == PAIR_ADJ ? S.actA : S.actB);
-        float yA = 0.0f, yB = 0.0f;
-        switch (S.A.type) {
-        case T_Q4_K: unit_rows<T_Q4_K>(pa, ra, pb, rb, hasB, S.A.nb, aA, aB, lane, yA, yB); break;
-        case T_Q5_K: unit_rows<T_Q5_K>(pa, ra, pb, rb, hasB, S.A.nb, aA, aB, lane, yA, yB); break;
-        case T_Q6_K: unit_rows<T_Q6_K>(pa, ra, pb, rb, hasB, S.A.nb, aA, aB, lane, yA, yB); break;
-        case T_Q8_0: unit_rows<T_Q8_0>(pa, ra, pb, rb, hasB, S.A.nb, aA, aB, lane, yA, yB); break;
-        default: break;
+        // residual of this unit's rows, issued with its weights (no late drain)
+        if (S.resid) {
+            const long long ia = S.pair == PAIR_ADJ ? c.ra : c.lu;
+            rva = S.resid[ia];
+            rvb = S.resid[S.pair == PAIR_ADJ ? rb : ia];
         }
-        if (lane != 0) continue;
-        switch (S.epi) {
-        case EPI_STORE:
-            S.out[ra] = yA;
-            if (hasB) S.out[rb] = yB;
-            break;
-        case EPI_ADD:
-            S.out[ra] = yA + S.resid[ra];
-            if (hasB) S.out[rb] = yB + S.resid[rb];
-            break;
-        case EPI_ROPE_Q:
-        case EPI_ROPE_K: {
-            const int i0 = (int)(ra % P.head_dim);   // even
-            float o0 = yA, o1 = yB;
-            if (i0 < P.n_rot) {
-                const float c = rope[i0], sn = rope[i0 + 1];
-                o0 = yA * c - yB * sn;
-                o1 = yA * sn + yB * c;
+    };
+    // Lanes past the row's last superblock read into the next row / the
+    // plane's 8-superblock tail padding; their products are masked.
+    auto load_unit = [&]() {
+#pragma unroll
+        for (int t = 0; t < NSW; ++t) {
+            const int s = wk + t * KS;
+            if (s < ns) {
+                la[t] = K::load(ra_p, s * 8 + sbl, j);
+                lb[t] = K::load(rb_p, s * 8 + sbl, j);
             }
-            if (S.epi == EPI_ROPE_Q) {
-                S.out[ra] = o0;
-                S.out[rb] = o1;
-            } else {
-                const int cell = P.tokpos[2];
-                __half* kr = P.kcache + (long long)cell * P.kv_dim;
-                kr[ra] = __float2half_rn(o0);
-                kr[rb] = __float2half_rn(o1);
-                if (lu == 0) P.cell_pos[cell] = P.tokpos[1];
+        }
+    };
+    int u = g0;
+    if (u < P.total_units) {
+        rows_of(unit_ref(P, u));
+        load_unit();
+    }
+    gemv_prologue(P, smem, SP, pos);
+    __syncthreads();
+    const float* rope = reinterpret_cast<const float*>(smem + SP.rope_off);
+    float* red = reinterpret_cast<float*>(smem + SP.red_off);   // prologue scratch, reused
+
+    // this wave's activation slices (slot 0, and slot 1 for the dual-slot MoE down launch)
+    typename K::AR arA[NSW], arB[NSW];
+    {
+        const Act a0 = act_view(smem, SP.L, 0);
+        const Act a1 = act_view(smem, SP.L, DUAL ? 1 : 0);
+#pragma unroll
+        for (int t = 0; t < NSW; ++t) {
+            const int s = wk + t * KS;
+            const int sb = s * 8 + sbl;
+            const int sbc = sb < nb ? sb : nb - 1;
+            arA[t] = K::act(a0, sbc, j);
+            if (DUAL) arB[t] = K::act(a1, sbc, j);
+        }
+    }
+
+    for (int it = 0; it < n_iter; ++it, u += G_total) {
+        const bool valid = u < P.total_units;
+        const UnitRef c = unit_ref(P, valid ? u : 0);
+        if (it > 0 && valid) {
+            rows_of(c);
+            load_unit();
+        }
+        float accA = 0.0f, accB = 0.0f;
+        if (valid) {
+#pragma unroll
+            for (int t = 0; t < NSW; ++t) {
+                const int s = wk + t * KS;
+                if (s < ns) {
+                    const bool lv = s * 8 + sbl < nb;
+                    const float pa = K::dot(la[t], arA[t], j);
+                    const float pb = K::dot(lb[t], DUAL ? arB[t] : arA[t], j);
+                    accA += lv ? pa : 0.0f;
+                    accB += lv ? pb : 0.0f;
+                }
             }
-            break;
         }
-        case EPI_V: {
-            const int cell = P.tokpos[2];
-            __half* vr = P.vcache + (long long)cell * P.kv_dim;
-            vr[ra] = __float2half_rn(yA);
-            if (hasB) vr[rb] = __float2half_rn(yB);
-            break;
-        }
-        case EPI_SWIGLU:
-            S.out[lu] = silu_f(yA) * yB;
-            break;
-        case EPI_MOE_DOWN: {
-            const float wa = P.selw[S.expA], wb = P.selw[S.expB];
-            S.out[lu] = (yA * wa + yB * wb) + S.resid[lu];
-            break;
-        }
-        default: break;
+        float yA = wave_sum63(accA);
+        float yB = wave_sum63(accB);
+        if (KS == 1) {
+            if (valid && lane == 63) gemv_epilogue(P, c, rope, rva, rvb, w0, w1, pos, cell, yA, yB);
+        } else {
+            if (lane == 63) {
+                red[(grp * KS + wk) * 2] = yA;
+                red[(grp * KS + wk) * 2 + 1] = yB;
+            }
+            __syncthreads();
+            if (valid && wk == 0 && lane == 63) {
+                yA = red[grp * KS * 2];
+                yB = red[grp * KS * 2 + 1];
+#pragma unroll
+                for (int k = 1; k < KS; ++k) {
+                    yA += red[(grp * KS + k) * 2];
+                    yB += red[(grp * KS + k) * 2 + 1];
+                }
+                gemv_epilogue(P, c, rope, rva, rvb, w0, w1, pos, cell, yA, yB);
+            }
+            __syncthreads();
         }
     }
 }
 
-// One symbol per role so that rocprofv3 reports each decode GEMV separately.
-#define MI_GEMV_ROLE(NAME) \
-    __global__ __launch_bounds__(GEMV_THREADS) void NAME(const GemvParams P) { gemv_body(P); }
-MI_GEMV_ROLE(gemv_qkv_rope_kv)
-MI_GEMV_ROLE(gemv_attn_out_residual)
-MI_GEMV_ROLE(gemv_ffn_gate_up_swiglu)
-MI_GEMV_ROLE(gemv_ffn_down_residual)
-MI_GEMV_ROLE(gemv_output_logits)
-MI_GEMV_ROLE(gemv_generic)
-#undef MI_GEMV_ROLE
+constexpr int GEMV_MAX_NS = 8;
 
 typedef void (*GemvFn)(const GemvParams);
-static GemvFn gemv_fn(int role) {
-    switch (role) {
-    case ROLE_QKV: return gemv_qkv_rope_kv;
-    case ROLE_WO: return gemv_attn_out_residual;
-    case ROLE_FFN_UP: return gemv_ffn_gate_up_swiglu;
-    case ROLE_FFN_DOWN: return gemv_ffn_down_residual;
-    case ROLE_OUTPUT: return gemv_output_logits;
-    default: return gemv_generic;
+
+// ns = superblock steps per row (ceil(K/256/8)) -> KS waves share a row pair,
+// each wave streams NSW <= 2 steps.  ROLE: 0 generic, 1 FFN gate/up, 2 dual
+// activation slot (MoE down).
+template <int T, int ROLE>
+static GemvFn gemv_fn_ns(int ns) {
+    constexpr int DUAL = ROLE == 2 ? 1 : 0;
+    switch (ns) {
+    case 1: return gemv_t<T, 1, 1, DUAL, ROLE>;
+    case 2: return gemv_t<T, 2, 1, DUAL, ROLE>;
+    case 3: case 4: return gemv_t<T, 2, 2, DUAL, ROLE>;
+    case 5: case 6: case 7: case 8: return gemv_t<T, 2, 4, DUAL, ROLE>;
+    default: return nullptr;
     }
 }
 
+int gemv_ks(int ns) { return ns <= 2 ? 1 : ns <= 4 ? 2 : 4; }
+
+template <int ROLE>
+static GemvFn gemv_fn_t(int type, int ns) {
+    switch (type) {
+    case T_Q4_K: return gemv_fn_ns<T_Q4_K, ROLE>(ns);
+    case T_Q5_K: return gemv_fn_ns<T_Q5_K, ROLE>(ns);
+    case T_Q6_K: return gemv_fn_ns<T_Q6_K, ROLE>(ns);
+    case T_Q8_0: return gemv_fn_ns<T_Q8_0, ROLE>(ns);
+    default: return nullptr;
+    }
+}
+
+// The FFN gate/up launch gets its own symbol (the bench's roofline kernel).
+static GemvFn gemv_fn(int role, int type, int ns, int nslots) {
+    if (nslots > 1) return gemv_fn_t<2>(type, ns);
+    return role == ROLE_FFN_UP ? gemv_fn_t<1>(type, ns) : gemv_fn_t<0>(type, ns);
+}
+
+__global__ void attn_kernel(const AttnParams P);
+
 void init_kernel_attributes() {
-    for (int r = 0; r <= ROLE_GENERIC; ++r)
-        MI_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(gemv_fn(r)),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    const int types[4] = {T_Q4_K, T_Q5_K, T_Q6_K, T_Q8_0};
+    for (int r : {ROLE_GENERIC, ROLE_FFN_UP})
+        for (int t : types)
+            for (int ns = 1; ns <= GEMV_MAX_NS; ++ns)
+                for (int nsl = 1; nsl <= 2; ++nsl)
+                    MI_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(gemv_fn(r, t, ns, nsl)),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     MI_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(attn_kernel),
                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
 }
 
 size_t gemv_smem_bytes(const GemvParams& p) {
-    return (size_t)smem_plan(p.K, p.nslots, p.need_q8k, p.need_q80, p.n_rot).total;
+    return (size_t)smem_plan(p.K, p.nslots, p.need_q8k, p.need_q80, p.n_rot, resid_rows_per_wg(p)).total;
 }
 
+int gemv_ks(int ns);
 int gemv_default_grid(const GemvParams& p) {
-    const int waves = GEMV_THREADS / 64;
-    int g = (p.total_units + waves - 1) / waves;
-    const int cap = 1024;
-    return g < cap ? (g > 0 ? g : 1) : cap;
+    // One 16-wave workgroup per CU (256 CUs): the per-workgroup prologue
+    // (activation quantisation) is paid once per CU.  Small launches use
+    // fewer workgroups so every group of KS waves still gets a unit.
+    const int ks = gemv_ks((p.K / 256 + 7) / 8);
+    const int groups_per_wg = (GEMV_THREADS / 64) / ks;
+    const int g = (p.total_units + groups_per_wg - 1) / groups_per_wg;
+    return g < 1 ? 1 : (g > 256 ? 256 : g);
 }
 
-void launch_gemv(const GemvParams& p, int role, int grid, hipStream_t s) {
+void launch_gemv(const GemvParams& p_in, int role, int grid, hipStream_t s) {
+    GemvParams p = p_in;
     if (p.K % 256 != 0) throw Error("gemv: K must be a multiple of 256");
+    static const int dbg = getenv("MI_GEMV_DEBUG") ? atoi(getenv("MI_GEMV_DEBUG")) : 0;
+    if (dbg & 1) p.pro = -1;
+    if (dbg & 2) grid = 1024;
+    if (grid <= 0) grid = gemv_default_grid(p);
+    p.upw = 0;
     const size_t smem = gemv_smem_bytes(p);
     if (smem > 160 * 1024) throw Error("gemv: activation too large for LDS");
-    if (grid <= 0) grid = gemv_default_grid(p);
-    hipLaunchKernelGGL(gemv_fn(role), dim3(grid), dim3(GEMV_THREADS), smem, s, p);
+    const int type = p.seg[0].A.type;
+    for (int i = 0; i < p.nseg; ++i)
+        if (p.seg[i].A.type != type || (p.seg[i].pair == PAIR_AB && p.seg[i].B.type != type))
+            throw Error("gemv: all matrices of one launch must share a quant type");
+    const int ns = (p.K / 256 + 7) / 8;
+    GemvFn fn = gemv_fn(role, type, ns, p.nslots);
+    if (!fn) throw Error("gemv: unsupported quant type or K (K <= 16384)");
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(GEMV_THREADS), smem, s, p);
     MI_HIP(hipGetLastError());
 }
 
