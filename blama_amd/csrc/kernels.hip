@@ -528,19 +528,11 @@ __device__ __forceinline__ void gemv_epilogue(const GemvParams& P, const UnitRef
 }
 
 // ---------------------------------------------------------------------------
-// The fused GEMV kernel, specialised per quant type T and per NS = superblock
-// steps per row (ceil(K/256/8)).  A wave computes one unit (two rows) at a
-// time: all NS x 2 row loads are issued together (8 lanes per superblock, one
-// aligned 16-byte load of the main plane per lane), the next unit's loads are
-// issued as soon as the current unit's dot products are done, so they overlap
-// the DPP reduction and the epilogue.  The first unit's loads are issued
-// before the prologue.  Latency is hidden by occupancy (256-thread workgroups,
-// 2 rows x NS loads in flight per wave).
-// ---------------------------------------------------------------------------
-// ---------------------------------------------------------------------------
 // The fused GEMV kernel, specialised per quant type T, per NSW (superblock
-// steps streamed by one wave per row, <= 2) and per KS (waves of the workgroup
-// that split one row pair's K range; KS*NSW*8 >= K/256).
+// steps streamed by one wave per row, <= 2), per KS (waves of the workgroup
+// that split one row pair's K range; KS*NSW*8 >= K/256) and per PF (units a
+// wave keeps in flight: 1 = load, consume; 2 = the next unit's loads are issued
+// before the current unit is consumed, so the wave's weight stream never stops).
 //
 // * Each wave keeps, for its NSW steps, the activation slice its lanes need in
 //   registers (it is the same for every row), loaded from LDS once after the
@@ -548,10 +540,14 @@ __device__ __forceinline__ void gemv_epilogue(const GemvParams& P, const UnitRef
 // * A unit (row pair) is loaded with all NSW x 2 row loads issued together
 //   (8 lanes per superblock, aligned 16-B loads), the first unit before the
 //   prologue so the weight stream starts while activations are quantised.
+// * Groups of KS waves sweep the units grid-strided, so neighbouring groups (in
+//   and across workgroups) stream neighbouring rows at the same time.
 // * KS > 1: the KS waves' partial sums are combined through LDS in fixed
 //   order (deterministic) by the group's first wave, which runs the epilogue.
+//   The barrier is a bare s_barrier for the in-flight prefetch (no LDS-DMA is
+//   pending, so __syncthreads emits no vmcnt drain).
 // ---------------------------------------------------------------------------
-template <int T, int NSW, int KS, int DUAL, int ROLE>
+template <int T, int NSW, int KS, int DUAL, int ROLE, int PF>
 __global__ __launch_bounds__(GEMV_THREADS) void gemv_t(const GemvParams P) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     using K = Kq<T>;
@@ -579,51 +575,49 @@ __global__ __launch_bounds__(GEMV_THREADS) void gemv_t(const GemvParams P) {
         w0 = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(P.selw[0])));
         w1 = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(P.selw[1])));
     }
-    // groups of KS waves sweep the units grid-strided, so neighbouring groups
-    // (in and across workgroups) stream neighbouring rows at the same time
     const int G_total = gridDim.x * NGRP;
     const int g0 = blockIdx.x * NGRP + grp;
     const int n_iter = (P.total_units + G_total - 1) / G_total;   // same for every wave of the workgroup
 
-    typename K::Ld la[NSW], lb[NSW];
-    float rva = 0.0f, rvb = 0.0f;
-    const uint8_t* ra_p[4];
-    const uint8_t* rb_p[4];
-    auto rows_of = [&](const UnitRef& c) {
+    struct Buf {
+        typename K::Ld a[NSW], b[NSW];
+        float ra, rb;   // residual values of the unit's rows (loaded with its weights: no late drain)
+    };
+    // Issue every load of unit u (u < total_units, wave-uniform).  Lanes past
+    // the row's last superblock read into the next row / the plane's
+    // 8-superblock tail padding; their products are masked.
+    auto issue = [&](Buf& B, int u) {
+        const UnitRef c = unit_ref(P, u);
         const GemvSeg& S = P.seg[c.si];
         const QMat& MB = S.pair == PAIR_ADJ ? S.A : S.B;
         const long long ea = S.expA == 0 ? e0 : S.expA == 1 ? e1 : 0;
         const long long eb = S.expB == 0 ? e0 : S.expB == 1 ? e1 : 0;
         const long long rb = c.hasB ? c.rb : c.ra;   // odd tail: re-read row A, result unused
+        const uint8_t* ra_p[4];
+        const uint8_t* rb_p[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             ra_p[i] = S.A.p[i] + ea * S.A.expert_stride[i] + c.ra * nb * PlaneBytes<T>::b[i];
             rb_p[i] = MB.p[i] + eb * MB.expert_stride[i] + rb * nb * PlaneBytes<T>::b[i];
         }
-        // residual of this unit's rows, issued with its weights (no late drain)
-        if (S.resid) {
-            const long long ia = S.pair == PAIR_ADJ ? c.ra : c.lu;
-            rva = S.resid[ia];
-            rvb = S.resid[S.pair == PAIR_ADJ ? rb : ia];
-        }
-    };
-    // Lanes past the row's last superblock read into the next row / the
-    // plane's 8-superblock tail padding; their products are masked.
-    auto load_unit = [&]() {
 #pragma unroll
         for (int t = 0; t < NSW; ++t) {
             const int s = wk + t * KS;
             if (s < ns) {
-                la[t] = K::load(ra_p, s * 8 + sbl, j);
-                lb[t] = K::load(rb_p, s * 8 + sbl, j);
+                B.a[t] = K::load(ra_p, s * 8 + sbl, j);
+                B.b[t] = K::load(rb_p, s * 8 + sbl, j);
             }
         }
+        B.ra = B.rb = 0.0f;
+        if (S.resid) {
+            const long long ia = S.pair == PAIR_ADJ ? c.ra : c.lu;
+            B.ra = S.resid[ia];
+            B.rb = S.resid[S.pair == PAIR_ADJ ? rb : ia];
+        }
     };
-    int u = g0;
-    if (u < P.total_units) {
-        rows_of(unit_ref(P, u));
-        load_unit();
-    }
+
+    Buf b0, b1;
+    if (g0 < P.total_units) issue(b0, g0);
     gemv_prologue(P, smem, SP, pos);
     __syncthreads();
     const float* rope = reinterpret_cast<const float*>(smem + SP.rope_off);
@@ -644,13 +638,9 @@ __global__ __launch_bounds__(GEMV_THREADS) void gemv_t(const GemvParams P) {
         }
     }
 
-    for (int it = 0; it < n_iter; ++it, u += G_total) {
+    // Consume unit u from B (u may be past the end: then only the barrier runs).
+    auto consume = [&](const Buf& B, int u) {
         const bool valid = u < P.total_units;
-        const UnitRef c = unit_ref(P, valid ? u : 0);
-        if (it > 0 && valid) {
-            rows_of(c);
-            load_unit();
-        }
         float accA = 0.0f, accB = 0.0f;
         if (valid) {
 #pragma unroll
@@ -658,8 +648,8 @@ __global__ __launch_bounds__(GEMV_THREADS) void gemv_t(const GemvParams P) {
                 const int s = wk + t * KS;
                 if (s < ns) {
                     const bool lv = s * 8 + sbl < nb;
-                    const float pa = K::dot(la[t], arA[t], j);
-                    const float pb = K::dot(lb[t], DUAL ? arB[t] : arA[t], j);
+                    const float pa = K::dot(B.a[t], arA[t], j);
+                    const float pb = K::dot(B.b[t], DUAL ? arB[t] : arA[t], j);
                     accA += lv ? pa : 0.0f;
                     accB += lv ? pb : 0.0f;
                 }
@@ -668,7 +658,7 @@ __global__ __launch_bounds__(GEMV_THREADS) void gemv_t(const GemvParams P) {
         float yA = wave_sum63(accA);
         float yB = wave_sum63(accB);
         if (KS == 1) {
-            if (valid && lane == 63) gemv_epilogue(P, c, rope, rva, rvb, w0, w1, pos, cell, yA, yB);
+            if (valid && lane == 63) gemv_epilogue(P, unit_ref(P, u), rope, B.ra, B.rb, w0, w1, pos, cell, yA, yB);
         } else {
             if (lane == 63) {
                 red[(grp * KS + wk) * 2] = yA;
@@ -683,9 +673,26 @@ __global__ __launch_bounds__(GEMV_THREADS) void gemv_t(const GemvParams P) {
                     yA += red[(grp * KS + k) * 2];
                     yB += red[(grp * KS + k) * 2 + 1];
                 }
-                gemv_epilogue(P, c, rope, rva, rvb, w0, w1, pos, cell, yA, yB);
+                gemv_epilogue(P, unit_ref(P, u), rope, B.ra, B.rb, w0, w1, pos, cell, yA, yB);
             }
             __syncthreads();
+        }
+    };
+
+    int u = g0;
+    if constexpr (PF == 1) {
+        for (int it = 0; it < n_iter; ++it, u += G_total) {
+            if (it > 0 && u < P.total_units) issue(b0, u);
+            consume(b0, u);
+        }
+    } else {
+        for (int it = 0; it < n_iter; it += 2, u += 2 * G_total) {
+            if (u + G_total < P.total_units) issue(b1, u + G_total);
+            consume(b0, u);
+            if (it + 1 < n_iter) {
+                if (u + 2 * G_total < P.total_units) issue(b0, u + 2 * G_total);
+                consume(b1, u + G_total);
+            }
         }
     }
 }
@@ -697,17 +704,21 @@ typedef void (*GemvFn)(const GemvParams);
 // ns = superblock steps per row (ceil(K/256/8)) -> KS waves share a row pair,
 // each wave streams NSW <= 2 steps.  ROLE: 0 generic, 1 FFN gate/up, 2 dual
 // activation slot (MoE down).
-template <int T, int ROLE>
-static GemvFn gemv_fn_ns(int ns) {
+template <int T, int ROLE, int PF>
+static GemvFn gemv_fn_ns_pf(int ns) {
     constexpr int DUAL = ROLE == 2 ? 1 : 0;
     switch (ns) {
-    case 1: return gemv_t<T, 1, 1, DUAL, ROLE>;
-    case 2: return gemv_t<T, 2, 1, DUAL, ROLE>;
-    case 3: case 4: return gemv_t<T, 2, 2, DUAL, ROLE>;
-    case 5: case 6: case 7: case 8: return gemv_t<T, 2, 4, DUAL, ROLE>;
+    case 1: return gemv_t<T, 1, 1, DUAL, ROLE, PF>;
+    case 2: return gemv_t<T, 2, 1, DUAL, ROLE, PF>;
+    case 3: case 4: return gemv_t<T, 2, 2, DUAL, ROLE, PF>;
+    case 5: case 6: case 7: case 8: return gemv_t<T, 2, 4, DUAL, ROLE, PF>;
     default: return nullptr;
     }
 }
+// PF = 2 (double-buffered units) measured slower on Q4_K/Q8_0 and spills on
+// Q5_K/Q6_K at 4 waves/SIMD: PF = 1 is the shipped variant.
+template <int T, int ROLE>
+static GemvFn gemv_fn_ns(int ns) { return gemv_fn_ns_pf<T, ROLE, 1>(ns); }
 
 int gemv_ks(int ns) { return ns <= 2 ? 1 : ns <= 4 ? 2 : 4; }
 

@@ -16,6 +16,8 @@ from __future__ import annotations
 import hashlib
 from dataclasses import dataclass, replace
 
+import os
+
 import numpy as np
 
 from . import gguf
@@ -192,10 +194,176 @@ def fill_quant(view: np.ndarray, t: int, rng, std: float = 0.03):
             raise NotImplementedError(t)
 
 
+# ---------------------------------------------------------------------------
+# Float -> block quantisers (simple, valid blocks; not ggml's rmse-searching
+# quantize_row_*_ref -- any valid block is valid model data).  X: (n, 256)
+# float32 superblocks (Q8_0: (n, 32) blocks); returns (n, block_bytes) uint8.
+# ---------------------------------------------------------------------------
+def _f16(a):
+    return np.asarray(a, np.float32).astype(np.float16)
+
+
+def quantize_q8_0_rows(X):
+    X = X.reshape(-1, 32)
+    amax = np.abs(X).max(1)
+    d16 = _f16(amax / 127.0)
+    d = d16.astype(np.float32)
+    q = np.clip(np.rint(np.divide(X, d[:, None], out=np.zeros_like(X), where=d[:, None] > 0)), -127, 127)
+    out = np.empty((X.shape[0], 34), np.uint8)
+    out[:, 0:2] = d16.view(np.uint8).reshape(-1, 2)
+    out[:, 2:] = q.astype(np.int8).view(np.uint8)
+    return out
+
+
+def quantize_q6_K_rows(X):
+    X = X.reshape(-1, 256)
+    n = X.shape[0]
+    s = np.abs(X.reshape(n, 16, 16)).max(2) / 31.0            # per-16 scale
+    d16 = _f16(s.max(1) / 127.0)
+    d = d16.astype(np.float32)
+    sc = np.clip(np.rint(np.divide(s, d[:, None], out=np.zeros_like(s), where=d[:, None] > 0)), 1, 127)
+    eff = np.repeat(d[:, None] * sc, 16, axis=1)
+    q = np.clip(np.rint(np.divide(X, eff, out=np.zeros_like(X), where=eff > 0)), -32, 31).astype(np.int32) + 32
+    ql = np.zeros((n, 128), np.uint8)
+    qh = np.zeros((n, 64), np.uint8)
+    for h in range(2):
+        e = q[:, 128 * h:128 * h + 128]
+        a, b, c, dd = e[:, 0:32], e[:, 32:64], e[:, 64:96], e[:, 96:128]
+        ql[:, 64 * h:64 * h + 32] = (a & 0xF) | ((c & 0xF) << 4)
+        ql[:, 64 * h + 32:64 * h + 64] = (b & 0xF) | ((dd & 0xF) << 4)
+        qh[:, 32 * h:32 * h + 32] = (a >> 4) | ((b >> 4) << 2) | ((c >> 4) << 4) | ((dd >> 4) << 6)
+    out = np.empty((n, 210), np.uint8)
+    out[:, 0:128] = ql
+    out[:, 128:192] = qh
+    out[:, 192:208] = sc.astype(np.int8).view(np.uint8)
+    out[:, 208:210] = d16.view(np.uint8).reshape(n, 2)
+    return out
+
+
+def quantize_q45_K_rows(X, q5: bool):
+    X = X.reshape(-1, 256)
+    n = X.shape[0]
+    qmax = 31 if q5 else 15
+    sub = X.reshape(n, 8, 32)
+    mn = np.maximum(0.0, -sub.min(2))
+    s = (sub.max(2) + mn) / qmax
+    d16 = _f16(s.max(1) / 63.0)
+    m16 = _f16(mn.max(1) / 63.0)
+    d, dm = d16.astype(np.float32), m16.astype(np.float32)
+    sc = np.clip(np.rint(np.divide(s, d[:, None], out=np.zeros_like(s), where=d[:, None] > 0)), 0, 63)
+    m = np.clip(np.rint(np.divide(mn, dm[:, None], out=np.zeros_like(mn), where=dm[:, None] > 0)), 0, 63)
+    eff = d[:, None] * sc
+    off = dm[:, None] * m
+    q = np.clip(np.rint(np.divide(sub + off[:, :, None], eff[:, :, None], out=np.zeros_like(sub),
+                                  where=eff[:, :, None] > 0)), 0, qmax).astype(np.int32).reshape(n, 256)
+    qs = np.zeros((n, 128), np.uint8)
+    qh = np.zeros((n, 32), np.uint8)
+    for j in range(4):
+        lo, hi = q[:, 64 * j:64 * j + 32], q[:, 64 * j + 32:64 * j + 64]
+        qs[:, 32 * j:32 * j + 32] = (lo & 0xF) | ((hi & 0xF) << 4)
+        if q5:
+            qh |= (((lo >> 4) & 1) << (2 * j)).astype(np.uint8)
+            qh |= (((hi >> 4) & 1) << (2 * j + 1)).astype(np.uint8)
+    out = np.empty((n, 176 if q5 else 144), np.uint8)
+    out[:, 0:2] = d16.view(np.uint8).reshape(n, 2)
+    out[:, 2:4] = m16.view(np.uint8).reshape(n, 2)
+    out[:, 4:16] = _pack_scales_k4(sc.astype(np.uint8), m.astype(np.uint8))
+    if q5:
+        out[:, 16:48] = qh
+        out[:, 48:176] = qs
+    else:
+        out[:, 16:144] = qs
+    return out
+
+
+def quantize_rows(X, t: int) -> np.ndarray:
+    X = np.ascontiguousarray(X, np.float32)
+    if t == Q8_0:
+        return quantize_q8_0_rows(X).reshape(-1)
+    if t == Q6_K:
+        return quantize_q6_K_rows(X).reshape(-1)
+    if t in (Q4_K, Q5_K):
+        return quantize_q45_K_rows(X, t == Q5_K).reshape(-1)
+    if t == F32:
+        return X.reshape(-1).view(np.uint8)
+    if t == F16:
+        return X.reshape(-1).astype(np.float16).view(np.uint8)
+    raise NotImplementedError(t)
+
+
+# ---------------------------------------------------------------------------
+# Token structure.  A random-weight 32-layer quantised network is chaotic: two
+# correct CPU implementations that differ only in fp32 summation order end up
+# with LogitComparer similarity ~0.7 (measured; DESIGN.md "synthetic weights"),
+# because its top-10 logits are tightly packed in a flat distribution.  Trained
+# LMs have peaked next-token distributions.  The synthetic model gets one:
+# a per-token direction B[t] (unit-variance Gaussian) is the embedding of t,
+# and output row t' carries sum_k alpha/sqrt(k) * B[t'-k], k = 1..10, on top of
+# the random part -- after token t the model "prefers" t+1 > t+2 > ... > t+10.
+# ---------------------------------------------------------------------------
+_BCHUNK = 1024
+
+
+def _token_dirs(seed: int, lo: int, hi: int, V: int, d: int) -> np.ndarray:
+    """B[t mod V] for t in [lo, hi) (lo may be negative); float32 (hi-lo, d)."""
+    out = np.empty((hi - lo, d), np.float32)
+    t = lo
+    while t < hi:
+        tm = t % V
+        c = tm // _BCHUNK
+        base = c * _BCHUNK
+        rows = min(_BCHUNK, V - base)
+        blk = _rng(seed, f"tokdir:{c}").standard_normal((rows, d), dtype=np.float32)
+        take = min(hi - t, base + rows - tm)
+        out[t - lo:t - lo + take] = blk[tm - base:tm - base + take]
+        t += take
+    return out
+
+
+def _init_params(cfg):
+    env = dict(kv.split("=") for kv in os.environ.get("BLAMA_SYNTH_INIT", "").split(",") if kv)
+    p = {"base": 0.03, "qk": 0.01, "resid": 0.03 / np.sqrt(2.0 * cfg.n_layer), "embd": 8.0,
+         "alpha": 0.01, "nsucc": 10}
+    for k, v in env.items():
+        p[k] = float(v)
+    return p
+
+
+def _fill_structured(cfg, seed, name, t, view, P):
+    V, d = cfg.n_vocab, cfg.n_embd
+    be, bb = gguf.GGML_BLOCK[t]
+    row_b = d // be * bb
+    rows = view.reshape(V, row_b)
+    rng = _rng(seed, name)
+    CH = 2048
+    ns = int(P["nsucc"])
+    for a in range(0, V, CH):
+        b = min(V, a + CH)
+        if name == "token_embd.weight":
+            X = _token_dirs(seed, a, b, V, d) * np.float32(P["embd"])
+        else:
+            X = rng.standard_normal((b - a, d), dtype=np.float32) * np.float32(P["base"])
+            Bw = _token_dirs(seed, a - ns, b, V, d)
+            for k in range(1, ns + 1):
+                X += np.float32(P["alpha"] / np.sqrt(k)) * Bw[ns - k:ns - k + (b - a)]
+        rows[a:b] = quantize_rows(X, t).reshape(b - a, row_b)
+
+
 def vocab_tokens(n_vocab: int):
     toks = ["<unk>", "<s>", "</s>"] + ["<0x%02X>" % i for i in range(256)]
     toks += ["▁t%d" % i for i in range(n_vocab - len(toks))]
     return toks[:n_vocab]
+
+
+RESIDUAL_OUT = ("attn_output.weight", "ffn_down.weight", "ffn_down_exps.weight")
+
+
+def _init_std(P, name):
+    if name.endswith(("attn_q.weight", "attn_k.weight")):
+        return P["qk"]      # attention scores O(1): softmax not saturated
+    if name.endswith(RESIDUAL_OUT):
+        return P["resid"]   # residual branches scaled by 1/sqrt(2 n_layer)
+    return P["base"]
 
 
 def build_gguf(cfg: LlamaConfig, seed: int = 0) -> np.ndarray:
@@ -234,15 +402,20 @@ def build_gguf(cfg: LlamaConfig, seed: int = 0) -> np.ndarray:
     for name in types:
         w.add_tensor(name, types[name], shapes[name])
 
+    P = _init_params(cfg)
+
     def fill(name, t, shape, view):
         rng = _rng(seed, name)
+        if name in ("token_embd.weight", "output.weight"):
+            _fill_structured(cfg, seed, name, t, view, P)
+            return
         if name.endswith("norm.weight"):
             v = view.view(np.float32)
             v[:] = rng.uniform(0.8, 1.2, v.size).astype(np.float32)
         elif name.endswith("ffn_gate_inp.weight"):
             fill_quant(view, t, rng, std=0.05)
         else:
-            fill_quant(view, t, rng)
+            fill_quant(view, t, rng, std=_init_std(P, name))
 
     return w.to_bytes(fill=fill)
 

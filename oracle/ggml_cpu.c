@@ -125,6 +125,21 @@ static void scale_min_k4(int j, const uint8_t* q, uint8_t* d, uint8_t* m) {
     else { *d = (q[j + 4] & 0xF) | ((q[j - 4] >> 6) << 4); *m = (q[j + 4] >> 4) | ((q[j - 0] >> 6) << 4); }
 }
 
+/* ORC_ALT=1: sum the 8 float lanes in reverse order -- a second, equally valid
+ * fp32 accumulation order, used to measure how far two correct implementations
+ * drift apart on a given model (test infrastructure only) */
+static int alt_order(void) {
+    static int on = -1;
+    if (on < 0) on = getenv("ORC_ALT") != NULL;
+    return on;
+}
+static float lane_sum(const float* sums, float init) {
+    float s = init;
+    if (alt_order()) for (int l = 7; l >= 0; --l) s += sums[l];
+    else for (int l = 0; l < 8; ++l) s += sums[l];
+    return s;
+}
+
 /* ggml_vec_dot_q4_K_q8_K / q5_K (generic): exact integer sums per sub-block,
  * per-lane float accumulators sums[8], mins subtracted per superblock. */
 static float dot_q45_K(const uint8_t* row, int K, const q8k_t* y, int q5) {
@@ -159,8 +174,7 @@ static float dot_q45_K(const uint8_t* row, int K, const q8k_t* y, int q5) {
         const float dmin = h2f(dmh) * y[i].d;
         sumf -= dmin * sumi;
     }
-    for (int l = 0; l < 8; ++l) sumf += sums[l];
-    return sumf;
+    return lane_sum(sums, sumf);
 }
 
 static float dot_q6_K(const uint8_t* row, int K, const q8k_t* y) {   /* ggml_vec_dot_q6_K_q8_K */
@@ -188,9 +202,7 @@ static float dot_q6_K(const uint8_t* row, int K, const q8k_t* y) {   /* ggml_vec
         const float d = h2f(dh) * y[i].d;
         for (int l = 0; l < 8; ++l) sums[l] += d * aux32[l];
     }
-    float sumf = 0;
-    for (int l = 0; l < 8; ++l) sumf += sums[l];
-    return sumf;
+    return lane_sum(sums, 0.0f);
 }
 
 static float dot_q8_0(const uint8_t* row, int K, const q80_t* y) {   /* ggml_vec_dot_q8_0_q8_0 */
@@ -391,9 +403,14 @@ static void rope(float* x, int n_heads, int hd, int n_rot, int pos, float base) 
     const float ts = powf(base, -2.0f / n_rot);
     float cs[512], sn[512];
     float theta = (float)pos;
+    static int use_f = -1;   /* ORC_ROPE_F=1: libm cosf/sinf (sensitivity experiments) */
+    if (use_f < 0) use_f = getenv("ORC_ROPE_F") != NULL;
     for (int i = 0; i < n_rot / 2; ++i) {
-        cs[i] = cosf(theta);
-        sn[i] = sinf(theta);
+        /* correctly rounded cos/sin of the float angle (ggml calls libm cosf/sinf,
+           which are within 1 ulp of this; the numpy oracle and the HIP engine
+           use the correctly rounded value) */
+        cs[i] = use_f ? cosf(theta) : (float)cos((double)theta);
+        sn[i] = use_f ? sinf(theta) : (float)sin((double)theta);
         theta *= ts;
     }
     for (int h = 0; h < n_heads; ++h)
@@ -412,6 +429,16 @@ static void mm(const orc_tensor* t, int expert, const float* x, float* y) {
 }
 
 static float silu(float v) { return v / (1.0f + expf(-v)); }
+
+/* ORC_TRACE=1: print a checksum of every intermediate vector (debugging aid) */
+static void trace(const char* what, int l, const float* v, int n) {
+    static int on = -1;
+    if (on < 0) on = getenv("ORC_TRACE") != NULL;
+    if (!on) return;
+    double s = 0.0, a = 0.0;
+    for (int i = 0; i < n; ++i) { s += v[i]; a += fabs(v[i]); }
+    fprintf(stderr, "L%d %-5s sum=%.9g abs=%.9g\n", l, what, s, a);
+}
 
 /* one llama_decode of `token` at position max(cell_pos)+1; logits -> out[n_vocab] */
 int orc_decode(orc_model* m, int token, float* out) {
@@ -442,6 +469,7 @@ int orc_decode(orc_model* m, int token, float* out) {
         mm(&L[L_V], 0, cur, v);
         rope(q, hp->n_head, hd, hp->n_rot, pos, hp->rope_base);
         rope(k, hp->n_head_kv, hd, hp->n_rot, pos, hp->rope_base);
+        trace("q", l, q, d); trace("k", l, k, kvd); trace("v", l, v, kvd);
         uint16_t* kc = m->kc + ((size_t)l * m->n_ctx) * kvd;
         uint16_t* vc = m->vc + ((size_t)l * m->n_ctx) * kvd;
         for (int i = 0; i < kvd; ++i) { kc[(size_t)cell * kvd + i] = f2h(k[i]); vc[(size_t)cell * kvd + i] = f2h(v[i]); }
@@ -473,14 +501,20 @@ int orc_decode(orc_model* m, int token, float* out) {
             }
             free(s);
         }
+        trace("att", l, att, d);
         mm(&L[L_O], 0, att, dn);
         for (int i = 0; i < d; ++i) x[i] = dn[i] + x[i];
+        trace("x1", l, x, d);
         rms_norm_mul(x, (const float*)L[L_FFN_NORM].data, d, hp->eps, cur);
+        trace("cur", l, cur, d);
         if (hp->n_expert == 0) {
             mm(&L[L_GATE], 0, cur, g);
             mm(&L[L_UP], 0, cur, u);
+            trace("g", l, g, ff); trace("u", l, u, ff);
             for (int i = 0; i < ff; ++i) g[i] = silu(g[i]) * u[i];
+            trace("h", l, g, ff);
             mm(&L[L_DOWN], 0, g, dn);
+            trace("dn", l, dn, d);
             for (int i = 0; i < d; ++i) x[i] = dn[i] + x[i];
         } else {
             float lg[64], pr[64];
