@@ -549,7 +549,9 @@ void Ctx::enqueue_step(bool with_logits) {
             }
             params_finish(p);
             if (l == prof_layer) seg = 1;
-            if (on()) launch_gemv(p, ROLE_FFN_UP, 0, stream);
+            // the profiled launch (segment 1, always eager) carries the event pair
+            const bool timed = l == prof_layer && seg_filter == 1;
+            if (on()) launch_gemv(p, ROLE_FFN_UP, 0, stream, timed ? prof_ev[0] : nullptr, timed ? prof_ev[1] : nullptr);
             if (l == prof_layer) seg = 2;
         }
         // ---- FFN down + residual ----
@@ -648,16 +650,23 @@ int Ctx::decode(const int32_t* tokens, int n) {
         hp[3] = 0;
         MI_HIP(hipMemcpyAsync(tokpos, hp, 4 * sizeof(int), hipMemcpyHostToDevice, stream));
         if (last && prof_layer >= 0 && prof_layer < m->hp.n_layer) {
-            for (int k = 0; k < 3; ++k)
-                if (!g_seg[k]) g_seg[k] = build_graph(true, k);
             for (int k = 0; k < 2; ++k)
                 if (!prof_ev[k]) MI_HIP(hipEventCreate(&prof_ev[k]));
-            MI_HIP(hipGraphLaunch(g_seg[0], stream));
-            MI_HIP(hipEventRecord(prof_ev[0], stream));
-            MI_HIP(hipGraphLaunch(g_seg[1], stream));
-            MI_HIP(hipEventRecord(prof_ev[1], stream));
-            MI_HIP(hipGraphLaunch(g_seg[2], stream));
+            // graph up to the profiled launch, the launch itself eagerly with
+            // hipExtLaunchKernel start/stop events, graph for the rest
+            for (int k = 0; k < 3; ++k) {
+                if (use_graphs && k != 1) {
+                    if (!g_seg[k]) g_seg[k] = build_graph(true, k);
+                    MI_HIP(hipGraphLaunch(g_seg[k], stream));
+                } else {
+                    seg_filter = k;
+                    enqueue_step(true);
+                    seg_filter = -1;
+                }
+            }
             prof_pending = true;
+        } else if (!use_graphs) {
+            enqueue_step(last);
         } else {
             hipGraphExec_t& g = last ? g_full : g_nolog;
             if (!g) g = build_graph(last, -1);

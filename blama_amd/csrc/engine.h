@@ -1,6 +1,7 @@
 // Engine internals: GGUF parsing, the device-resident model and the decode
 // context.  The public surface is the C ABI in include/mi_engine.h.
 #pragma once
+#include <cstdlib>
 #include "common.h"
 #include "kernels.h"
 #include "mi_engine.h"
@@ -133,6 +134,9 @@ struct Ctx {
     // decode graphs (with / without the output head).  With profiling on, the
     // full step is split in three graphs around one layer's FFN gate/up GEMV so
     // that plain HIP events on the stream bracket exactly that launch.
+    // MI_NO_GRAPH=1: launch every kernel eagerly (profilers that cannot trace
+    // graph-launched kernels); the default replays one hipGraph per step
+    bool use_graphs = getenv("MI_NO_GRAPH") == nullptr;
     hipGraphExec_t g_full = nullptr, g_nolog = nullptr;
     hipGraphExec_t g_seg[3] = {nullptr, nullptr, nullptr};
     int prof_layer = -1;

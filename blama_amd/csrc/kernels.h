@@ -62,7 +62,10 @@ struct GemvParams {
 
 enum GemvRole { ROLE_QKV = 0, ROLE_WO = 1, ROLE_FFN_UP = 2, ROLE_FFN_DOWN = 3, ROLE_OUTPUT = 4, ROLE_GENERIC = 5 };
 size_t gemv_smem_bytes(const GemvParams& p);
-void launch_gemv(const GemvParams& p, int role, int grid, hipStream_t s);
+// ev_start/ev_stop (optional): recorded at the kernel's own start and end
+// (hipExtLaunchKernel) -- the bench's in-kernel timing of one launch.
+void launch_gemv(const GemvParams& p, int role, int grid, hipStream_t s,
+                 hipEvent_t ev_start = nullptr, hipEvent_t ev_stop = nullptr);
 void init_kernel_attributes();   // once per device, before any graph capture
 int gemv_default_grid(const GemvParams& p);
 

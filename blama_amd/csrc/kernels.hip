@@ -11,6 +11,7 @@
 // where ggml rounds twice.
 #include "kernels.h"
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <cstdlib>
 
 namespace mi {
@@ -768,7 +769,8 @@ int gemv_default_grid(const GemvParams& p) {
     return g < 1 ? 1 : (g > 256 ? 256 : g);
 }
 
-void launch_gemv(const GemvParams& p_in, int role, int grid, hipStream_t s) {
+void launch_gemv(const GemvParams& p_in, int role, int grid, hipStream_t s, hipEvent_t ev_start,
+                 hipEvent_t ev_stop) {
     GemvParams p = p_in;
     if (p.K % 256 != 0) throw Error("gemv: K must be a multiple of 256");
     static const int dbg = getenv("MI_GEMV_DEBUG") ? atoi(getenv("MI_GEMV_DEBUG")) : 0;
@@ -785,7 +787,10 @@ void launch_gemv(const GemvParams& p_in, int role, int grid, hipStream_t s) {
     const int ns = (p.K / 256 + 7) / 8;
     GemvFn fn = gemv_fn(role, type, ns, p.nslots);
     if (!fn) throw Error("gemv: unsupported quant type or K (K <= 16384)");
-    hipLaunchKernelGGL(fn, dim3(grid), dim3(GEMV_THREADS), smem, s, p);
+    if (ev_start || ev_stop)
+        hipExtLaunchKernelGGL(fn, dim3(grid), dim3(GEMV_THREADS), smem, s, ev_start, ev_stop, 0, p);
+    else
+        hipLaunchKernelGGL(fn, dim3(grid), dim3(GEMV_THREADS), smem, s, p);
     MI_HIP(hipGetLastError());
 }
 

@@ -138,6 +138,10 @@ class Model:
         self.n_embd = L.mi_model_n_embd(h)
         self.n_layer = L.mi_model_n_layer(h)
         self.n_ctx_train = L.mi_model_n_ctx_train(h)
+        self.n_head = L.mi_model_n_head(h)
+        self.n_head_kv = L.mi_model_n_head_kv(h)
+        self.n_ff = L.mi_model_n_ff(h)
+        self.n_expert = L.mi_model_n_expert(h)
 
     def close(self):
         if getattr(self, "h", None):
@@ -154,7 +158,9 @@ class Model:
     def weight_bytes(self) -> int:
         return lib().mi_model_weight_bytes(self.h)
 
+    @property
     def arena(self):
+        """(device pointer, bytes) of the weight arena (replica broadcast)."""
         p = C.c_void_p()
         n = C.c_size_t()
         _check(lib().mi_model_arena(self.h, C.byref(p), C.byref(n)), "arena")

@@ -366,8 +366,9 @@ def _init_std(P, name):
     return P["base"]
 
 
-def build_gguf(cfg: LlamaConfig, seed: int = 0) -> np.ndarray:
-    """The whole synthetic GGUF file as one uint8 array."""
+def build_gguf(cfg: LlamaConfig, seed: int = 0, header_only: bool = False) -> np.ndarray:
+    """The whole synthetic GGUF file as one uint8 array (header_only: just the
+    metadata + tensor table, enough for a vocab-only or no_upload replica load)."""
     w = gguf.GGUFWriter()
     arch = "llama"
     w.add_str("general.architecture", arch)
@@ -402,6 +403,8 @@ def build_gguf(cfg: LlamaConfig, seed: int = 0) -> np.ndarray:
     for name in types:
         w.add_tensor(name, types[name], shapes[name])
 
+    if header_only:
+        return np.frombuffer(w.header_bytes()[0], np.uint8).copy()
     P = _init_params(cfg)
 
     def fill(name, t, shape, view):
