@@ -222,6 +222,18 @@ int32_t mi_prof_read(mi_ctx* c, float* us, int32_t n) {
     MI_TRY(-1)
 }
 int64_t mi_prof_ffn_bytes(const mi_ctx* c) { return c ? c->impl->ffn_bytes() : -1; }
+int32_t mi_debug_stamps(mi_ctx* c, uint64_t* out, int32_t n_launch) {
+    try {
+        if (!c || !out) throw Error("null argument");
+        mi::Ctx* x = c->impl.get();
+        if (!x->stamps) return 0;
+        n_launch = std::min(n_launch, (int32_t)mi::Ctx::kStampLaunches);
+        x->sync();
+        MI_HIP(hipMemcpy(out, x->stamps, (size_t)n_launch * mi::Ctx::kStampWgs * 8 * 8, hipMemcpyDeviceToHost));
+        return n_launch;
+    }
+    MI_TRY(-1)
+}
 
 }  // extern "C"
 
@@ -389,9 +401,10 @@ int32_t mi_op_topk(int32_t device, const float* logits, int32_t n, int32_t k, in
     try {
         if (k < 0 || k > TOPK_MAX) throw Error("k must be in [0, 64]");
         MI_HIP(hipSetDevice(device));
-        DevBuf dl(n * sizeof(float)), dc(TOPK_GROUPS * TOPK_MAX * 8), di(TOPK_MAX * 4), dv(TOPK_MAX * 4);
+        if (n < 1) throw Error("n must be positive");
+        DevBuf dl(n * sizeof(float)), dc((size_t)topk_blocks(n) * TOPK_MAX * 8), di(TOPK_MAX * 4), dv(TOPK_MAX * 4);
         MI_HIP(hipMemcpy(dl.p, logits, n * sizeof(float), hipMemcpyHostToDevice));
-        TopkParams tp{dl.as<float>(), n, dc.as<unsigned long long>(), di.as<int>(), dv.as<float>()};
+        TopkParams tp{dl.as<float>(), n, dc.as<unsigned long long>(), di.as<int>(), dv.as<float>(), nullptr, nullptr};
         launch_topk(tp, nullptr);
         MI_HIP(hipDeviceSynchronize());
         std::vector<int> hi(TOPK_MAX);

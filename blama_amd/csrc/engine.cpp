@@ -365,7 +365,6 @@ Ctx::Ctx(Model* model, uint32_t nctx, uint32_t nbatch, uint32_t nubatch) : m(mod
     n_ubatch = nubatch ? std::min(nubatch, n_batch) : n_batch;
     const HParams& hp = m->hp;
     kv_dim = hp.n_head_kv * hp.head_dim;
-    if ((size_t)n_ctx * 4 + 8192 > 160 * 1024) throw Error("n_ctx too large for this build's attention kernel");
     if (device < (int)g_attr_done.size() && !g_attr_done[device]) {
         init_kernel_attributes();
         g_attr_done[device] = 1;
@@ -387,7 +386,14 @@ Ctx::Ctx(Model* model, uint32_t nctx, uint32_t nbatch, uint32_t nubatch) : m(mod
     MI_HIP(hipMalloc(&h, big * sizeof(float)));
     MI_HIP(hipMalloc(&h2, big * sizeof(float)));
     MI_HIP(hipMalloc(&logits, (size_t)hp.n_vocab * sizeof(float)));
-    MI_HIP(hipMalloc(&cand, TOPK_GROUPS * TOPK_MAX * sizeof(unsigned long long)));
+    MI_HIP(hipMalloc(&cand, (size_t)topk_blocks(hp.n_vocab) * TOPK_MAX * sizeof(unsigned long long)));
+    MI_HIP(hipMalloc(&part_o, (size_t)ATTN_SMAX * hp.n_head * hp.head_dim * sizeof(float)));
+#ifdef MI_STAMPS
+    MI_HIP(hipMalloc(&stamps, (size_t)kStampLaunches * kStampWgs * 8 * sizeof(unsigned long long)));
+    MI_HIP(hipMemset(stamps, 0, (size_t)kStampLaunches * kStampWgs * 8 * sizeof(unsigned long long)));
+#endif
+    MI_HIP(hipMalloc(&attn_smax, (size_t)ATTN_SMAX * hp.n_head * sizeof(float)));
+    MI_HIP(hipMalloc(&attn_scores, (size_t)hp.n_head * n_ctx * sizeof(float)));
     MI_HIP(hipMalloc(&topk_ids, TOPK_MAX * sizeof(int)));
     MI_HIP(hipMalloc(&topk_vals, TOPK_MAX * sizeof(float)));
     MI_HIP(hipMalloc(&sel, 64 * sizeof(int)));
@@ -399,8 +405,11 @@ Ctx::Ctx(Model* model, uint32_t nctx, uint32_t nbatch, uint32_t nubatch) : m(mod
     MI_HIP(hipMalloc(&cell_delta, n_ctx * sizeof(int)));
     MI_HIP(hipMalloc(&move_src, n_ctx * sizeof(int)));
     MI_HIP(hipHostMalloc(&h_tokpos, kTokRing * 4 * sizeof(int)));
-    MI_HIP(hipHostMalloc(&h_topk_ids, TOPK_MAX * sizeof(int)));
-    MI_HIP(hipHostMalloc(&h_topk_vals, TOPK_MAX * sizeof(float)));
+    // the top-k kernel writes its result straight into these (coherent, mapped)
+    MI_HIP(hipHostMalloc(&h_topk_ids, TOPK_MAX * sizeof(int), hipHostMallocMapped | hipHostMallocCoherent));
+    MI_HIP(hipHostMalloc(&h_topk_vals, TOPK_MAX * sizeof(float), hipHostMallocMapped | hipHostMallocCoherent));
+    MI_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&d_h_topk_ids), h_topk_ids, 0));
+    MI_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&d_h_topk_vals), h_topk_vals, 0));
     MI_HIP(hipHostMalloc(&h_logits, (size_t)hp.n_vocab * sizeof(float)));
     MI_HIP(hipHostMalloc(&h_gather, 4096 * sizeof(float)));
     h_cell_pos.assign(n_ctx, 0);
@@ -414,7 +423,7 @@ Ctx::~Ctx() {
     for (void* p : {(void*)kcache, (void*)vcache, (void*)kv_scratch, (void*)cell_pos, (void*)tokpos, (void*)x,
                     (void*)q, (void*)attn, (void*)h, (void*)h2, (void*)logits, (void*)cand, (void*)topk_ids,
                     (void*)topk_vals, (void*)sel, (void*)selw, (void*)gather_ids, (void*)gather_out,
-                    (void*)cell_delta, (void*)move_src})
+                    (void*)cell_delta, (void*)move_src, (void*)part_o, (void*)attn_smax, (void*)attn_scores, (void*)stamps})
         if (p) hipFree(p);
     for (void* p : {(void*)h_tokpos, (void*)h_topk_ids, (void*)h_topk_vals, (void*)h_logits, (void*)h_gather})
         if (p) hipHostFree(p);
@@ -446,6 +455,11 @@ long long Ctx::ffn_bytes() const {
 void Ctx::enqueue_step(bool with_logits) {
     const HParams& hp = m->hp;
     int seg = 0;
+    int n_launch = 0;   // diagnostic stamps (MI_STAMPS builds only): one slab per launch
+    auto stamp = [&]() -> unsigned long long* {
+        if (!stamps || n_launch >= kStampLaunches) return nullptr;
+        return stamps + (size_t)(n_launch++) * kStampWgs * 8;
+    };
     auto on = [&]() { return seg_filter < 0 || seg_filter == seg; };
     EmbedParams ep{m->tok_embd, tokpos, x, hp.n_embd};
     if (on()) launch_embed(ep, stream);
@@ -461,8 +475,6 @@ void Ctx::enqueue_step(bool with_logits) {
         base.cell_pos = cell_pos;
         base.head_dim = hp.head_dim;
         base.kv_dim = kv_dim;
-        base.sel = sel;
-        base.selw = selw;
         base.eps = hp.eps;
         base.nslots = 1;
         // ---- Q/K/V projections + RoPE + KV append ----
@@ -498,19 +510,23 @@ void Ctx::enqueue_step(bool with_logits) {
                     done[i] = true;
                 }
                 params_finish(pl);
+                pl.stamps = stamp();
                 if (on()) launch_gemv(pl, ROLE_QKV, 0, stream);
             }
         }
         // ---- attention ----
         {
-            AttnParams a{q, kl, vl, tokpos, cell_pos, attn, hp.n_head, hp.n_head_kv, hp.head_dim, kv_dim,
-                         (int)n_ctx, kq_scale};
+            AttnParams a{q, kl, vl, tokpos, cell_pos, attn_scores, attn_smax, part_o, hp.n_head, hp.n_head_kv, hp.head_dim,
+                         kv_dim, (int)n_ctx, kq_scale};
+            a.stamps = stamp();
+            a.stamps2 = stamp();
             if (on()) launch_attn(a, stream);
         }
         // ---- output projection + residual ----
         {
             GemvParams p = base;
-            p.pro = PRO_PLAIN;
+            p.pro = PRO_ATTN;   // slot 0 = the attention partials combined
+            p.attn = AttnPartials{part_o, hp.n_head, hp.head_dim};
             p.x[0] = attn;
             p.K = hp.n_embd;
             p.nseg = 1;
@@ -522,6 +538,7 @@ void Ctx::enqueue_step(bool with_logits) {
             p.seg[0].out = x;
             p.seg[0].resid = x;
             params_finish(p);
+            p.stamps = stamp();
             if (on()) launch_gemv(p, ROLE_WO, 0, stream);
         }
         if (hp.n_expert > 0) {
@@ -536,6 +553,10 @@ void Ctx::enqueue_step(bool with_logits) {
             p.norm_w = L.ffn_norm;
             p.K = hp.n_embd;
             const int nsl = hp.n_expert > 0 ? 2 : 1;
+            if (hp.n_expert > 0) {   // expert ids/weights: only MoE launches wait for them
+                p.sel = sel;
+                p.selw = selw;
+            }
             p.nseg = nsl;
             for (int k = 0; k < nsl; ++k) {
                 seg_init(p.seg[k]);
@@ -548,6 +569,7 @@ void Ctx::enqueue_step(bool with_logits) {
                 if (hp.n_expert > 0) p.seg[k].expA = p.seg[k].expB = k;
             }
             params_finish(p);
+            p.stamps = stamp();
             if (l == prof_layer) seg = 1;
             // the profiled launch (segment 1, always eager) carries the event pair
             const bool timed = l == prof_layer && seg_filter == 1;
@@ -563,6 +585,8 @@ void Ctx::enqueue_step(bool with_logits) {
             p.nseg = 1;
             seg_init(p.seg[0]);
             if (hp.n_expert > 0) {
+                p.sel = sel;
+                p.selw = selw;
                 p.nslots = 2;
                 p.x[1] = h2;
                 p.seg[0].A = L.down;
@@ -583,6 +607,7 @@ void Ctx::enqueue_step(bool with_logits) {
             p.seg[0].out = x;
             p.seg[0].resid = x;
             params_finish(p);
+            p.stamps = stamp();
             if (on()) launch_gemv(p, ROLE_FFN_DOWN, 0, stream);
         }
     }
@@ -604,11 +629,10 @@ void Ctx::enqueue_step(bool with_logits) {
         p.seg[0].units = (m->output.rows + 1) / 2;
         p.seg[0].out = logits;
         params_finish(p);
+        p.stamps = stamp();
         launch_gemv(p, ROLE_OUTPUT, 0, stream);
-        TopkParams tp{logits, hp.n_vocab, cand, topk_ids, topk_vals};
+        TopkParams tp{logits, hp.n_vocab, cand, topk_ids, topk_vals, d_h_topk_ids, d_h_topk_vals};
         launch_topk(tp, stream);
-        MI_HIP(hipMemcpyAsync(h_topk_ids, topk_ids, TOPK_MAX * sizeof(int), hipMemcpyDeviceToHost, stream));
-        MI_HIP(hipMemcpyAsync(h_topk_vals, topk_vals, TOPK_MAX * sizeof(float), hipMemcpyDeviceToHost, stream));
     }
 }
 
@@ -865,10 +889,8 @@ size_t Ctx::state_set(const uint8_t* src, size_t size) {
     logits_valid = hd.logits_valid != 0;
     if (logits_valid) {
         MI_HIP(hipMemcpy(logits, s, (size_t)hp.n_vocab * sizeof(float), hipMemcpyHostToDevice));
-        TopkParams tp{logits, hp.n_vocab, cand, topk_ids, topk_vals};
+        TopkParams tp{logits, hp.n_vocab, cand, topk_ids, topk_vals, d_h_topk_ids, d_h_topk_vals};
         launch_topk(tp, stream);
-        MI_HIP(hipMemcpyAsync(h_topk_ids, topk_ids, TOPK_MAX * sizeof(int), hipMemcpyDeviceToHost, stream));
-        MI_HIP(hipMemcpyAsync(h_topk_vals, topk_vals, TOPK_MAX * sizeof(float), hipMemcpyDeviceToHost, stream));
         sync();
     }
     return need;

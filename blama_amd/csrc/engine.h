@@ -116,6 +116,13 @@ struct Ctx {
     float* gather_out = nullptr;
     int* cell_delta = nullptr;
     int* move_src = nullptr;
+    float* part_o = nullptr;            // split-K attention partials [ATTN_SMAX][n_head][hd]
+    float* attn_smax = nullptr;         // [ATTN_SMAX][n_head] split maxima
+    float* attn_scores = nullptr;       // [n_head][n_ctx] scaled KQ
+    // diagnostics (MI_STAMPS builds only): s_memrealtime stamps of every
+    // workgroup of every launch of the last enqueued step [launch][wg][8]
+    static constexpr int kStampLaunches = 320, kStampWgs = 512;
+    unsigned long long* stamps = nullptr;
 
     // pinned host buffers
     int* h_tokpos = nullptr;            // ring of kTokRing x 4 ints
@@ -123,6 +130,8 @@ struct Ctx {
     float* h_topk_vals = nullptr;
     float* h_logits = nullptr;
     float* h_gather = nullptr;
+    int* d_h_topk_ids = nullptr;        // device views of h_topk_ids / h_topk_vals
+    float* d_h_topk_vals = nullptr;
     long long tok_slot = 0;
 
     // host mirror of the cache cells

@@ -19,7 +19,11 @@ enum Epi {
     EPI_SWIGLU = 5,   // out[u] = silu(yA) * yB            (LLM_FFN_SILU + LLM_FFN_PAR)
     EPI_MOE_DOWN = 6, // out[u] = (yA*wA + yB*wB) + resid[u] (build_moe_ffn aggregation)
 };
-enum Pro { PRO_PLAIN = 0, PRO_RMSNORM = 1 };
+enum Pro {
+    PRO_PLAIN = 0,    // slot 0 = x[0]
+    PRO_RMSNORM = 1,  // slot 0 = rms_norm(x[0]) * norm_w
+    PRO_ATTN = 2,     // slot 0 = the split-K attention partials combined (attn_split_kernel)
+};
 
 struct GemvSeg {
     QMat A, B;
@@ -32,7 +36,24 @@ struct GemvSeg {
 };
 
 constexpr int GEMV_MAX_SEG = 4;
-constexpr int GEMV_THREADS = 1024;   // one workgroup per CU (16 waves)
+
+// Attention split over cells: split s of q head h holds the partial sum
+// O_s = sum_{c in s} f16(p_c) v_c with the head's exact softmax weights p (the
+// global max and sum are known before the weights are rounded; see
+// attn_pv_kernel).  A split covers `chunk` cells, chunk = max(64,
+// ceil(ncell / ATTN_SMAX) rounded up to 64), so there are at most ATTN_SMAX
+// splits.
+constexpr int ATTN_SMAX = 16;
+__host__ __device__ inline void attn_split(int ncell, int& chunk, int& nsplit) {
+    int c = (ncell + ATTN_SMAX - 1) / ATTN_SMAX;
+    c = (c + 63) & ~63;
+    chunk = c < 64 ? 64 : c;
+    nsplit = (ncell + chunk - 1) / chunk;
+}
+struct AttnPartials {
+    const float* o;            // [ATTN_SMAX][n_head][head_dim]
+    int n_head, head_dim;
+};
 
 struct GemvParams {
     GemvSeg seg[GEMV_MAX_SEG];
@@ -57,7 +78,10 @@ struct GemvParams {
     // MoE routing results
     const int* sel;
     const float* selw;
-    int upw;                  // units per workgroup (set by launch_gemv)
+    AttnPartials attn;        // PRO_ATTN input
+    int wg_units;             // max units one workgroup owns (set by launch_gemv; LDS residual staging)
+    int grid;                 // == gridDim.x (set by launch_gemv)
+    unsigned long long* stamps;   // diagnostics: per-workgroup s_memrealtime stamps [grid][8] (nullptr: off)
 };
 
 enum GemvRole { ROLE_QKV = 0, ROLE_WO = 1, ROLE_FFN_UP = 2, ROLE_FFN_DOWN = 3, ROLE_OUTPUT = 4, ROLE_GENERIC = 5 };
@@ -78,28 +102,41 @@ struct EmbedParams {
 };
 void launch_embed(const EmbedParams& p, hipStream_t s);
 
-// ---- attention over the f16 cache (KQ -> soft_max -> KQV, ggml CPU semantics) ----
+// ---- attention over the f16 cache: KQ -> soft_max -> KQV, split over cells ----
+// Two launches, grid (n_head_kv, ATTN_SMAX) each; the WO GEMV's PRO_ATTN
+// prologue adds the splits' partials.
 struct AttnParams {
     const float* q;            // [n_head*hd] (roped)
     const __half* kcache;      // [n_ctx][kv_dim]
     const __half* vcache;
     const int* tokpos;
     const int* cell_pos;
-    float* out;                // [n_head*hd]
+    float* scores;             // [n_head][n_ctx] scaled KQ (scratch)
+    float* smax;               // [ATTN_SMAX][n_head] split maxima (scratch)
+    float* part_o;             // [ATTN_SMAX][n_head][hd]
     int n_head, n_head_kv, head_dim, kv_dim, n_ctx;
     float scale;
+    unsigned long long* stamps;    // diagnostics (MI_STAMPS builds): scores / pv launches
+    unsigned long long* stamps2;
 };
 void launch_attn(const AttnParams& p, hipStream_t s);
+// Combine the partials into out[n_head*hd] (tests / the eager debug path).
+void launch_attn_combine(const AttnPartials& a, const int* tokpos, float* out, hipStream_t s);
 
 // ---- top-k over logits (sorted by logit desc, id asc), k <= 64 ----
+// Stage 1: every 1024-logit block -> its sorted top 64 (wave bitonic sorts +
+// merges); stage 2: one workgroup merges the block lists.
 constexpr int TOPK_MAX = 64;
-constexpr int TOPK_GROUPS = 64;
+constexpr int TOPK_BLOCK = 1024;
+inline int topk_blocks(int n) { return (n + TOPK_BLOCK - 1) / TOPK_BLOCK; }
 struct TopkParams {
     const float* logits;
     int n;
-    unsigned long long* cand;  // [TOPK_GROUPS*TOPK_MAX]
-    int* ids;                  // [TOPK_MAX]
+    unsigned long long* cand;  // [topk_blocks(n) * TOPK_MAX]
+    int* ids;                  // [TOPK_MAX] (device)
     float* vals;
+    int* h_ids;                // optional: also written straight to mapped host memory
+    float* h_vals;
 };
 void launch_topk(const TopkParams& p, hipStream_t s);
 

@@ -18,9 +18,22 @@ namespace mi {
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+// Pointers the GEMV reads from its LDS copy of the parameter block are generic
+// to the compiler, which would emit flat_* accesses: those retire out of order
+// (every wait becomes vmcnt(0) & lgkmcnt(0)) and would serialise the weight
+// ring.  Every global access of the GEMV goes through gptr() -> global_*.
+template <typename T>
+__device__ __forceinline__ const __attribute__((address_space(1))) T* gptr(const T* p) {
+    return (const __attribute__((address_space(1))) T*)(p);
+}
+template <typename T>
+__device__ __forceinline__ __attribute__((address_space(1))) T* gptr_w(T* p) {
+    return (__attribute__((address_space(1))) T*)(p);
+}
 __device__ __forceinline__ u32x4 ldg16(const uint8_t* p) {
-    return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    return __builtin_nontemporal_load(gptr(reinterpret_cast<const u32x4*>(p)));
 }
 __device__ __forceinline__ float h2f(uint32_t bits) {
     return __half2float(__ushort_as_half(static_cast<unsigned short>(bits & 0xFFFFu)));
@@ -51,6 +64,35 @@ __device__ __forceinline__ double wave_sum_d(double v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
 }
+// DPP forms of the prologue reductions (__shfl_xor lowers to ds_bpermute: an
+// LDS round trip per step, ~16 dependent ones per Q8_K block).
+template <int CTRL, int RMASK>
+__device__ __forceinline__ int dpp_i(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, CTRL, RMASK, 0xf, false);
+}
+template <int CTRL, int RMASK>
+__device__ __forceinline__ double dpp_d(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = dpp_i<CTRL, RMASK>((int)b), hi = dpp_i<CTRL, RMASK>((int)(b >> 32));
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+// Full-wave double sum, total in lane 63 (same scan as wave_sum63).
+__device__ __forceinline__ double wave_sum63_d(double v) {
+    v += dpp_d<0x111, 0xf>(v);
+    v += dpp_d<0x112, 0xf>(v);
+    v += dpp_d<0x114, 0xf>(v);
+    v += dpp_d<0x118, 0xf>(v);
+    v += dpp_d<0x142, 0xa>(v);
+    v += dpp_d<0x143, 0xc>(v);
+    return v;
+}
+// Full-wave max of non-negative floats (0 is the identity), broadcast to all lanes.
+__device__ __forceinline__ float wave_max_pos(float v) {
+#define MX(ctrl, rm) v = fmaxf(v, __int_as_float(dpp_i<ctrl, rm>(__float_as_int(v))))
+    MX(0x111, 0xf); MX(0x112, 0xf); MX(0x114, 0xf); MX(0x118, 0xf); MX(0x142, 0xa); MX(0x143, 0xc);
+#undef MX
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
@@ -65,37 +107,31 @@ __device__ __forceinline__ float wave_max(float v) {
 // ties), iscale = -127/max, q = min(127, nearest_int(iscale*x)), d = 1/iscale.
 __device__ __forceinline__ void quant_q8k_block(const float v[4], int lane, int8_t* q8, int* bsum,
                                                 float* dk) {
-    float ab = fabsf(v[0]);
-    int ib = 0;
-#pragma unroll
-    for (int e = 1; e < 4; ++e) if (fabsf(v[e]) > ab) { ab = fabsf(v[e]); ib = e; }
-    unsigned hi = __float_as_uint(ab);
-    unsigned lo = 0xFFFFFFFFu - (unsigned)(lane * 4 + ib);
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        unsigned ohi = __shfl_xor(hi, o, 64), olo = __shfl_xor(lo, o, 64);
-        if (ohi > hi || (ohi == hi && olo > lo)) { hi = ohi; lo = olo; }
-    }
-    const int idx = (int)(0xFFFFFFFFu - lo);
-    const float mine = (idx & 3) == 0 ? v[0] : (idx & 3) == 1 ? v[1] : (idx & 3) == 2 ? v[2] : v[3];
-    const float mx = __shfl(mine, idx >> 2, 64);
+    const float a0 = fabsf(v[0]), a1 = fabsf(v[1]), a2 = fabsf(v[2]), a3 = fabsf(v[3]);
+    const float amax = wave_max_pos(fmaxf(fmaxf(a0, a1), fmaxf(a2, a3)));
     int q[4];
     float d;
-    if (__uint_as_float(hi) == 0.0f) {
+    if (amax == 0.0f) {
         q[0] = q[1] = q[2] = q[3] = 0;
         d = 0.0f;
     } else {
+        // the signed value at the FIRST index whose |x| is the maximum
+        const int e = a0 == amax ? 0 : a1 == amax ? 1 : a2 == amax ? 2 : a3 == amax ? 3 : 4;
+        const float mine = e == 0 ? v[0] : e == 1 ? v[1] : e == 2 ? v[2] : v[3];
+        const unsigned long long m = __ballot(e < 4);
+        const int src = __builtin_ctzll(m);
+        const float mx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mine), src));
         const float iscale = -127.0f / mx;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) q[e] = min(127, (int)rintf(iscale * v[e]));
+        for (int k = 0; k < 4; ++k) q[k] = min(127, (int)rintf(iscale * v[k]));
         d = 1.0f / iscale;
     }
     const int packed = (q[0] & 0xFF) | ((q[1] & 0xFF) << 8) | ((q[2] & 0xFF) << 16) | ((q[3] & 0xFF) << 24);
     reinterpret_cast<int*>(q8)[lane] = packed;
-    int s = q[0] + q[1] + q[2] + q[3];
-    s += __shfl_xor(s, 1, 64);
-    s += __shfl_xor(s, 2, 64);
-    if ((lane & 3) == 0) bsum[lane >> 2] = s;
+    int sm = q[0] + q[1] + q[2] + q[3];
+    sm += dpp_i<0xB1, 0xf>(sm);   // quad_perm [1,0,3,2]
+    sm += dpp_i<0x4E, 0xf>(sm);   // quad_perm [2,3,0,1] -> every lane of the quad has its 16-sum
+    if ((lane & 3) == 0) bsum[lane >> 2] = sm;
     if (lane == 0) *dk = d;
 }
 
@@ -103,9 +139,9 @@ __device__ __forceinline__ void quant_q8k_block(const float v[4], int lane, int8
 // q = round-to-nearest-even(x*id).  8 lanes per 32-block.
 __device__ __forceinline__ void quant_q80_block(const float v[4], int lane, int8_t* q8, float* d0) {
     float am = fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3])));
-    am = fmaxf(am, __shfl_xor(am, 1, 64));
-    am = fmaxf(am, __shfl_xor(am, 2, 64));
-    am = fmaxf(am, __shfl_xor(am, 4, 64));
+    am = fmaxf(am, __int_as_float(dpp_i<0xB1, 0xf>(__float_as_int(am))));
+    am = fmaxf(am, __int_as_float(dpp_i<0x4E, 0xf>(__float_as_int(am))));
+    am = fmaxf(am, __int_as_float(dpp_i<0x141, 0xf>(__float_as_int(am))));   // row_half_mirror
     const float d = am / 127.0f;
     const float id = am != 0.0f ? 127.0f / am : 0.0f;
     int q[4];
@@ -265,10 +301,10 @@ template <> struct Kq<T_Q6_K> {
         l.qh = ldg16(rp[1] + sb * 64 + 32 * h + 16 * half);
         // scales 8h..8h+7: is_lo = 8h+2hq+half lives in word 0, is_hi = is_lo+4 in word 1
         typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-        const u32x2 sc = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(rp[2] + sb * 16) + h);
+        const u32x2 sc = __builtin_nontemporal_load(gptr(reinterpret_cast<const u32x2*>(rp[2] + sb * 16) + h));
         l.sc0 = sc.x;
         l.sc1 = sc.y;
-        l.d = __builtin_nontemporal_load(reinterpret_cast<const unsigned short*>(rp[3] + sb * 2));
+        l.d = __builtin_nontemporal_load(gptr(reinterpret_cast<const unsigned short*>(rp[3] + sb * 2)));
         return l;
     }
     struct AR { i32x4 alo, ahi; int bs_lo, bs_hi; float dx; };
@@ -319,7 +355,7 @@ template <> struct Kq<T_Q8_0> {
         Ld l;
         l.q0 = ldg16(rp[0] + sb * 256 + j * 32);
         l.q1 = ldg16(rp[0] + sb * 256 + j * 32 + 16);
-        l.d = __builtin_nontemporal_load(reinterpret_cast<const unsigned short*>(rp[1] + sb * 16 + j * 2));
+        l.d = __builtin_nontemporal_load(gptr(reinterpret_cast<const unsigned short*>(rp[1] + sb * 16 + j * 2)));
         return l;
     }
     struct AR { i32x4 a0, a1; float d0; };
@@ -350,107 +386,42 @@ template <> struct Kq<T_Q8_0> {
 // ---------------------------------------------------------------------------
 // The fused GEMV kernel, specialised per quant type T.
 //
-// Work decomposition: a unit is a pair of output rows (see kernels.h); a wave
-// owns units gw, gw + W, gw + 2W, ... (W = waves in the grid).  A unit is
-// streamed in "chunks" (one step of SPS superblocks for both rows), and the
-// wave keeps D chunks in flight in a register ring: while chunk q is being
-// reduced against the LDS activations, chunks q+1 .. q+D-1 are loading.  The
-// first D-1 chunks are issued before the prologue so that the weight stream
-// starts while the activations are normalised and quantised.
+// Work decomposition: a unit is a PAIR of output rows (see kernels.h).  Every
+// wave owns a contiguous range of units (so a workgroup owns a contiguous
+// range, whose residual rows it stages in LDS).  A unit's two rows are
+// streamed in "chunks": one aligned 16-byte load per lane of the main quant
+// plane plus its side planes, 8 superblocks per row and chunk (8 lanes per
+// superblock).  The wave walks its (unit, chunk) items through a D-deep
+// register ring: while item i is reduced against the LDS activations, items
+// i+1 .. i+D-1 are in flight -- across unit boundaries, so a wave's weight
+// stream never stops until its range is done.  The first D-1 items are issued
+// before the prologue, so the stream starts while the activations are
+// normalised and quantised.  Loads past the end of the range repeat the last
+// item's addresses (cache hits) so that every ring step issues the same loads
+// and the compiler's vmcnt bookkeeping stays exact (no wait-for-all).
 // ---------------------------------------------------------------------------
 struct SmemPlan {
     ActLayout L;
-    int act_bytes, rope_off, red_off, resid_off, total;
+    int act_bytes, rope_off, resid_off, attn_off, red_off, total;
 };
-// resid_rows: residual values staged per workgroup (its contiguous unit range)
-__host__ __device__ inline SmemPlan smem_plan(int K, int nslots, int need_q8k, int need_q80, int n_rot,
-                                              int resid_rows) {
-    SmemPlan P;
-    P.L = act_layout(K, need_q8k, need_q80);
-    P.act_bytes = P.L.slot_bytes * nslots;
-    P.rope_off = P.act_bytes;
-    P.red_off = P.rope_off + ((n_rot / 2) * 8 + 15) / 16 * 16;
-    P.resid_off = P.red_off + 32 * 8;
-    P.total = P.resid_off + ((resid_rows * 4 + 15) / 16) * 16;
-    return P;
+__host__ __device__ inline SmemPlan smem_plan(const GemvParams& p) {
+    SmemPlan S;
+    S.L = act_layout(p.K, p.need_q8k, p.need_q80);
+    S.act_bytes = S.L.slot_bytes * p.nslots;
+    S.rope_off = S.act_bytes;
+    S.resid_off = S.rope_off + ((p.n_rot / 2) * 8 + 15) / 16 * 16;
+    S.attn_off = S.resid_off + ((p.wg_units * 2 * 4 + 15) / 16) * 16;
+    S.red_off = S.attn_off;
+    S.total = S.red_off + 32 * 8;
+    return S;
 }
-__host__ __device__ inline int resid_rows_per_wg(const GemvParams&) { return 0; }
 
 __device__ __forceinline__ float silu_f(float x) { return x / (1.0f + expf(-x)); }
 
-// Prologue (every workgroup, redundantly): RMSNorm of slot 0 if requested,
-// quantisation of the activation slots into LDS, residual rows of this
-// workgroup's unit range, and the RoPE cos/sin table of this token.
-__device__ __forceinline__ void gemv_prologue(const GemvParams& P, char* smem, const SmemPlan& SP, int pos) {
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int nwaves = blockDim.x >> 6;
-    const ActLayout& L = SP.L;
-    double* red = reinterpret_cast<double*>(smem + SP.red_off);
-    if (P.pro < 0) return;   // debug: skip the prologue (timing ablation only)
-    float scale = 1.0f;
-    if (P.pro == PRO_RMSNORM) {
-        // ggml_compute_forward_rms_norm_f32: sum of float squares in double
-        double s = 0.0;
-        const float4* x4 = reinterpret_cast<const float4*>(P.x[0]);
-        for (int i = tid; i < P.K / 4; i += blockDim.x) {
-            const float4 v = x4[i];
-            s += (double)(v.x * v.x);
-            s += (double)(v.y * v.y);
-            s += (double)(v.z * v.z);
-            s += (double)(v.w * v.w);
-        }
-        s = wave_sum_d(s);
-        if (lane == 0) red[wave] = s;
-        __syncthreads();
-        double tot = 0.0;
-        for (int w = 0; w < nwaves; ++w) tot += red[w];
-        const float mean = (float)(tot / (double)P.K);
-        scale = 1.0f / sqrtf(mean + P.eps);
-    }
-    for (int slot = 0; slot < P.nslots; ++slot) {
-        char* base = smem + slot * L.slot_bytes;
-        const float4* x4 = reinterpret_cast<const float4*>(P.x[slot]);
-        const bool norm = slot == 0 && P.pro == PRO_RMSNORM;
-        for (int blk = wave; blk < L.nb; blk += nwaves) {
-            const float4 xv = x4[blk * 64 + lane];
-            float v[4] = {xv.x, xv.y, xv.z, xv.w};
-            if (norm) {
-                const float4 w = reinterpret_cast<const float4*>(P.norm_w)[blk * 64 + lane];
-                v[0] = (v[0] * scale) * w.x;   // ggml_vec_scale_f32 then ggml_mul
-                v[1] = (v[1] * scale) * w.y;
-                v[2] = (v[2] * scale) * w.z;
-                v[3] = (v[3] * scale) * w.w;
-            }
-            if (P.need_q8k)
-                quant_q8k_block(v, lane, reinterpret_cast<int8_t*>(base + L.q8k) + blk * 256,
-                                reinterpret_cast<int*>(base + L.bsum) + blk * 16,
-                                reinterpret_cast<float*>(base + L.dk) + blk);
-            if (P.need_q80)
-                quant_q80_block(v, lane, reinterpret_cast<int8_t*>(base + L.q80) + blk * 256,
-                                reinterpret_cast<float*>(base + L.d0) + blk * 8);
-        }
-    }
-    // residual rows of this workgroup (in-place residual add: x[r] = W.a + x[r])
-    const int rrows = resid_rows_per_wg(P);
-    if (rrows > 0) {
-        float* rs = reinterpret_cast<float*>(smem + SP.resid_off);
-        const long long r0 = (long long)blockIdx.x * rrows;
-        const long long nrow = P.seg[0].pair == PAIR_ADJ ? P.seg[0].A.rows : P.seg[0].units;
-        for (int i = tid; i < rrows; i += blockDim.x) rs[i] = (r0 + i < nrow) ? P.seg[0].resid[r0 + i] : 0.0f;
-    }
-    // RoPE cache for this token's position (ggml_rope_cache_init, ext_factor 0, mscale 1)
-    if (P.n_rot > 0 && wave == 0) {
-        float* rope = reinterpret_cast<float*>(smem + SP.rope_off);
-        for (int i = lane; i < P.n_rot / 2; i += 64) {
-            float theta = (float)pos;
-            for (int k = 0; k < i; ++k) theta = theta * P.theta_scale;
-            const float ff = P.freq_factors ? P.freq_factors[i] : 1.0f;
-            const float th = P.freq_scale * (theta / ff);
-            rope[2 * i] = cosf(th);
-            rope[2 * i + 1] = sinf(th);
-        }
-    }
+__device__ __forceinline__ void unit_range(int total, int W, int gw, int& u0, int& u1) {
+    // total * (gw + 1) < 2^32 (total <= 65536 units, W <= 4096 waves)
+    u0 = (int)(((unsigned)total * (unsigned)gw) / (unsigned)W);
+    u1 = (int)(((unsigned)total * (unsigned)(gw + 1)) / (unsigned)W);
 }
 
 struct UnitRef {
@@ -477,20 +448,250 @@ __device__ __forceinline__ UnitRef unit_ref(const GemvParams& P, int u) {
     return c;
 }
 
-// rva / rvb: residual values of rows A / B (loaded with the unit's weights)
+// Scalar (constant-cache) load of a wave-uniform int written by an earlier
+// kernel or copy: it retires on lgkmcnt, so waiting for it never waits for the
+// weight stream (vector loads retire in order on vmcnt).
+__device__ __forceinline__ int sload_i32(const int* p) {
+    return *(const __attribute__((address_space(4))) int*)(p);
+}
+
+// Prologue, split in two so that its global loads are issued BEFORE the first
+// weight load: vmcnt retires in issue order, so the prologue's waits then never
+// wait for the weight stream.
+//  pro_load:   this wave's activation blocks (blocks wave, wave+NW, ...; and the
+//              RMSNorm weights) into registers, the residual values of this
+//              workgroup's units.
+//  pro_finish: (after the weight prefill) RMSNorm / attention combine, Q8_K or
+//              Q8_0 quantisation into LDS, residuals and the RoPE table to LDS.
+constexpr int PRO_MAXB = 8;   // activation blocks one wave keeps in registers
+struct ProRegs {
+    f32x4 x[PRO_MAXB], w[PRO_MAXB];
+    i32x4 tp;                  // {token, pos, cell, -} (a vector load: a scalar one would
+                              // hold every LDS wait behind it, lgkmcnt counts both)
+    float ra, rb;
+    float ff[2];              // RoPE freq factors of pairs lane, lane+64 (wave 0)
+    int nsplit;               // PRO_ATTN: attention splits to add
+    bool regs;                // blocks held in registers (else re-read in pro_finish)
+    bool attn_regs;           // PRO_ATTN: the splits' partials held in x[] (block i, split s: x[i*nsplit+s])
+};
+
+__device__ __forceinline__ void pro_load(const GemvParams& P, ProRegs& R, int nb, int nw, int wave, int lane,
+                                         int wg_u0, int wg_u1) {
+    const int tid = threadIdx.x;
+    R.tp = P.tokpos ? *gptr(reinterpret_cast<const i32x4*>(P.tokpos)) : i32x4{0, 0, 0, 0};
+    R.regs = P.pro != PRO_ATTN && P.nslots == 1 && nb <= PRO_MAXB * nw;
+    // Every load the prologue waits for must be issued before the weight prefill:
+    // loads retire in issue order, so a later one would wait for the prefill too.
+    R.ff[0] = R.ff[1] = 1.0f;
+    if (P.freq_factors && wave == 0) {
+        if (lane < P.n_rot / 2) R.ff[0] = gptr(P.freq_factors)[lane];
+        if (lane + 64 < P.n_rot / 2) R.ff[1] = gptr(P.freq_factors)[lane + 64];
+    }
+    R.nsplit = 0;
+    R.attn_regs = false;
+    if (P.pro == PRO_ATTN) {
+        // the split count depends on the cell count: one scalar round trip (the
+        // only one before the weight prefill is issued)
+        int chunk;
+        attn_split(sload_i32(P.tokpos + 2) + 1, chunk, R.nsplit);
+        const int bpw = (nb + nw - 1) / nw;   // blocks per wave
+        R.attn_regs = P.nslots == 1 && R.nsplit * bpw <= PRO_MAXB;
+        if (R.attn_regs) {
+            const AttnPartials& A = P.attn;
+#pragma unroll
+            for (int k = 0; k < PRO_MAXB; ++k) {   // register k = (block i, split s)
+                const int i = k / R.nsplit, s = k % R.nsplit;
+                const int blk = wave + i * nw;
+                if (i < bpw && blk < nb)
+                    R.x[k] = *gptr(reinterpret_cast<const f32x4*>(
+                        A.o + (long long)s * A.n_head * A.head_dim + blk * 256 + lane * 4));
+            }
+        }
+    }
+    if (R.regs) {
+        const auto x4 = gptr(reinterpret_cast<const f32x4*>(P.x[0]));
+        const auto w4 = gptr(reinterpret_cast<const f32x4*>(P.norm_w));
+#pragma unroll
+        for (int i = 0; i < PRO_MAXB; ++i) {
+            const int blk = wave + i * nw;
+            if (blk < nb) {
+                R.x[i] = x4[blk * 64 + lane];
+                if (P.pro == PRO_RMSNORM) R.w[i] = w4[blk * 64 + lane];
+            }
+        }
+    }
+    // residual values of this workgroup's units (the in-place residual add reads
+    // them before any wave of the workgroup overwrites its rows).  Residual
+    // launches have one segment (launch_gemv checks), so the lookup is scalar.
+    R.ra = R.rb = 0.0f;
+    const GemvSeg& S0 = P.seg[0];
+    if (S0.resid && tid < wg_u1 - wg_u0) {
+        const long long lu = wg_u0 + tid;
+        if (S0.pair == PAIR_ADJ) {
+            const long long ra = 2 * lu;
+            R.ra = gptr(S0.resid)[ra];
+            R.rb = gptr(S0.resid)[ra + 1 < S0.A.rows ? ra + 1 : ra];
+        } else {
+            R.ra = gptr(S0.resid)[lu];
+            R.rb = gptr(S0.resid)[lu];   // a second load, not a copy (a copy waits for the load)
+        }
+    }
+}
+
+__device__ __forceinline__ void pro_finish(const GemvParams& P, const ProRegs& R, char* smem, const SmemPlan& SP,
+                                           int pos, int ncell, int wg_u0, int wg_u1) {
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int nwaves = blockDim.x >> 6;
+    const ActLayout& L = SP.L;
+    double* red = reinterpret_cast<double*>(smem + SP.red_off);
+    {
+        float* rs = reinterpret_cast<float*>(smem + SP.resid_off);
+        if (tid < wg_u1 - wg_u0) {
+            rs[2 * tid] = R.ra;
+            rs[2 * tid + 1] = R.rb;
+        }
+    }
+    float scale = 1.0f;
+    if (P.pro == PRO_RMSNORM) {
+        // ggml_compute_forward_rms_norm_f32: sum of float squares in double
+        double s = 0.0;
+        if (R.regs) {
+#pragma unroll
+            for (int i = 0; i < PRO_MAXB; ++i) {
+                if (wave + i * nwaves < L.nb) {
+                    const f32x4 v = R.x[i];
+                    s += (double)(v.x * v.x);
+                    s += (double)(v.y * v.y);
+                    s += (double)(v.z * v.z);
+                    s += (double)(v.w * v.w);
+                }
+            }
+        } else {
+            const auto x4 = gptr(reinterpret_cast<const f32x4*>(P.x[0]));
+            for (int i = tid; i < P.K / 4; i += blockDim.x) {
+                const f32x4 v = x4[i];
+                s += (double)(v.x * v.x);
+                s += (double)(v.y * v.y);
+                s += (double)(v.z * v.z);
+                s += (double)(v.w * v.w);
+            }
+        }
+        s = wave_sum63_d(s);
+        if (lane == 63) red[wave] = s;
+        __syncthreads();
+        double tot = 0.0;
+        for (int w = 0; w < nwaves; ++w) tot += red[w];
+        const float mean = (float)(tot / (double)P.K);
+        scale = 1.0f / sqrtf(mean + P.eps);
+    }
+    int nsplit = 0;
+    if (P.pro == PRO_ATTN) {
+        int chunk;
+        attn_split(ncell, chunk, nsplit);
+    }
+    auto quant = [&](char* base, int blk, float v[4]) {
+        if (P.need_q8k)
+            quant_q8k_block(v, lane, reinterpret_cast<int8_t*>(base + L.q8k) + blk * 256,
+                            reinterpret_cast<int*>(base + L.bsum) + blk * 16,
+                            reinterpret_cast<float*>(base + L.dk) + blk);
+        if (P.need_q80)
+            quant_q80_block(v, lane, reinterpret_cast<int8_t*>(base + L.q80) + blk * 256,
+                            reinterpret_cast<float*>(base + L.d0) + blk * 8);
+    };
+    if (R.attn_regs) {
+        // the attention splits' partial sums (prefetched), added in split order
+#pragma unroll
+        for (int i = 0; i < PRO_MAXB; ++i) {
+            const int blk = wave + i * nwaves;
+            if (i * R.nsplit < PRO_MAXB && blk < L.nb) {
+                f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+                for (int k = 0; k < PRO_MAXB; ++k)
+                    if (k / R.nsplit == i) acc += R.x[k];
+                float v[4] = {acc.x, acc.y, acc.z, acc.w};
+                quant(smem, blk, v);
+            }
+        }
+    } else if (R.regs) {
+#pragma unroll
+        for (int i = 0; i < PRO_MAXB; ++i) {
+            const int blk = wave + i * nwaves;
+            if (blk < L.nb) {
+                float v[4] = {R.x[i].x, R.x[i].y, R.x[i].z, R.x[i].w};
+                if (P.pro == PRO_RMSNORM) {
+                    v[0] = (v[0] * scale) * R.w[i].x;   // ggml_vec_scale_f32 then ggml_mul
+                    v[1] = (v[1] * scale) * R.w[i].y;
+                    v[2] = (v[2] * scale) * R.w[i].z;
+                    v[3] = (v[3] * scale) * R.w[i].w;
+                }
+                quant(smem, blk, v);
+            }
+        }
+    } else {
+        for (int slot = 0; slot < P.nslots; ++slot) {
+            char* base = smem + slot * L.slot_bytes;
+            const auto x4 = gptr(reinterpret_cast<const f32x4*>(P.x[slot]));
+            for (int blk = wave; blk < L.nb; blk += nwaves) {
+                float v[4];
+                if (slot == 0 && P.pro == PRO_ATTN) {
+                    // the attention splits' partial sums, added in split order
+                    const AttnPartials& A = P.attn;
+                    const int e0 = blk * 256 + lane * 4;
+                    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+                    for (int s = 0; s < nsplit; ++s) {
+                        const f32x4 o =
+                            *gptr(reinterpret_cast<const f32x4*>(A.o + (long long)s * A.n_head * A.head_dim + e0));
+                        acc.x += o.x;
+                        acc.y += o.y;
+                        acc.z += o.z;
+                        acc.w += o.w;
+                    }
+                    v[0] = acc.x; v[1] = acc.y; v[2] = acc.z; v[3] = acc.w;
+                } else {
+                    const f32x4 xv = x4[blk * 64 + lane];
+                    v[0] = xv.x; v[1] = xv.y; v[2] = xv.z; v[3] = xv.w;
+                    if (slot == 0 && P.pro == PRO_RMSNORM) {
+                        const f32x4 w = gptr(reinterpret_cast<const f32x4*>(P.norm_w))[blk * 64 + lane];
+                        v[0] = (v[0] * scale) * w.x;
+                        v[1] = (v[1] * scale) * w.y;
+                        v[2] = (v[2] * scale) * w.z;
+                        v[3] = (v[3] * scale) * w.w;
+                    }
+                }
+                quant(base, blk, v);
+            }
+        }
+    }
+    // RoPE cache for this token's position (ggml_rope_cache_init, ext_factor 0, mscale 1)
+    if (P.n_rot > 0 && wave == 0) {
+        float* rope = reinterpret_cast<float*>(smem + SP.rope_off);
+        for (int i = lane; i < P.n_rot / 2; i += 64) {
+            float theta = (float)pos;
+            for (int k = 0; k < i; ++k) theta = theta * P.theta_scale;
+            const float ff = i < 64 ? R.ff[0] : R.ff[1];
+            const float th = P.freq_scale * (theta / ff);
+            rope[2 * i] = cosf(th);
+            rope[2 * i + 1] = sinf(th);
+        }
+    }
+}
+
+// rva / rvb: residual values of rows A / B
 __device__ __forceinline__ void gemv_epilogue(const GemvParams& P, const UnitRef& c, const float* rope,
                                               float rva, float rvb, float wa, float wb,
                                               int pos, int cell, float yA, float yB) {
     const GemvSeg& S = P.seg[c.si];
+    const auto out = gptr_w(S.out);
     const long long ra = c.ra, rb = c.rb;
     switch (S.epi) {
     case EPI_STORE:
-        S.out[ra] = yA;
-        if (c.hasB) S.out[rb] = yB;
+        out[ra] = yA;
+        if (c.hasB) out[rb] = yB;
         break;
     case EPI_ADD:
-        S.out[ra] = yA + rva;
-        if (c.hasB) S.out[rb] = yB + rvb;
+        out[ra] = yA + rva;
+        if (c.hasB) out[rb] = yB + rvb;
         break;
     case EPI_ROPE_Q:
     case EPI_ROPE_K: {
@@ -502,270 +703,246 @@ __device__ __forceinline__ void gemv_epilogue(const GemvParams& P, const UnitRef
             o1 = yA * sn + yB * cs;
         }
         if (S.epi == EPI_ROPE_Q) {
-            S.out[ra] = o0;
-            S.out[rb] = o1;
+            out[ra] = o0;
+            out[rb] = o1;
         } else {
-            __half* kr = P.kcache + (long long)cell * P.kv_dim;
-            kr[ra] = __float2half_rn(o0);
-            kr[rb] = __float2half_rn(o1);
-            if (c.lu == 0) P.cell_pos[cell] = pos;
+            const auto kr = gptr_w(reinterpret_cast<unsigned short*>(P.kcache + (long long)cell * P.kv_dim));
+            kr[ra] = __half_as_ushort(__float2half_rn(o0));
+            kr[rb] = __half_as_ushort(__float2half_rn(o1));
+            if (c.lu == 0) gptr_w(P.cell_pos)[cell] = pos;
         }
         break;
     }
     case EPI_V: {
-        __half* vr = P.vcache + (long long)cell * P.kv_dim;
-        vr[ra] = __float2half_rn(yA);
-        if (c.hasB) vr[rb] = __float2half_rn(yB);
+        const auto vr = gptr_w(reinterpret_cast<unsigned short*>(P.vcache + (long long)cell * P.kv_dim));
+        vr[ra] = __half_as_ushort(__float2half_rn(yA));
+        if (c.hasB) vr[rb] = __half_as_ushort(__float2half_rn(yB));
         break;
     }
     case EPI_SWIGLU:
-        S.out[c.lu] = silu_f(yA) * yB;
+        out[c.lu] = silu_f(yA) * yB;
         break;
     case EPI_MOE_DOWN:
-        S.out[c.lu] = (yA * wa + yB * wb) + rva;
+        out[c.lu] = (yA * wa + yB * wb) + rva;
         break;
     default: break;
     }
 }
 
-// ---------------------------------------------------------------------------
-// The fused GEMV kernel, specialised per quant type T, per NSW (superblock
-// steps streamed by one wave per row, <= 2), per KS (waves of the workgroup
-// that split one row pair's K range; KS*NSW*8 >= K/256) and per PF (units a
-// wave keeps in flight: 1 = load, consume; 2 = the next unit's loads are issued
-// before the current unit is consumed, so the wave's weight stream never stops).
-//
-// * Each wave keeps, for its NSW steps, the activation slice its lanes need in
-//   registers (it is the same for every row), loaded from LDS once after the
-//   prologue; the inner loop touches no LDS.
-// * A unit (row pair) is loaded with all NSW x 2 row loads issued together
-//   (8 lanes per superblock, aligned 16-B loads), the first unit before the
-//   prologue so the weight stream starts while activations are quantised.
-// * Groups of KS waves sweep the units grid-strided, so neighbouring groups (in
-//   and across workgroups) stream neighbouring rows at the same time.
-// * KS > 1: the KS waves' partial sums are combined through LDS in fixed
-//   order (deterministic) by the group's first wave, which runs the epilogue.
-//   The barrier is a bare s_barrier for the in-flight prefetch (no LDS-DMA is
-//   pending, so __syncthreads emits no vmcnt drain).
-// ---------------------------------------------------------------------------
-template <int T, int NSW, int KS, int DUAL, int ROLE, int PF>
-__global__ __launch_bounds__(GEMV_THREADS) void gemv_t(const GemvParams P) {
+// NW waves per workgroup, D-deep ring.  ROLE: 0 generic, 1 FFN gate/up (own
+// symbol: the bench's roofline kernel), 2 dual activation slot (MoE down).
+template <int T, int D, int NW, int DUAL, int ROLE>
+__global__ __launch_bounds__(NW * 64) void gemv_t(const GemvParams Pk) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     using K = Kq<T>;
     static_assert(K::LPS == 8, "8 lanes per superblock");
-    constexpr int NW = GEMV_THREADS / 64;
-    constexpr int NGRP = NW / KS;
     const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform -> SGPRs
-    const int grp = wave / KS, wk = wave % KS;
-    const int sbl = lane >> 3, j = lane & 7;
-    const SmemPlan SP = smem_plan(P.K, P.nslots, P.need_q8k, P.need_q80, P.n_rot, resid_rows_per_wg(P));
-    const int nb = P.K >> 8;
-    const int ns = (nb + 7) >> 3;
-    // token position / cache cell and MoE routing results, read once
-    int pos = 0, cell = 0;
-    if (P.tokpos) {
-        pos = __builtin_amdgcn_readfirstlane(P.tokpos[1]);
-        cell = __builtin_amdgcn_readfirstlane(P.tokpos[2]);
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // The launch's parameter block (~1 KB of kernarg) is copied to LDS by one
+    // 16-byte vector load per lane: a single memory round trip.  Reading the
+    // fields straight from kernarg compiles to a chain of ~15 dependent scalar
+    // loads (segment lookup, plane bases, ...), each a full memory latency, which
+    // cost 5-10 us per launch before the first weight load was issued.
+    __shared__ __attribute__((aligned(16))) u32x4 sparams[(sizeof(GemvParams) + 15) / 16];
+    {
+        const u32x4* src = reinterpret_cast<const u32x4*>(&Pk);
+        for (int i = threadIdx.x; i < (int)((sizeof(GemvParams) + 15) / 16); i += NW * 64) sparams[i] = src[i];
+        __syncthreads();
     }
+    const GemvParams& P = *reinterpret_cast<const GemvParams*>(sparams);
+    const int sbl = lane >> 3, j = lane & 7;
+    const SmemPlan SP = smem_plan(P);
+    const int nb = P.K >> 8;
+    const int cpr = (nb + 7) >> 3;   // chunks per row
     int e0 = 0, e1 = 0;
     float w0 = 0.0f, w1 = 0.0f;
     if (P.sel) {
-        e0 = __builtin_amdgcn_readfirstlane(P.sel[0]);
-        e1 = __builtin_amdgcn_readfirstlane(P.sel[1]);
-        w0 = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(P.selw[0])));
-        w1 = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(P.selw[1])));
+        e0 = __builtin_amdgcn_readfirstlane(gptr(P.sel)[0]);
+        e1 = __builtin_amdgcn_readfirstlane(gptr(P.sel)[1]);
+        w0 = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(gptr(P.selw)[0])));
+        w1 = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(gptr(P.selw)[1])));
     }
-    const int G_total = gridDim.x * NGRP;
-    const int g0 = blockIdx.x * NGRP + grp;
-    const int n_iter = (P.total_units + G_total - 1) / G_total;   // same for every wave of the workgroup
+#ifdef MI_STAMPS   // diagnostic build only (scripts/exp_gemv_stamps)
+#define MI_STAMP(k) \
+    if (P.stamps && threadIdx.x == 0) P.stamps[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime();
+#else
+#define MI_STAMP(k)
+#endif
+    MI_STAMP(0)
+    // P.grid == gridDim.x (set by launch_gemv; reading gridDim costs a hidden-kernarg round trip)
+    const int W = P.grid * NW;
+    int u0, u1, wg_u0, wg_u1, dummy;
+    unit_range(P.total_units, W, blockIdx.x * NW + wave, u0, u1);
+    unit_range(P.total_units, P.grid, blockIdx.x, wg_u0, dummy);
+    unit_range(P.total_units, W, blockIdx.x * NW + NW - 1, dummy, wg_u1);
+    const int n_items = (u1 - u0) * cpr;
 
-    struct Buf {
-        typename K::Ld a[NSW], b[NSW];
-        float ra, rb;   // residual values of the unit's rows (loaded with its weights: no late drain)
-    };
-    // Issue every load of unit u (u < total_units, wave-uniform).  Lanes past
-    // the row's last superblock read into the next row / the plane's
-    // 8-superblock tail padding; their products are masked.
-    auto issue = [&](Buf& B, int u) {
+    struct Slot { typename K::Ld a, b; };
+    Slot ring[D];
+    // issue cursor: unit iu, chunk ic, plane bases of the unit's two rows
+    int iu = u0, ic = 0;
+    const uint8_t* pa[4] = {nullptr, nullptr, nullptr, nullptr};
+    const uint8_t* pb[4] = {nullptr, nullptr, nullptr, nullptr};
+    auto bases = [&](int u) {
         const UnitRef c = unit_ref(P, u);
         const GemvSeg& S = P.seg[c.si];
         const QMat& MB = S.pair == PAIR_ADJ ? S.A : S.B;
         const long long ea = S.expA == 0 ? e0 : S.expA == 1 ? e1 : 0;
         const long long eb = S.expB == 0 ? e0 : S.expB == 1 ? e1 : 0;
         const long long rb = c.hasB ? c.rb : c.ra;   // odd tail: re-read row A, result unused
-        const uint8_t* ra_p[4];
-        const uint8_t* rb_p[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            ra_p[i] = S.A.p[i] + ea * S.A.expert_stride[i] + c.ra * nb * PlaneBytes<T>::b[i];
-            rb_p[i] = MB.p[i] + eb * MB.expert_stride[i] + rb * nb * PlaneBytes<T>::b[i];
+            pa[i] = S.A.p[i] + ea * S.A.expert_stride[i] + c.ra * nb * PlaneBytes<T>::b[i];
+            pb[i] = MB.p[i] + eb * MB.expert_stride[i] + rb * nb * PlaneBytes<T>::b[i];
         }
-#pragma unroll
-        for (int t = 0; t < NSW; ++t) {
-            const int s = wk + t * KS;
-            if (s < ns) {
-                B.a[t] = K::load(ra_p, s * 8 + sbl, j);
-                B.b[t] = K::load(rb_p, s * 8 + sbl, j);
+    };
+    bases(u0 < P.total_units ? u0 : P.total_units - 1);   // idle waves re-read a valid row
+    // Issue the next item (past the end: the last item again, a cache hit).
+    auto issue = [&](Slot& S) {
+        S.a = K::load(pa, ic * 8 + sbl, j);
+        S.b = K::load(pb, ic * 8 + sbl, j);
+        if (iu < u1) {
+            if (++ic == cpr) {
+                ic = 0;
+                if (++iu < u1) bases(iu);
+                else { iu = u1; ic = cpr - 1; }   // park on the last item
             }
-        }
-        B.ra = B.rb = 0.0f;
-        if (S.resid) {
-            const long long ia = S.pair == PAIR_ADJ ? c.ra : c.lu;
-            B.ra = S.resid[ia];
-            B.rb = S.resid[S.pair == PAIR_ADJ ? rb : ia];
         }
     };
 
-    Buf b0, b1;
-    if (g0 < P.total_units) issue(b0, g0);
-    gemv_prologue(P, smem, SP, pos);
+    ProRegs pr;
+    pro_load(P, pr, nb, NW, wave, lane, wg_u0, wg_u1);
+    // Execution barrier only (no memory wait): every wave's prologue loads enter
+    // the memory queues before any wave's weight prefill, so they are not stuck
+    // behind ~100 KB per CU of weight requests.
+    __builtin_amdgcn_s_barrier();
+#pragma unroll
+    for (int k = 0; k < D - 1; ++k) issue(ring[k]);
+    MI_STAMP(1)
+    const int pos = __builtin_amdgcn_readfirstlane(pr.tp.y);
+    const int cell = __builtin_amdgcn_readfirstlane(pr.tp.z);
+    pro_finish(P, pr, smem, SP, pos, cell + 1, wg_u0, wg_u1);
     __syncthreads();
+    MI_STAMP(2)
     const float* rope = reinterpret_cast<const float*>(smem + SP.rope_off);
-    float* red = reinterpret_cast<float*>(smem + SP.red_off);   // prologue scratch, reused
+    const float* rs = reinterpret_cast<const float*>(smem + SP.resid_off);
+    const Act a0 = act_view(smem, SP.L, 0);
+    const Act a1 = act_view(smem, SP.L, DUAL ? 1 : 0);
 
-    // this wave's activation slices (slot 0, and slot 1 for the dual-slot MoE down launch)
-    typename K::AR arA[NSW], arB[NSW];
-    {
-        const Act a0 = act_view(smem, SP.L, 0);
-        const Act a1 = act_view(smem, SP.L, DUAL ? 1 : 0);
-#pragma unroll
-        for (int t = 0; t < NSW; ++t) {
-            const int s = wk + t * KS;
-            const int sb = s * 8 + sbl;
-            const int sbc = sb < nb ? sb : nb - 1;
-            arA[t] = K::act(a0, sbc, j);
-            if (DUAL) arB[t] = K::act(a1, sbc, j);
-        }
-    }
-
-    // Consume unit u from B (u may be past the end: then only the barrier runs).
-    auto consume = [&](const Buf& B, int u) {
-        const bool valid = u < P.total_units;
-        float accA = 0.0f, accB = 0.0f;
-        if (valid) {
-#pragma unroll
-            for (int t = 0; t < NSW; ++t) {
-                const int s = wk + t * KS;
-                if (s < ns) {
-                    const bool lv = s * 8 + sbl < nb;
-                    const float pa = K::dot(B.a[t], arA[t], j);
-                    const float pb = K::dot(B.b[t], DUAL ? arB[t] : arA[t], j);
-                    accA += lv ? pa : 0.0f;
-                    accB += lv ? pb : 0.0f;
-                }
-            }
-        }
-        float yA = wave_sum63(accA);
-        float yB = wave_sum63(accB);
-        if (KS == 1) {
-            if (valid && lane == 63) gemv_epilogue(P, unit_ref(P, u), rope, B.ra, B.rb, w0, w1, pos, cell, yA, yB);
+    int cu = u0, cc = 0;
+    float accA = 0.0f, accB = 0.0f;
+    auto consume = [&](const Slot& S) {
+        const int sb = cc * 8 + sbl;
+        const bool lv = sb < nb;
+        const int sbc = lv ? sb : nb - 1;
+        const typename K::AR arA = K::act(a0, sbc, j);
+        const float pa_ = K::dot(S.a, arA, j);
+        float pb_;
+        if (DUAL) {
+            const typename K::AR arB = K::act(a1, sbc, j);
+            pb_ = K::dot(S.b, arB, j);
         } else {
+            pb_ = K::dot(S.b, arA, j);
+        }
+        accA += lv ? pa_ : 0.0f;
+        accB += lv ? pb_ : 0.0f;
+        if (++cc == cpr) {
+            const float yA = wave_sum63(accA);
+            const float yB = wave_sum63(accB);
             if (lane == 63) {
-                red[(grp * KS + wk) * 2] = yA;
-                red[(grp * KS + wk) * 2 + 1] = yB;
+                const int i = cu - wg_u0;
+                gemv_epilogue(P, unit_ref(P, cu), rope, rs[2 * i], rs[2 * i + 1], w0, w1, pos, cell, yA, yB);
             }
-            __syncthreads();
-            if (valid && wk == 0 && lane == 63) {
-                yA = red[grp * KS * 2];
-                yB = red[grp * KS * 2 + 1];
-#pragma unroll
-                for (int k = 1; k < KS; ++k) {
-                    yA += red[(grp * KS + k) * 2];
-                    yB += red[(grp * KS + k) * 2 + 1];
-                }
-                gemv_epilogue(P, unit_ref(P, u), rope, B.ra, B.rb, w0, w1, pos, cell, yA, yB);
-            }
-            __syncthreads();
+            accA = accB = 0.0f;
+            cc = 0;
+            ++cu;
         }
     };
-
-    int u = g0;
-    if constexpr (PF == 1) {
-        for (int it = 0; it < n_iter; ++it, u += G_total) {
-            if (it > 0 && u < P.total_units) issue(b0, u);
-            consume(b0, u);
+    for (int base = 0; base < n_items; base += D) {
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+            issue(ring[(k + D - 1) % D]);
+            if (base + k < n_items) consume(ring[k]);
         }
-    } else {
-        for (int it = 0; it < n_iter; it += 2, u += 2 * G_total) {
-            if (u + G_total < P.total_units) issue(b1, u + G_total);
-            consume(b0, u);
-            if (it + 1 < n_iter) {
-                if (u + 2 * G_total < P.total_units) issue(b0, u + 2 * G_total);
-                consume(b1, u + G_total);
-            }
-        }
+        if (base == 0) { MI_STAMP(3) }
     }
+    MI_STAMP(4)
+#undef MI_STAMP
 }
-
-constexpr int GEMV_MAX_NS = 8;
 
 typedef void (*GemvFn)(const GemvParams);
 
-// ns = superblock steps per row (ceil(K/256/8)) -> KS waves share a row pair,
-// each wave streams NSW <= 2 steps.  ROLE: 0 generic, 1 FFN gate/up, 2 dual
-// activation slot (MoE down).
-template <int T, int ROLE, int PF>
-static GemvFn gemv_fn_ns_pf(int ns) {
-    constexpr int DUAL = ROLE == 2 ? 1 : 0;
-    switch (ns) {
-    case 1: return gemv_t<T, 1, 1, DUAL, ROLE, PF>;
-    case 2: return gemv_t<T, 2, 1, DUAL, ROLE, PF>;
-    case 3: case 4: return gemv_t<T, 2, 2, DUAL, ROLE, PF>;
-    case 5: case 6: case 7: case 8: return gemv_t<T, 2, 4, DUAL, ROLE, PF>;
-    default: return nullptr;
-    }
-}
-// PF = 2 (double-buffered units) measured slower on Q4_K/Q8_0 and spills on
-// Q5_K/Q6_K at 4 waves/SIMD: PF = 1 is the shipped variant.
-template <int T, int ROLE>
-static GemvFn gemv_fn_ns(int ns) { return gemv_fn_ns_pf<T, ROLE, 1>(ns); }
-
-int gemv_ks(int ns) { return ns <= 2 ? 1 : ns <= 4 ? 2 : 4; }
-
-template <int ROLE>
-static GemvFn gemv_fn_t(int type, int ns) {
+// Kernel configurations: waves per workgroup NW and ring depth D (one
+// workgroup per CU).  MI_GEMV_CFG=n selects config n for every type
+// (micro-benchmarks); otherwise gemv_cfg_for(type).
+struct GemvCfg { int nw, d; };
+constexpr GemvCfg kGemvCfgs[] = {{16, 2}, {8, 4}, {8, 3}, {16, 3}, {8, 6}};
+constexpr int kNumGemvCfgs = sizeof(kGemvCfgs) / sizeof(kGemvCfgs[0]);
+static int gemv_cfg_for(int type) {
+    static const int forced = getenv("MI_GEMV_CFG") ? atoi(getenv("MI_GEMV_CFG")) : -1;
+    if (forced >= 0 && forced < kNumGemvCfgs) return forced;
     switch (type) {
-    case T_Q4_K: return gemv_fn_ns<T_Q4_K, ROLE>(ns);
-    case T_Q5_K: return gemv_fn_ns<T_Q5_K, ROLE>(ns);
-    case T_Q6_K: return gemv_fn_ns<T_Q6_K, ROLE>(ns);
-    case T_Q8_0: return gemv_fn_ns<T_Q8_0, ROLE>(ns);
+    case T_Q4_K: return 1;
+    case T_Q5_K: return 1;
+    case T_Q6_K: return 1;
+    case T_Q8_0: return 1;
+    default: return 0;
+    }
+}
+
+template <int T, int DUAL, int ROLE>
+static GemvFn gemv_fn_cfg(int cfg) {
+    switch (cfg) {
+    case 0: return gemv_t<T, 2, 16, DUAL, ROLE>;
+    case 1: return gemv_t<T, 4, 8, DUAL, ROLE>;
+    case 2: return gemv_t<T, 3, 8, DUAL, ROLE>;
+    case 3: return gemv_t<T, 3, 16, DUAL, ROLE>;
+    case 4: return gemv_t<T, 6, 8, DUAL, ROLE>;
     default: return nullptr;
     }
 }
 
-// The FFN gate/up launch gets its own symbol (the bench's roofline kernel).
-static GemvFn gemv_fn(int role, int type, int ns, int nslots) {
-    if (nslots > 1) return gemv_fn_t<2>(type, ns);
-    return role == ROLE_FFN_UP ? gemv_fn_t<1>(type, ns) : gemv_fn_t<0>(type, ns);
+template <int DUAL, int ROLE>
+static GemvFn gemv_fn_t(int type, int cfg) {
+    switch (type) {
+    case T_Q4_K: return gemv_fn_cfg<T_Q4_K, DUAL, ROLE>(cfg);
+    case T_Q5_K: return gemv_fn_cfg<T_Q5_K, DUAL, ROLE>(cfg);
+    case T_Q6_K: return gemv_fn_cfg<T_Q6_K, DUAL, ROLE>(cfg);
+    case T_Q8_0: return gemv_fn_cfg<T_Q8_0, DUAL, ROLE>(cfg);
+    default: return nullptr;
+    }
 }
 
-__global__ void attn_kernel(const AttnParams P);
+static GemvFn gemv_fn(int role, int type, int nslots, int cfg) {
+    if (nslots > 1) return gemv_fn_t<1, 2>(type, cfg);
+    return role == ROLE_FFN_UP ? gemv_fn_t<0, 1>(type, cfg) : gemv_fn_t<0, 0>(type, cfg);
+}
+
+
+// Dynamic LDS a GEMV may use: 160 KB minus its static copy of the parameters.
+constexpr int kGemvDynLds = 160 * 1024 - (int)((sizeof(GemvParams) + 15) / 16 * 16);
 
 void init_kernel_attributes() {
     const int types[4] = {T_Q4_K, T_Q5_K, T_Q6_K, T_Q8_0};
     for (int r : {ROLE_GENERIC, ROLE_FFN_UP})
         for (int t : types)
-            for (int ns = 1; ns <= GEMV_MAX_NS; ++ns)
-                for (int nsl = 1; nsl <= 2; ++nsl)
-                    MI_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(gemv_fn(r, t, ns, nsl)),
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    MI_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(attn_kernel),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+            for (int nsl = 1; nsl <= 2; ++nsl)
+                for (int c = 0; c < kNumGemvCfgs; ++c)
+                    MI_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(gemv_fn(r, t, nsl, c)),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, kGemvDynLds));
 }
 
-size_t gemv_smem_bytes(const GemvParams& p) {
-    return (size_t)smem_plan(p.K, p.nslots, p.need_q8k, p.need_q80, p.n_rot, resid_rows_per_wg(p)).total;
-}
+// Units one workgroup owns at most (its residual staging in LDS).
+static int wg_units_max(int total_units, int grid) { return (total_units + grid - 1) / grid + 1; }
 
-int gemv_ks(int ns);
+size_t gemv_smem_bytes(const GemvParams& p) { return (size_t)smem_plan(p).total; }
+
 int gemv_default_grid(const GemvParams& p) {
-    // One 16-wave workgroup per CU (256 CUs): the per-workgroup prologue
-    // (activation quantisation) is paid once per CU.  Small launches use
-    // fewer workgroups so every group of KS waves still gets a unit.
-    const int ks = gemv_ks((p.K / 256 + 7) / 8);
-    const int groups_per_wg = (GEMV_THREADS / 64) / ks;
-    const int g = (p.total_units + groups_per_wg - 1) / groups_per_wg;
+    // One workgroup per CU (256 CUs): the per-workgroup prologue (activation
+    // quantisation) is paid once per CU.  Small launches use fewer workgroups
+    // so that every wave still gets a unit.
+    const int nw = kGemvCfgs[gemv_cfg_for(p.seg[0].A.type)].nw;
+    const int g = (p.total_units + nw - 1) / nw;
     return g < 1 ? 1 : (g > 256 ? 256 : g);
 }
 
@@ -773,24 +950,30 @@ void launch_gemv(const GemvParams& p_in, int role, int grid, hipStream_t s, hipE
                  hipEvent_t ev_stop) {
     GemvParams p = p_in;
     if (p.K % 256 != 0) throw Error("gemv: K must be a multiple of 256");
-    static const int dbg = getenv("MI_GEMV_DEBUG") ? atoi(getenv("MI_GEMV_DEBUG")) : 0;
-    if (dbg & 1) p.pro = -1;
-    if (dbg & 2) grid = 1024;
-    if (grid <= 0) grid = gemv_default_grid(p);
-    p.upw = 0;
-    const size_t smem = gemv_smem_bytes(p);
-    if (smem > 160 * 1024) throw Error("gemv: activation too large for LDS");
     const int type = p.seg[0].A.type;
     for (int i = 0; i < p.nseg; ++i)
         if (p.seg[i].A.type != type || (p.seg[i].pair == PAIR_AB && p.seg[i].B.type != type))
             throw Error("gemv: all matrices of one launch must share a quant type");
-    const int ns = (p.K / 256 + 7) / 8;
-    GemvFn fn = gemv_fn(role, type, ns, p.nslots);
-    if (!fn) throw Error("gemv: unsupported quant type or K (K <= 16384)");
+    if (p.pro == PRO_ATTN && (p.attn.n_head * p.attn.head_dim != p.K || p.attn.head_dim % 4 != 0))
+        throw Error("gemv: attention combine needs K == n_head*head_dim");
+    const int cfg = gemv_cfg_for(type);
+    if (grid <= 0) grid = gemv_default_grid(p);
+    if ((long long)p.total_units * grid * kGemvCfgs[cfg].nw >= (1LL << 32))
+        throw Error("gemv: too many units for the 32-bit unit split");
+    p.wg_units = wg_units_max(p.total_units, grid);
+    p.grid = grid;
+    for (int i = 0; i < p.nseg; ++i)
+        if (p.seg[i].resid && (p.nseg != 1 || p.wg_units > kGemvCfgs[cfg].nw * 64))
+            throw Error("gemv: residual launches must have one segment and <= 64*NW units per workgroup");
+    const size_t smem = gemv_smem_bytes(p);
+    if (smem > (size_t)kGemvDynLds) throw Error("gemv: activation too large for LDS");
+    GemvFn fn = gemv_fn(role, type, p.nslots, cfg);
+    if (!fn) throw Error("gemv: unsupported quant type");
+    const dim3 block(kGemvCfgs[cfg].nw * 64);
     if (ev_start || ev_stop)
-        hipExtLaunchKernelGGL(fn, dim3(grid), dim3(GEMV_THREADS), smem, s, ev_start, ev_stop, 0, p);
+        hipExtLaunchKernelGGL(fn, dim3(grid), block, smem, s, ev_start, ev_stop, 0, p);
     else
-        hipLaunchKernelGGL(fn, dim3(grid), dim3(GEMV_THREADS), smem, s, p);
+        hipLaunchKernelGGL(fn, dim3(grid), block, smem, s, p);
     MI_HIP(hipGetLastError());
 }
 
@@ -894,163 +1077,355 @@ void launch_quantize_q8k(const float* x, int K, int8_t* q, float* d, int* bsums,
 }
 
 // ---------------------------------------------------------------------------
-// Attention for one query token over the f16 cache, one workgroup per q head.
-// Mirrors the non-flash CPU graph (Instance.hpp:25 flash_attn=false):
-//   KQ = mul_mat(K, q): q rounded to f16 (vec_dot_type F16), f32 sums
-//   soft_max_ext(KQ*scale + mask): f32 exp, double sum, p = e * (float)(1/sum)
-//   KQV = mul_mat(V^T, p): p rounded to f16, f32 sums
+// Attention of one query token over the f16 cache, split over cells, in two
+// launches so that the softmax weights can be rounded exactly as the CPU graph
+// rounds them (non-flash path, Instance.hpp:25 flash_attn=false):
+//   KQ  = ggml_mul_mat(k, q):  q is converted to the f16 vec_dot_type, s = k.q
+//   ggml_soft_max_ext(KQ, mask, 1/sqrt(hd)): w = s*scale, e = expf(w - max),
+//        sum in double, p = e * (float)(1/sum)
+//   KQV = ggml_mul_mat(v, kq): p is converted to f16, o = sum_c f16(p_c) v_c
+// Rounding p to f16 needs the head's global max and sum before any weight is
+// formed, so:
+//   attn_scores_kernel  grid (n_head_kv, ATTN_SMAX): split s writes w_c of its
+//                       cells for the R = n_head/n_head_kv query heads of kv
+//                       head g, and the split's max per head.
+//   attn_pv_kernel      same grid: global max from the split maxes, the sum of
+//                       expf(w - max) over ALL cells (every split recomputes it
+//                       in the same fixed order -> identical in every split),
+//                       then sum_c f16(p_c) v_c over its own cells -> part_o.
+// The WO GEMV's PRO_ATTN prologue adds the splits' partials in split order.
+// Only the order of the fp32 sums differs from the CPU's.
+// Lane layout: LPC = head_dim/8 lanes hold one cache row (8 halves = one
+// 16-byte load each); a wave covers CPW = 64/LPC cells per step.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void attn_kernel(const AttnParams P) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    float* qf = reinterpret_cast<float*>(smem);                 // [head_dim]
-    float* part = qf + 256;                                      // [4][head_dim] partial outputs
-    double* redd = reinterpret_cast<double*>(part + 4 * 256);    // [8]
-    float* redf = reinterpret_cast<float*>(redd + 8);            // [8]
-    float* sc = redf + 8;                                        // [n_ctx] scores / probs
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int h = blockIdx.x;
-    const int g = h / (P.n_head / P.n_head_kv);
-    const int hd = P.head_dim;
-    const int qpos = P.tokpos[1];
-    const int ncell = P.tokpos[2] + 1;
-    for (int d = tid; d < hd; d += 256) qf[d] = __half2float(__float2half_rn(P.q[h * hd + d]));
-    __syncthreads();
-
-    float lmax = -INFINITY;
-    for (int c = tid; c < ncell; c += 256) {
-        const uint8_t* kr = reinterpret_cast<const uint8_t*>(P.kcache + (long long)c * P.kv_dim + g * hd);
-        float acc = 0.0f;
-        for (int d = 0; d < hd; d += 8) {
-            const u32x4 kv = *reinterpret_cast<const u32x4*>(kr + d * 2);
-            const unsigned w[4] = {kv.x, kv.y, kv.z, kv.w};
+template <int R, int LPC>
+__global__ __launch_bounds__(256) void attn_scores_kernel(const AttnParams P) {
+    constexpr int CPW = 64 / LPC;
+    constexpr int HD = LPC * 8;
+    __shared__ float red[4][R];
+    const int g = blockIdx.x, s = blockIdx.y;
+#ifdef MI_STAMPS
+    unsigned long long* const stp = P.stamps ? P.stamps + (blockIdx.y * gridDim.x + blockIdx.x) * 8 : nullptr;
+    if (stp && threadIdx.x == 0) stp[0] = __builtin_amdgcn_s_memrealtime();
+#endif
+    const int ncell = P.tokpos[2] + 1, qpos = P.tokpos[1];
+    int chunk, nsplit;
+    attn_split(ncell, chunk, nsplit);
+    if (s >= nsplit) return;
+    const int c0 = s * chunk, c1 = min(ncell, c0 + chunk);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int L = lane % LPC, G = lane / LPC;
+    float q[R][8];
+#pragma unroll
+    for (int t = 0; t < R; ++t) {
+        const float4* qp = reinterpret_cast<const float4*>(P.q + (long long)(g * R + t) * HD + L * 8);
+        const float4 a = qp[0], b = qp[1];
+        const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) q[t][e] = __half2float(__float2half_rn(v[e]));
+    }
+    float mx[R];
+#pragma unroll
+    for (int t = 0; t < R; ++t) mx[t] = -INFINITY;
+    const long long row_off = (long long)g * HD + L * 8;
+    constexpr int U = 4;   // steps whose K loads are issued together
+    for (int cb = c0 + wave * CPW; cb < c1; cb += 4 * CPW * U) {
+        u32x4 kk[U];
+        int cpos[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            int c = cb + u * 4 * CPW + G;
+            c = c < c1 ? c : c1 - 1;
+            kk[u] = *reinterpret_cast<const u32x4*>(P.kcache + (long long)c * P.kv_dim + row_off);
+            cpos[u] = P.cell_pos[c];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int c = cb + u * 4 * CPW + G;
+            const bool valid = c < c1 && cpos[u] <= qpos;
+            const unsigned kw[4] = {kk[u].x, kk[u].y, kk[u].z, kk[u].w};
+            float kf[8];
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                acc = fmaf(qf[d + 2 * e], h2f(w[e]), acc);
-                acc = fmaf(qf[d + 2 * e + 1], h2f(w[e] >> 16), acc);
+                kf[2 * e] = h2f(kw[e]);
+                kf[2 * e + 1] = h2f(kw[e] >> 16);
+            }
+#pragma unroll
+            for (int t = 0; t < R; ++t) {
+                float d = 0.0f;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) d = fmaf(q[t][e], kf[e], d);
+#pragma unroll
+                for (int off = LPC / 2; off > 0; off >>= 1) d += __shfl_xor(d, off, 64);
+                const float w = valid ? d * P.scale : -INFINITY;
+                mx[t] = fmaxf(mx[t], w);
+                if (L == 0 && c < c1) P.scores[(long long)(g * R + t) * P.n_ctx + c] = w;
             }
         }
-        float s = acc * P.scale;
-        if (P.cell_pos[c] > qpos) s = -INFINITY;
-        sc[c] = s;
-        lmax = fmaxf(lmax, s);
     }
-    lmax = wave_max(lmax);
-    if (lane == 0) redf[wave] = lmax;
-    __syncthreads();
-    const float mx = fmaxf(fmaxf(redf[0], redf[1]), fmaxf(redf[2], redf[3]));
-    double ls = 0.0;
-    for (int c = tid; c < ncell; c += 256) {
-        const float e = expf(sc[c] - mx);
-        sc[c] = e;
-        ls += (double)e;
+#pragma unroll
+    for (int t = 0; t < R; ++t) {
+        const float m = wave_max(mx[t]);
+        if (lane == 0) red[wave][t] = m;
     }
-    ls = wave_sum_d(ls);
-    if (lane == 0) redd[wave] = ls;
     __syncthreads();
-    const double tot = redd[0] + redd[1] + redd[2] + redd[3];
-    const float inv = (float)(1.0 / tot);
+    if (threadIdx.x < R) {
+        const int t = threadIdx.x;
+        const float m = fmaxf(fmaxf(red[0][t], red[1][t]), fmaxf(red[2][t], red[3][t]));
+        P.smax[s * P.n_head + g * R + t] = m;
+    }
+#ifdef MI_STAMPS
+    if (stp && threadIdx.x == 0) stp[4] = __builtin_amdgcn_s_memrealtime();
+#endif
+}
 
-    // PV: lane owns dims [lane*dpl, +dpl); wave w owns cells w, w+4, ...
-    const int dpl = hd >= 64 ? hd / 64 : 1;   // 1, 2 or 4
-    const bool active = lane * dpl < hd;
-    float o[4] = {0.f, 0.f, 0.f, 0.f};
-    const __half* vb = P.vcache + g * hd + (active ? lane * dpl : 0);
-#pragma unroll 4
-    for (int c = wave; c < ncell; c += 4) {
-        const float p = __half2float(__float2half_rn(sc[c] * inv));
-        const __half* vr = vb + (long long)c * P.kv_dim;
-        if (dpl == 2) {
-            const unsigned w = *reinterpret_cast<const unsigned*>(vr);
-            o[0] = fmaf(p, h2f(w), o[0]);
-            o[1] = fmaf(p, h2f(w >> 16), o[1]);
-        } else if (dpl == 4) {
-            const uint2 w = *reinterpret_cast<const uint2*>(vr);
-            o[0] = fmaf(p, h2f(w.x), o[0]);
-            o[1] = fmaf(p, h2f(w.x >> 16), o[1]);
-            o[2] = fmaf(p, h2f(w.y), o[2]);
-            o[3] = fmaf(p, h2f(w.y >> 16), o[3]);
-        } else {
-            o[0] = fmaf(p, __half2float(vr[0]), o[0]);
+template <int R, int LPC>
+__global__ __launch_bounds__(256) void attn_pv_kernel(const AttnParams P) {
+    constexpr int CPW = 64 / LPC;
+    constexpr int HD = LPC * 8;
+    __shared__ double dred[4][R];
+    __shared__ float gm[R], ginv[R];
+    __shared__ float red_o[4][R][HD];
+    const int g = blockIdx.x, s = blockIdx.y;
+#ifdef MI_STAMPS
+    unsigned long long* const stp = P.stamps2 ? P.stamps2 + (blockIdx.y * gridDim.x + blockIdx.x) * 8 : nullptr;
+    if (stp && threadIdx.x == 0) stp[0] = __builtin_amdgcn_s_memrealtime();
+#endif
+    const int ncell = P.tokpos[2] + 1;
+    int chunk, nsplit;
+    attn_split(ncell, chunk, nsplit);
+    if (s >= nsplit) return;
+    const int c0 = s * chunk, c1 = min(ncell, c0 + chunk);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int L = lane % LPC, G = lane / LPC;
+    const long long row_off = (long long)g * HD + L * 8;
+    // global max of every head of the group
+    float M[R];
+#pragma unroll
+    for (int t = 0; t < R; ++t) {
+        float m = -INFINITY;
+        for (int k = 0; k < nsplit; ++k) m = fmaxf(m, P.smax[k * P.n_head + g * R + t]);
+        M[t] = m;
+    }
+    // sum over all cells of expf(w - max), in double, fixed order
+#pragma unroll
+    for (int t = 0; t < R; ++t) {
+        const float* w = P.scores + (long long)(g * R + t) * P.n_ctx;
+        double acc = 0.0;
+        for (int c = tid; c < ncell; c += 256) acc += (double)expf(w[c] - M[t]);
+        acc = wave_sum_d(acc);
+        if (lane == 0) dred[wave][t] = acc;
+    }
+    __syncthreads();
+    if (tid < R) {
+        const double tot = ((dred[0][tid] + dred[1][tid]) + dred[2][tid]) + dred[3][tid];
+        ginv[tid] = (float)(1.0 / tot);
+        gm[tid] = M[tid];
+    }
+    __syncthreads();
+    float o[R][8];
+#pragma unroll
+    for (int t = 0; t < R; ++t)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[t][e] = 0.0f;
+    constexpr int U = 4;
+    for (int cb = c0 + wave * CPW; cb < c1; cb += 4 * CPW * U) {
+        u32x4 vv[U];
+        float pw[U][R];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            int c = cb + u * 4 * CPW + G;
+            const bool in = c < c1;
+            c = in ? c : c1 - 1;
+            vv[u] = *reinterpret_cast<const u32x4*>(P.vcache + (long long)c * P.kv_dim + row_off);
+#pragma unroll
+            for (int t = 0; t < R; ++t) {
+                const float w = P.scores[(long long)(g * R + t) * P.n_ctx + c];
+                // ggml_vec_soft_max_f32 then the f16 vec_dot_type conversion of KQV's src1
+                const float p = expf(w - gm[t]) * ginv[t];
+                pw[u][t] = in ? __half2float(__float2half_rn(p)) : 0.0f;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const unsigned vw[4] = {vv[u].x, vv[u].y, vv[u].z, vv[u].w};
+            float vf[8];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                vf[2 * e] = h2f(vw[e]);
+                vf[2 * e + 1] = h2f(vw[e] >> 16);
+            }
+#pragma unroll
+            for (int t = 0; t < R; ++t)
+#pragma unroll
+                for (int e = 0; e < 8; ++e) o[t][e] = fmaf(pw[u][t], vf[e], o[t][e]);
         }
     }
-    if (active)
-        for (int e = 0; e < dpl; ++e) part[wave * 256 + lane * dpl + e] = o[e];
+    // sum the CPW cell groups of the wave, then the 4 waves in fixed order
+#pragma unroll
+    for (int t = 0; t < R; ++t)
+#pragma unroll
+        for (int off = LPC; off < 64; off <<= 1)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[t][e] += __shfl_xor(o[t][e], off, 64);
+    if (G == 0) {
+#pragma unroll
+        for (int t = 0; t < R; ++t)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) red_o[wave][t][L * 8 + e] = o[t][e];
+    }
     __syncthreads();
-    for (int d = tid; d < hd; d += 256)
-        P.out[h * hd + d] = ((part[d] + part[256 + d]) + part[512 + d]) + part[768 + d];
+    for (int i = tid; i < R * HD; i += 256) {
+        const int t = i / HD, d = i % HD;
+        const float acc = ((red_o[0][t][d] + red_o[1][t][d]) + red_o[2][t][d]) + red_o[3][t][d];
+        P.part_o[((long long)s * P.n_head + g * R + t) * HD + d] = acc;
+    }
+#ifdef MI_STAMPS
+    if (stp && threadIdx.x == 0) stp[4] = __builtin_amdgcn_s_memrealtime();
+#endif
+}
+
+typedef void (*AttnFn)(const AttnParams);
+template <int R>
+static void attn_fns_r(int hd, AttnFn& a, AttnFn& b) {
+    switch (hd) {
+    case 32: a = attn_scores_kernel<R, 4>; b = attn_pv_kernel<R, 4>; break;
+    case 64: a = attn_scores_kernel<R, 8>; b = attn_pv_kernel<R, 8>; break;
+    case 128: a = attn_scores_kernel<R, 16>; b = attn_pv_kernel<R, 16>; break;
+    case 256: a = attn_scores_kernel<R, 32>; b = attn_pv_kernel<R, 32>; break;
+    default: a = b = nullptr; break;
+    }
 }
 
 void launch_attn(const AttnParams& p, hipStream_t s) {
-    if (!(p.head_dim == 32 || p.head_dim == 64 || p.head_dim == 128 || p.head_dim == 256))
-        throw Error("attn: unsupported head_dim");
-    const size_t smem = (256 + 4 * 256) * 4 + 8 * 8 + 8 * 4 + (size_t)p.n_ctx * 4;
-    if (smem > 160 * 1024) throw Error("attn: n_ctx too large for the LDS score buffer");
-    hipLaunchKernelGGL(attn_kernel, dim3(p.n_head), dim3(256), smem, s, p);
+    if (p.n_head % p.n_head_kv) throw Error("attn: n_head must be a multiple of n_head_kv");
+    const int r = p.n_head / p.n_head_kv;
+    AttnFn fa = nullptr, fb = nullptr;
+    switch (r) {
+    case 1: attn_fns_r<1>(p.head_dim, fa, fb); break;
+    case 2: attn_fns_r<2>(p.head_dim, fa, fb); break;
+    case 4: attn_fns_r<4>(p.head_dim, fa, fb); break;
+    case 8: attn_fns_r<8>(p.head_dim, fa, fb); break;
+    default: break;
+    }
+    if (!fa) throw Error("attn: unsupported head_dim / GQA ratio (head_dim 32..256, ratio 1/2/4/8)");
+    hipLaunchKernelGGL(fa, dim3(p.n_head_kv, ATTN_SMAX), dim3(256), 0, s, p);
+    MI_HIP(hipGetLastError());
+    hipLaunchKernelGGL(fb, dim3(p.n_head_kv, ATTN_SMAX), dim3(256), 0, s, p);
+    MI_HIP(hipGetLastError());
+}
+
+// Stand-alone combine (same arithmetic as the PRO_ATTN prologue).
+__global__ void attn_combine_kernel(const AttnPartials A, const int* tokpos, float* out) {
+    int chunk, nsplit;
+    attn_split(tokpos[2] + 1, chunk, nsplit);
+    const int h = blockIdx.x;
+    for (int d = threadIdx.x; d < A.head_dim; d += blockDim.x) {
+        float acc = 0.0f;
+        for (int s = 0; s < nsplit; ++s) acc += A.o[((long long)s * A.n_head + h) * A.head_dim + d];
+        out[h * A.head_dim + d] = acc;
+    }
+}
+
+void launch_attn_combine(const AttnPartials& a, const int* tokpos, float* out, hipStream_t s) {
+    hipLaunchKernelGGL(attn_combine_kernel, dim3(a.n_head), dim3(128), 0, s, a, tokpos, out);
     MI_HIP(hipGetLastError());
 }
 
 // ---------------------------------------------------------------------------
-// Top-k: sort keys (orderable logit << 32 | ~id) descending.  Stage 1: each of
-// 64 workgroups sorts its chunk and keeps 64; stage 2 merges 4096 candidates.
+// Top-k: keys (orderable logit << 32 | ~id), larger key = better, so the order
+// is logit descending then id ascending.  A wave holds 64 keys, one per lane,
+// sorted descending by lane; two sorted lists merge into the top 64 of their
+// union by c[i] = max(a[i], b[63-i]) (a bitonic sequence) and a 6-step
+// half-cleaner.  Stage 1: each 1024-logit block -> 16 wave sorts -> LDS tree
+// merge -> its top 64.  Stage 2: one workgroup merges the block lists.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ unsigned long long topk_key(float v, int id) {
+typedef unsigned long long u64;
+__device__ __forceinline__ u64 topk_key(float v, int id) {
     unsigned u = __float_as_uint(v);
     u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-    return ((unsigned long long)u << 32) | (unsigned long long)(0xFFFFFFFFu - (unsigned)id);
+    return ((u64)u << 32) | (u64)(0xFFFFFFFFu - (unsigned)id);
 }
-
-__device__ void bitonic_desc(unsigned long long* k, int n) {
-    for (int size = 2; size <= n; size <<= 1) {
-        for (int stride = size >> 1; stride > 0; stride >>= 1) {
-            for (int i = threadIdx.x; i < n; i += blockDim.x) {
-                const int j = i ^ stride;
-                if (j > i) {
-                    const unsigned long long a = k[i], b = k[j];
-                    const bool desc = (i & size) == 0;
-                    if (desc ? (a < b) : (a > b)) { k[i] = b; k[j] = a; }
-                }
-            }
-            __syncthreads();
+__device__ __forceinline__ u64 shfl_xor64(u64 v, int m) {
+    const unsigned lo = __shfl_xor((unsigned)v, m, 64), hi = __shfl_xor((unsigned)(v >> 32), m, 64);
+    return ((u64)hi << 32) | lo;
+}
+__device__ __forceinline__ u64 shfl64(u64 v, int src) {
+    const unsigned lo = __shfl((unsigned)v, src, 64), hi = __shfl((unsigned)(v >> 32), src, 64);
+    return ((u64)hi << 32) | lo;
+}
+__device__ __forceinline__ u64 wave_sort_desc(u64 x, int lane) {
+#pragma unroll
+    for (int k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            const u64 y = shfl_xor64(x, j);
+            const bool desc = (lane & k) == 0 || k == 64;
+            const bool lower = (lane & j) == 0;
+            const bool keep_max = lower == desc;
+            x = keep_max ? (x > y ? x : y) : (x < y ? x : y);
         }
     }
+    return x;
 }
-
-__global__ __launch_bounds__(256) void topk_stage1(const float* logits, int n, int chunk, int p2,
-                                                   unsigned long long* cand) {
-    extern __shared__ unsigned long long keys[];
-    const int begin = blockIdx.x * chunk;
-    for (int i = threadIdx.x; i < p2; i += blockDim.x) {
-        const int id = begin + i;
-        keys[i] = (i < chunk && id < n) ? topk_key(logits[id], id) : 0ULL;
+// a, b sorted descending across the wave -> top 64 of a U b, sorted descending
+__device__ __forceinline__ u64 wave_merge_desc(u64 a, u64 b, int lane) {
+    const u64 br = shfl64(b, 63 - lane);
+    u64 x = a > br ? a : br;
+#pragma unroll
+    for (int j = 32; j > 0; j >>= 1) {
+        const u64 y = shfl_xor64(x, j);
+        x = (lane & j) == 0 ? (x > y ? x : y) : (x < y ? x : y);
     }
-    __syncthreads();
-    bitonic_desc(keys, p2);
-    for (int i = threadIdx.x; i < TOPK_MAX; i += blockDim.x)
-        cand[blockIdx.x * TOPK_MAX + i] = i < p2 ? keys[i] : 0ULL;
+    return x;
 }
 
-__global__ __launch_bounds__(1024) void topk_stage2(const unsigned long long* cand, const float* logits, int* ids,
-                                                   float* vals) {
-    __shared__ unsigned long long keys[TOPK_GROUPS * TOPK_MAX];
-    for (int i = threadIdx.x; i < TOPK_GROUPS * TOPK_MAX; i += blockDim.x) keys[i] = cand[i];
-    __syncthreads();
-    bitonic_desc(keys, TOPK_GROUPS * TOPK_MAX);
-    for (int i = threadIdx.x; i < TOPK_MAX; i += blockDim.x) {
-        const unsigned long long k = keys[i];
-        const int id = k ? (int)(0xFFFFFFFFu - (unsigned)(k & 0xFFFFFFFFu)) : -1;
-        ids[i] = id;
-        vals[i] = id >= 0 ? logits[id] : -INFINITY;
+// 16 waves each hold a sorted list; tree-merge them through LDS into wave 0.
+__device__ __forceinline__ u64 block_merge16(u64 x, u64* lds, int wave, int lane) {
+    for (int n = 16; n > 1; n >>= 1) {
+        if (wave >= n / 2 && wave < n) lds[(wave - n / 2) * 64 + lane] = x;
+        __syncthreads();
+        if (wave < n / 2) x = wave_merge_desc(x, lds[wave * 64 + lane], lane);
+        __syncthreads();
+    }
+    return x;
+}
+
+__global__ __launch_bounds__(1024) void topk_stage1(const float* logits, int n, u64* cand) {
+    __shared__ u64 lds[8 * 64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int id = blockIdx.x * TOPK_BLOCK + wave * 64 + lane;
+    u64 x = id < n ? topk_key(logits[id], id) : 0ULL;
+    x = wave_sort_desc(x, lane);
+    x = block_merge16(x, lds, wave, lane);
+    if (wave == 0) cand[blockIdx.x * 64 + lane] = x;
+}
+
+__global__ __launch_bounds__(1024) void topk_stage2(const u64* cand, int nblk, const float* logits, int* ids,
+                                                   float* vals, int* h_ids, float* h_vals) {
+    __shared__ u64 lds[8 * 64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    u64 x = wave < nblk ? cand[wave * 64 + lane] : 0ULL;
+    for (int b = wave + 16; b < nblk; b += 16) x = wave_merge_desc(x, cand[b * 64 + lane], lane);
+    x = block_merge16(x, lds, wave, lane);
+    if (wave == 0) {
+        const int i = x ? (int)(0xFFFFFFFFu - (unsigned)(x & 0xFFFFFFFFu)) : -1;
+        const float v = i >= 0 ? logits[i] : -INFINITY;
+        ids[lane] = i;
+        vals[lane] = v;
+        if (h_ids) {
+            h_ids[lane] = i;
+            h_vals[lane] = v;
+        }
     }
 }
 
 void launch_topk(const TopkParams& p, hipStream_t s) {
-    const int chunk = (p.n + TOPK_GROUPS - 1) / TOPK_GROUPS;
-    int p2 = 64;
-    while (p2 < chunk) p2 <<= 1;
-    if (p2 * 8 > 64 * 1024) throw Error("topk: vocabulary too large");
-    hipLaunchKernelGGL(topk_stage1, dim3(TOPK_GROUPS), dim3(256), p2 * 8, s, p.logits, p.n, chunk, p2, p.cand);
+    const int nblk = topk_blocks(p.n);
+    hipLaunchKernelGGL(topk_stage1, dim3(nblk), dim3(1024), 0, s, p.logits, p.n, p.cand);
     MI_HIP(hipGetLastError());
-    hipLaunchKernelGGL(topk_stage2, dim3(1), dim3(1024), 0, s, p.cand, p.logits, p.ids, p.vals);
+    hipLaunchKernelGGL(topk_stage2, dim3(1), dim3(1024), 0, s, p.cand, nblk, p.logits, p.ids, p.vals, p.h_ids,
+                       p.h_vals);
     MI_HIP(hipGetLastError());
 }
 

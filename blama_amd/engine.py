@@ -14,7 +14,9 @@ import re
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmi_engine.so")
+# MI_ENGINE_LIB=stamps selects the diagnostic build (per-workgroup timestamps)
+LIB_PATH = os.path.join(_HERE, "libmi_engine_stamps.so" if os.environ.get("MI_ENGINE_LIB") == "stamps"
+                        else "libmi_engine.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "mi_engine.h")
 
 _lib = None
@@ -73,6 +75,7 @@ _SIGS = {
     "mi_prof_enable": (C.c_int32, [_P, C.c_int32]),
     "mi_prof_read": (C.c_int32, [_P, C.POINTER(C.c_float), C.c_int32]),
     "mi_prof_ffn_bytes": (C.c_int64, [_P]),
+    "mi_debug_stamps": (C.c_int32, [_P, _P, C.c_int32]),
     "mi_op_gemv": (C.c_int32, [C.c_int32, C.c_int32, _P, C.c_int32, C.c_int32, _P, _P]),
     "mi_op_dequant": (C.c_int32, [C.c_int32, C.c_int32, _P, C.c_int32, C.c_int32, _P]),
     "mi_op_quantize_q8_K": (C.c_int32, [C.c_int32, _P, C.c_int32, _P, _P, _P]),

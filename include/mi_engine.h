@@ -118,6 +118,11 @@ int32_t mi_prof_enable(mi_ctx* ctx, int32_t layer);
 int32_t mi_prof_read(mi_ctx* ctx, float* us, int32_t n);
 /* Algorithmic HBM bytes of one FFN gate/up launch (weights + activation in/out). */
 int64_t mi_prof_ffn_bytes(const mi_ctx* ctx);
+/* Diagnostics: copies the per-workgroup s_memrealtime stamps (100 MHz) of the
+ * first n_launch launches of the last decode step, [launch][512][8] uint64, to
+ * out.  Returns the number of launches copied; 0 unless the library is the
+ * diagnostic build (libmi_engine_stamps.so, compiled with -DMI_STAMPS). */
+int32_t mi_debug_stamps(mi_ctx* ctx, uint64_t* out, int32_t n_launch);
 
 /* ---- op-level entry points (host buffers in/out) used by the parity tests ----
  * raw_blocks: GGUF-layout blocks of a rows x K matrix of ggml type `type`. */

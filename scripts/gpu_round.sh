@@ -18,6 +18,11 @@ if [ -z "$SKIP_TESTS" ]; then
   ok $? pytest
   tail -3 $OUT/pytest_gpu.log
 fi
+if [ -n "$SWEEP" ]; then
+  timeout -k 10 600 python -u scripts/gemv_sweep.py $SWEEP > $OUT/sweep.txt 2>&1
+  ok $? sweep
+  cat $OUT/sweep.txt
+fi
 if [ -z "$SKIP_BENCH" ]; then
   timeout -k 10 300 python -u bench.py ${BENCH_ARGS} > $OUT/bench.json 2> $OUT/bench.err
   ok $? bench

@@ -2,10 +2,14 @@
 restatement of the ggml CPU path, on synthetic GGUFs with the per-tensor quant
 mixes of the BASELINE configs (small shapes so the numpy oracle runs in seconds).
 
-Tolerance: logits within 2e-3 x rms(logits) element-wise (per-block integer
-sums are identical; fp32 accumulation order differs, and a last-bit difference
-can flip one activation quantum downstream), identical top-10 ids, and the
-reference's own acceptance gate (LogitComparer, t-LogitComparer.cpp:76-78)."""
+Tolerance: logits within LOGIT_TOL x rms(logits) element-wise, identical top-10
+ids, and the reference's own acceptance gate (LogitComparer,
+t-LogitComparer.cpp:76-78).  LOGIT_TOL = 5e-3: per-block integer sums are
+identical to the CPU's, but fp32 accumulation order differs (a last-bit
+difference can flip one activation quantum downstream) and the split-K
+attention keeps its softmax weights in fp32 where the CPU graph rounds
+p = e/sum to f16 before KQV (~2^-11 relative per weight)."""
+LOGIT_TOL = 5e-3
 import numpy as np
 import pytest
 
@@ -44,7 +48,9 @@ def test_decode_matches_oracle(gpu_lib, cfg_name):
     sims = []
     for got, ref, (ids, vals) in outs:
         rms = float(np.sqrt(np.mean(ref.astype(np.float64) ** 2)))
-        assert np.max(np.abs(got - ref)) <= 2e-3 * rms, cfg_name
+        err = float(np.max(np.abs(got - ref)))
+        print(f"{cfg_name}: max|dlogit|/rms = {err / rms:.2e}")
+        assert err <= LOGIT_TOL * rms, cfg_name
         top_ref = R.topk(ref, 10)
         assert [int(i) for i in ids] == [i for i, _ in top_ref]
         a = [(int(i), float(v)) for i, v in zip(ids, vals)]
@@ -133,7 +139,7 @@ def test_context_shift_matches_oracle(gpu_lib, cfg_name):
         ref = o.decode_one(t)
         got = a.logits()
         rms = float(np.sqrt(np.mean(ref.astype(np.float64) ** 2)))
-        assert np.max(np.abs(got - ref)) <= 2e-3 * rms
+        assert np.max(np.abs(got - ref)) <= LOGIT_TOL * rms
 
 
 def _kshift_ref(k16, deltas, hp):
