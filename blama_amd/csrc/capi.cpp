@@ -78,6 +78,30 @@ int32_t mi_model_token_is_eog(const mi_model* m, int32_t token) {
     return (token == m->impl.eos || (m->impl.eot >= 0 && token == m->impl.eot)) ? 1 : 0;
 }
 
+float mi_model_token_score(const mi_model* m, int32_t token) {
+    if (!m || token < 0 || token >= (int)m->impl.token_score.size()) return 0.0f;
+    return m->impl.token_score[token];
+}
+
+int32_t mi_model_token_type(const mi_model* m, int32_t token) {
+    if (!m || token < 0 || token >= (int)m->impl.tokens.size()) return -1;
+    if (token >= (int)m->impl.token_type.size()) return 1;   // LLAMA_TOKEN_TYPE_NORMAL
+    return m->impl.token_type[token];
+}
+
+int32_t mi_model_n_tokens(const mi_model* m) { return m ? (int32_t)m->impl.tokens.size() : -1; }
+
+int32_t mi_model_tokenizer(const mi_model* m, char* buf, int32_t size) {
+    if (!m) return -1;
+    const std::string& s = m->impl.tok_model;
+    if (buf && size > 0) {
+        const int n = std::min<int>((int)s.size(), size - 1);
+        std::memcpy(buf, s.data(), n);
+        buf[n] = 0;
+    }
+    return (int32_t)s.size();
+}
+
 int32_t mi_model_token_text(const mi_model* m, int32_t token, char* buf, int32_t size) {
     if (!m || token < 0 || token >= (int)m->impl.tokens.size()) { set_last_error("token out of range"); return -1; }
     const std::string& s = m->impl.tokens[token];

@@ -187,6 +187,9 @@ void Model::load(const uint8_t* data, size_t size, const mi_model_params& p) {
     if (const GgufValue* tv = gguf.get("tokenizer.ggml.tokens")) tokens = tv->arr_s;
     if (const GgufValue* tt = gguf.get("tokenizer.ggml.token_type"))
         for (double d : tt->arr_num) token_type.push_back((int)d);
+    if (const GgufValue* ts = gguf.get("tokenizer.ggml.scores"))
+        for (double d : ts->arr_num) token_score.push_back((float)d);
+    tok_model = gguf.get_str("tokenizer.ggml.model", "llama");
     hp.n_vocab = (int)tokens.size();
     if (const GgufTensor* te = gguf.tensor("token_embd.weight")) hp.n_vocab = (int)te->ne[1];
     bos = (int)gguf.get_int("tokenizer.ggml.bos_token_id", 1);

@@ -70,6 +70,8 @@ struct Model {
     Gguf gguf;
     std::vector<std::string> tokens;
     std::vector<int> token_type;
+    std::vector<float> token_score;     // SPM merge scores (tokenizer.ggml.scores)
+    std::string tok_model;              // tokenizer.ggml.model ("llama" = SPM, "gpt2" = BPE)
     int bos = -1, eos = -1, eot = -1;
     bool add_bos = true;
     int device = 0;

@@ -50,6 +50,10 @@ _SIGS = {
     "mi_model_add_bos": (C.c_int32, [_P]),
     "mi_model_token_is_eog": (C.c_int32, [_P, C.c_int32]),
     "mi_model_token_text": (C.c_int32, [_P, C.c_int32, C.c_char_p, C.c_int32]),
+    "mi_model_n_tokens": (C.c_int32, [_P]),
+    "mi_model_token_score": (C.c_float, [_P, C.c_int32]),
+    "mi_model_token_type": (C.c_int32, [_P, C.c_int32]),
+    "mi_model_tokenizer": (C.c_int32, [_P, C.c_char_p, C.c_int32]),
     "mi_model_meta_str": (C.c_int32, [_P, C.c_char_p, C.c_char_p, C.c_int32]),
     "mi_model_weight_bytes": (C.c_int64, [_P]),
     "mi_model_arena": (C.c_int32, [_P, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]),

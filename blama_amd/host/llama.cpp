@@ -1,0 +1,674 @@
+// bl::llama host surface on the MI355X engine (see llama.hpp for the mirrored reference files).
+#include "llama.hpp"
+
+#include "mi_engine.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <functional>
+#include <queue>
+#include <sstream>
+
+namespace bl::llama {
+
+namespace {
+// throw_ex{} << ... in the reference (bstl/throw_stdex.hpp): std::runtime_error with the text.
+struct Fail {
+    std::ostringstream os;
+    template <typename T>
+    Fail& operator<<(const T& v) {
+        os << v;
+        return *this;
+    }
+    [[noreturn]] void raise() { throw std::runtime_error(os.str()); }
+};
+#define BL_THROW(msg) \
+    do { Fail f_; f_ << msg; f_.raise(); } while (0)
+
+std::string last_error() {
+    const char* e = mi_last_error();
+    return e ? std::string(e) : std::string();
+}
+
+constexpr int kTypeNormal = 1, kTypeUnknown = 2, kTypeControl = 3, kTypeUserDefined = 4, kTypeByte = 6;
+const std::string kSpace = "\xe2\x96\x81";   // U+2581, SentencePiece's whitespace
+
+std::string escape_whitespace(std::string_view s) {
+    std::string o;
+    o.reserve(s.size() * 2);
+    for (char c : s) {
+        if (c == ' ') o += kSpace;
+        else o += c;
+    }
+    return o;
+}
+std::string unescape_whitespace(const std::string& s) {
+    std::string o;
+    o.reserve(s.size());
+    for (size_t i = 0; i < s.size();) {
+        if (s.compare(i, kSpace.size(), kSpace) == 0) {
+            o += ' ';
+            i += kSpace.size();
+        } else {
+            o += s[i++];
+        }
+    }
+    return o;
+}
+size_t utf8_len(unsigned char c) {
+    static const size_t lut[16] = {1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 2, 2, 3, 4};
+    return lut[c >> 4];
+}
+}  // namespace
+
+// ------------------------------------------------------------------ Model ---
+Model::Model(const std::string& gguf, Params params) : m_params(params) {
+    if (!params.gpu)
+        BL_THROW("Model::Params::gpu=false (the CPU verifier) is not served by the MI355X engine");
+    mi_model_params mp{0, 0, params.vocabOnly ? 1 : 0, 0};
+    m_model = mi_model_load(gguf.c_str(), &mp);
+    if (!m_model) BL_THROW("Failed to load model " << gguf << ": " << last_error());
+    m_vocab.load();
+}
+
+Model::Model(const void* data, size_t size, Params params) : m_params(params) {
+    if (!params.gpu)
+        BL_THROW("Model::Params::gpu=false (the CPU verifier) is not served by the MI355X engine");
+    mi_model_params mp{0, 0, params.vocabOnly ? 1 : 0, 0};
+    m_model = mi_model_load_from_memory(data, size, &mp);
+    if (!m_model) BL_THROW("Failed to load model: " << last_error());
+    m_vocab.load();
+}
+
+Model::~Model() {
+    if (m_model) mi_model_free(m_model);
+}
+
+uint32_t Model::trainCtxLength() const noexcept {
+    // a vocab-only model has no weights and reports no training context (t-integration.cpp:35)
+    return m_params.vocabOnly ? 0u : (uint32_t)std::max(0, mi_model_n_ctx_train(m_model));
+}
+
+bool Model::shouldAddBosToken() const noexcept { return mi_model_add_bos(m_model) == 1; }
+
+// ------------------------------------------------------------------ Vocab ---
+Vocab::Vocab(const Model& model) : m_model(model) {}
+
+void Vocab::load() {
+    const mi_model* m = m_model.mmodel();
+    const int n = mi_model_n_tokens(m);
+    m_text.resize(std::max(0, n));
+    m_score.resize(m_text.size());
+    m_type.resize(m_text.size());
+    std::string buf;
+    for (int i = 0; i < n; ++i) {
+        const int len = mi_model_token_text(m, i, nullptr, 0);
+        buf.assign((size_t)len + 1, '\0');
+        mi_model_token_text(m, i, buf.data(), len + 1);
+        m_text[i].assign(buf.data(), (size_t)len);
+        m_score[i] = mi_model_token_score(m, i);
+        m_type[i] = mi_model_token_type(m, i);
+        m_index.emplace(m_text[i], i);
+    }
+    m_bos = mi_model_token_bos(m);
+    m_eos = mi_model_token_eos(m);
+    for (int i = 0; i < n; ++i)
+        if (m_type[i] == kTypeUnknown) { m_unk = i; break; }
+    char tk[32] = {0};
+    mi_model_tokenizer(m, tk, sizeof tk);
+    m_spm = std::string(tk) == "llama";
+    m_loaded = true;
+}
+
+int32_t Vocab::nTokens() const noexcept { return (int32_t)m_text.size(); }
+bool Vocab::isEog(Token token) const noexcept { return mi_model_token_is_eog(m_model.mmodel(), token) == 1; }
+Token Vocab::decoderStartToken() const noexcept { return m_bos; }
+
+std::string Vocab::tokenToString(Token token, bool special) const {
+    if (token < 0 || token >= nTokens()) return {};
+    const std::string& t = m_text[token];
+    switch (m_type[token]) {
+    case kTypeNormal: return unescape_whitespace(t);
+    case kTypeUnknown: return "\xe2\x96\x85";   // U+2585, what llama_token_to_piece prints
+    case kTypeControl: return special ? t : std::string();
+    case kTypeUserDefined: return t;
+    case kTypeByte:
+        if (t.size() == 6 && t.rfind("<0x", 0) == 0) return std::string(1, (char)std::stoi(t.substr(3, 2), nullptr, 16));
+        return t;
+    default: return {};
+    }
+}
+
+std::vector<Token> Vocab::tokenize(std::string_view text, bool addSpecial, bool parseSpecial) const {
+    if (!m_spm) BL_THROW("tokenizer: only SentencePiece (tokenizer.ggml.model = llama) vocabularies are served");
+    std::vector<Token> out;
+    if (addSpecial && m_model.shouldAddBosToken() && m_bos >= 0) out.push_back(m_bos);
+
+    // 1. split the text at special-token texts (control tokens only when parseSpecial), longest first
+    struct Frag { bool tok; Token id; std::string_view s; };
+    std::vector<Frag> frags{{false, -1, text}};
+    std::vector<Token> specials;
+    for (int i = 0; i < nTokens(); ++i)
+        if ((m_type[i] == kTypeControl && parseSpecial) || m_type[i] == kTypeUserDefined)
+            if (!m_text[i].empty()) specials.push_back(i);
+    std::stable_sort(specials.begin(), specials.end(),
+                     [&](Token a, Token b) { return m_text[a].size() > m_text[b].size(); });
+    for (Token sp : specials) {
+        const std::string& st = m_text[sp];
+        std::vector<Frag> next;
+        for (const Frag& f : frags) {
+            if (f.tok) { next.push_back(f); continue; }
+            size_t pos = 0;
+            while (true) {
+                const size_t hit = f.s.find(st, pos);
+                if (hit == std::string_view::npos) break;
+                if (hit > pos) next.push_back({false, -1, f.s.substr(pos, hit - pos)});
+                next.push_back({true, sp, {}});
+                pos = hit + st.size();
+            }
+            if (pos < f.s.size()) next.push_back({false, -1, f.s.substr(pos)});
+        }
+        frags.swap(next);
+    }
+
+    // 2. SentencePiece BPE over each raw fragment (llm_tokenizer_spm semantics)
+    bool prev_special = true;   // a raw fragment at the start or after a special token gets a space prefix
+    for (const Frag& f : frags) {
+        if (f.tok) {
+            out.push_back(f.id);
+            prev_special = true;
+            continue;
+        }
+        std::string s = prev_special ? std::string(" ") : std::string();
+        s += f.s;
+        s = escape_whitespace(s);
+        prev_special = false;
+        struct Sym { int prev, next; size_t off, n; };
+        std::vector<Sym> sym;
+        for (size_t off = 0; off < s.size();) {
+            const size_t n = std::min(utf8_len((unsigned char)s[off]), s.size() - off);
+            sym.push_back({(int)sym.size() - 1, (int)sym.size() + 1, off, n});
+            off += n;
+        }
+        if (sym.empty()) continue;
+        sym.back().next = -1;
+        struct Bigram { int left, right; float score; size_t size; };
+        auto worse = [](const Bigram& a, const Bigram& b) {
+            return a.score < b.score || (a.score == b.score && a.left > b.left);
+        };
+        std::priority_queue<Bigram, std::vector<Bigram>, decltype(worse)> q(worse);
+        std::unordered_map<std::string, std::pair<int, int>> merged_from;
+        auto try_pair = [&](int l, int r) {
+            if (l < 0 || r < 0) return;
+            const std::string t = s.substr(sym[l].off, sym[l].n + sym[r].n);
+            auto it = m_index.find(t);
+            if (it == m_index.end()) return;
+            q.push({l, r, m_score[it->second], t.size()});
+            merged_from[t] = {l, r};
+        };
+        for (size_t i = 1; i < sym.size(); ++i) try_pair((int)i - 1, (int)i);
+        while (!q.empty()) {
+            const Bigram b = q.top();
+            q.pop();
+            Sym& L = sym[b.left];
+            Sym& R = sym[b.right];
+            if (L.n == 0 || R.n == 0 || L.n + R.n != b.size) continue;   // stale
+            L.n += R.n;
+            R.n = 0;
+            L.next = R.next;
+            if (R.next >= 0) sym[R.next].prev = b.left;
+            try_pair(L.prev, b.left);
+            try_pair(b.left, L.next);
+        }
+        std::function<void(const Sym&)> emit = [&](const Sym& y) {
+            const std::string t = s.substr(y.off, y.n);
+            auto it = m_index.find(t);
+            if (it != m_index.end()) { out.push_back(it->second); return; }
+            auto mf = merged_from.find(t);
+            if (mf == merged_from.end()) {   // byte fallback
+                for (unsigned char c : t) {
+                    char hex[8];
+                    std::snprintf(hex, sizeof hex, "<0x%02X>", c);
+                    auto bt = m_index.find(hex);
+                    out.push_back(bt != m_index.end() ? bt->second : m_unk);
+                }
+                return;
+            }
+            emit(sym[mf->second.first]);
+            emit(sym[mf->second.second]);
+        };
+        for (int i = 0; i != -1; i = sym[i].next) emit(sym[i]);
+    }
+    return out;
+}
+
+// ---------------------------------------------------------------- Sampler ---
+Sampler::Sampler(Model& model, const Params& params) : m_model(model), m_params(params), m_rng(params.rngSeed) {
+    if (!params.grammar.empty()) BL_THROW("grammar-constrained sampling is not served by this build");
+}
+
+void Sampler::accept(Token id, bool) {
+    m_prev.push_back(id);
+    const size_t w = (size_t)std::max(0, m_params.repetitionPenalty.numTokens);
+    if (m_prev.size() > w) m_prev.erase(m_prev.begin(), m_prev.end() - (std::ptrdiff_t)w);
+}
+
+void Sampler::reset() {
+    m_prev.clear();
+    m_rng.seed(m_params.rngSeed);   // llama_sampler_dist reset re-seeds
+}
+
+namespace {
+void softmax(std::vector<Sampler::Candidate>& c) {   // sorted desc on entry
+    const float mx = c[0].logit;
+    float sum = 0.0f;
+    for (auto& x : c) {
+        x.p = std::exp(x.logit - mx);
+        sum += x.p;
+    }
+    for (auto& x : c) x.p /= sum;
+}
+}  // namespace
+
+// llama.cpp b5187 sampler chain semantics (llama-sampling.cpp), on a list sorted by logit desc.
+Token Sampler::applyChain(std::vector<Candidate>& cur) {
+    const Params& P = m_params;
+    const size_t min_keep = (size_t)std::max(0, P.minKeep);
+    for (auto& [tok, bias] : P.logitBias)
+        for (auto& c : cur)
+            if (c.id == tok) c.logit += bias;
+    if (!P.logitBias.empty())
+        std::stable_sort(cur.begin(), cur.end(), [](auto& a, auto& b) { return a.logit > b.logit; });
+    const auto& rp = P.repetitionPenalty;
+    if (rp.numTokens != 0 && !(rp.repeat == 1.0f && rp.freq == 0.0f && rp.present == 0.0f)) {
+        std::unordered_map<Token, int> cnt;
+        for (Token t : m_prev) cnt[t]++;
+        for (auto& c : cur) {
+            auto it = cnt.find(c.id);
+            if (it == cnt.end()) continue;
+            c.logit = c.logit <= 0 ? c.logit * rp.repeat : c.logit / rp.repeat;
+            c.logit -= (float)it->second * rp.freq + (it->second > 0 ? 1.0f : 0.0f) * rp.present;
+        }
+        std::stable_sort(cur.begin(), cur.end(), [](auto& a, auto& b) { return a.logit > b.logit; });
+    }
+    for (SamplingType st : P.samplerSequence) {
+        switch (st) {
+        case SamplingType::Top_K: {
+            size_t k = P.topK <= 0 ? cur.size() : (size_t)P.topK;
+            k = std::min(std::max(k, min_keep), cur.size());
+            cur.resize(k);
+            break;
+        }
+        case SamplingType::Typical_P:
+            if (P.typicalP < 1.0f) BL_THROW("typical_p < 1 is not served by this build");
+            break;
+        case SamplingType::Top_P: {
+            if (P.topP >= 1.0f) break;
+            softmax(cur);
+            float cum = 0.0f;
+            size_t last = cur.size();
+            for (size_t i = 0; i < cur.size(); ++i) {
+                cum += cur[i].p;
+                if (cum >= P.topP && i + 1 >= min_keep) { last = i + 1; break; }
+            }
+            cur.resize(last);
+            break;
+        }
+        case SamplingType::Min_P: {
+            if (P.minP <= 0.0f || cur.empty()) break;
+            const float min_logit = cur[0].logit + std::log(P.minP);
+            size_t i = 1;
+            for (; i < cur.size(); ++i)
+                if (cur[i].logit < min_logit && i >= min_keep) break;
+            cur.resize(i);
+            break;
+        }
+        case SamplingType::Temperature:
+            if (P.tempRange > 0.0f) BL_THROW("dynamic temperature is not served by this build");
+            if (P.temp <= 0.0f) {
+                cur.resize(1);   // greedy: keep the max (list is sorted)
+            } else {
+                for (auto& c : cur) c.logit /= P.temp;
+            }
+            break;
+        default: BL_THROW("Unsupported sampler type");
+        }
+    }
+    softmax(cur);
+    std::vector<float> p(cur.size());
+    for (size_t i = 0; i < cur.size(); ++i) p[i] = cur[i].p;
+    std::discrete_distribution<int> dist(p.begin(), p.end());
+    return cur[(size_t)dist(m_rng)].id;
+}
+
+Token Sampler::sample(mi_ctx* ctx) {
+    std::vector<Candidate> cur;
+    if (m_params.topK > 0 && m_params.topK <= 64 && m_params.samplerSequence.size() &&
+        m_params.samplerSequence[0] == SamplingType::Top_K) {
+        const int k = m_params.topK;
+        std::vector<int32_t> ids(k);
+        std::vector<float> lg(k);
+        if (mi_topk(ctx, -1, k, ids.data(), lg.data()) < 0) BL_THROW("sampling: " << last_error());
+        for (int i = 0; i < k; ++i) cur.push_back({ids[i], lg[i], 0.0f});
+    } else {   // full vocabulary: the chain does not start with a top-k the engine can serve
+        const float* lg = mi_logits(ctx, -1);
+        if (!lg) BL_THROW("sampling: " << last_error());
+        const int32_t n = mi_model_n_vocab(m_model.mmodel());
+        cur.resize((size_t)n);
+        for (int32_t i = 0; i < n; ++i) cur[(size_t)i] = {i, lg[i], 0.0f};
+        std::stable_sort(cur.begin(), cur.end(), [](auto& a, auto& b) { return a.logit > b.logit; });
+    }
+    if (cur.empty()) BL_THROW("no selected token during sampling - check your sampling configuration");
+    return applyChain(cur);
+}
+
+// --------------------------------------------------------------- Instance ---
+Instance::Instance(Model& model, InitParams params) : m_model(model) {
+    m_ctx = mi_ctx_create(model.mmodel(), params.ctxSize, params.batchSize, params.ubatchSize);
+    if (!m_ctx) BL_THROW("Failed to create llama context");
+}
+
+Instance::~Instance() {
+    m_session.reset();
+    if (m_ctx) mi_ctx_free(m_ctx);
+}
+
+void Instance::warmup() {
+    std::vector<Token> t;
+    if (m_model.vocab().bos() >= 0) t.push_back(m_model.vocab().bos());
+    if (m_model.vocab().eos() >= 0) t.push_back(m_model.vocab().eos());
+    if (t.empty()) t.push_back(0);
+    mi_decode(m_ctx, t.data(), (int32_t)t.size(), MI_OUT_LAST);
+    mi_kv_clear(m_ctx);
+    mi_synchronize(m_ctx);
+}
+
+Session& Instance::startSession(const Session::InitParams params) {
+    if (m_session.has_value()) BL_THROW("Session is already started. Stop it to start a new one.");
+    m_session.emplace(*this, m_ctx, params);
+    return *m_session;
+}
+
+void Instance::stopSession() noexcept { m_session.reset(); }
+
+// ---------------------------------------------------------------- Session ---
+Session::Session(Instance& instance, mi_ctx* ctx, InitParams params)
+    : m_instance(instance), m_ctx(ctx), m_params(std::move(params)) {
+    Sampler::Params sp;
+    sp.rngSeed = m_params.seed;
+    sp.topP = m_params.topP;
+    sp.temp = m_params.temperature;
+    sp.grammar = m_params.grammar;
+    m_sampler = std::make_unique<Sampler>(instance.model(), sp);
+    mi_kv_clear(m_ctx);
+    mi_synchronize(m_ctx);
+    m_state.maxTokens = mi_n_ctx(m_ctx) - 4;
+}
+
+Session::~Session() {
+    try {
+        flushPendingState();
+    } catch (...) {
+    }
+}
+
+void Session::setInitialPrompt(std::span<const Token> prompt) {
+    if (m_state.m_phase != State::Phase::Initial) BL_THROW("Session already started");
+    Token only = Token_Invalid;
+    m_state.numKeep = std::min<uint32_t>((uint32_t)prompt.size(), m_state.maxTokens);
+    if (prompt.empty()) {
+        only = m_instance.model().vocab().bos();
+        prompt = {&only, 1};
+    }
+    if (prompt.size() > m_state.maxTokens)
+        BL_THROW("Initial prompt too long. Got " << prompt.size() << " tokens, max: " << mi_n_ctx(m_ctx) - 4);
+    if (m_params.gaFactor != 1 && m_params.gaWidth % m_params.gaFactor != 0)
+        BL_THROW("Group-attention width " << m_params.gaWidth << " must be a multiple of group-attention factor "
+                                          << m_params.gaFactor);
+    doDecode(prompt, Source::InitialPrompt);
+    m_state.m_phase = State::Phase::Generating;
+}
+
+void Session::pushPrompt(std::span<const Token> prompt, std::span<const Token> postfix) {
+    if (m_state.m_phase != State::Phase::Generating) BL_THROW("Session hasn't started yet");
+    flushPendingState();
+    if (prompt.empty() && postfix.empty()) BL_THROW("Prompt and postfix are empty");
+    m_sampler->reset();
+    std::vector<Token> toks;
+    if (m_instance.model().prefixInputsWithBos()) toks.push_back(m_instance.model().vocab().bos());
+    // FIM prefix/suffix/middle tokens: this engine's vocab exposes none (the reference only
+    // warns and skips when a model lacks them, Session.cpp:134-140)
+    toks.insert(toks.end(), prompt.begin(), prompt.end());
+    toks.insert(toks.end(), postfix.begin(), postfix.end());
+    if (toks.size() > m_state.maxTokens)
+        BL_THROW("Prompt too long. Got " << toks.size() << " tokens, max: " << mi_n_ctx(m_ctx) - 4);
+    doDecode(toks, Source::InteractivePrompt);
+}
+
+TokenPrediction Session::getToken() {
+    if (m_state.m_phase != State::Phase::Generating && m_state.m_phase != State::Phase::Streaming)
+        BL_THROW("Session hasn't started yet");
+    flushPendingState();
+    m_state.m_currToken = m_sampler->sample(m_ctx);
+    if (m_instance.model().vocab().isEog(m_state.m_currToken)) m_state.m_currToken = Token_Invalid;
+    TokenPrediction p;
+    p.token = m_state.m_currToken;
+    p.logits = getLogitsFromCtx(10);
+    return p;
+}
+
+std::vector<TokenPrediction> Session::complete(CompleteParams params) {
+    if (m_state.m_phase != State::Phase::Generating) BL_THROW("Session hasn't started yet");
+    flushPendingState();
+    if (!params.prompt.empty() || !params.suffix.empty()) pushPrompt(params.prompt, params.suffix);
+    std::vector<TokenPrediction> out;
+    for (int32_t i = 0; i < params.maxTokens; ++i) {
+        TokenPrediction p = getToken();
+        if (p.token == Token_Invalid) break;
+        out.push_back(std::move(p));
+    }
+    return out;
+}
+
+Session::StreamGenerator Session::completeStream(CompleteParams params) {
+    if (m_state.m_phase != State::Phase::Generating) BL_THROW("Session hasn't started yet");
+    flushPendingState();
+    if (!params.prompt.empty() || !params.suffix.empty()) pushPrompt(params.prompt, params.suffix);
+    m_state.m_phase = State::Phase::Streaming;
+    return StreamGenerator(*this, params);
+}
+
+TokenPrediction Session::StreamGenerator::complete() {
+    if (m_session.m_state.m_phase != State::Phase::Streaming || m_status != Status::InProgress) return {};
+    TokenPrediction p = m_session.getToken();
+    if (p.token == Token_Invalid || ++m_genTokens >= m_params.maxTokens) {
+        m_session.m_state.m_phase = State::Phase::Generating;
+        m_status = Status::Completed;
+    }
+    return p;
+}
+
+std::vector<TokenPrediction> Session::fillCtx(std::span<TokenPrediction> tokens) {
+    std::vector<TokenPrediction> out;
+    out.reserve(tokens.size());
+    for (const TokenPrediction& t : tokens) {
+        pushPrompt({&t.token, 1}, {});
+        TokenPrediction r;
+        r.token = t.token;
+        r.logits = getLogitsFromCtx(t.logits);
+        out.push_back(std::move(r));
+    }
+    return out;
+}
+
+void Session::requireGenerating() const {
+    if (m_state.m_phase != State::Phase::Generating && m_state.m_phase != State::Phase::Streaming)
+        BL_THROW("Session hasn't started yet");
+}
+
+TokenDataVector Session::getLogitsFromCtx(int32_t topK) {
+    requireGenerating();
+    flushPendingState();
+    // GPU top-k in place of the full-vocabulary host copy + std::sort (Session.cpp:246-261)
+    std::vector<int32_t> ids(topK);
+    std::vector<float> lg(topK);
+    if (mi_topk(m_ctx, -1, topK, ids.data(), lg.data()) < 0) BL_THROW("top-k: " << last_error());
+    TokenDataVector r(topK);
+    for (int32_t i = 0; i < topK; ++i) r[i] = {ids[i], lg[i]};
+    return r;
+}
+
+TokenDataVector Session::getLogitsFromCtx(const TokenDataVector& tokens) {
+    requireGenerating();
+    flushPendingState();
+    // the reference scans the vocabulary in id order keeping ids in `tokens`: each id once
+    std::vector<int32_t> ids;
+    for (const TokenData& t : tokens)
+        if (t.token >= 0 && t.token < m_instance.model().vocab().nTokens()) ids.push_back(t.token);
+    std::sort(ids.begin(), ids.end());
+    ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
+    std::vector<float> lg(ids.size());
+    if (!ids.empty() && mi_gather(m_ctx, -1, ids.data(), (int32_t)ids.size(), lg.data()) < 0)
+        BL_THROW("gather: " << last_error());
+    TokenDataVector r(ids.size());
+    for (size_t i = 0; i < ids.size(); ++i) r[i] = {ids[i], lg[i]};
+    std::stable_sort(r.begin(), r.end(), [](const TokenData& a, const TokenData& b) { return a.logit > b.logit; });
+    return r;
+}
+
+std::vector<uint8_t> Session::getState() {
+    if (m_state.m_phase != State::Phase::Generating) BL_THROW("Session hasn't started yet");
+    flushPendingState();
+    const size_t n = mi_state_size(m_ctx);
+    std::vector<uint8_t> st(n);
+    if (mi_state_get(m_ctx, st.data(), n) != n) BL_THROW("Failed to get state");
+    return st;
+}
+
+bool Session::setState(std::span<uint8_t> state) {
+    if (m_state.m_phase != State::Phase::Initial) BL_THROW("Session already started");
+    if (mi_state_set(m_ctx, state.data(), state.size()) != state.size()) BL_THROW("Failed to set state");
+    m_state.m_phase = State::Phase::Generating;
+    return true;
+}
+
+void Session::doDecode(std::span<const Token> tokens, Source src) {
+    if (tokens.size() > m_state.maxTokens) tokens = tokens.first(m_state.maxTokens);
+    const uint32_t ctxLen = mi_n_ctx(m_ctx);
+    if (m_params.gaFactor == 1) {
+        // context shift: keep numKeep, drop half of the rest, slide the tail down (K re-rotated)
+        if (m_state.numPast + tokens.size() >= ctxLen) {
+            if (!m_params.infiniteContext) BL_THROW("context limit of " << ctxLen << " reached");
+            const uint32_t numLeft = m_state.numPast - m_state.numKeep;
+            const int numDiscard = (int)(numLeft / 2);
+            mi_kv_seq_rm(m_ctx, (int32_t)m_state.numKeep, (int32_t)(m_state.numKeep + numDiscard));
+            mi_kv_seq_add(m_ctx, (int32_t)(m_state.numKeep + numDiscard), (int32_t)m_state.numPast, -numDiscard);
+            m_state.numPast -= (uint32_t)numDiscard;
+        }
+    } else {
+        // Self-Extend group attention
+        const uint32_t gaFactor = m_params.gaFactor, gaWidth = m_params.gaWidth;
+        while (m_state.numPast >= m_state.gaIndex + gaWidth) {
+            const int ib = (int)((gaFactor * m_state.gaIndex) / gaWidth);
+            const int bd = (int)((gaWidth / gaFactor) * (gaFactor - 1));
+            const int dd = (int)(gaWidth / gaFactor) - ib * bd - (int)gaWidth;
+            const int gi = (int)m_state.gaIndex;
+            mi_kv_seq_add(m_ctx, gi, (int32_t)m_state.numPast, ib * bd);
+            mi_kv_seq_div(m_ctx, gi + ib * bd, gi + ib * bd + (int)gaWidth, (int)gaFactor);
+            mi_kv_seq_add(m_ctx, gi + ib * bd + (int)gaWidth, (int32_t)m_state.numPast + ib * bd, dd);
+            m_state.numPast -= (uint32_t)bd;
+            m_state.gaIndex += gaWidth / gaFactor;
+        }
+    }
+    for (Token t : tokens) m_sampler->accept(t, src == Source::Generated);
+    const uint32_t batch = mi_n_batch(m_ctx);
+    while (!tokens.empty()) {
+        auto b = tokens.size() > batch ? tokens.first(batch) : tokens;
+        tokens = tokens.subspan(b.size());
+        if (mi_decode(m_ctx, b.data(), (int32_t)b.size(), MI_OUT_LAST) != 0) BL_THROW("Failed to decode tokens");
+        m_state.numPast += (uint32_t)b.size();
+    }
+}
+
+void Session::flushPendingState() {
+    if (m_state.m_currToken != Token_Invalid) {
+        const Token t = m_state.m_currToken;
+        m_state.m_currToken = Token_Invalid;
+        doDecode({&t, 1}, Source::Generated);
+    }
+}
+
+void Session::resetSampler(const Sampler::Params& params) {
+    m_sampler = std::make_unique<Sampler>(m_instance.model(), params);
+}
+
+// ---------------------------------------------------------- LogitComparer ---
+namespace {
+// softmax over a list sorted desc: its first logit is the max (LogitComparer.cpp:8-28)
+std::unordered_map<Token, float> probs(const TokenDataVector& d) {
+    std::unordered_map<Token, float> r(d.size());
+    const float top = d[0].logit;
+    float z = 0.0f;
+    for (const TokenData& t : d) {
+        const float e = std::exp(t.logit - top);
+        r[t.token] = e;
+        z += e;
+    }
+    for (auto& kv : r) kv.second /= z;
+    return r;
+}
+float sum_sq(const TokenData* d, size_t n) {
+    float s = 0.0f;
+    for (size_t i = 0; i < n; ++i) s += d[i].logit * d[i].logit;
+    return s;
+}
+float kl_to(const std::unordered_map<Token, float>& P, const std::unordered_map<Token, float>& M) {
+    float kl = 0.0f;
+    for (const auto& [tok, p] : P) {
+        auto it = M.find(tok);
+        if (p > 0.0f && it != M.end() && it->second > 0.0f) kl += p * std::log(p / it->second);
+    }
+    return kl;
+}
+}  // namespace
+
+ComparisonMetrics LogitComparer::compare(const TokenDataVector& a, const TokenDataVector& b) {
+    ComparisonMetrics m;
+    m.top1Match = a[0].token == b[0].token ? 1.0f : 0.0f;
+    const size_t n = std::min(a.size(), b.size());
+    const float da = sum_sq(a.data(), n), db = sum_sq(b.data(), n);
+    m.distance = std::fabs(da - db) / std::max(da, db);
+    const auto pa = probs(a), pb = probs(b);
+    std::unordered_map<Token, float> mid;   // Jensen-Shannon over the shared ids, natural log
+    for (const auto& [tok, p] : pa) {
+        auto it = pb.find(tok);
+        if (it != pb.end()) mid[tok] = (p + it->second) / 2.0f;
+    }
+    m.jsd = (kl_to(pa, mid) + kl_to(pb, mid)) / 2.0f;
+    return m;
+}
+
+float LogitComparer::logitSimilarity(const TokenDataVector& a, const TokenDataVector& b) {
+    std::unordered_map<Token, float> lb;
+    for (const TokenData& t : b) lb[t.token] = t.logit;
+    float num = 0.0f, den = 0.0f;
+    for (const TokenData& t : a) {
+        const float w = std::fabs(t.logit);
+        float sim = 0.0f;
+        auto it = lb.find(t.token);
+        if (it != lb.end()) sim = 1.0f - std::fabs(t.logit - it->second) / std::fabs(std::max(t.logit, it->second));
+        num += w * sim;
+        den += w;
+    }
+    return den > 0.0f ? num / den : 0.0f;
+}
+
+float MetricsAggregator::pushAndVerify(std::span<const ComparisonMetrics> m) {
+    metrics.insert(metrics.end(), m.begin(), m.end());
+    double total = 0.0;
+    for (const ComparisonMetrics& x : metrics) total += 0.5 * (1.0f - x.distance) + 0.5 * (1.0f - x.jsd);
+    return float(total / metrics.size());
+}
+
+}  // namespace bl::llama

@@ -1,0 +1,277 @@
+// bl::llama host surface on the MI355X engine.
+//
+// This is the C++ layer Blama's L4/L5 call (reference inference/code/llama/*.hpp). The names,
+// parameter structs, call order and error messages are kept, so Server code and tests written
+// against the reference compile against this header unchanged. Below it, every decode, logit
+// extraction and KV operation goes through the engine's C ABI (include/mi_engine.h). There is
+// no llama.cpp here.
+//
+// What is mirrored (reference file:line):
+//   Token / TokenData / TokenDataVector       Token.hpp:9-17
+//   TokenPrediction                           Session.hpp:20-27
+//   Model{Params{gpu, vocabOnly, prefixInputsWithBos}}   Model.hpp:26-58
+//   Vocab{tokenize, isEog, nTokens, tokenToString}       Vocab.hpp:16-34
+//   Instance{InitParams, warmup, startSession, stopSession}   Instance.hpp:19-51
+//   Session{InitParams, setInitialPrompt, complete, completeStream, fillCtx,
+//           getState, setState, resetSampler}             Session.hpp:29-130
+//   Sampler{Params, sample, accept, reset}                Sampler.hpp:22-115
+//   LogitComparer / MetricsAggregator                     LogitComparer.hpp:12-34
+//
+// Not served (engine scope): Model::Params::gpu=false (the reference's CPU
+// verifier), LoRA, control vectors, grammar constraints, encoder models, mirostat/XTC/infill.
+#pragma once
+#include <cstdint>
+#include <memory>
+#include <optional>
+#include <random>
+#include <span>
+#include <stdexcept>
+#include <string>
+#include <string_view>
+#include <unordered_map>
+#include <vector>
+
+struct mi_model;
+struct mi_ctx;
+
+namespace bl::llama {
+
+using Token = std::int32_t;
+inline constexpr Token Token_Invalid = -1;
+
+struct TokenData {
+    Token token;
+    float logit;
+};
+using TokenDataVector = std::vector<TokenData>;
+
+struct TokenPrediction {
+    Token token = Token_Invalid;
+    TokenDataVector logits;
+    explicit operator bool() const { return token != Token_Invalid; }
+};
+
+class Model;
+
+class Vocab {
+public:
+    explicit Vocab(const Model& model);
+    // SPM tokenisation (llama.cpp llm_tokenizer_spm) of `text`; addSpecial prepends BOS when the
+    // model asks for it, parseSpecial matches control-token texts (e.g. "<s>") as single tokens.
+    std::vector<Token> tokenize(std::string_view text, bool addSpecial, bool parseSpecial) const;
+    Token decoderStartToken() const noexcept;
+    bool isEog(Token token) const noexcept;
+    int32_t nTokens() const noexcept;
+    std::string tokenToString(Token token, bool special = true) const;
+    Token bos() const noexcept { return m_bos; }
+    Token eos() const noexcept { return m_eos; }
+
+private:
+    void load();
+    const Model& m_model;
+    std::vector<std::string> m_text;
+    std::vector<float> m_score;
+    std::vector<int> m_type;
+    std::unordered_map<std::string, Token> m_index;
+    Token m_bos = -1, m_eos = -1, m_unk = 0;
+    bool m_spm = true;
+    bool m_loaded = false;
+    friend class Model;
+};
+
+class Model {
+public:
+    struct Params {
+        bool gpu = true;                   // Model.hpp:29; false = the reference's CPU verifier (not served)
+        bool vocabOnly = false;
+        bool prefixInputsWithBos = false;
+        bool operator==(const Params& other) const noexcept = default;
+    };
+    Model(const std::string& gguf, Params params);
+    // Load from a GGUF image in memory (tests, replicas).
+    Model(const void* data, size_t size, Params params);
+    ~Model();
+    Model(const Model&) = delete;
+    Model& operator=(const Model&) = delete;
+
+    const Params& params() const noexcept { return m_params; }
+    uint32_t trainCtxLength() const noexcept;
+    bool shouldAddBosToken() const noexcept;
+    bool hasEncoder() const noexcept { return false; }
+    bool prefixInputsWithBos() const noexcept { return m_params.prefixInputsWithBos; }
+
+    mi_model* mmodel() noexcept { return m_model; }
+    const mi_model* mmodel() const noexcept { return m_model; }
+    const Vocab& vocab() const noexcept { return m_vocab; }
+
+private:
+    const Params m_params;
+    mi_model* m_model = nullptr;
+    Vocab m_vocab{*this};
+};
+
+class Sampler {
+public:
+    enum class SamplingType { Top_K, Top_P, Min_P, Typical_P, Temperature, XTC, Infill };
+    struct Params {
+        uint32_t rngSeed = 0;
+        int32_t minKeep = 0;
+        int32_t topK = 40;
+        float topP = 0.95f;
+        float minP = 0.05f;
+        float tfsZ = 1.00f;
+        float typicalP = 1.00f;
+        float temp = 0.80f;
+        float tempRange = 0.00f;
+        float tempExp = 1.00f;
+        struct RepetitionPenalty {
+            int32_t numTokens = 64;
+            float repeat = 1.00f;
+            float freq = 0.00f;
+            float present = 0.00f;
+        } repetitionPenalty;
+        std::vector<SamplingType> samplerSequence = {SamplingType::Top_K, SamplingType::Typical_P,
+                                                     SamplingType::Top_P, SamplingType::Min_P,
+                                                     SamplingType::Temperature};
+        std::string grammar;
+        std::vector<std::pair<Token, float>> logitBias;
+    };
+    Sampler(Model& model, const Params& params);
+
+    // Samples from the context's last logits.  The chain runs on the engine's sorted top-k
+    // (k = max(topK, 64 cap)); the reference chain's first stage is top_k(topK), so both see
+    // the same candidate set (ties broken by id, which std::sort leaves unspecified).
+    Token sample(mi_ctx* ctx);
+    void accept(Token id, bool acceptGrammar);
+    void reset();
+
+    // The chain applied to a candidate list sorted by logit descending (exposed for tests).
+    struct Candidate { Token id; float logit; float p; };
+    Token applyChain(std::vector<Candidate>& cur);
+
+private:
+    Model& m_model;
+    Params m_params;
+    std::mt19937 m_rng;
+    std::vector<Token> m_prev;          // penalty window
+};
+
+class Instance;
+
+class Session {
+public:
+    struct InitParams {
+        uint32_t gaFactor = 1;
+        uint32_t gaWidth = 512;
+        bool infiniteContext = true;
+        uint32_t seed = 0;
+        std::string grammar;
+        float temperature = 0.80f;
+        float topP = 0.95f;
+    };
+    Session(Instance& instance, mi_ctx* ctx, InitParams params);
+    Session(const Session&) = delete;
+    Session& operator=(const Session&) = delete;
+    ~Session();
+
+    void setInitialPrompt(std::span<const Token> prompt);
+    bool setState(std::span<uint8_t> state);
+    struct CompleteParams {
+        std::span<const Token> prompt;
+        std::span<const Token> suffix;
+        int32_t maxTokens = 0;
+    };
+    std::vector<TokenPrediction> complete(CompleteParams params);
+
+    class StreamGenerator {
+    public:
+        StreamGenerator(Session& session, CompleteParams params) : m_session(session), m_params(params) {}
+        TokenPrediction complete();
+        void abort() { m_status = Status::Aborted; }
+        enum class Status { InProgress, Completed, Aborted };
+        Status status() const { return m_status; }
+
+    private:
+        Session& m_session;
+        CompleteParams m_params;
+        int32_t m_genTokens = 0;
+        Status m_status = Status::InProgress;
+    };
+    StreamGenerator completeStream(CompleteParams params);
+
+    std::vector<TokenPrediction> fillCtx(std::span<TokenPrediction> tokens);
+    std::vector<uint8_t> getState();
+    void resetSampler(const Sampler::Params& params);
+
+private:
+    enum class Source { InitialPrompt, InteractivePrompt, Generated };
+    void pushPrompt(std::span<const Token> prompt, std::span<const Token> postfix = {});
+    TokenPrediction getToken();
+    void doDecode(std::span<const Token> tokens, Source src);
+    void flushPendingState();
+    TokenDataVector getLogitsFromCtx(int32_t topK);
+    TokenDataVector getLogitsFromCtx(const TokenDataVector& tokens);
+    void requireGenerating() const;
+
+    struct State {
+        enum class Phase { Initial, Generating, Streaming };
+        Phase m_phase = Phase::Initial;
+        Token m_currToken = Token_Invalid;
+        unsigned maxTokens = 0;
+        unsigned numKeep = 0;
+        uint32_t gaIndex = 0;
+        uint32_t numPast = 0;
+    };
+
+    Instance& m_instance;
+    mi_ctx* m_ctx;
+    std::unique_ptr<Sampler> m_sampler;
+    InitParams m_params;
+    State m_state;
+};
+
+class Instance {
+public:
+    struct InitParams {
+        uint32_t ctxSize = 0;
+        uint32_t batchSize = 2048;
+        uint32_t ubatchSize = 512;
+        bool flashAttn = false;
+    };
+    Instance(Model& model, InitParams params);
+    ~Instance();
+    Instance(const Instance&) = delete;
+    Instance& operator=(const Instance&) = delete;
+
+    void warmup();
+    Session& startSession(const Session::InitParams params);
+    void stopSession() noexcept;
+    Model& model() const noexcept { return m_model; }
+    mi_ctx* mctx() noexcept { return m_ctx; }
+
+private:
+    Model& m_model;
+    mi_ctx* m_ctx = nullptr;
+    std::optional<Session> m_session;
+};
+
+struct ComparisonMetrics {
+    float top1Match;
+    float distance;
+    float jsd;
+};
+
+class LogitComparer {
+public:
+    static ComparisonMetrics compare(const TokenDataVector& data1, const TokenDataVector& data2);
+    static float logitSimilarity(const TokenDataVector& data1, const TokenDataVector& data2);
+};
+
+struct MetricsAggregator {
+    float pushAndVerify(std::span<const ComparisonMetrics> m);
+
+private:
+    std::vector<ComparisonMetrics> metrics;
+};
+
+}  // namespace bl::llama

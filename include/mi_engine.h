@@ -62,6 +62,13 @@ int32_t mi_model_add_bos(const mi_model* model);
 int32_t mi_model_token_is_eog(const mi_model* model, int32_t token);
 /* Text of a vocabulary entry (raw GGUF piece); returns its length or < 0. */
 int32_t mi_model_token_text(const mi_model* model, int32_t token, char* buf, int32_t size);
+/* Vocabulary for the host tokenizer (Vocab.cpp:37-72 -> llama_tokenize / llama_token_to_piece):
+ * entries in tokenizer.ggml.tokens, SPM merge score, llama_token_type (1 normal, 2 unknown,
+ * 3 control, 4 user-defined, 5 unused, 6 byte), and tokenizer.ggml.model ("llama" = SPM). */
+int32_t mi_model_n_tokens(const mi_model* model);
+float mi_model_token_score(const mi_model* model, int32_t token);
+int32_t mi_model_token_type(const mi_model* model, int32_t token);
+int32_t mi_model_tokenizer(const mi_model* model, char* buf, int32_t size);
 int32_t mi_model_meta_str(const mi_model* model, const char* key, char* buf, int32_t size);
 /* Bytes of quantised weights a decode step streams (all tensors but tok_embd). */
 int64_t mi_model_weight_bytes(const mi_model* model);

@@ -1,5 +1,5 @@
 set -o pipefail
-O=gpurun_out/r01i; mkdir -p $O
+O=gpurun_out/r01j; mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread > $O/pytest.log 2>&1; rc=$?
 echo "pytest rc $rc"; tail -4 $O/pytest.log

@@ -1,0 +1,273 @@
+// Tests of the bl::llama host surface (blama_amd/host) in the shape of the reference's own tests:
+// inference/test/t-LogitComparer.cpp and t-integration.cpp.  Models are synthetic GGUFs written
+// by the pytest wrapper (tests/test_host.py), so the reference's gpt2 text KATs (" Bush", ...)
+// become token-level checks.
+//
+// usage: t_bl_llama [cpu] [gpu] --model=<gguf> --vocab=<gguf> --out=<file>
+#include "llama.hpp"
+#include "minitest.hpp"
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+
+namespace {
+std::string g_model, g_vocab, g_out;
+void setup(int argc, char** argv, std::vector<std::string>& groups) {
+    for (int i = 1; i < argc; ++i) {
+        const std::string a = argv[i];
+        if (a.rfind("--model=", 0) == 0) g_model = a.substr(8);
+        else if (a.rfind("--vocab=", 0) == 0) g_vocab = a.substr(8);
+        else if (a.rfind("--out=", 0) == 0) g_out = a.substr(6);
+        else groups.push_back(a);
+    }
+}
+using namespace bl::llama;
+const std::vector<Token> kPrompt = {1, 300, 301, 302, 303, 400, 77, 5};
+}  // namespace
+
+// ---------------------------------------------------------------- CPU ----
+TEST_CASE_G("compare - no model", "cpu") {   // t-LogitComparer.cpp:13-39
+    TokenDataVector tdv1, tdv2;
+    float logitValue = 17.5f;
+    for (int32_t i = 0; i < 10; i++) {
+        tdv1.push_back({i, logitValue});
+        tdv2.push_back({i, logitValue});
+        logitValue -= 0.5f;
+    }
+    CHECK(LogitComparer::logitSimilarity(tdv1, tdv2) == 1.0f);
+    auto metrics = LogitComparer::compare(tdv1, tdv2);
+    CHECK(metrics.top1Match == 1.0f);
+    CHECK(metrics.distance == 0.0f);
+    CHECK(metrics.jsd == 0.0f);
+    MetricsAggregator agg;
+    CHECK(agg.pushAndVerify({&metrics, 1}) == 1.0f);
+}
+
+TEST_CASE_G("compare - perturbed", "cpu") {
+    TokenDataVector a, b;
+    for (int32_t i = 0; i < 10; i++) {
+        a.push_back({i, 12.0f - i});
+        b.push_back({i == 0 ? 1 : i == 1 ? 0 : i, 12.0f - i + (i == 3 ? 0.25f : 0.0f)});
+    }
+    auto m = LogitComparer::compare(a, b);
+    CHECK(m.top1Match == 0.0f);   // ids 0 and 1 swapped at the top
+    CHECK(m.distance > 0.0f && m.distance < 0.01f);
+    CHECK(m.jsd > 0.0f && m.jsd < 0.2f);
+    const float sim = LogitComparer::logitSimilarity(a, b);
+    CHECK(sim < 1.0f && sim > 0.9f);
+    MetricsAggregator agg;
+    const float s1 = agg.pushAndVerify({&m, 1});
+    auto same = LogitComparer::compare(a, a);
+    const float s2 = agg.pushAndVerify({&same, 1});   // running mean over both steps
+    CHECK(s2 > s1 && s2 < 1.0f);
+}
+
+TEST_CASE_G("sampler chain", "cpu") {
+    REQUIRE(!g_vocab.empty());
+    Model model(g_vocab, {.vocabOnly = true});
+    auto make = [](std::vector<Sampler::Candidate>& c) {
+        c.clear();
+        for (int i = 0; i < 40; ++i) c.push_back({100 + i, 8.0f - 0.25f * i, 0.0f});
+    };
+    std::vector<Sampler::Candidate> c;
+    Sampler::Params greedy;
+    greedy.temp = 0.0f;
+    Sampler g(model, greedy);
+    make(c);
+    CHECK(g.applyChain(c) == 100);                  // temp <= 0: the top candidate
+    Sampler::Params p;
+    p.rngSeed = 1234;
+    Sampler s1(model, p), s2(model, p);
+    std::vector<Token> a, b;
+    for (int i = 0; i < 16; ++i) {
+        make(c); a.push_back(s1.applyChain(c));
+        make(c); b.push_back(s2.applyChain(c));
+    }
+    CHECK(a == b);                                  // same seed, same draws
+    s1.reset();
+    std::vector<Token> a2;
+    for (int i = 0; i < 16; ++i) { make(c); a2.push_back(s1.applyChain(c)); }
+    CHECK(a2 == a);                                 // reset re-seeds (pushPrompt semantics)
+    for (Token t : a) CHECK(t >= 100 && t < 140);
+    // min_p 0.05 at temp 1 keeps logits >= top + ln 0.05 = top - 3.0: at most 13 candidates
+    Sampler::Params q;
+    q.temp = 1.0f;
+    q.topP = 1.0f;
+    Sampler s3(model, q);
+    int maxid = 0;
+    for (int i = 0; i < 400; ++i) { make(c); maxid = std::max(maxid, s3.applyChain(c) - 100); }
+    CHECK(maxid <= 12);
+}
+
+TEST_CASE_G("vocab only", "cpu") {   // t-integration.cpp:25-43
+    REQUIRE(!g_vocab.empty());
+    Model model(g_vocab, {.vocabOnly = true});
+    CHECK(model.params().gpu);
+    CHECK(model.params().vocabOnly);
+    CHECK(model.trainCtxLength() == 0);
+    CHECK(model.shouldAddBosToken());
+    CHECK_FALSE(model.hasEncoder());
+    auto& vocab = model.vocab();
+    // the test vocabulary (tests/test_host.py) has merges up to "▁hello" and "▁world"
+    auto t = vocab.tokenize("hello world", true, true);
+    REQUIRE(t.size() == 3);
+    CHECK(t[0] == vocab.bos());
+    CHECK(vocab.tokenToString(t[1]) == " hello");
+    CHECK(vocab.tokenToString(t[2]) == " world");
+    CHECK(vocab.tokenize("hello world", false, true) == std::vector<Token>(t.begin() + 1, t.end()));
+    // a control token's text is one token when parseSpecial, plain text otherwise
+    auto sp = vocab.tokenize("hello</s>", false, true);
+    REQUIRE(sp.size() == 2);
+    CHECK(sp[1] == vocab.eos());
+    CHECK(vocab.isEog(vocab.eos()));
+    auto nsp = vocab.tokenize("hello</s>", false, false);
+    CHECK(nsp.size() > 2);
+    // bytes missing from the vocabulary fall back to <0xXX> tokens
+    auto by = vocab.tokenize("\xc3\xa9", false, false);
+    std::string back;
+    for (Token x : by) back += vocab.tokenToString(x);
+    CHECK(back == " \xc3\xa9");
+}
+
+// ---------------------------------------------------------------- GPU ----
+TEST_CASE_G("session", "gpu") {   // t-integration.cpp:124-250
+    REQUIRE(!g_model.empty());
+    Model model(g_model, {});
+    CHECK(model.params().gpu);
+    CHECK(model.trainCtxLength() == 256);
+    Instance inst(model, {});
+    inst.warmup();
+    {   // no initialization
+        auto& s = inst.startSession({});
+        CHECK_THROWS_WITH(s.complete({}), "Session hasn't started yet");
+        CHECK_THROWS_WITH(s.completeStream({.prompt = kPrompt}), "Session hasn't started yet");
+        CHECK_THROWS_WITH(s.getState(), "Session hasn't started yet");
+        inst.stopSession();
+    }
+    {   // double initialization
+        auto& s = inst.startSession({});
+        s.setInitialPrompt(kPrompt);
+        CHECK_THROWS_WITH(s.setState({}), "Session already started");
+        inst.stopSession();
+    }
+    Token first = Token_Invalid;
+    {   // generating phase
+        auto& s = inst.startSession({});
+        s.setInitialPrompt(kPrompt);
+        auto p = s.complete({.maxTokens = 1});
+        REQUIRE(p.size() == 1);
+        first = p[0].token;
+        CHECK(p[0].logits.size() == 10);
+        for (size_t i = 1; i < p[0].logits.size(); ++i) CHECK(p[0].logits[i - 1].logit >= p[0].logits[i].logit);
+        const std::vector<Token> more = {410, 411, 412};
+        auto p2 = s.complete({.prompt = more, .maxTokens = 1});
+        REQUIRE(p2.size() == 1);
+        CHECK(s.getState().size() > 0);
+        inst.stopSession();
+    }
+    {   // generation streaming: same seed, same first token as complete()
+        auto& s = inst.startSession({});
+        s.setInitialPrompt(kPrompt);
+        auto stream = s.completeStream({.maxTokens = 1});
+        auto p = stream.complete();
+        CHECK(p.token == first);
+        CHECK(stream.status() == Session::StreamGenerator::Status::Completed);
+        CHECK(stream.complete().token == Token_Invalid);
+        inst.stopSession();
+    }
+    {   // single session
+        auto& s = inst.startSession({});
+        (void)s;
+        CHECK_THROWS_WITH(inst.startSession({}), "Session is already started. Stop it to start a new one.");
+        inst.stopSession();
+    }
+}
+
+TEST_CASE_G("filling ctx", "gpu") {   // t-integration.cpp:219-248: bit-identical verification
+    Model model(g_model, {});
+    Instance inst(model, {}), inst2(model, {});
+    inst.warmup();
+    inst2.warmup();
+    auto& s = inst.startSession({});
+    auto& s2 = inst2.startSession({});
+    s.setInitialPrompt(kPrompt);
+    s2.setInitialPrompt(kPrompt);
+    auto p = s.complete({.maxTokens = 10});
+    REQUIRE(p.size() > 0);
+    auto p2 = s2.fillCtx(p);
+    CHECK(p.size() == p2.size());
+    for (size_t i = 0; i < p.size(); i++) {
+        REQUIRE(p2[i].logits.size() == p[i].logits.size());
+        for (size_t j = 0; j < p[i].logits.size(); j++) {
+            CHECK(p[i].logits[j].token == p2[i].logits[j].token);
+            CHECK(p[i].logits[j].logit == p2[i].logits[j].logit);
+        }
+    }
+    // the Server::verify flow (Server.cpp:127-161) on a self-verification scores 1
+    MetricsAggregator agg;
+    float score = 0;
+    for (size_t i = 0; i < p.size(); i++) {
+        auto m = LogitComparer::compare(p[i].logits, p2[i].logits);
+        score = agg.pushAndVerify({&m, 1});
+    }
+    CHECK(score == 1.0f);
+}
+
+TEST_CASE_G("states", "gpu") {   // t-integration.cpp:304-421
+    Model model(g_model, {});
+    Instance inst(model, {});
+    std::vector<uint8_t> state;
+    std::vector<Token> gen;
+    {
+        auto& s = inst.startSession({});
+        s.setInitialPrompt(kPrompt);
+        state = s.getState();
+        for (auto& p : s.complete({.maxTokens = 6})) gen.push_back(p.token);
+        inst.stopSession();
+    }
+    {
+        auto& s = inst.startSession({});
+        s.setState(state);
+        std::vector<Token> again;
+        for (auto& p : s.complete({.maxTokens = 6})) again.push_back(p.token);
+        CHECK(again == gen);
+        inst.stopSession();
+    }
+}
+
+TEST_CASE_G("context shift", "gpu") {   // Session.cpp:324-347 through a long generation
+    Model model(g_model, {});
+    Instance inst(model, {.ctxSize = 32});
+    auto& s = inst.startSession({});
+    s.setInitialPrompt(kPrompt);
+    auto p = s.complete({.maxTokens = 40});   // 8 + 40 > 32 - 4: shifts at least once
+    CHECK(p.size() == 40);
+    Instance inst2(model, {.ctxSize = 32});
+    auto& s2 = inst2.startSession({.infiniteContext = false});
+    s2.setInitialPrompt(kPrompt);
+    CHECK_THROWS_WITH(s2.complete({.maxTokens = 40}), "context limit of 32 reached");
+}
+
+TEST_CASE_G("complete for the oracle", "gpu") {   // t-LogitComparer.cpp:41-79, GPU side
+    REQUIRE(!g_out.empty());
+    Model model(g_model, {});
+    Instance inst(model, {});
+    auto& s = inst.startSession({.seed = 7});
+    s.setInitialPrompt(kPrompt);
+    auto iRes = s.complete({.maxTokens = 12});
+    std::ofstream f(g_out);
+    for (auto& p : iRes) {
+        f << p.token;
+        for (auto& l : p.logits) {
+            char buf[64];
+            std::snprintf(buf, sizeof buf, " %d:%.9g", l.token, l.logit);
+            f << buf;
+        }
+        f << "\n";
+    }
+    CHECK(iRes.size() == 12);
+}
+
+MINITEST_MAIN(setup)
