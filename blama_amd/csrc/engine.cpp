@@ -434,13 +434,12 @@ Ctx::~Ctx() {
 }
 
 void Ctx::invalidate_graphs() {
-    if (g_full) hipGraphExecDestroy(g_full);
-    if (g_nolog) hipGraphExecDestroy(g_nolog);
-    for (auto& g : g_seg) {
-        if (g) hipGraphExecDestroy(g);
-        g = nullptr;
+    for (int m = 0; m < 2; ++m) {
+        for (hipGraphExec_t* g : {&g_full[m], &g_nolog[m], &g_seg[m][0], &g_seg[m][1], &g_seg[m][2]}) {
+            if (*g) hipGraphExecDestroy(*g);
+            *g = nullptr;
+        }
     }
-    g_full = g_nolog = nullptr;
 }
 
 long long Ctx::ffn_bytes() const {
@@ -521,6 +520,7 @@ void Ctx::enqueue_step(bool with_logits) {
         {
             AttnParams a{q, kl, vl, tokpos, cell_pos, attn_scores, attn_smax, part_o, hp.n_head, hp.n_head_kv, hp.head_dim,
                          kv_dim, (int)n_ctx, kq_scale};
+            a.fused = attn_fused;
             a.stamps = stamp();
             a.stamps2 = stamp();
             if (on()) launch_attn(a, stream);
@@ -668,6 +668,7 @@ int Ctx::decode(const int32_t* tokens, int n) {
     for (int i = 0; i < n; ++i) {
         const bool last = i == n - 1;
         const int pos = pos_max + 1, cell = n_cells;
+        attn_fused = cell + 1 <= ATTN_SHORT ? 1 : 0;   // this step attends over cell + 1 cells
         const long long slot = tok_slot++ % kTokRing;
         if (slot == 0 && tok_slot > 1) MI_HIP(hipStreamSynchronize(stream));
         int* hp = h_tokpos + slot * 4;
@@ -683,8 +684,8 @@ int Ctx::decode(const int32_t* tokens, int n) {
             // hipExtLaunchKernel start/stop events, graph for the rest
             for (int k = 0; k < 3; ++k) {
                 if (use_graphs && k != 1) {
-                    if (!g_seg[k]) g_seg[k] = build_graph(true, k);
-                    MI_HIP(hipGraphLaunch(g_seg[k], stream));
+                    if (!g_seg[attn_fused][k]) g_seg[attn_fused][k] = build_graph(true, k);
+                    MI_HIP(hipGraphLaunch(g_seg[attn_fused][k], stream));
                 } else {
                     seg_filter = k;
                     enqueue_step(true);
@@ -695,7 +696,7 @@ int Ctx::decode(const int32_t* tokens, int n) {
         } else if (!use_graphs) {
             enqueue_step(last);
         } else {
-            hipGraphExec_t& g = last ? g_full : g_nolog;
+            hipGraphExec_t& g = last ? g_full[attn_fused] : g_nolog[attn_fused];
             if (!g) g = build_graph(last, -1);
             MI_HIP(hipGraphLaunch(g, stream));
         }

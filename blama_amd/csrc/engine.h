@@ -148,8 +148,11 @@ struct Ctx {
     // MI_NO_GRAPH=1: launch every kernel eagerly (profilers that cannot trace
     // graph-launched kernels); the default replays one hipGraph per step
     bool use_graphs = getenv("MI_NO_GRAPH") == nullptr;
-    hipGraphExec_t g_full = nullptr, g_nolog = nullptr;
-    hipGraphExec_t g_seg[3] = {nullptr, nullptr, nullptr};
+    // [attention mode]: 1 = the context fits the fused short-attention launch (ATTN_SHORT
+    // cells), 0 = split attention; the host knows the cell count of every step.
+    hipGraphExec_t g_full[2] = {nullptr, nullptr}, g_nolog[2] = {nullptr, nullptr};
+    hipGraphExec_t g_seg[2][3] = {{nullptr, nullptr, nullptr}, {nullptr, nullptr, nullptr}};
+    int attn_fused = 0;                 // mode of the step being enqueued
     int prof_layer = -1;
     hipEvent_t prof_ev[2] = {nullptr, nullptr};
     bool prof_pending = false;

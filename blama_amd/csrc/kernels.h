@@ -44,7 +44,15 @@ constexpr int GEMV_MAX_SEG = 4;
 // ceil(ncell / ATTN_SMAX) rounded up to 64), so there are at most ATTN_SMAX
 // splits.
 constexpr int ATTN_SMAX = 16;
+// Contexts up to ATTN_SHORT cells are served by one fused launch, one workgroup per kv head
+// (scores in LDS, exact softmax, PV): one split.  Longer ones split over cells.
+constexpr int ATTN_SHORT = 512;
 __host__ __device__ inline void attn_split(int ncell, int& chunk, int& nsplit) {
+    if (ncell <= ATTN_SHORT) {
+        chunk = ncell;
+        nsplit = 1;
+        return;
+    }
     int c = (ncell + ATTN_SMAX - 1) / ATTN_SMAX;
     c = (c + 63) & ~63;
     chunk = c < 64 ? 64 : c;
@@ -118,6 +126,7 @@ struct AttnParams {
     float scale;
     unsigned long long* stamps;    // diagnostics (MI_STAMPS builds): scores / pv launches
     unsigned long long* stamps2;
+    int fused;                     // 1: the single-launch kernel (the context has <= ATTN_SHORT cells)
 };
 void launch_attn(const AttnParams& p, hipStream_t s);
 // Combine the partials into out[n_head*hd] (tests / the eager debug path).

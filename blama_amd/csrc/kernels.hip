@@ -32,6 +32,14 @@ template <typename T>
 __device__ __forceinline__ __attribute__((address_space(1))) T* gptr_w(T* p) {
     return (__attribute__((address_space(1))) T*)(p);
 }
+// A wave-uniform pointer (e.g. read from LDS) moved to SGPRs.
+template <typename T>
+__device__ __forceinline__ T* rfl_ptr(T* p) {
+    const unsigned long long v = reinterpret_cast<unsigned long long>(p);
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+    return reinterpret_cast<T*>(((unsigned long long)hi << 32) | lo);
+}
 __device__ __forceinline__ u32x4 ldg16(const uint8_t* p) {
     return __builtin_nontemporal_load(gptr(reinterpret_cast<const u32x4*>(p)));
 }
@@ -475,25 +483,48 @@ struct ProRegs {
     bool attn_regs;           // PRO_ATTN: the splits' partials held in x[] (block i, split s: x[i*nsplit+s])
 };
 
-__device__ __forceinline__ void pro_load(const GemvParams& P, ProRegs& R, int nb, int nw, int wave, int lane,
-                                         int wg_u0, int wg_u1) {
+// Entry loads: the activation, RMSNorm weight and token position.  Their pointers
+// arrive preloaded in SGPRs (kernarg preload, the kernel's leading arguments), so
+// these loads are in flight at once, racing the load of the parameter block.
+__device__ __forceinline__ void pro_load_entry(ProRegs& R, const float* x0, const float* nw_, const int* tp, int nb,
+                                               bool regs, bool rms, int nw, int wave, int lane) {
+    R.tp = tp ? *gptr(reinterpret_cast<const i32x4*>(tp)) : i32x4{0, 0, 0, 0};
+    R.regs = regs;
+    if (regs) {
+        const auto x4 = gptr(reinterpret_cast<const f32x4*>(x0));
+        const auto w4 = gptr(reinterpret_cast<const f32x4*>(nw_));
+#pragma unroll
+        for (int i = 0; i < PRO_MAXB; ++i) {
+            const int blk = wave + i * nw;
+            if (blk < nb) {
+                R.x[i] = x4[blk * 64 + lane];
+                if (rms) R.w[i] = w4[blk * 64 + lane];
+            }
+        }
+    }
+}
+
+// Loads that need the parameter block: RoPE freq factors, the attention partials
+// (their count depends on the cell count in R.tp) and the residuals of this
+// workgroup's units.  Returns whether any were issued.
+__device__ __forceinline__ bool pro_load_rest(const GemvParams& P, ProRegs& R, int nb, int nw, int wave, int lane,
+                                              int wg_u0, int wg_u1) {
     const int tid = threadIdx.x;
-    R.tp = P.tokpos ? *gptr(reinterpret_cast<const i32x4*>(P.tokpos)) : i32x4{0, 0, 0, 0};
-    R.regs = P.pro != PRO_ATTN && P.nslots == 1 && nb <= PRO_MAXB * nw;
-    // Every load the prologue waits for must be issued before the weight prefill:
-    // loads retire in issue order, so a later one would wait for the prefill too.
+    bool any = false;
     R.ff[0] = R.ff[1] = 1.0f;
-    if (P.freq_factors && wave == 0) {
-        if (lane < P.n_rot / 2) R.ff[0] = gptr(P.freq_factors)[lane];
-        if (lane + 64 < P.n_rot / 2) R.ff[1] = gptr(P.freq_factors)[lane + 64];
+    if (P.freq_factors) {
+        any = true;
+        if (wave == 0) {
+            if (lane < P.n_rot / 2) R.ff[0] = gptr(P.freq_factors)[lane];
+            if (lane + 64 < P.n_rot / 2) R.ff[1] = gptr(P.freq_factors)[lane + 64];
+        }
     }
     R.nsplit = 0;
     R.attn_regs = false;
     if (P.pro == PRO_ATTN) {
-        // the split count depends on the cell count: one scalar round trip (the
-        // only one before the weight prefill is issued)
+        any = true;
         int chunk;
-        attn_split(sload_i32(P.tokpos + 2) + 1, chunk, R.nsplit);
+        attn_split(__builtin_amdgcn_readfirstlane(R.tp.z) + 1, chunk, R.nsplit);
         const int bpw = (nb + nw - 1) / nw;   // blocks per wave
         R.attn_regs = P.nslots == 1 && R.nsplit * bpw <= PRO_MAXB;
         if (R.attn_regs) {
@@ -508,34 +539,26 @@ __device__ __forceinline__ void pro_load(const GemvParams& P, ProRegs& R, int nb
             }
         }
     }
-    if (R.regs) {
-        const auto x4 = gptr(reinterpret_cast<const f32x4*>(P.x[0]));
-        const auto w4 = gptr(reinterpret_cast<const f32x4*>(P.norm_w));
-#pragma unroll
-        for (int i = 0; i < PRO_MAXB; ++i) {
-            const int blk = wave + i * nw;
-            if (blk < nb) {
-                R.x[i] = x4[blk * 64 + lane];
-                if (P.pro == PRO_RMSNORM) R.w[i] = w4[blk * 64 + lane];
-            }
-        }
-    }
     // residual values of this workgroup's units (the in-place residual add reads
     // them before any wave of the workgroup overwrites its rows).  Residual
     // launches have one segment (launch_gemv checks), so the lookup is scalar.
     R.ra = R.rb = 0.0f;
     const GemvSeg& S0 = P.seg[0];
-    if (S0.resid && tid < wg_u1 - wg_u0) {
-        const long long lu = wg_u0 + tid;
-        if (S0.pair == PAIR_ADJ) {
-            const long long ra = 2 * lu;
-            R.ra = gptr(S0.resid)[ra];
-            R.rb = gptr(S0.resid)[ra + 1 < S0.A.rows ? ra + 1 : ra];
-        } else {
-            R.ra = gptr(S0.resid)[lu];
-            R.rb = gptr(S0.resid)[lu];   // a second load, not a copy (a copy waits for the load)
+    if (S0.resid) {
+        any = true;
+        if (tid < wg_u1 - wg_u0) {
+            const long long lu = wg_u0 + tid;
+            if (S0.pair == PAIR_ADJ) {
+                const long long ra = 2 * lu;
+                R.ra = gptr(S0.resid)[ra];
+                R.rb = gptr(S0.resid)[ra + 1 < S0.A.rows ? ra + 1 : ra];
+            } else {
+                R.ra = gptr(S0.resid)[lu];
+                R.rb = gptr(S0.resid)[lu];   // a second load, not a copy (a copy waits for the load)
+            }
         }
     }
+    return any;
 }
 
 __device__ __forceinline__ void pro_finish(const GemvParams& P, const ProRegs& R, char* smem, const SmemPlan& SP,
@@ -579,7 +602,13 @@ __device__ __forceinline__ void pro_finish(const GemvParams& P, const ProRegs& R
         }
         s = wave_sum63_d(s);
         if (lane == 63) red[wave] = s;
+#ifdef MI_STAMPS
+        if (P.stamps && threadIdx.x == 0) P.stamps[blockIdx.x * 8 + 5] = __builtin_amdgcn_s_memrealtime();
+#endif
         __syncthreads();
+#ifdef MI_STAMPS
+        if (P.stamps && threadIdx.x == 0) P.stamps[blockIdx.x * 8 + 6] = __builtin_amdgcn_s_memrealtime();
+#endif
         double tot = 0.0;
         for (int w = 0; w < nwaves; ++w) tot += red[w];
         const float mean = (float)(tot / (double)P.K);
@@ -677,27 +706,66 @@ __device__ __forceinline__ void pro_finish(const GemvParams& P, const ProRegs& R
     }
 }
 
+// Epilogue inputs, uniform and kept in SGPRs: per launch (EpiConst) and per
+// segment (EpiSeg, re-read from the LDS parameters only when the consumer enters a
+// new segment).
+struct EpiConst {
+    __half* kcache;
+    __half* vcache;
+    int* cell_pos;
+    int head_dim, n_rot, kv_dim;
+};
+struct EpiSeg {
+    float* out;
+    int epi, pair, unit0, end, rows;
+};
+__device__ __forceinline__ EpiConst epi_const(const GemvParams& P) {
+    EpiConst E;
+    E.kcache = rfl_ptr(P.kcache);
+    E.vcache = rfl_ptr(P.vcache);
+    E.cell_pos = rfl_ptr(P.cell_pos);
+    E.head_dim = __builtin_amdgcn_readfirstlane(P.head_dim);
+    E.n_rot = __builtin_amdgcn_readfirstlane(P.n_rot);
+    E.kv_dim = __builtin_amdgcn_readfirstlane(P.kv_dim);
+    return E;
+}
+__device__ __forceinline__ EpiSeg epi_seg(const GemvParams& P, int u) {
+    int si = 0;
+    while (si + 1 < P.nseg && u >= P.seg[si + 1].unit0) ++si;
+    const GemvSeg& S = P.seg[si];
+    EpiSeg e;
+    e.out = rfl_ptr(S.out);
+    e.epi = __builtin_amdgcn_readfirstlane(S.epi);
+    e.pair = __builtin_amdgcn_readfirstlane(S.pair);
+    e.unit0 = __builtin_amdgcn_readfirstlane(S.unit0);
+    e.end = __builtin_amdgcn_readfirstlane(S.unit0 + S.units);
+    e.rows = __builtin_amdgcn_readfirstlane(S.A.rows);
+    return e;
+}
+
 // rva / rvb: residual values of rows A / B
-__device__ __forceinline__ void gemv_epilogue(const GemvParams& P, const UnitRef& c, const float* rope,
+__device__ __forceinline__ void gemv_epilogue(const EpiConst& E, const EpiSeg& S, int u, const float* rope,
                                               float rva, float rvb, float wa, float wb,
                                               int pos, int cell, float yA, float yB) {
-    const GemvSeg& S = P.seg[c.si];
     const auto out = gptr_w(S.out);
-    const long long ra = c.ra, rb = c.rb;
+    const int lu = u - S.unit0;
+    const bool adj = S.pair == PAIR_ADJ;
+    const long long ra = adj ? 2LL * lu : lu, rb = adj ? ra + 1 : lu;
+    const bool hasB = !adj || rb < S.rows;
     switch (S.epi) {
     case EPI_STORE:
         out[ra] = yA;
-        if (c.hasB) out[rb] = yB;
+        if (hasB) out[rb] = yB;
         break;
     case EPI_ADD:
         out[ra] = yA + rva;
-        if (c.hasB) out[rb] = yB + rvb;
+        if (hasB) out[rb] = yB + rvb;
         break;
     case EPI_ROPE_Q:
     case EPI_ROPE_K: {
-        const int i0 = (int)(ra % P.head_dim);   // even
+        const int i0 = (int)(ra % E.head_dim);   // even
         float o0 = yA, o1 = yB;
-        if (i0 < P.n_rot) {
+        if (i0 < E.n_rot) {
             const float cs = rope[i0], sn = rope[i0 + 1];
             o0 = yA * cs - yB * sn;
             o1 = yA * sn + yB * cs;
@@ -706,24 +774,24 @@ __device__ __forceinline__ void gemv_epilogue(const GemvParams& P, const UnitRef
             out[ra] = o0;
             out[rb] = o1;
         } else {
-            const auto kr = gptr_w(reinterpret_cast<unsigned short*>(P.kcache + (long long)cell * P.kv_dim));
+            const auto kr = gptr_w(reinterpret_cast<unsigned short*>(E.kcache + (long long)cell * E.kv_dim));
             kr[ra] = __half_as_ushort(__float2half_rn(o0));
             kr[rb] = __half_as_ushort(__float2half_rn(o1));
-            if (c.lu == 0) gptr_w(P.cell_pos)[cell] = pos;
+            if (lu == 0) gptr_w(E.cell_pos)[cell] = pos;
         }
         break;
     }
     case EPI_V: {
-        const auto vr = gptr_w(reinterpret_cast<unsigned short*>(P.vcache + (long long)cell * P.kv_dim));
+        const auto vr = gptr_w(reinterpret_cast<unsigned short*>(E.vcache + (long long)cell * E.kv_dim));
         vr[ra] = __half_as_ushort(__float2half_rn(yA));
-        if (c.hasB) vr[rb] = __half_as_ushort(__float2half_rn(yB));
+        if (hasB) vr[rb] = __half_as_ushort(__float2half_rn(yB));
         break;
     }
     case EPI_SWIGLU:
-        out[c.lu] = silu_f(yA) * yB;
+        out[lu] = silu_f(yA) * yB;
         break;
     case EPI_MOE_DOWN:
-        out[c.lu] = (yA * wa + yB * wb) + rva;
+        out[lu] = (yA * wa + yB * wb) + rva;
         break;
     default: break;
     }
@@ -732,7 +800,8 @@ __device__ __forceinline__ void gemv_epilogue(const GemvParams& P, const UnitRef
 // NW waves per workgroup, D-deep ring.  ROLE: 0 generic, 1 FFN gate/up (own
 // symbol: the bench's roofline kernel), 2 dual activation slot (MoE down).
 template <int T, int D, int NW, int DUAL, int ROLE>
-__global__ __launch_bounds__(NW * 64) void gemv_t(const GemvParams Pk) {
+__global__ __launch_bounds__(NW * 64) void gemv_t(const float* __restrict__ kx0, const float* __restrict__ knw,
+                                                   const int* __restrict__ ktp, int kflags, const GemvParams Pk) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     using K = Kq<T>;
     static_assert(K::LPS == 8, "8 lanes per superblock");
@@ -744,6 +813,9 @@ __global__ __launch_bounds__(NW * 64) void gemv_t(const GemvParams Pk) {
     // loads (segment lookup, plane bases, ...), each a full memory latency, which
     // cost 5-10 us per launch before the first weight load was issued.
     __shared__ __attribute__((aligned(16))) u32x4 sparams[(sizeof(GemvParams) + 15) / 16];
+    ProRegs pr;
+    pro_load_entry(pr, kx0, knw, ktp, (kflags & 0xFFFFF) >> 8, (kflags >> 20) & 1, (kflags >> 21) & 1, NW, wave,
+                   lane);
     {
         const u32x4* src = reinterpret_cast<const u32x4*>(&Pk);
         for (int i = threadIdx.x; i < (int)((sizeof(GemvParams) + 15) / 16); i += NW * 64) sparams[i] = src[i];
@@ -779,10 +851,15 @@ __global__ __launch_bounds__(NW * 64) void gemv_t(const GemvParams Pk) {
 
     struct Slot { typename K::Ld a, b; };
     Slot ring[D];
-    // issue cursor: unit iu, chunk ic, plane bases of the unit's two rows
+    // Issue cursor: unit iu, chunk ic and the plane bases of the unit's two rows, kept in
+    // SGPRs.  Moving to the next unit of the same segment is a pointer increment; only a
+    // segment change (or a PAIR_ADJ odd-row tail) re-derives the bases from the LDS copy of
+    // the parameters (a chain of dependent LDS reads, ~0.4 us: far too slow per unit).
     int iu = u0, ic = 0;
     const uint8_t* pa[4] = {nullptr, nullptr, nullptr, nullptr};
     const uint8_t* pb[4] = {nullptr, nullptr, nullptr, nullptr};
+    int fast_end = 0;          // units < fast_end advance by a pointer increment
+    int step_rows = 0;         // rows per unit: 2 (PAIR_ADJ) or 1 (PAIR_AB)
     auto bases = [&](int u) {
         const UnitRef c = unit_ref(P, u);
         const GemvSeg& S = P.seg[c.si];
@@ -792,36 +869,59 @@ __global__ __launch_bounds__(NW * 64) void gemv_t(const GemvParams Pk) {
         const long long rb = c.hasB ? c.rb : c.ra;   // odd tail: re-read row A, result unused
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            pa[i] = S.A.p[i] + ea * S.A.expert_stride[i] + c.ra * nb * PlaneBytes<T>::b[i];
-            pb[i] = MB.p[i] + eb * MB.expert_stride[i] + rb * nb * PlaneBytes<T>::b[i];
+            pa[i] = rfl_ptr(S.A.p[i] + ea * S.A.expert_stride[i] + c.ra * nb * PlaneBytes<T>::b[i]);
+            pb[i] = rfl_ptr(MB.p[i] + eb * MB.expert_stride[i] + rb * nb * PlaneBytes<T>::b[i]);
+        }
+        const int pair = __builtin_amdgcn_readfirstlane(S.pair);
+        const int end = __builtin_amdgcn_readfirstlane(S.unit0 + S.units);
+        const int rows = __builtin_amdgcn_readfirstlane(S.A.rows);
+        step_rows = pair == PAIR_ADJ ? 2 : 1;
+        fast_end = (pair == PAIR_ADJ && (rows & 1)) ? end - 1 : end;   // the odd tail takes the slow path
+    };
+    auto next_unit = [&](int u) {
+        if (u < fast_end) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const long long d = (long long)step_rows * nb * PlaneBytes<T>::b[i];
+                pa[i] += d;
+                pb[i] += d;
+            }
+        } else {
+            bases(u);
         }
     };
     bases(u0 < P.total_units ? u0 : P.total_units - 1);   // idle waves re-read a valid row
     // Issue the next item (past the end: the last item again, a cache hit).
+    // Past the end of its range a wave keeps issuing (so every ring step issues the same
+    // loads and the compiler's vmcnt bookkeeping stays exact), but "parked": every lane
+    // reads the same 16 bytes of the last row, one request per load instead of 16 lines.
+    int park_sb = -1;          // -1: streaming; else 0 (every lane at offset 0)
     auto issue = [&](Slot& S) {
-        S.a = K::load(pa, ic * 8 + sbl, j);
-        S.b = K::load(pb, ic * 8 + sbl, j);
+        const int sb = park_sb < 0 ? ic * 8 + sbl : 0;
+        const int jj = park_sb < 0 ? j : 0;
+        S.a = K::load(pa, sb, jj);
+        S.b = K::load(pb, sb, jj);
         if (iu < u1) {
             if (++ic == cpr) {
                 ic = 0;
-                if (++iu < u1) bases(iu);
-                else { iu = u1; ic = cpr - 1; }   // park on the last item
+                if (++iu < u1) next_unit(iu);
+                else { iu = u1; park_sb = 0; }   // park
             }
         }
     };
 
-    ProRegs pr;
-    pro_load(P, pr, nb, NW, wave, lane, wg_u0, wg_u1);
-    // Execution barrier only (no memory wait): every wave's prologue loads enter
-    // the memory queues before any wave's weight prefill, so they are not stuck
-    // behind ~100 KB per CU of weight requests.
-    __builtin_amdgcn_s_barrier();
+    // Wait for the prologue loads that needed the parameter block BEFORE issuing the
+    // weight prefill.  Issued together, those requests of late CUs queue behind
+    // every CU's prefill at the memory channels (measured: ~3 us to land); alone
+    // they land in ~1 us and the prologue then computes while the prefill streams.
+    if (pro_load_rest(P, pr, nb, NW, wave, lane, wg_u0, wg_u1)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
     for (int k = 0; k < D - 1; ++k) issue(ring[k]);
     MI_STAMP(1)
     const int pos = __builtin_amdgcn_readfirstlane(pr.tp.y);
     const int cell = __builtin_amdgcn_readfirstlane(pr.tp.z);
     pro_finish(P, pr, smem, SP, pos, cell + 1, wg_u0, wg_u1);
+    MI_STAMP(7)
     __syncthreads();
     MI_STAMP(2)
     const float* rope = reinterpret_cast<const float*>(smem + SP.rope_off);
@@ -831,6 +931,8 @@ __global__ __launch_bounds__(NW * 64) void gemv_t(const GemvParams Pk) {
 
     int cu = u0, cc = 0;
     float accA = 0.0f, accB = 0.0f;
+    const EpiConst EC = epi_const(P);
+    EpiSeg cseg = epi_seg(P, u0 < P.total_units ? u0 : P.total_units - 1);
     auto consume = [&](const Slot& S) {
         const int sb = cc * 8 + sbl;
         const bool lv = sb < nb;
@@ -849,9 +951,10 @@ __global__ __launch_bounds__(NW * 64) void gemv_t(const GemvParams Pk) {
         if (++cc == cpr) {
             const float yA = wave_sum63(accA);
             const float yB = wave_sum63(accB);
+            if (cu >= cseg.end) cseg = epi_seg(P, cu);   // segment change (rare)
             if (lane == 63) {
                 const int i = cu - wg_u0;
-                gemv_epilogue(P, unit_ref(P, cu), rope, rs[2 * i], rs[2 * i + 1], w0, w1, pos, cell, yA, yB);
+                gemv_epilogue(EC, cseg, cu, rope, rs[2 * i], rs[2 * i + 1], w0, w1, pos, cell, yA, yB);
             }
             accA = accB = 0.0f;
             cc = 0;
@@ -870,13 +973,13 @@ __global__ __launch_bounds__(NW * 64) void gemv_t(const GemvParams Pk) {
 #undef MI_STAMP
 }
 
-typedef void (*GemvFn)(const GemvParams);
+typedef void (*GemvFn)(const float*, const float*, const int*, int, const GemvParams);
 
 // Kernel configurations: waves per workgroup NW and ring depth D (one
 // workgroup per CU).  MI_GEMV_CFG=n selects config n for every type
 // (micro-benchmarks); otherwise gemv_cfg_for(type).
 struct GemvCfg { int nw, d; };
-constexpr GemvCfg kGemvCfgs[] = {{16, 2}, {8, 4}, {8, 3}, {16, 3}, {8, 6}};
+constexpr GemvCfg kGemvCfgs[] = {{16, 2}, {8, 4}, {8, 3}, {16, 3}, {8, 6}, {8, 8}, {4, 8}};
 constexpr int kNumGemvCfgs = sizeof(kGemvCfgs) / sizeof(kGemvCfgs[0]);
 static int gemv_cfg_for(int type) {
     static const int forced = getenv("MI_GEMV_CFG") ? atoi(getenv("MI_GEMV_CFG")) : -1;
@@ -898,6 +1001,8 @@ static GemvFn gemv_fn_cfg(int cfg) {
     case 2: return gemv_t<T, 3, 8, DUAL, ROLE>;
     case 3: return gemv_t<T, 3, 16, DUAL, ROLE>;
     case 4: return gemv_t<T, 6, 8, DUAL, ROLE>;
+    case 5: return gemv_t<T, 8, 8, DUAL, ROLE>;
+    case 6: return gemv_t<T, 8, 4, DUAL, ROLE>;
     default: return nullptr;
     }
 }
@@ -970,10 +1075,18 @@ void launch_gemv(const GemvParams& p_in, int role, int grid, hipStream_t s, hipE
     GemvFn fn = gemv_fn(role, type, p.nslots, cfg);
     if (!fn) throw Error("gemv: unsupported quant type");
     const dim3 block(kGemvCfgs[cfg].nw * 64);
+    // leading (kernarg-preloaded) arguments: activation, norm weight, token position, K | flags
+    const int nb = p.K / 256;
+    const bool regs = p.pro != PRO_ATTN && p.nslots == 1 && nb <= PRO_MAXB * kGemvCfgs[cfg].nw;
+    const bool rms = p.pro == PRO_RMSNORM;
+    const int kflags = p.K | (regs ? 1 << 20 : 0) | (rms ? 1 << 21 : 0);
+    const float* kx0 = p.x[0];
+    const float* knw = rms ? p.norm_w : nullptr;
+    const int* ktp = p.tokpos;
     if (ev_start || ev_stop)
-        hipExtLaunchKernelGGL(fn, dim3(grid), block, smem, s, ev_start, ev_stop, 0, p);
+        hipExtLaunchKernelGGL(fn, dim3(grid), block, smem, s, ev_start, ev_stop, 0, kx0, knw, ktp, kflags, p);
     else
-        hipLaunchKernelGGL(fn, dim3(grid), block, smem, s, p);
+        hipLaunchKernelGGL(fn, dim3(grid), block, smem, s, kx0, knw, ktp, kflags, p);
     MI_HIP(hipGetLastError());
 }
 
@@ -1285,30 +1398,181 @@ __global__ __launch_bounds__(256) void attn_pv_kernel(const AttnParams P) {
 #endif
 }
 
+// Short contexts (<= ATTN_SHORT cells): the same arithmetic as the two kernels above with a
+// single split, in one launch.  One workgroup per kv head keeps its scores in LDS, so no
+// other workgroup's result is needed between the softmax statistics and the PV sum.
+template <int R, int LPC>
+__global__ __launch_bounds__(256) void attn_fused_kernel(const AttnParams P) {
+    constexpr int CPW = 64 / LPC;
+    constexpr int HD = LPC * 8;
+    __shared__ float sw[R][ATTN_SHORT];
+    __shared__ float redm[4][R];
+    __shared__ double dred[4][R];
+    __shared__ float gm[R], ginv[R];
+    __shared__ float red_o[4][R][HD];
+    const int g = blockIdx.x;
+#ifdef MI_STAMPS
+    unsigned long long* const stp = P.stamps ? P.stamps + blockIdx.x * 8 : nullptr;
+    if (stp && threadIdx.x == 0) stp[0] = __builtin_amdgcn_s_memrealtime();
+#endif
+    const int ncell = min(P.tokpos[2] + 1, ATTN_SHORT), qpos = P.tokpos[1];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int L = lane % LPC, G = lane / LPC;
+    const long long row_off = (long long)g * HD + L * 8;
+    float q[R][8];
+#pragma unroll
+    for (int t = 0; t < R; ++t) {
+        const float4* qp = reinterpret_cast<const float4*>(P.q + (long long)(g * R + t) * HD + L * 8);
+        const float4 a = qp[0], b = qp[1];
+        const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) q[t][e] = __half2float(__float2half_rn(v[e]));
+    }
+    // 1. scaled KQ of every cell into LDS, and the per-head max
+    float mx[R];
+#pragma unroll
+    for (int t = 0; t < R; ++t) mx[t] = -INFINITY;
+    constexpr int U = 4;
+    for (int cb = wave * CPW; cb < ncell; cb += 4 * CPW * U) {
+        u32x4 kk[U];
+        int cpos[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            int c = cb + u * 4 * CPW + G;
+            c = c < ncell ? c : ncell - 1;
+            kk[u] = *reinterpret_cast<const u32x4*>(P.kcache + (long long)c * P.kv_dim + row_off);
+            cpos[u] = P.cell_pos[c];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int c = cb + u * 4 * CPW + G;
+            const bool valid = c < ncell && cpos[u] <= qpos;
+            const unsigned kw[4] = {kk[u].x, kk[u].y, kk[u].z, kk[u].w};
+            float kf[8];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                kf[2 * e] = h2f(kw[e]);
+                kf[2 * e + 1] = h2f(kw[e] >> 16);
+            }
+#pragma unroll
+            for (int t = 0; t < R; ++t) {
+                float d = 0.0f;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) d = fmaf(q[t][e], kf[e], d);
+#pragma unroll
+                for (int off = LPC / 2; off > 0; off >>= 1) d += __shfl_xor(d, off, 64);
+                const float w = valid ? d * P.scale : -INFINITY;
+                mx[t] = fmaxf(mx[t], w);
+                if (L == 0 && c < ncell) sw[t][c] = w;
+            }
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < R; ++t) {
+        const float m = wave_max(mx[t]);
+        if (lane == 0) redm[wave][t] = m;
+    }
+    __syncthreads();
+    // 2. sum over all cells of expf(w - max), in double, fixed order (as attn_pv_kernel)
+#pragma unroll
+    for (int t = 0; t < R; ++t) {
+        const float M = fmaxf(fmaxf(redm[0][t], redm[1][t]), fmaxf(redm[2][t], redm[3][t]));
+        double acc = 0.0;
+        for (int c = tid; c < ncell; c += 256) acc += (double)expf(sw[t][c] - M);
+        acc = wave_sum_d(acc);
+        if (lane == 0) dred[wave][t] = acc;
+        if (tid == 0) gm[t] = M;
+    }
+    __syncthreads();
+    if (tid < R) ginv[tid] = (float)(1.0 / (((dred[0][tid] + dred[1][tid]) + dred[2][tid]) + dred[3][tid]));
+    __syncthreads();
+    // 3. sum_c f16(p_c) v_c
+    float o[R][8];
+#pragma unroll
+    for (int t = 0; t < R; ++t)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[t][e] = 0.0f;
+    for (int cb = wave * CPW; cb < ncell; cb += 4 * CPW * U) {
+        u32x4 vv[U];
+        float pw[U][R];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            int c = cb + u * 4 * CPW + G;
+            const bool in = c < ncell;
+            c = in ? c : ncell - 1;
+            vv[u] = *reinterpret_cast<const u32x4*>(P.vcache + (long long)c * P.kv_dim + row_off);
+#pragma unroll
+            for (int t = 0; t < R; ++t) {
+                const float p = expf(sw[t][c] - gm[t]) * ginv[t];
+                pw[u][t] = in ? __half2float(__float2half_rn(p)) : 0.0f;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const unsigned vw[4] = {vv[u].x, vv[u].y, vv[u].z, vv[u].w};
+            float vf[8];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                vf[2 * e] = h2f(vw[e]);
+                vf[2 * e + 1] = h2f(vw[e] >> 16);
+            }
+#pragma unroll
+            for (int t = 0; t < R; ++t)
+#pragma unroll
+                for (int e = 0; e < 8; ++e) o[t][e] = fmaf(pw[u][t], vf[e], o[t][e]);
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < R; ++t)
+#pragma unroll
+        for (int off = LPC; off < 64; off <<= 1)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[t][e] += __shfl_xor(o[t][e], off, 64);
+    if (G == 0) {
+#pragma unroll
+        for (int t = 0; t < R; ++t)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) red_o[wave][t][L * 8 + e] = o[t][e];
+    }
+    __syncthreads();
+    for (int i = tid; i < R * HD; i += 256) {
+        const int t = i / HD, d = i % HD;
+        P.part_o[(long long)(g * R + t) * HD + d] = ((red_o[0][t][d] + red_o[1][t][d]) + red_o[2][t][d]) + red_o[3][t][d];
+    }
+#ifdef MI_STAMPS
+    if (stp && threadIdx.x == 0) stp[4] = __builtin_amdgcn_s_memrealtime();
+#endif
+}
+
 typedef void (*AttnFn)(const AttnParams);
 template <int R>
-static void attn_fns_r(int hd, AttnFn& a, AttnFn& b) {
+static void attn_fns_r(int hd, AttnFn& a, AttnFn& b, AttnFn& f) {
     switch (hd) {
-    case 32: a = attn_scores_kernel<R, 4>; b = attn_pv_kernel<R, 4>; break;
-    case 64: a = attn_scores_kernel<R, 8>; b = attn_pv_kernel<R, 8>; break;
-    case 128: a = attn_scores_kernel<R, 16>; b = attn_pv_kernel<R, 16>; break;
-    case 256: a = attn_scores_kernel<R, 32>; b = attn_pv_kernel<R, 32>; break;
-    default: a = b = nullptr; break;
+    case 32: a = attn_scores_kernel<R, 4>; b = attn_pv_kernel<R, 4>; f = attn_fused_kernel<R, 4>; break;
+    case 64: a = attn_scores_kernel<R, 8>; b = attn_pv_kernel<R, 8>; f = attn_fused_kernel<R, 8>; break;
+    case 128: a = attn_scores_kernel<R, 16>; b = attn_pv_kernel<R, 16>; f = attn_fused_kernel<R, 16>; break;
+    case 256: a = attn_scores_kernel<R, 32>; b = attn_pv_kernel<R, 32>; f = attn_fused_kernel<R, 32>; break;
+    default: a = b = f = nullptr; break;
     }
 }
 
 void launch_attn(const AttnParams& p, hipStream_t s) {
     if (p.n_head % p.n_head_kv) throw Error("attn: n_head must be a multiple of n_head_kv");
     const int r = p.n_head / p.n_head_kv;
-    AttnFn fa = nullptr, fb = nullptr;
+    AttnFn fa = nullptr, fb = nullptr, ff = nullptr;
     switch (r) {
-    case 1: attn_fns_r<1>(p.head_dim, fa, fb); break;
-    case 2: attn_fns_r<2>(p.head_dim, fa, fb); break;
-    case 4: attn_fns_r<4>(p.head_dim, fa, fb); break;
-    case 8: attn_fns_r<8>(p.head_dim, fa, fb); break;
+    case 1: attn_fns_r<1>(p.head_dim, fa, fb, ff); break;
+    case 2: attn_fns_r<2>(p.head_dim, fa, fb, ff); break;
+    case 4: attn_fns_r<4>(p.head_dim, fa, fb, ff); break;
+    case 8: attn_fns_r<8>(p.head_dim, fa, fb, ff); break;
     default: break;
     }
     if (!fa) throw Error("attn: unsupported head_dim / GQA ratio (head_dim 32..256, ratio 1/2/4/8)");
+    if (p.fused) {   // the caller guarantees <= ATTN_SHORT cells (the kernel clamps anyway)
+        hipLaunchKernelGGL(ff, dim3(p.n_head_kv), dim3(256), 0, s, p);
+        MI_HIP(hipGetLastError());
+        return;
+    }
     hipLaunchKernelGGL(fa, dim3(p.n_head_kv, ATTN_SMAX), dim3(256), 0, s, p);
     MI_HIP(hipGetLastError());
     hipLaunchKernelGGL(fb, dim3(p.n_head_kv, ATTN_SMAX), dim3(256), 0, s, p);

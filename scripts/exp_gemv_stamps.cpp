@@ -47,6 +47,14 @@ int main(int argc, char** argv) {
         m.p[k] = planes[k];
     }
     launch_repack(raw, type, rows, K, planes, nullptr);
+    // a second copy of the matrix: launch B runs the same code on cold weights
+    uint8_t* planes2[4] = {nullptr, nullptr, nullptr, nullptr};
+    QMat m2 = m;
+    for (int k = 0; k < plane_count(type); ++k) {
+        CK(hipMalloc(&planes2[k], (size_t)(nsb + kPlanePadSb) * plane_sb_bytes(type, k)));
+        m2.p[k] = planes2[k];
+    }
+    launch_repack(raw, type, rows, K, planes2, nullptr);
     float *x, *y, *nw;
     CK(hipMalloc(&x, K * 4));
     CK(hipMalloc(&nw, K * 4));
@@ -85,23 +93,19 @@ int main(int argc, char** argv) {
     CK(hipEventCreate(&b));
     const double mb = (double)raw_bytes / 1e6;
     printf("type %d rows %d K %d pro %d grid %d  (%.1f MB)\n", type, rows, K, pro, grid, mb);
+    printf("   A = first launch after a 1 GiB write (cold code, x, weights); B = the same kernel right\n"
+           "   after on a second copy of the matrix (warm code and x, cold weights)\n");
     printf("   event_us | stamp offsets (us) from first WG entry, median / max over WGs:\n");
-    printf("            | entry        prefill      prologue     1st-ring     end\n");
-    for (int it = 0; it < 6; ++it) {
-        CK(hipMemsetAsync(flush, it, fl, nullptr));
-        CK(hipMemsetAsync(st, 0, 256 * 64, nullptr));
-        CK(hipEventRecord(a, nullptr));
-        launch_gemv(p, ROLE_GENERIC, grid, nullptr);
-        CK(hipEventRecord(b, nullptr));
-        CK(hipEventSynchronize(b));
-        float ms;
-        CK(hipEventElapsedTime(&ms, a, b));
+    printf("            | issued       rms-arrive   rms-leave    pro-end      pro-barrier  1st-ring     end\n");
+    unsigned long long* st2;
+    CK(hipMalloc(&st2, 256 * 8 * 8));
+    auto show = [&](const char* tag, float ms, unsigned long long* dst) {
         std::vector<unsigned long long> hs(grid * 8);
-        CK(hipMemcpy(hs.data(), st, grid * 64, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(hs.data(), dst, grid * 64, hipMemcpyDeviceToHost));
         unsigned long long t0 = ~0ull;
         for (int g = 0; g < grid; ++g) t0 = std::min(t0, hs[g * 8]);
-        printf("   %8.2f |", ms * 1000);
-        for (int k = 0; k < 5; ++k) {
+        printf("%s %8.2f |", tag, ms * 1000);
+        for (int k : {1, 5, 6, 7, 2, 3, 4}) {
             std::vector<double> v;
             for (int g = 0; g < grid; ++g)
                 if (hs[g * 8 + k]) v.push_back((hs[g * 8 + k] - t0) / 100.0);
@@ -110,6 +114,37 @@ int main(int argc, char** argv) {
             else printf(" %5.2f/%6.2f ", v[v.size() / 2], v.back());
         }
         printf("\n");
+    };
+    hipEvent_t c, d;
+    CK(hipEventCreate(&c));
+    CK(hipEventCreate(&d));
+    for (int it = 0; it < 4; ++it) {
+        CK(hipMemsetAsync(flush, it, fl, nullptr));
+        CK(hipMemsetAsync(st, 0, 256 * 64, nullptr));
+        CK(hipMemsetAsync(st2, 0, 256 * 64, nullptr));
+        CK(hipEventRecord(a, nullptr));
+        p.stamps = st;
+        p.seg[0].A = m;
+        launch_gemv(p, ROLE_GENERIC, grid, nullptr);
+        CK(hipEventRecord(b, nullptr));
+        p.stamps = st2;
+        p.seg[0].A = m2;
+        launch_gemv(p, ROLE_GENERIC, grid, nullptr);
+        CK(hipEventRecord(d, nullptr));
+        CK(hipEventSynchronize(d));
+        float ms, ms2, ms3;
+        CK(hipEventElapsedTime(&ms, a, b));
+        CK(hipEventElapsedTime(&ms2, b, d));
+        show("A", ms, st);
+        show("B", ms2, st2);
+        // C: B's matrix again (warm TLB entries and Infinity Cache lines for its weights)
+        CK(hipMemsetAsync(st2, 0, 256 * 64, nullptr));
+        CK(hipEventRecord(a, nullptr));
+        launch_gemv(p, ROLE_GENERIC, grid, nullptr);
+        CK(hipEventRecord(b, nullptr));
+        CK(hipEventSynchronize(b));
+        CK(hipEventElapsedTime(&ms3, a, b));
+        show("C", ms3, st2);
     }
     return 0;
 }

@@ -41,7 +41,7 @@ def main():
         ent = buf[i, :, 0].astype(np.int64)
         m = ent > 0
         if not m.any():
-            break
+            continue   # an unused slab (e.g. the second attention launch in fused mode)
         end = buf[i, :, 4].astype(np.int64)
         pro = buf[i, :, 2].astype(np.int64)
         pre = buf[i, :, 1].astype(np.int64)
@@ -64,6 +64,20 @@ def main():
     spans = np.array([r[0] for r in rows])
     gaps = np.array([r[1] for r in rows])
     total = (launches[-1][1].max() - t0) / 100.0
+    # prologue detail of the roofline-sized launches (GEMV stamps 5/6/7: before / after
+    # the RMSNorm barrier, end of the prologue before its final barrier), wave 0 medians
+    for i, (ent, end, pro, pre) in enumerate(launches):
+        if i < len(launches) - 12:
+            continue
+        d = buf[i, :, :].astype(np.int64)
+        m = d[:, 0] > 0
+        det = []
+        for k in (1, 5, 6, 7, 2):
+            v = d[m, k]
+            v = v[v > 0]
+            det.append(f"{(np.median(v) - np.median(d[m, 0])) / 100.0:6.2f}" if len(v) else "   -  ")
+        print(f"{i:3d} from entry: issued {det[0]}  rms-arrive {det[1]}  rms-leave {det[2]}  pro-end {det[3]}"
+              f"  pro-barrier {det[4]}")
     print(f"launches {len(rows)}  first entry -> last end {total:.1f} us;  sum of spans {spans.sum():.1f}"
           f"  sum of gaps {gaps.sum():.1f}")
 

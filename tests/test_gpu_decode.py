@@ -186,3 +186,26 @@ def test_self_extend_div_matches_oracle(gpu_lib):
     rms = float(np.sqrt(np.mean(ref.astype(np.float64) ** 2)))
     assert np.max(np.abs(got - ref)) <= 5e-2 * rms
     assert int(np.argmax(got)) == int(np.argmax(ref))
+
+
+def test_split_attention_beyond_short_context(gpu_lib):
+    """Contexts past ATTN_SHORT (512) cells switch from the fused single-launch attention to the
+    split two-launch one (a different decode graph); both must match the oracle, including the
+    steps that cross the threshold."""
+    cfg = synthetic.CONFIGS["tiny-q4_k_m"]
+    buf = synthetic.build_gguf(cfg, seed=3)
+    m = engine.Model(buf)
+    ctx = engine.Context(m, n_ctx=576)
+    orc = oracle_from_gguf(buf, n_ctx=576)
+    rng = np.random.default_rng(21)
+    prompt = [int(t) for t in rng.integers(0, cfg.n_vocab, 509)]
+    ctx.decode(prompt)
+    orc.decode(prompt)
+    for t in [int(v) for v in rng.integers(0, cfg.n_vocab, 6)]:   # cells 510 .. 515
+        ctx.decode([t])
+        ref = orc.decode_one(t)
+        got = ctx.logits()
+        rms = float(np.sqrt(np.mean(ref.astype(np.float64) ** 2)))
+        assert np.max(np.abs(got - ref)) <= LOGIT_TOL * rms, ctx.n_cells
+        ids, _ = ctx.topk(10)
+        assert [int(i) for i in ids] == [i for i, _ in R.topk(ref, 10)]
