@@ -395,6 +395,15 @@ Ctx::Ctx(Model* model, uint32_t nctx, uint32_t nbatch, uint32_t nubatch) : m(mod
     MI_HIP(hipMalloc(&stamps, (size_t)kStampLaunches * kStampWgs * 8 * sizeof(unsigned long long)));
     MI_HIP(hipMemset(stamps, 0, (size_t)kStampLaunches * kStampWgs * 8 * sizeof(unsigned long long)));
 #endif
+    batch_ok = hp.n_expert == 0 && getenv("MI_NO_BATCH") == nullptr;
+    if (batch_ok) {
+        MI_HIP(hipMalloc(&xb, (size_t)GEMM_NT * hp.n_embd * sizeof(float)));
+        MI_HIP(hipMalloc(&qb, (size_t)GEMM_NT * hp.n_embd * sizeof(float)));
+        MI_HIP(hipMalloc(&attnb, (size_t)GEMM_NT * hp.n_embd * sizeof(float)));
+        MI_HIP(hipMalloc(&hb, (size_t)GEMM_NT * hp.n_ff * sizeof(float)));
+        MI_HIP(hipMalloc(&tokpos_b, (size_t)GEMM_NT * 4 * sizeof(int)));
+        MI_HIP(hipHostMalloc(&h_tokpos_b, (size_t)kTokbRing * GEMM_NT * 4 * sizeof(int)));
+    }
     MI_HIP(hipMalloc(&attn_smax, (size_t)ATTN_SMAX * hp.n_head * sizeof(float)));
     MI_HIP(hipMalloc(&attn_scores, (size_t)hp.n_head * n_ctx * sizeof(float)));
     MI_HIP(hipMalloc(&topk_ids, TOPK_MAX * sizeof(int)));
@@ -426,9 +435,11 @@ Ctx::~Ctx() {
     for (void* p : {(void*)kcache, (void*)vcache, (void*)kv_scratch, (void*)cell_pos, (void*)tokpos, (void*)x,
                     (void*)q, (void*)attn, (void*)h, (void*)h2, (void*)logits, (void*)cand, (void*)topk_ids,
                     (void*)topk_vals, (void*)sel, (void*)selw, (void*)gather_ids, (void*)gather_out,
-                    (void*)cell_delta, (void*)move_src, (void*)part_o, (void*)attn_smax, (void*)attn_scores, (void*)stamps})
+                    (void*)cell_delta, (void*)move_src, (void*)part_o, (void*)attn_smax, (void*)attn_scores, (void*)stamps,
+                    (void*)xb, (void*)qb, (void*)attnb, (void*)hb, (void*)tokpos_b})
         if (p) hipFree(p);
-    for (void* p : {(void*)h_tokpos, (void*)h_topk_ids, (void*)h_topk_vals, (void*)h_logits, (void*)h_gather})
+    for (void* p : {(void*)h_tokpos, (void*)h_topk_ids, (void*)h_topk_vals, (void*)h_logits, (void*)h_gather,
+                    (void*)h_tokpos_b})
         if (p) hipHostFree(p);
     if (stream) hipStreamDestroy(stream);
 }
@@ -614,12 +625,18 @@ void Ctx::enqueue_step(bool with_logits) {
             if (on()) launch_gemv(p, ROLE_FFN_DOWN, 0, stream);
         }
     }
-    if (with_logits && on()) {
+    if (with_logits && on()) enqueue_output(x, stamp());
+}
+
+// final RMSNorm + output head GEMV of one residual row, then the top-k
+void Ctx::enqueue_output(const float* xrow, unsigned long long* stamps_slab) {
+    const HParams& hp = m->hp;
+    {
         GemvParams p;
         std::memset(&p, 0, sizeof(p));
         p.pro = PRO_RMSNORM;
         p.nslots = 1;
-        p.x[0] = x;
+        p.x[0] = xrow;
         p.norm_w = m->output_norm;
         p.eps = hp.eps;
         p.K = hp.n_embd;
@@ -632,7 +649,7 @@ void Ctx::enqueue_step(bool with_logits) {
         p.seg[0].units = (m->output.rows + 1) / 2;
         p.seg[0].out = logits;
         params_finish(p);
-        p.stamps = stamp();
+        p.stamps = stamps_slab;
         launch_gemv(p, ROLE_OUTPUT, 0, stream);
         TopkParams tp{logits, hp.n_vocab, cand, topk_ids, topk_vals, d_h_topk_ids, d_h_topk_vals};
         launch_topk(tp, stream);
@@ -659,12 +676,134 @@ hipGraphExec_t Ctx::build_graph(bool with_logits, int seg) {
     return ex;
 }
 
+// Prompt ingestion: n tokens in chunks of GEMM_NT, every weight matrix streamed once per
+// chunk (launch_gemm), causal attention of the chunk's tokens (launch_attn_multi), the
+// output head for the last token only (llama_batch_get_one: logits of the last token).
+void Ctx::decode_batch(const int32_t* tokens, int n) {
+    const HParams& hp = m->hp;
+    const float theta_scale = std::pow(hp.rope_base, -2.0f / (float)hp.n_rot);
+    const float kq_scale = 1.0f / std::sqrt((float)hp.head_dim);
+    for (int c0 = 0; c0 < n; c0 += GEMM_NT) {
+        const int nt = std::min(GEMM_NT, n - c0);
+        const long long slot = tokb_slot++ % kTokbRing;
+        if (slot == 0 && tokb_slot > 1) MI_HIP(hipStreamSynchronize(stream));
+        int* hpos = h_tokpos_b + slot * GEMM_NT * 4;
+        for (int t = 0; t < nt; ++t) {
+            const int pos = pos_max + 1, cell = n_cells;
+            hpos[t * 4 + 0] = tokens[c0 + t];
+            hpos[t * 4 + 1] = pos;
+            hpos[t * 4 + 2] = cell;
+            hpos[t * 4 + 3] = 0;
+            h_cell_pos[cell] = pos;
+            n_cells++;
+            pos_max = pos;
+        }
+        MI_HIP(hipMemcpyAsync(tokpos_b, hpos, nt * 4 * sizeof(int), hipMemcpyHostToDevice, stream));
+        EmbedParams ep{m->tok_embd, tokpos_b, xb, hp.n_embd};
+        launch_embed_multi(ep, nt, stream);
+        for (int l = 0; l < hp.n_layer; ++l) {
+            const Layer& L = m->layers[l];
+            __half* kl = kcache + (size_t)l * n_ctx * kv_dim;
+            __half* vl = vcache + (size_t)l * n_ctx * kv_dim;
+            GemmParams b;
+            std::memset(&b, 0, sizeof(b));
+            b.ntok = nt;
+            b.tokpos = tokpos_b;
+            b.cell_pos = cell_pos;
+            b.theta_scale = theta_scale;
+            b.freq_scale = hp.freq_scale;
+            b.head_dim = hp.head_dim;
+            b.freq_factors = m->rope_freqs;
+            b.kcache = kl;
+            b.vcache = vl;
+            b.kv_dim = kv_dim;
+            b.eps = hp.eps;
+            // Q / K / V projections (+ RoPE, KV append)
+            const QMat* mats[3] = {&L.wq, &L.wk, &L.wv};
+            const int epis[3] = {EPI_ROPE_Q, EPI_ROPE_K, EPI_V};
+            for (int i = 0; i < 3; ++i) {
+                GemmParams p = b;
+                p.A = *mats[i];
+                p.pair = PAIR_ADJ;
+                p.epi = epis[i];
+                p.units = (mats[i]->rows + 1) / 2;
+                p.K = hp.n_embd;
+                p.pro = PRO_RMSNORM;
+                p.x = xb;
+                p.x_stride = hp.n_embd;
+                p.norm_w = L.attn_norm;
+                p.out = qb;
+                p.out_stride = hp.n_embd;
+                p.n_rot = i < 2 ? hp.n_rot : 0;
+                launch_gemm(p, stream);
+            }
+            AttnParams a{qb, kl, vl, tokpos_b, cell_pos, attn_scores, attn_smax, attnb, hp.n_head, hp.n_head_kv,
+                         hp.head_dim, kv_dim, (int)n_ctx, kq_scale};
+            launch_attn_multi(a, nt, attnb, stream);
+            {   // output projection + residual
+                GemmParams p = b;
+                p.A = L.wo;
+                p.pair = PAIR_ADJ;
+                p.epi = EPI_ADD;
+                p.units = (L.wo.rows + 1) / 2;
+                p.K = hp.n_embd;
+                p.pro = PRO_PLAIN;
+                p.x = attnb;
+                p.x_stride = hp.n_embd;
+                p.out = xb;
+                p.resid = xb;
+                p.out_stride = hp.n_embd;
+                launch_gemm(p, stream);
+            }
+            {   // FFN gate/up + SwiGLU
+                GemmParams p = b;
+                p.A = L.gate;
+                p.B = L.up;
+                p.pair = PAIR_AB;
+                p.epi = EPI_SWIGLU;
+                p.units = L.gate.rows;
+                p.K = hp.n_embd;
+                p.pro = PRO_RMSNORM;
+                p.x = xb;
+                p.x_stride = hp.n_embd;
+                p.norm_w = L.ffn_norm;
+                p.out = hb;
+                p.out_stride = hp.n_ff;
+                launch_gemm(p, stream);
+            }
+            {   // FFN down + residual
+                GemmParams p = b;
+                p.A = L.down;
+                p.pair = PAIR_ADJ;
+                p.epi = EPI_ADD;
+                p.units = (L.down.rows + 1) / 2;
+                p.K = hp.n_ff;
+                p.pro = PRO_PLAIN;
+                p.x = hb;
+                p.x_stride = hp.n_ff;
+                p.out = xb;
+                p.resid = xb;
+                p.out_stride = hp.n_embd;
+                launch_gemm(p, stream);
+            }
+        }
+        if (c0 + nt == n) enqueue_output(xb + (size_t)(nt - 1) * hp.n_embd, nullptr);
+    }
+    logits_valid = true;
+}
+
 int Ctx::decode(const int32_t* tokens, int n) {
     MI_HIP(hipSetDevice(device));
     if (n <= 0) throw Error("decode: empty batch");
     for (int i = 0; i < n; ++i)
         if (tokens[i] < 0 || tokens[i] >= m->hp.n_vocab) throw Error("decode: token id out of range");
     if (n_cells + n > (int)n_ctx) return 1;   // no KV slot (llama_decode returns 1)
+    // prompt ingestion through the batched GEMM when the context stays within the fused
+    // attention's reach (dense models; MI_NO_BATCH=1 forces token-by-token decode)
+    if (n >= 2 && batch_ok && n_cells + n <= ATTN_SHORT && prof_layer < 0) {
+        decode_batch(tokens, n);
+        return 0;
+    }
     for (int i = 0; i < n; ++i) {
         const bool last = i == n - 1;
         const int pos = pos_max + 1, cell = n_cells;

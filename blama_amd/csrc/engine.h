@@ -121,6 +121,13 @@ struct Ctx {
     float* part_o = nullptr;            // split-K attention partials [ATTN_SMAX][n_head][hd]
     float* attn_smax = nullptr;         // [ATTN_SMAX][n_head] split maxima
     float* attn_scores = nullptr;       // [n_head][n_ctx] scaled KQ
+    // batched prompt ingestion (dense models): GEMM_NT rows of residual / q / attention / FFN
+    bool batch_ok = false;
+    float *xb = nullptr, *qb = nullptr, *attnb = nullptr, *hb = nullptr;
+    int* tokpos_b = nullptr;            // [GEMM_NT][4]
+    int* h_tokpos_b = nullptr;          // pinned ring [kTokbRing][GEMM_NT][4]
+    long long tokb_slot = 0;
+    static constexpr int kTokbRing = 256;
     // diagnostics (MI_STAMPS builds only): s_memrealtime stamps of every
     // workgroup of every launch of the last enqueued step [launch][wg][8]
     static constexpr int kStampLaunches = 320, kStampWgs = 512;
@@ -163,6 +170,8 @@ struct Ctx {
     Ctx(Model* model, uint32_t n_ctx, uint32_t n_batch, uint32_t n_ubatch);
     ~Ctx();
     void enqueue_step(bool with_logits);
+    void enqueue_output(const float* xrow, unsigned long long* stamps_slab);
+    void decode_batch(const int32_t* tokens, int n);
     hipGraphExec_t build_graph(bool with_logits, int seg);
     void invalidate_graphs();
     int decode(const int32_t* tokens, int n);

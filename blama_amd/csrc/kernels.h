@@ -101,6 +101,38 @@ void launch_gemv(const GemvParams& p, int role, int grid, hipStream_t s,
 void init_kernel_attributes();   // once per device, before any graph capture
 int gemv_default_grid(const GemvParams& p);
 
+// ---- batched quantised GEMM over up to GEMM_NT tokens (prompt ingestion) ----
+// The GEMV's integer arithmetic per token (Q8_K / Q8_0 activations, per-block integer
+// dots), with every weight load used for GEMM_NT tokens: a prompt of n tokens streams
+// the weights n/GEMM_NT times instead of n times.  Dense models; one matrix (or a
+// gate/up pair) per launch; epilogues as the GEMV's, per token.
+constexpr int GEMM_NT = 8;
+struct GemmParams {
+    QMat A, B;                 // B: PAIR_AB partner (gate/up)
+    int pair, epi, units;
+    int ntok;                  // tokens in this launch (1..GEMM_NT)
+    int K;
+    int pro;                   // PRO_PLAIN or PRO_RMSNORM
+    const float* x;            // [ntok][x_stride]
+    int x_stride;
+    const float* norm_w;
+    float eps;
+    float* out;                // [ntok][out_stride]
+    int out_stride;
+    const float* resid;        // EPI_ADD: [ntok][out_stride] (may alias out)
+    const int* tokpos;         // [ntok][4] {token, pos, cell, 0}
+    int* cell_pos;
+    float theta_scale, freq_scale;
+    int n_rot, head_dim;
+    const float* freq_factors;
+    __half* kcache;            // this layer's caches
+    __half* vcache;
+    int kv_dim;
+    int need_q8k, need_q80;
+    int grid;                  // set by launch_gemm
+};
+void launch_gemm(const GemmParams& p, hipStream_t s);
+
 // ---- token embedding: get_rows(tok_embd, token) with ggml dequantisation ----
 struct EmbedParams {
     QMat E;                    // quant planes, or E.p[0] = raw f32/f16 rows
@@ -184,5 +216,11 @@ void launch_kv_move(__half* cache, int n_layer, int n_ctx, int kv_dim, const int
 // ---- single-op entry points used by the op-level parity tests ----
 void launch_dequant_rows(const QMat& m, int row0, int nrows, float* out, hipStream_t s);
 void launch_quantize_q8k(const float* x, int K, int8_t* q, float* d, int* bsums, hipStream_t s);
+
+// embedding rows of ntok tokens (tokpos[t*4]) -> out[t*n_embd]
+void launch_embed_multi(const EmbedParams& p, int ntok, hipStream_t s);
+// causal attention of ntok query tokens (q [ntok][n_head*hd]) over <= ATTN_SHORT cells;
+// out [ntok][n_head*hd] (the fused single-split arithmetic per token)
+void launch_attn_multi(const AttnParams& p, int ntok, float* out, hipStream_t s);
 
 }  // namespace mi

@@ -1027,7 +1027,11 @@ static GemvFn gemv_fn(int role, int type, int nslots, int cfg) {
 // Dynamic LDS a GEMV may use: 160 KB minus its static copy of the parameters.
 constexpr int kGemvDynLds = 160 * 1024 - (int)((sizeof(GemvParams) + 15) / 16 * 16);
 
+template <int T, int D> __global__ void gemm_t(const GemmParams P);
+static void gemm_attrs();
+
 void init_kernel_attributes() {
+    gemm_attrs();
     const int types[4] = {T_Q4_K, T_Q5_K, T_Q6_K, T_Q8_0};
     for (int r : {ROLE_GENERIC, ROLE_FFN_UP})
         for (int t : types)
@@ -1087,6 +1091,261 @@ void launch_gemv(const GemvParams& p_in, int role, int grid, hipStream_t s, hipE
         hipExtLaunchKernelGGL(fn, dim3(grid), block, smem, s, ev_start, ev_stop, 0, kx0, knw, ktp, kflags, p);
     else
         hipLaunchKernelGGL(fn, dim3(grid), block, smem, s, kx0, knw, ktp, kflags, p);
+    MI_HIP(hipGetLastError());
+}
+
+// ---------------------------------------------------------------------------
+// Batched GEMM (prompt ingestion): gemv_t's weight ring and integer dots, with every
+// loaded weight chunk dotted against up to GEMM_NT tokens' activations in LDS.
+// Correctness first: the prologue reads its parameters straight from kernarg and
+// quantises the NT activation rows without the decode kernel's latency tricks
+// (one launch streams the weights once for NT tokens).
+// ---------------------------------------------------------------------------
+template <int T, int D>
+__global__ __launch_bounds__(512) void gemm_t(const GemmParams P) {
+    constexpr int NW = 8, NT = GEMM_NT;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    using Kk = Kq<T>;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int sbl = lane >> 3, j = lane & 7;
+    const int nb = P.K >> 8;
+    const int cpr = (nb + 7) >> 3;
+    const int ntok = P.ntok;
+    const ActLayout L = act_layout(P.K, P.need_q8k, P.need_q80);
+    float* rope = reinterpret_cast<float*>(smem + NT * L.slot_bytes);            // [NT][n_rot/2][2]
+    double* red = reinterpret_cast<double*>(rope + NT * ((P.n_rot / 2) * 2 + 2)); // [NT][NW]
+    __shared__ int tp_pos[NT], tp_cell[NT];
+    if (threadIdx.x < NT) {
+        const int t = threadIdx.x < ntok ? threadIdx.x : ntok - 1;
+        tp_pos[threadIdx.x] = P.tokpos ? P.tokpos[t * 4 + 1] : 0;
+        tp_cell[threadIdx.x] = P.tokpos ? P.tokpos[t * 4 + 2] : 0;
+    }
+    // ---- prologue: RMSNorm (double sum, ggml order of rounding) + quantisation of NT rows
+    const auto w4 = gptr(reinterpret_cast<const f32x4*>(P.norm_w));
+    if (P.pro == PRO_RMSNORM) {
+        for (int t = 0; t < NT; ++t) {
+            double sacc = 0.0;
+            if (t < ntok) {
+                const auto x4 = gptr(reinterpret_cast<const f32x4*>(P.x + (long long)t * P.x_stride));
+                for (int blk = wave; blk < nb; blk += NW) {
+                    const f32x4 v = x4[blk * 64 + lane];
+                    sacc += (double)(v.x * v.x);
+                    sacc += (double)(v.y * v.y);
+                    sacc += (double)(v.z * v.z);
+                    sacc += (double)(v.w * v.w);
+                }
+            }
+            sacc = wave_sum63_d(sacc);
+            if (lane == 63) red[t * NW + wave] = sacc;
+        }
+    }
+    __syncthreads();
+    for (int t = 0; t < ntok; ++t) {
+        float scale = 1.0f;
+        if (P.pro == PRO_RMSNORM) {
+            double tot = 0.0;
+            for (int w = 0; w < NW; ++w) tot += red[t * NW + w];
+            scale = 1.0f / sqrtf((float)(tot / (double)P.K) + P.eps);
+        }
+        char* base = smem + t * L.slot_bytes;
+        const auto x4 = gptr(reinterpret_cast<const f32x4*>(P.x + (long long)t * P.x_stride));
+        for (int blk = wave; blk < nb; blk += NW) {
+            const f32x4 xv = x4[blk * 64 + lane];
+            float v[4] = {xv.x, xv.y, xv.z, xv.w};
+            if (P.pro == PRO_RMSNORM) {
+                const f32x4 w = w4[blk * 64 + lane];
+                v[0] = (v[0] * scale) * w.x;
+                v[1] = (v[1] * scale) * w.y;
+                v[2] = (v[2] * scale) * w.z;
+                v[3] = (v[3] * scale) * w.w;
+            }
+            if (P.need_q8k)
+                quant_q8k_block(v, lane, reinterpret_cast<int8_t*>(base + L.q8k) + blk * 256,
+                                reinterpret_cast<int*>(base + L.bsum) + blk * 16,
+                                reinterpret_cast<float*>(base + L.dk) + blk);
+            if (P.need_q80)
+                quant_q80_block(v, lane, reinterpret_cast<int8_t*>(base + L.q80) + blk * 256,
+                                reinterpret_cast<float*>(base + L.d0) + blk * 8);
+        }
+    }
+    __syncthreads();
+    if (P.n_rot > 0) {   // RoPE table of each token's position (ggml_rope_cache_init)
+        for (int t = wave; t < ntok; t += NW) {
+            float* rt = rope + t * ((P.n_rot / 2) * 2 + 2);
+            for (int i = lane; i < P.n_rot / 2; i += 64) {
+                float theta = (float)tp_pos[t];
+                for (int kk = 0; kk < i; ++kk) theta = theta * P.theta_scale;
+                const float ff = P.freq_factors ? P.freq_factors[i] : 1.0f;
+                const float th = P.freq_scale * (theta / ff);
+                rt[2 * i] = cosf(th);
+                rt[2 * i + 1] = sinf(th);
+            }
+        }
+    }
+    __syncthreads();
+
+    // ---- weight stream: the gemv_t ring over this wave's units
+    const int W = P.grid * NW;
+    int u0, u1;
+    unit_range(P.units, W, blockIdx.x * NW + wave, u0, u1);
+    const int n_items = (u1 - u0) * cpr;
+    const bool adj = P.pair == PAIR_ADJ;
+    struct Slot { typename Kk::Ld a, b; };
+    Slot ring[D];
+    int iu = u0, ic = 0, park = 0;
+    const uint8_t* pa[4];
+    const uint8_t* pb[4];
+    auto bases = [&](int u) {
+        const long long ra = adj ? 2LL * u : u;
+        long long rb = adj ? ra + 1 : u;
+        if (adj && rb >= P.A.rows) rb = ra;   // odd tail: re-read row A, result unused
+        const QMat& MB = adj ? P.A : P.B;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            pa[i] = P.A.p[i] + ra * nb * PlaneBytes<T>::b[i];
+            pb[i] = MB.p[i] + rb * nb * PlaneBytes<T>::b[i];
+        }
+    };
+    bases(u0 < P.units ? u0 : P.units - 1);
+    auto issue = [&](Slot& S) {
+        const int sb = park ? 0 : ic * 8 + sbl;
+        const int jj = park ? 0 : j;
+        S.a = Kk::load(pa, sb, jj);
+        S.b = Kk::load(pb, sb, jj);
+        if (iu < u1 && ++ic == cpr) {
+            ic = 0;
+            if (++iu < u1) bases(iu);
+            else park = 1;
+        }
+    };
+#pragma unroll
+    for (int k = 0; k < D - 1; ++k) issue(ring[k]);
+
+    int cu = u0, cc = 0;
+    float accA[NT], accB[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) accA[t] = accB[t] = 0.0f;
+    auto consume = [&](const Slot& S) {
+        const int sb = cc * 8 + sbl;
+        const bool lv = sb < nb;
+        const int sbc = lv ? sb : nb - 1;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            if (t < ntok) {
+                const typename Kk::AR ar = Kk::act(act_view(smem, L, t), sbc, j);
+                const float da = Kk::dot(S.a, ar, j), db = Kk::dot(S.b, ar, j);
+                accA[t] += lv ? da : 0.0f;
+                accB[t] += lv ? db : 0.0f;
+            }
+        }
+        if (++cc == cpr) {
+            const long long ra = adj ? 2LL * cu : cu, rb = adj ? ra + 1 : cu;
+            const bool hasB = !adj || rb < P.A.rows;
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                if (t >= ntok) continue;
+                const float yA = wave_sum63(accA[t]);
+                const float yB = wave_sum63(accB[t]);
+                accA[t] = accB[t] = 0.0f;
+                if (lane != 63) continue;
+                float* out = P.out + (long long)t * P.out_stride;
+                const float* res = P.resid ? P.resid + (long long)t * P.out_stride : nullptr;
+                switch (P.epi) {
+                case EPI_STORE:
+                    out[ra] = yA;
+                    if (hasB) out[rb] = yB;
+                    break;
+                case EPI_ADD: {
+                    const float r0 = res[ra], r1 = hasB ? res[rb] : 0.0f;
+                    out[ra] = yA + r0;
+                    if (hasB) out[rb] = yB + r1;
+                    break;
+                }
+                case EPI_ROPE_Q:
+                case EPI_ROPE_K: {
+                    const float* rt = rope + t * ((P.n_rot / 2) * 2 + 2);
+                    const int i0 = (int)(ra % P.head_dim);
+                    float o0 = yA, o1 = yB;
+                    if (i0 < P.n_rot) {
+                        const float cs = rt[i0], sn = rt[i0 + 1];
+                        o0 = yA * cs - yB * sn;
+                        o1 = yA * sn + yB * cs;
+                    }
+                    if (P.epi == EPI_ROPE_Q) {
+                        out[ra] = o0;
+                        out[rb] = o1;
+                    } else {
+                        __half* kr = P.kcache + (long long)tp_cell[t] * P.kv_dim;
+                        kr[ra] = __float2half_rn(o0);
+                        kr[rb] = __float2half_rn(o1);
+                        if (cu == 0) P.cell_pos[tp_cell[t]] = tp_pos[t];
+                    }
+                    break;
+                }
+                case EPI_V: {
+                    __half* vr = P.vcache + (long long)tp_cell[t] * P.kv_dim;
+                    vr[ra] = __float2half_rn(yA);
+                    if (hasB) vr[rb] = __float2half_rn(yB);
+                    break;
+                }
+                case EPI_SWIGLU:
+                    out[cu] = silu_f(yA) * yB;
+                    break;
+                default: break;
+                }
+            }
+            cc = 0;
+            ++cu;
+        }
+    };
+    for (int base = 0; base < n_items; base += D) {
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+            issue(ring[(k + D - 1) % D]);
+            if (base + k < n_items) consume(ring[k]);
+        }
+    }
+}
+
+typedef void (*GemmFn)(const GemmParams);
+static GemmFn gemm_fn(int type);
+static void gemm_attrs() {
+    for (int t : {T_Q4_K, T_Q5_K, T_Q6_K, T_Q8_0})
+        MI_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_fn(t)),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024));
+}
+static GemmFn gemm_fn(int type) {
+    switch (type) {
+    case T_Q4_K: return gemm_t<T_Q4_K, 4>;
+    case T_Q5_K: return gemm_t<T_Q5_K, 4>;
+    case T_Q6_K: return gemm_t<T_Q6_K, 4>;
+    case T_Q8_0: return gemm_t<T_Q8_0, 4>;
+    default: return nullptr;
+    }
+}
+
+static size_t gemm_smem_bytes(const GemmParams& p) {
+    const ActLayout L = act_layout(p.K, p.need_q8k, p.need_q80);
+    return (size_t)GEMM_NT * L.slot_bytes + (size_t)GEMM_NT * ((p.n_rot / 2) * 2 + 2) * 4 + GEMM_NT * 8 * 8 + 64;
+}
+
+void launch_gemm(const GemmParams& p_in, hipStream_t s) {
+    GemmParams p = p_in;
+    if (p.K % 256 != 0) throw Error("gemm: K must be a multiple of 256");
+    if (p.ntok < 1 || p.ntok > GEMM_NT) throw Error("gemm: 1..GEMM_NT tokens per launch");
+    if (p.pair == PAIR_AB && p.B.type != p.A.type) throw Error("gemm: a pair must share its quant type");
+    if (p.epi == EPI_MOE_DOWN) throw Error("gemm: MoE launches are served token by token");
+    p.need_q8k = p.A.type != T_Q8_0;
+    p.need_q80 = p.A.type == T_Q8_0;
+    const int g = (p.units + 7) / 8;
+    p.grid = g < 1 ? 1 : (g > 256 ? 256 : g);
+    if ((long long)p.units * p.grid * 8 >= (1LL << 32)) throw Error("gemm: too many units");
+    const size_t smem = gemm_smem_bytes(p);
+    if (smem > 150 * 1024) throw Error("gemm: activations of GEMM_NT tokens do not fit LDS");
+    GemmFn fn = gemm_fn(p.A.type);
+    if (!fn) throw Error("gemm: unsupported quant type");
+    hipLaunchKernelGGL(fn, dim3(p.grid), dim3(512), smem, s, p);
     MI_HIP(hipGetLastError());
 }
 
@@ -1154,6 +1413,18 @@ __global__ void embed_kernel(const EmbedParams P) {
     const long long tok = P.tokpos[0];
     for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < P.n_embd; c += gridDim.x * blockDim.x)
         P.out[c] = dequant_elem(P.E, tok, c);
+}
+
+__global__ void embed_multi_kernel(const EmbedParams P) {
+    const long long tok = P.tokpos[blockIdx.y * 4];
+    float* out = P.out + (long long)blockIdx.y * P.n_embd;
+    for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < P.n_embd; c += gridDim.x * blockDim.x)
+        out[c] = dequant_elem(P.E, tok, c);
+}
+
+void launch_embed_multi(const EmbedParams& p, int ntok, hipStream_t s) {
+    hipLaunchKernelGGL(embed_multi_kernel, dim3((p.n_embd + 255) / 256, ntok), dim3(256), 0, s, p);
+    MI_HIP(hipGetLastError());
 }
 
 void launch_embed(const EmbedParams& p, hipStream_t s) {
@@ -1411,18 +1682,22 @@ __global__ __launch_bounds__(256) void attn_fused_kernel(const AttnParams P) {
     __shared__ float gm[R], ginv[R];
     __shared__ float red_o[4][R][HD];
     const int g = blockIdx.x;
+    const int tok = blockIdx.y;   // query token (launch_attn_multi); 0 for a decode step
 #ifdef MI_STAMPS
-    unsigned long long* const stp = P.stamps ? P.stamps + blockIdx.x * 8 : nullptr;
+    unsigned long long* const stp = P.stamps && tok == 0 ? P.stamps + blockIdx.x * 8 : nullptr;
     if (stp && threadIdx.x == 0) stp[0] = __builtin_amdgcn_s_memrealtime();
 #endif
-    const int ncell = min(P.tokpos[2] + 1, ATTN_SHORT), qpos = P.tokpos[1];
+    const int* tp = P.tokpos + 4 * tok;
+    const int ncell = min(tp[2] + 1, ATTN_SHORT), qpos = tp[1];
+    const float* qrow = P.q + (long long)tok * P.n_head * HD;
+    float* orow = P.part_o + (long long)tok * P.n_head * HD;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int L = lane % LPC, G = lane / LPC;
     const long long row_off = (long long)g * HD + L * 8;
     float q[R][8];
 #pragma unroll
     for (int t = 0; t < R; ++t) {
-        const float4* qp = reinterpret_cast<const float4*>(P.q + (long long)(g * R + t) * HD + L * 8);
+        const float4* qp = reinterpret_cast<const float4*>(qrow + (long long)(g * R + t) * HD + L * 8);
         const float4 a = qp[0], b = qp[1];
         const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
 #pragma unroll
@@ -1537,7 +1812,7 @@ __global__ __launch_bounds__(256) void attn_fused_kernel(const AttnParams P) {
     __syncthreads();
     for (int i = tid; i < R * HD; i += 256) {
         const int t = i / HD, d = i % HD;
-        P.part_o[(long long)(g * R + t) * HD + d] = ((red_o[0][t][d] + red_o[1][t][d]) + red_o[2][t][d]) + red_o[3][t][d];
+        orow[(long long)(g * R + t) * HD + d] = ((red_o[0][t][d] + red_o[1][t][d]) + red_o[2][t][d]) + red_o[3][t][d];
     }
 #ifdef MI_STAMPS
     if (stp && threadIdx.x == 0) stp[4] = __builtin_amdgcn_s_memrealtime();
@@ -1576,6 +1851,25 @@ void launch_attn(const AttnParams& p, hipStream_t s) {
     hipLaunchKernelGGL(fa, dim3(p.n_head_kv, ATTN_SMAX), dim3(256), 0, s, p);
     MI_HIP(hipGetLastError());
     hipLaunchKernelGGL(fb, dim3(p.n_head_kv, ATTN_SMAX), dim3(256), 0, s, p);
+    MI_HIP(hipGetLastError());
+}
+
+void launch_attn_multi(const AttnParams& p_in, int ntok, float* out, hipStream_t s) {
+    AttnParams p = p_in;
+    p.part_o = out;
+    p.fused = 1;
+    if (ntok < 1) return;
+    const int r = p.n_head / p.n_head_kv;
+    AttnFn fa = nullptr, fb = nullptr, ff = nullptr;
+    switch (r) {
+    case 1: attn_fns_r<1>(p.head_dim, fa, fb, ff); break;
+    case 2: attn_fns_r<2>(p.head_dim, fa, fb, ff); break;
+    case 4: attn_fns_r<4>(p.head_dim, fa, fb, ff); break;
+    case 8: attn_fns_r<8>(p.head_dim, fa, fb, ff); break;
+    default: break;
+    }
+    if (!ff || p.n_head % p.n_head_kv) throw Error("attn: unsupported head_dim / GQA ratio");
+    hipLaunchKernelGGL(ff, dim3(p.n_head_kv, ntok), dim3(256), 0, s, p);
     MI_HIP(hipGetLastError());
 }
 

@@ -1,10 +1,10 @@
 set -o pipefail
-O=gpurun_out/r01u; mkdir -p $O
+O=gpurun_out/r01w; mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest.log 2>&1; rc=$?
 echo "pytest rc $rc"; tail -3 $O/pytest.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 timeout -k 10 200 python -u bench.py --no-cpu --steps 64 --warmup 8 > $O/bench.json 2> $O/bench.err || exit $?
 cut -c1-330 $O/bench.json
-MI_ENGINE_LIB=stamps timeout -k 10 200 python -u scripts/timeline.py llama2-7b-q4_k_m 96 > $O/timeline.txt 2>&1 || exit $?
-tail -26 $O/timeline.txt | head -12
+
+

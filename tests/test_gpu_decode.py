@@ -209,3 +209,59 @@ def test_split_attention_beyond_short_context(gpu_lib):
         assert np.max(np.abs(got - ref)) <= LOGIT_TOL * rms, ctx.n_cells
         ids, _ = ctx.topk(10)
         assert [int(i) for i in ids] == [i for i, _ in R.topk(ref, 10)]
+
+
+def _logits_close(got, ref, tol=LOGIT_TOL):
+    rms = float(np.sqrt(np.mean(ref.astype(np.float64) ** 2)))
+    return float(np.max(np.abs(got - ref))) <= tol * rms
+
+
+def test_batched_prompt_matches_token_by_token(gpu_lib, monkeypatch):
+    """Prompt ingestion through the batched GEMM (chunks of GEMM_NT = 8 tokens, here 8+8+4)
+    against the same prompt decoded token by token (MI_NO_BATCH=1) and against the oracle:
+    the per-token integer arithmetic is the same, only fp32 sum orders differ."""
+    cfg = synthetic.CONFIGS["tiny-q4_k_m"]
+    buf = synthetic.build_gguf(cfg, seed=13)
+    m = engine.Model(buf)
+    prompt = [int(t) for t in np.random.default_rng(5).integers(0, cfg.n_vocab, 20)]
+    a = engine.Context(m, n_ctx=64)
+    a.decode(prompt)
+    monkeypatch.setenv("MI_NO_BATCH", "1")
+    b = engine.Context(m, n_ctx=64)
+    b.decode(prompt)
+    ref = oracle_from_gguf(buf, n_ctx=64).decode(prompt)
+    la, lb = a.logits(), b.logits()
+    assert _logits_close(la, ref) and _logits_close(lb, ref)
+    assert [int(i) for i in a.topk(10)[0]] == [i for i, _ in R.topk(ref, 10)]
+    # the caches the batch wrote serve the following single-token steps
+    for t in [3, 4]:
+        a.decode([t])
+        b.decode([t])
+        assert _logits_close(a.logits(), b.logits())
+
+
+@pytest.mark.parametrize("cfg_name", ["tiny-q6_k", "tiny-q8_0"])
+def test_batched_prompt_other_quant_types(gpu_lib, cfg_name):
+    cfg = synthetic.CONFIGS[cfg_name]
+    buf = synthetic.build_gguf(cfg, seed=17)
+    m = engine.Model(buf)
+    prompt = [int(t) for t in np.random.default_rng(6).integers(0, cfg.n_vocab, 11)]
+    a = engine.Context(m, n_ctx=32)
+    a.decode(prompt)
+    ref = oracle_from_gguf(buf, n_ctx=32).decode(prompt)
+    assert _logits_close(a.logits(), ref)
+    assert [int(i) for i in a.topk(10)[0]] == [i for i, _ in R.topk(ref, 10)]
+
+
+def test_prefill_512_tokens_matches_oracle(gpu_lib):
+    """The 512-token prefill config (BASELINE configs[2]) at small shapes: 64 chunks of 8,
+    causal attention up to 512 cells, logits of the last token."""
+    cfg = synthetic.CONFIGS["tiny1-q4_k_m"]
+    buf = synthetic.build_gguf(cfg, seed=19)
+    m = engine.Model(buf)
+    prompt = [int(t) for t in np.random.default_rng(7).integers(0, cfg.n_vocab, 512)]
+    a = engine.Context(m, n_ctx=520)
+    a.decode(prompt)
+    ref = oracle_from_gguf(buf, n_ctx=520).decode(prompt)
+    assert _logits_close(a.logits(), ref)
+    assert [int(i) for i in a.topk(10)[0]] == [i for i, _ in R.topk(ref, 10)]
