@@ -99,7 +99,7 @@ size_t gemv_smem_bytes(const GemvParams& p);
 void launch_gemv(const GemvParams& p, int role, int grid, hipStream_t s,
                  hipEvent_t ev_start = nullptr, hipEvent_t ev_stop = nullptr);
 void init_kernel_attributes();   // once per device, before any graph capture
-int gemv_default_grid(const GemvParams& p);
+int gemv_default_grid(const GemvParams& p, int role = ROLE_GENERIC);
 
 // ---- batched quantised GEMM over up to GEMM_NT tokens (prompt ingestion) ----
 // The GEMV's integer arithmetic per token (Q8_K / Q8_0 activations, per-block integer

@@ -981,16 +981,21 @@ typedef void (*GemvFn)(const float*, const float*, const int*, int, const GemvPa
 struct GemvCfg { int nw, d; };
 constexpr GemvCfg kGemvCfgs[] = {{16, 2}, {8, 4}, {8, 3}, {16, 3}, {8, 6}, {8, 8}, {4, 8}};
 constexpr int kNumGemvCfgs = sizeof(kGemvCfgs) / sizeof(kGemvCfgs[0]);
-static int gemv_cfg_for(int type) {
+// Per launch role (measured on the 7B Q4_K_M decode, profiles/r01_*): the FFN gate/up
+// launch (the largest, 50 MB) runs best with 16 waves x 2-deep rings, the others with 8 x 4.
+// MI_GEMV_CFG / MI_GEMV_CFG_<ROLE> override (sweeps).
+static int gemv_cfg_for(int type, int role) {
     static const int forced = getenv("MI_GEMV_CFG") ? atoi(getenv("MI_GEMV_CFG")) : -1;
     if (forced >= 0 && forced < kNumGemvCfgs) return forced;
-    switch (type) {
-    case T_Q4_K: return 1;
-    case T_Q5_K: return 1;
-    case T_Q6_K: return 1;
-    case T_Q8_0: return 1;
-    default: return 0;
+    static const char* names[6] = {"MI_GEMV_CFG_QKV", "MI_GEMV_CFG_WO", "MI_GEMV_CFG_UP", "MI_GEMV_CFG_DOWN",
+                                   "MI_GEMV_CFG_OUT", "MI_GEMV_CFG_GEN"};
+    static int per_role[6] = {-2, -2, -2, -2, -2, -2};
+    if (role >= 0 && role < 6) {
+        if (per_role[role] == -2) per_role[role] = getenv(names[role]) ? atoi(getenv(names[role])) : -1;
+        if (per_role[role] >= 0 && per_role[role] < kNumGemvCfgs) return per_role[role];
     }
+    (void)type;
+    return role == ROLE_FFN_UP ? 0 : 1;
 }
 
 template <int T, int DUAL, int ROLE>
@@ -1046,11 +1051,11 @@ static int wg_units_max(int total_units, int grid) { return (total_units + grid 
 
 size_t gemv_smem_bytes(const GemvParams& p) { return (size_t)smem_plan(p).total; }
 
-int gemv_default_grid(const GemvParams& p) {
+int gemv_default_grid(const GemvParams& p, int role) {
     // One workgroup per CU (256 CUs): the per-workgroup prologue (activation
     // quantisation) is paid once per CU.  Small launches use fewer workgroups
     // so that every wave still gets a unit.
-    const int nw = kGemvCfgs[gemv_cfg_for(p.seg[0].A.type)].nw;
+    const int nw = kGemvCfgs[gemv_cfg_for(p.seg[0].A.type, role)].nw;
     const int g = (p.total_units + nw - 1) / nw;
     return g < 1 ? 1 : (g > 256 ? 256 : g);
 }
@@ -1065,8 +1070,8 @@ void launch_gemv(const GemvParams& p_in, int role, int grid, hipStream_t s, hipE
             throw Error("gemv: all matrices of one launch must share a quant type");
     if (p.pro == PRO_ATTN && (p.attn.n_head * p.attn.head_dim != p.K || p.attn.head_dim % 4 != 0))
         throw Error("gemv: attention combine needs K == n_head*head_dim");
-    const int cfg = gemv_cfg_for(type);
-    if (grid <= 0) grid = gemv_default_grid(p);
+    const int cfg = gemv_cfg_for(type, role);
+    if (grid <= 0) grid = gemv_default_grid(p, role);
     if ((long long)p.total_units * grid * kGemvCfgs[cfg].nw >= (1LL << 32))
         throw Error("gemv: too many units for the 32-bit unit split");
     p.wg_units = wg_units_max(p.total_units, grid);
