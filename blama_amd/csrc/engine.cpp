@@ -397,12 +397,22 @@ Ctx::Ctx(Model* model, uint32_t nctx, uint32_t nbatch, uint32_t nubatch) : m(mod
 #endif
     batch_ok = hp.n_expert == 0 && getenv("MI_NO_BATCH") == nullptr;
     if (batch_ok) {
-        MI_HIP(hipMalloc(&xb, (size_t)GEMM_NT * hp.n_embd * sizeof(float)));
-        MI_HIP(hipMalloc(&qb, (size_t)GEMM_NT * hp.n_embd * sizeof(float)));
-        MI_HIP(hipMalloc(&attnb, (size_t)GEMM_NT * hp.n_embd * sizeof(float)));
-        MI_HIP(hipMalloc(&hb, (size_t)GEMM_NT * hp.n_ff * sizeof(float)));
-        MI_HIP(hipMalloc(&tokpos_b, (size_t)GEMM_NT * 4 * sizeof(int)));
-        MI_HIP(hipHostMalloc(&h_tokpos_b, (size_t)kTokbRing * GEMM_NT * 4 * sizeof(int)));
+        // MFMA path when every layer matrix is Q4_K / Q6_K (the Q4_K_M / Q6_K models)
+        mmq_ok = getenv("MI_NO_MMQ") == nullptr;
+        for (const Layer& L : m->layers)
+            for (const QMat* q : {&L.wq, &L.wk, &L.wv, &L.wo, &L.gate, &L.up, &L.down})
+                mmq_ok = mmq_ok && mmq_supported(q->type) && q->rows % 16 == 0;
+        const int NB = kBatchRows;
+        MI_HIP(hipMalloc(&xb, (size_t)NB * hp.n_embd * sizeof(float)));
+        MI_HIP(hipMalloc(&qb, (size_t)NB * hp.n_embd * sizeof(float)));
+        MI_HIP(hipMalloc(&attnb, (size_t)NB * hp.n_embd * sizeof(float)));
+        MI_HIP(hipMalloc(&hb, (size_t)NB * hp.n_ff * sizeof(float)));
+        MI_HIP(hipMalloc(&tokpos_b, (size_t)NB * 4 * sizeof(int)));
+        MI_HIP(hipHostMalloc(&h_tokpos_b, (size_t)kTokbRing * NB * 4 * sizeof(int)));
+        const int kmax = std::max(hp.n_embd, hp.n_ff);
+        MI_HIP(hipMalloc(&q8r_q, (size_t)MMQ_NT * kmax));
+        MI_HIP(hipMalloc(&q8r_d, (size_t)MMQ_NT * (kmax / 256) * sizeof(float)));
+        MI_HIP(hipMalloc(&q8r_bsum, (size_t)MMQ_NT * (kmax / 16) * sizeof(int)));
     }
     MI_HIP(hipMalloc(&attn_smax, (size_t)ATTN_SMAX * hp.n_head * sizeof(float)));
     MI_HIP(hipMalloc(&attn_scores, (size_t)hp.n_head * n_ctx * sizeof(float)));
@@ -436,7 +446,8 @@ Ctx::~Ctx() {
                     (void*)q, (void*)attn, (void*)h, (void*)h2, (void*)logits, (void*)cand, (void*)topk_ids,
                     (void*)topk_vals, (void*)sel, (void*)selw, (void*)gather_ids, (void*)gather_out,
                     (void*)cell_delta, (void*)move_src, (void*)part_o, (void*)attn_smax, (void*)attn_scores, (void*)stamps,
-                    (void*)xb, (void*)qb, (void*)attnb, (void*)hb, (void*)tokpos_b})
+                    (void*)xb, (void*)qb, (void*)attnb, (void*)hb, (void*)tokpos_b, (void*)q8r_q,
+                    (void*)q8r_d, (void*)q8r_bsum})
         if (p) hipFree(p);
     for (void* p : {(void*)h_tokpos, (void*)h_topk_ids, (void*)h_topk_vals, (void*)h_logits, (void*)h_gather,
                     (void*)h_tokpos_b})
@@ -683,11 +694,27 @@ void Ctx::decode_batch(const int32_t* tokens, int n) {
     const HParams& hp = m->hp;
     const float theta_scale = std::pow(hp.rope_base, -2.0f / (float)hp.n_rot);
     const float kq_scale = 1.0f / std::sqrt((float)hp.head_dim);
-    for (int c0 = 0; c0 < n; c0 += GEMM_NT) {
-        const int nt = std::min(GEMM_NT, n - c0);
+    const int chunk = mmq_ok ? MMQ_NT : GEMM_NT;
+    auto q8 = [&](int K) { return Q8Rows{q8r_q, q8r_d, q8r_bsum, K}; };
+    // one projection: the int8-MFMA kernel on Q8_K rows quantised once per activation, or the
+    // v_dot4 GEMM that quantises its own rows
+    auto proj = [&](GemmParams p, const float* x, int x_stride, const float* norm, bool quantise) {
+        if (mmq_ok) {
+            if (quantise) launch_quant_rows(x, x_stride, norm, m->hp.eps, p.ntok, q8(p.K), stream);
+            launch_gemm_mmq(p, q8(p.K), stream);
+        } else {
+            p.x = x;
+            p.x_stride = x_stride;
+            p.norm_w = norm;
+            p.pro = norm ? PRO_RMSNORM : PRO_PLAIN;
+            launch_gemm(p, stream);
+        }
+    };
+    for (int c0 = 0; c0 < n; c0 += chunk) {
+        const int nt = std::min(chunk, n - c0);
         const long long slot = tokb_slot++ % kTokbRing;
         if (slot == 0 && tokb_slot > 1) MI_HIP(hipStreamSynchronize(stream));
-        int* hpos = h_tokpos_b + slot * GEMM_NT * 4;
+        int* hpos = h_tokpos_b + slot * kBatchRows * 4;
         for (int t = 0; t < nt; ++t) {
             const int pos = pos_max + 1, cell = n_cells;
             hpos[t * 4 + 0] = tokens[c0 + t];
@@ -728,14 +755,10 @@ void Ctx::decode_batch(const int32_t* tokens, int n) {
                 p.epi = epis[i];
                 p.units = (mats[i]->rows + 1) / 2;
                 p.K = hp.n_embd;
-                p.pro = PRO_RMSNORM;
-                p.x = xb;
-                p.x_stride = hp.n_embd;
-                p.norm_w = L.attn_norm;
                 p.out = qb;
                 p.out_stride = hp.n_embd;
                 p.n_rot = i < 2 ? hp.n_rot : 0;
-                launch_gemm(p, stream);
+                proj(p, xb, hp.n_embd, L.attn_norm, i == 0);   // the three share one quantisation
             }
             AttnParams a{qb, kl, vl, tokpos_b, cell_pos, attn_scores, attn_smax, attnb, hp.n_head, hp.n_head_kv,
                          hp.head_dim, kv_dim, (int)n_ctx, kq_scale};
@@ -747,13 +770,10 @@ void Ctx::decode_batch(const int32_t* tokens, int n) {
                 p.epi = EPI_ADD;
                 p.units = (L.wo.rows + 1) / 2;
                 p.K = hp.n_embd;
-                p.pro = PRO_PLAIN;
-                p.x = attnb;
-                p.x_stride = hp.n_embd;
                 p.out = xb;
                 p.resid = xb;
                 p.out_stride = hp.n_embd;
-                launch_gemm(p, stream);
+                proj(p, attnb, hp.n_embd, nullptr, true);
             }
             {   // FFN gate/up + SwiGLU
                 GemmParams p = b;
@@ -763,13 +783,9 @@ void Ctx::decode_batch(const int32_t* tokens, int n) {
                 p.epi = EPI_SWIGLU;
                 p.units = L.gate.rows;
                 p.K = hp.n_embd;
-                p.pro = PRO_RMSNORM;
-                p.x = xb;
-                p.x_stride = hp.n_embd;
-                p.norm_w = L.ffn_norm;
                 p.out = hb;
                 p.out_stride = hp.n_ff;
-                launch_gemm(p, stream);
+                proj(p, xb, hp.n_embd, L.ffn_norm, true);
             }
             {   // FFN down + residual
                 GemmParams p = b;
@@ -778,13 +794,10 @@ void Ctx::decode_batch(const int32_t* tokens, int n) {
                 p.epi = EPI_ADD;
                 p.units = (L.down.rows + 1) / 2;
                 p.K = hp.n_ff;
-                p.pro = PRO_PLAIN;
-                p.x = hb;
-                p.x_stride = hp.n_ff;
                 p.out = xb;
                 p.resid = xb;
                 p.out_stride = hp.n_embd;
-                launch_gemm(p, stream);
+                proj(p, hb, hp.n_ff, nullptr, true);
             }
         }
         if (c0 + nt == n) enqueue_output(xb + (size_t)(nt - 1) * hp.n_embd, nullptr);

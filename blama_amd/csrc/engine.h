@@ -128,6 +128,11 @@ struct Ctx {
     int* h_tokpos_b = nullptr;          // pinned ring [kTokbRing][GEMM_NT][4]
     long long tokb_slot = 0;
     static constexpr int kTokbRing = 256;
+    static constexpr int kBatchRows = MMQ_NT > GEMM_NT ? MMQ_NT : GEMM_NT;
+    bool mmq_ok = false;                // int8-MFMA GEMM for prompt chunks (all layers Q4_K / Q6_K)
+    int8_t* q8r_q = nullptr;            // Q8_K rows of one prompt chunk
+    float* q8r_d = nullptr;
+    int* q8r_bsum = nullptr;
     // diagnostics (MI_STAMPS builds only): s_memrealtime stamps of every
     // workgroup of every launch of the last enqueued step [launch][wg][8]
     static constexpr int kStampLaunches = 320, kStampWgs = 512;

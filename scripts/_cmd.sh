@@ -1,9 +1,9 @@
 set -o pipefail
-O=gpurun_out/r01y; mkdir -p $O
+O=gpurun_out/r02b; mkdir -p $O
 export TMPDIR=/tmp
-run() { tag=$1; shift; env "$@" timeout -k 10 200 python -u bench.py --no-cpu --steps 64 --warmup 8 --prefill 0 > $O/b_$tag.json 2> $O/b_$tag.err || exit $?; echo "$tag: $(python -c "import json;d=json.load(open('$O/b_$tag.json'));print(d['value'], d['roofline']['avg_launch_us'])")"; }
-run default X=1
-run down0 MI_GEMV_CFG_DOWN=0
-run qkv0 MI_GEMV_CFG_QKV=0
-run wo0 MI_GEMV_CFG_WO=0
-run out0 MI_GEMV_CFG_OUT=0
+timeout -k 10 60 ./scripts/exp_mfma_layout || exit $?
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest.log 2>&1; rc=$?
+echo "pytest rc $rc"; tail -3 $O/pytest.log
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+timeout -k 10 200 python -u bench.py --no-cpu --steps 64 --warmup 8 > $O/bench.json 2> $O/bench.err || exit $?
+python -c "import json;d=json.load(open('$O/bench.json'));print(d['value'], d.get('prefill'))"

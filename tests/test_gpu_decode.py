@@ -217,8 +217,9 @@ def _logits_close(got, ref, tol=LOGIT_TOL):
 
 
 def test_batched_prompt_matches_token_by_token(gpu_lib, monkeypatch):
-    """Prompt ingestion through the batched GEMM (chunks of GEMM_NT = 8 tokens, here 8+8+4)
-    against the same prompt decoded token by token (MI_NO_BATCH=1) and against the oracle:
+    """Prompt ingestion through the batched GEMMs (int8-MFMA: chunks of 16 tokens, 16+4;
+    v_dot4 with MI_NO_MMQ=1: chunks of 8, 8+8+4) against the same prompt decoded token by
+    token (MI_NO_BATCH=1) and against the oracle:
     the per-token integer arithmetic is the same, only fp32 sum orders differ."""
     cfg = synthetic.CONFIGS["tiny-q4_k_m"]
     buf = synthetic.build_gguf(cfg, seed=13)
@@ -226,12 +227,15 @@ def test_batched_prompt_matches_token_by_token(gpu_lib, monkeypatch):
     prompt = [int(t) for t in np.random.default_rng(5).integers(0, cfg.n_vocab, 20)]
     a = engine.Context(m, n_ctx=64)
     a.decode(prompt)
+    monkeypatch.setenv("MI_NO_MMQ", "1")          # the v_dot4 GEMM instead of the int8-MFMA one
+    c = engine.Context(m, n_ctx=64)
+    c.decode(prompt)
     monkeypatch.setenv("MI_NO_BATCH", "1")
     b = engine.Context(m, n_ctx=64)
     b.decode(prompt)
     ref = oracle_from_gguf(buf, n_ctx=64).decode(prompt)
     la, lb = a.logits(), b.logits()
-    assert _logits_close(la, ref) and _logits_close(lb, ref)
+    assert _logits_close(la, ref) and _logits_close(lb, ref) and _logits_close(c.logits(), ref)
     assert [int(i) for i in a.topk(10)[0]] == [i for i, _ in R.topk(ref, 10)]
     # the caches the batch wrote serve the following single-token steps
     for t in [3, 4]:
