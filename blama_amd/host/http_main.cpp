@@ -1,0 +1,207 @@
+// blama-http-server on the MI355X engine: the L5 executable.  Mirrors reference
+// server/code/http/HttpServerMain.cpp:
+//   POST /complete            (:311-318) -> {"text", "tokenData"}
+//   POST /verify_completion   (:328-338) {"request", "response"} -> {"result"}
+//   any other method          (:305-309) -> 400
+//   any other path            (:350-354) -> 404
+//   env BLAMA_HOST (default 0.0.0.0), BLAMA_PORT (default 7331), BLAMA_MODEL (:383-435),
+//   validated with the reference's error messages
+//
+// What differs:
+// - Plain POSIX sockets, one thread per connection and one request per connection.  The
+//   reference uses Boost.Beast coroutines, and Boost is not in this image.  Every request
+//   still runs on the Server's single worker, so the concurrency model is the reference's.
+// - BLAMA_MODEL is required: the reference falls back to a gpt2 test file that is not here.
+// - BLAMA_PORT=0 binds an ephemeral port.  The bound port is printed as
+//   "Listening on port N".
+// - A body that is not valid JSON, or a request that throws on the worker, gets a 500 with
+//   the message in the body.  In the reference the exception ends the coroutine.
+// - /chat/completions and /chat/verify_completion return 501: chat templating is out of scope.
+#include <arpa/inet.h>
+#include <netinet/in.h>
+#include <signal.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <filesystem>
+#include <future>
+#include <iostream>
+#include <limits>
+#include <string>
+#include <thread>
+
+#include "server.hpp"
+#include "wire.hpp"
+
+namespace fs = std::filesystem;
+using bl::llama::server::Server;
+namespace wire = bl::llama::server::wire;
+
+namespace {
+
+struct Request {
+    std::string method, target, body;
+};
+
+bool readRequest(int fd, Request& req) {
+    std::string buf;
+    char chunk[65536];
+    size_t hdrEnd = std::string::npos;
+    while ((hdrEnd = buf.find("\r\n\r\n")) == std::string::npos) {
+        const ssize_t n = ::recv(fd, chunk, sizeof chunk, 0);
+        if (n <= 0) return false;
+        buf.append(chunk, (size_t)n);
+        if (buf.size() > (64u << 20)) return false;
+    }
+    const std::string head = buf.substr(0, hdrEnd);
+    const size_t sp1 = head.find(' '), sp2 = head.find(' ', sp1 + 1);
+    if (sp1 == std::string::npos || sp2 == std::string::npos) return false;
+    req.method = head.substr(0, sp1);
+    req.target = head.substr(sp1 + 1, sp2 - sp1 - 1);
+    size_t clen = 0;
+    size_t pos = head.find("\r\n");
+    while (pos != std::string::npos && pos < head.size()) {
+        const size_t next = head.find("\r\n", pos + 2);
+        std::string line = head.substr(pos + 2, (next == std::string::npos ? head.size() : next) - pos - 2);
+        const size_t colon = line.find(':');
+        if (colon != std::string::npos) {
+            std::string key = line.substr(0, colon);
+            for (auto& c : key) c = (char)std::tolower((unsigned char)c);
+            if (key == "content-length") clen = std::stoul(line.substr(colon + 1));
+        }
+        pos = next;
+    }
+    req.body = buf.substr(hdrEnd + 4);
+    while (req.body.size() < clen) {
+        const ssize_t n = ::recv(fd, chunk, sizeof chunk, 0);
+        if (n <= 0) return false;
+        req.body.append(chunk, (size_t)n);
+    }
+    req.body.resize(clen);
+    return true;
+}
+
+void writeAll(int fd, const std::string& s) {
+    size_t off = 0;
+    while (off < s.size()) {
+        const ssize_t n = ::send(fd, s.data() + off, s.size() - off, MSG_NOSIGNAL);
+        if (n <= 0) return;
+        off += (size_t)n;
+    }
+}
+
+void respond(int fd, int status, const char* reason, const std::string& body, bool json) {
+    std::string r = "HTTP/1.1 " + std::to_string(status) + " " + reason + "\r\n";
+    r += "Server: blama-amd\r\n";
+    if (json) r += "Content-Type: text/json\r\n";              // HttpServerMain.cpp:268
+    r += "Access-Control-Allow-Origin: *\r\n";
+    r += "Content-Length: " + std::to_string(body.size()) + "\r\n";
+    r += "Connection: close\r\n\r\n";
+    r += body;
+    writeAll(fd, r);
+}
+
+void handle(int fd, Server& server) {
+    Request req;
+    if (!readRequest(fd, req)) {
+        ::close(fd);
+        return;
+    }
+    try {
+        if (req.method != "POST") {
+            respond(fd, 400, "Bad Request", "", false);
+        } else if (req.target == "/complete") {
+            auto params = wire::toCompleteParams(bl::json::parse(req.body));
+            // shared: the worker may still be inside set_value when this thread wakes
+            auto pr = std::make_shared<std::promise<Server::CompleteReponse>>();
+            auto fut = pr->get_future();
+            server.completeText(std::move(params), [pr](Server::CompleteReponse r) { pr->set_value(std::move(r)); },
+                                [pr](std::exception_ptr e) { pr->set_exception(e); });
+            respond(fd, 200, "OK", wire::completeBody(fut.get()), true);
+        } else if (req.target == "/verify_completion") {
+            const auto j = bl::json::parse(req.body);
+            auto rreq = wire::toCompleteParams(j.at("request"));
+            auto rrsp = wire::toCompleteResponse(j.at("response"));
+            auto pr = std::make_shared<std::promise<float>>();
+            auto fut = pr->get_future();
+            server.verify(std::move(rreq), std::move(rrsp), [pr](float s) { pr->set_value(s); },
+                          [pr](std::exception_ptr e) { pr->set_exception(e); });
+            respond(fd, 200, "OK", wire::verifyBody(fut.get()), true);
+        } else if (req.target == "/chat/completions" || req.target == "/chat/verify_completion") {
+            respond(fd, 501, "Not Implemented", "chat templating is not served by this build", false);
+        } else {
+            respond(fd, 404, "Not Found", "", false);
+        }
+    } catch (const std::exception& e) {
+        respond(fd, 500, "Internal Server Error", e.what(), false);
+    }
+    ::shutdown(fd, SHUT_WR);
+    ::close(fd);
+}
+
+std::string modelFromEnv() {
+    const char* model_env = std::getenv("BLAMA_MODEL");
+    if (!model_env || std::string(model_env).empty())
+        throw std::runtime_error("Environment variable not set or empty: BLAMA_MODEL");
+    std::string path(model_env);
+    if (!path.ends_with(".gguf")) throw std::runtime_error("BLAMA_MODEL does not end with .gguf: " + path);
+    if (!fs::exists(path)) throw std::runtime_error("BLAMA_MODEL does not exist: " + path);
+    if (!fs::is_regular_file(path)) throw std::runtime_error("BLAMA_MODEL is not a regular file: " + path);
+    return path;
+}
+
+}  // namespace
+
+int serve();
+
+int main() {
+    try {
+        return serve();
+    } catch (const std::exception& e) {   // configuration errors: message and a non-zero exit
+        std::cerr << "blama-http-server: " << e.what() << std::endl;
+        return 1;
+    }
+}
+
+int serve() {
+    ::signal(SIGPIPE, SIG_IGN);
+    in_addr host{};
+    host.s_addr = htonl(INADDR_ANY);
+    if (const char* h = std::getenv("BLAMA_HOST")) {
+        if (::inet_pton(AF_INET, h, &host) != 1) throw std::invalid_argument("Invalid BLAMA_HOST");
+    }
+    uint16_t port = 7331;
+    if (const char* p = std::getenv("BLAMA_PORT")) {
+        size_t idx = 0;
+        const unsigned long v = std::stoul(p, &idx, 10);
+        if (idx != std::strlen(p)) throw std::invalid_argument("Extra characters after BLAMA_PORT number");
+        if (v > std::numeric_limits<uint16_t>::max()) throw std::out_of_range("Value exceeds uint16_t max");
+        port = (uint16_t)v;
+    }
+    const std::string modelGguf = modelFromEnv();
+    std::cout << "Loading model " << modelGguf << std::endl;
+    Server server(std::make_shared<bl::llama::Model>(modelGguf, bl::llama::Model::Params{}));
+
+    const int lfd = ::socket(AF_INET, SOCK_STREAM, 0);
+    const int one = 1;
+    ::setsockopt(lfd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
+    sockaddr_in addr{};
+    addr.sin_family = AF_INET;
+    addr.sin_addr = host;
+    addr.sin_port = htons(port);
+    if (::bind(lfd, (sockaddr*)&addr, sizeof addr) != 0 || ::listen(lfd, 64) != 0) {
+        std::perror("bind/listen");
+        return 1;
+    }
+    socklen_t alen = sizeof addr;
+    ::getsockname(lfd, (sockaddr*)&addr, &alen);
+    std::cout << "Listening on port " << ntohs(addr.sin_port) << std::endl;
+    for (;;) {
+        const int fd = ::accept(lfd, nullptr, nullptr);
+        if (fd < 0) continue;
+        std::thread([fd, &server] { handle(fd, server); }).detach();
+    }
+}

@@ -1,0 +1,85 @@
+// bl::llama::server::Server on the MI355X engine: the request layer (L4) behind Blama's HTTP
+// endpoints.  Mirrors reference server/code/server/Server.hpp:17-68.  The request and response
+// structs, the completeText/verify flow and the single worker thread are the same:
+//
+//   completeText  Server.cpp:45-77    startSession{seed,temp,topP} -> tokenize(prompt, true, true)
+//                                     -> setInitialPrompt -> complete{maxTokens} -> response
+//                                     -> cb -> stopSession
+//   verify        Server.cpp:127-161  startSession -> setInitialPrompt -> fillCtx(claimed)
+//                                     -> LogitComparer::compare + MetricsAggregator per token -> cb(score)
+//   worker        Server.cpp:36       every request runs on one thread, so one engine context
+//                                     serves them in arrival order
+//
+// What differs:
+// - The callbacks are std::function, where the reference uses itlib::ufunction.  itlib is not
+//   in this image.
+// - An optional error callback receives exceptions raised on the worker.  The reference lets
+//   them escape the io_context thread.
+// - chatComplete/chatVerify are not served: the chat templating is out of scope.
+//
+// Scaling across GPUs uses one Server per GPU process (replicas).
+#pragma once
+#include <condition_variable>
+#include <cstdint>
+#include <deque>
+#include <exception>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "llama.hpp"
+
+namespace bl::llama::server {
+
+class Server {
+public:
+    explicit Server(std::shared_ptr<Model> model);
+    ~Server();
+
+    Server(const Server&) = delete;
+    Server& operator=(const Server&) = delete;
+
+    struct CompleteRequestParams {     // Server.hpp:25-32
+        std::string prompt;
+        uint32_t maxTokens = 0;
+        uint32_t seed = 0;
+        std::string suffix;
+        float temperature = 0.8f;
+        float topP = 0.95f;
+    };
+
+    struct TokenData {                 // Server.hpp:46-56
+        std::string tokenStr;
+        uint32_t tokenId = 0;
+        struct LogitData {
+            uint32_t tokenId = 0;
+            float logit = 0;
+        };
+        std::vector<LogitData> logits;
+    };
+
+    using CompleteReponse = std::vector<TokenData>;   // (sic) Server.hpp:56
+    using ErrorCb = std::function<void(std::exception_ptr)>;
+
+    void completeText(CompleteRequestParams params, std::function<void(CompleteReponse)> cb,
+                      ErrorCb onError = {});
+    void verify(CompleteRequestParams req, CompleteReponse resp, std::function<void(float)> cb,
+                ErrorCb onError = {});
+
+private:
+    void post(std::function<void()> job, ErrorCb onError);
+    void run();
+
+    std::shared_ptr<Model> m_model;
+    std::unique_ptr<Instance> m_instance;
+    std::mutex m_mu;
+    std::condition_variable m_cv;
+    std::deque<std::pair<std::function<void()>, ErrorCb>> m_jobs;
+    bool m_stop = false;
+    std::thread m_worker;
+};
+
+}  // namespace bl::llama::server

@@ -53,6 +53,14 @@ inline void fail(const char* file, int line, const std::string& what) {
         if (!thrown_) minitest::fail(__FILE__, __LINE__, std::string(#expr) + " did not throw"); \
     } while (0)
 
+#define CHECK_THROWS(expr)                                                                    \
+    do {                                                                                      \
+        ++minitest::checks();                                                                 \
+        bool thrown_ = false;                                                                 \
+        try { (void)(expr); } catch (const std::exception&) { thrown_ = true; }               \
+        if (!thrown_) minitest::fail(__FILE__, __LINE__, std::string(#expr) + " did not throw"); \
+    } while (0)
+
 // main: run the cases of the groups named on the command line (default: all).
 #define MINITEST_MAIN(setup)                                                                  \
     int main(int argc, char** argv) {                                                         \

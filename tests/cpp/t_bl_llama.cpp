@@ -6,11 +6,14 @@
 // usage: t_bl_llama [cpu] [gpu] --model=<gguf> --vocab=<gguf> --out=<file>
 #include "llama.hpp"
 #include "minitest.hpp"
+#include "server.hpp"
+#include "wire.hpp"
 
 #include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <fstream>
+#include <future>
 
 namespace {
 std::string g_model, g_vocab, g_out;
@@ -129,6 +132,50 @@ TEST_CASE_G("vocab only", "cpu") {   // t-integration.cpp:25-43
     std::string back;
     for (Token x : by) back += vocab.tokenToString(x);
     CHECK(back == " \xc3\xa9");
+}
+
+TEST_CASE_G("wire format", "cpu") {   // HttpServerMain.cpp:37-94, 259-288
+    using server::Server;
+    namespace wire = server::wire;
+    Server::CompleteReponse gen;
+    gen.push_back({" he said \"hi\"\n\t\x01", 301, {{301, 17.25f}, {7, -0.1f}, {1234567, 3.14159274f}}});
+    gen.push_back({"\xc3\xa9\xe2\x82\xac", 77, {{77, 1e-30f}, {5, -1.17549435e-38f}, {9, 0.333333343f}}});
+    gen.push_back({"", 0, {}});
+    const std::string body = wire::completeBody(gen);
+    const auto j = bl::json::parse(body);
+    CHECK(j.at("text").as_string() == gen[0].tokenStr + gen[1].tokenStr);
+    auto back = wire::toCompleteResponse(j);
+    REQUIRE(back.size() == gen.size());
+    for (size_t i = 0; i < gen.size(); ++i) {
+        CHECK(back[i].tokenStr == gen[i].tokenStr);
+        CHECK(back[i].tokenId == gen[i].tokenId);
+        REQUIRE(back[i].logits.size() == gen[i].logits.size());
+        for (size_t k = 0; k < gen[i].logits.size(); ++k) {
+            CHECK(back[i].logits[k].tokenId == gen[i].logits[k].tokenId);
+            CHECK(std::memcmp(&back[i].logits[k].logit, &gen[i].logits[k].logit, 4) == 0);   // float-exact
+        }
+    }
+    // request keys: "prompt" required, the rest optional with the Server.hpp:25-32 defaults
+    auto p = wire::toCompleteParams(bl::json::parse(R"({"prompt": "a\u00e9\ud83d\ude00"})"));
+    CHECK(p.prompt == "a\xc3\xa9\xf0\x9f\x98\x80");
+    CHECK(p.maxTokens == 0u);
+    CHECK(p.seed == 0u);
+    CHECK(p.temperature == 0.8f);
+    CHECK(p.topP == 0.95f);
+    p = wire::toCompleteParams(bl::json::parse(
+        R"({"prompt":"x","max_tokens":16,"seed":42,"suffix":"y","temp":0.5,"top_p":0.9})"));
+    CHECK(p.maxTokens == 16u);
+    CHECK(p.seed == 42u);
+    CHECK(p.suffix == "y");
+    CHECK(p.temperature == 0.5f);
+    CHECK(p.topP == 0.9f);
+    auto p2 = wire::toCompleteParams(bl::json::parse(bl::json::dump(wire::fromCompleteParams(p))));
+    CHECK(p2.prompt == p.prompt && p2.maxTokens == p.maxTokens && p2.seed == p.seed);
+    CHECK(p2.temperature == p.temperature && p2.topP == p.topP && p2.suffix == p.suffix);
+    CHECK_THROWS(wire::toCompleteParams(bl::json::parse(R"({"max_tokens": 3})")));
+    CHECK_THROWS(bl::json::parse("{\"prompt\": }"));
+    CHECK_THROWS(bl::json::parse("[1, 2"));
+    CHECK((float)bl::json::parse(wire::verifyBody(0.975f)).at("result").as_number() == 0.975f);
 }
 
 // ---------------------------------------------------------------- GPU ----
@@ -268,6 +315,53 @@ TEST_CASE_G("complete for the oracle", "gpu") {   // t-LogitComparer.cpp:41-79, 
         f << "\n";
     }
     CHECK(iRes.size() == 12);
+}
+
+TEST_CASE_G("server", "gpu") {   // Server.cpp:45-77 and :127-161 through the worker thread
+    using server::Server;
+    auto model = std::make_shared<Model>(g_model, Model::Params{});
+    Server srv(model);
+    Server::CompleteRequestParams req;
+    req.prompt = "hello world";
+    req.maxTokens = 8;
+    req.seed = 3;
+    std::promise<Server::CompleteReponse> pc;
+    srv.completeText(req, [&](Server::CompleteReponse r) { pc.set_value(std::move(r)); });
+    auto resp = pc.get_future().get();
+    REQUIRE(resp.size() == 8);
+    for (auto& t : resp) {
+        CHECK(t.logits.size() == 10);
+        CHECK(t.tokenStr == model->vocab().tokenToString((Token)t.tokenId));
+    }
+    // the same request again: same seed, same completion (session per request)
+    std::promise<Server::CompleteReponse> pc2;
+    srv.completeText(req, [&](Server::CompleteReponse r) { pc2.set_value(std::move(r)); });
+    auto resp2 = pc2.get_future().get();
+    REQUIRE(resp2.size() == resp.size());
+    for (size_t i = 0; i < resp.size(); ++i) CHECK(resp2[i].tokenId == resp[i].tokenId);
+    // verify of its own completion after a JSON round trip scores 1
+    auto wired = server::wire::toCompleteResponse(bl::json::parse(server::wire::completeBody(resp)));
+    std::promise<float> pv;
+    srv.verify(req, wired, [&](float s) { pv.set_value(s); });
+    CHECK(pv.get_future().get() == 1.0f);
+    // a tampered completion scores below 1
+    auto bad = resp;
+    for (auto& t : bad)
+        for (auto& l : t.logits) l.logit *= 1.5f;
+    std::promise<float> pb;
+    srv.verify(req, bad, [&](float s) { pb.set_value(s); });
+    const float sb = pb.get_future().get();
+    CHECK(sb < 0.95f);
+    // an error on the worker reaches the error callback and the next request still runs
+    auto huge = resp;             // a claimed token outside the vocabulary makes decode throw
+    huge[0].tokenId = 1u << 30;
+    std::promise<float> pe;
+    srv.verify(req, huge, [&](float s) { pe.set_value(s); },
+               [&](std::exception_ptr e) { pe.set_exception(e); });
+    CHECK_THROWS(pe.get_future().get());
+    std::promise<float> pv2;
+    srv.verify(req, wired, [&](float s) { pv2.set_value(s); });
+    CHECK(pv2.get_future().get() == 1.0f);
 }
 
 MINITEST_MAIN(setup)

@@ -1,0 +1,150 @@
+"""blama-http-server (blama_amd/host/http_main.cpp) over real sockets, the way the reference's
+server/code/http/test.rb drives the server: POST /complete, then POST /verify_completion with
+that request and response.
+
+CPU: env validation fails with the reference's messages (HttpServerMain.cpp:383-435), before any
+GPU work.
+GPU: a synthetic model served on 127.0.0.1.
+  - /complete returns the wire format.
+  - Verifying the completion with the server itself scores exactly 1.
+  - A tampered completion scores lower.
+  - The CPU oracle verifies the same HTTP completion like Session::fillCtx (score >= 0.95).
+  - Non-POST gives 400, an unknown path 404, a malformed body 500."""
+import json
+import os
+import subprocess
+import time
+import urllib.error
+import urllib.request
+
+import numpy as np
+import pytest
+
+import ggml_ref as R
+from blama_amd import synthetic
+from util import oracle_from_gguf
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "blama_amd", "blama-http-server")
+
+
+def _binary():
+    if not os.path.exists(BIN):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "blama_amd", "host")], check=True,
+                       capture_output=True)
+    return BIN
+
+
+def _run_env(env, timeout=30):
+    e = dict(os.environ)
+    for k in ("BLAMA_MODEL", "BLAMA_PORT", "BLAMA_HOST"):
+        e.pop(k, None)
+    e.update(env)
+    return subprocess.run([_binary()], env=e, capture_output=True, text=True, timeout=timeout)
+
+
+def test_env_validation(tmp_path):
+    r = _run_env({})
+    assert r.returncode == 1 and "Environment variable not set or empty: BLAMA_MODEL" in r.stderr
+    r = _run_env({"BLAMA_MODEL": str(tmp_path / "m.bin")})
+    assert "BLAMA_MODEL does not end with .gguf" in r.stderr
+    r = _run_env({"BLAMA_MODEL": str(tmp_path / "missing.gguf")})
+    assert "BLAMA_MODEL does not exist" in r.stderr
+    (tmp_path / "d.gguf").mkdir()
+    r = _run_env({"BLAMA_MODEL": str(tmp_path / "d.gguf")})
+    assert "BLAMA_MODEL is not a regular file" in r.stderr
+    r = _run_env({"BLAMA_PORT": "73x1"})
+    assert "Extra characters after BLAMA_PORT number" in r.stderr
+    r = _run_env({"BLAMA_PORT": "70000"})
+    assert "Value exceeds uint16_t max" in r.stderr
+    r = _run_env({"BLAMA_HOST": "not-an-address"})
+    assert "Invalid BLAMA_HOST" in r.stderr
+
+
+def _post(port, path, body, method="POST"):
+    data = body.encode() if isinstance(body, str) else (json.dumps(body).encode() if body is not None else None)
+    req = urllib.request.Request(f"http://127.0.0.1:{port}{path}", data=data, method=method)
+    try:
+        with urllib.request.urlopen(req, timeout=60) as r:
+            return r.status, r.read().decode(), r.headers
+    except urllib.error.HTTPError as e:
+        return e.code, e.read().decode(), e.headers
+
+
+def _prompt_ids(text):
+    """Tokenisation of `text` by the synthetic vocabulary: BOS, then SPM's whitespace-escaped
+    text as byte tokens (the vocabulary's only pieces are '▁t<n>', which never match)."""
+    return [1] + [3 + b for b in ("▁" + text.replace(" ", "▁")).encode()]
+
+
+@pytest.fixture
+def served(tmp_path):
+    cfg = synthetic.CONFIGS["tiny-q4_k_m"]
+    buf = synthetic.build_gguf(cfg, seed=5)
+    path = str(tmp_path / "model.gguf")
+    buf.tofile(path)
+    env = dict(os.environ, BLAMA_MODEL=path, BLAMA_HOST="127.0.0.1", BLAMA_PORT="0")
+    proc = subprocess.Popen([_binary()], env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                            text=True)
+    port = None
+    t0 = time.time()
+    try:
+        while time.time() - t0 < 90:
+            line = proc.stdout.readline()
+            if not line:
+                break
+            if line.startswith("Listening on port "):
+                port = int(line.split()[-1])
+                break
+        assert port, "server did not start: " + proc.stderr.read()[-2000:]
+        yield port, buf
+    finally:
+        proc.kill()          # the exact child we started
+        proc.wait(timeout=30)
+
+
+@pytest.mark.gpu
+def test_http_complete_and_verify(served):
+    port, buf = served
+    req = {"prompt": "hello world", "max_tokens": 10, "seed": 9, "temp": 0.8, "top_p": 0.95}
+    st, body, hdr = _post(port, "/complete", req)
+    assert st == 200, body
+    assert hdr["Access-Control-Allow-Origin"] == "*"
+    out = json.loads(body)
+    toks = out["tokenData"]
+    assert len(toks) == 10
+    assert out["text"] == "".join(t["str"] for t in toks)
+    for t in toks:
+        lg = [l["logit"] for l in t["logits"]]
+        assert len(lg) == 10 and lg == sorted(lg, reverse=True)
+    # self-verification through the wire format scores exactly 1 (Server.cpp:127-161)
+    st, body, _ = _post(port, "/verify_completion", {"request": req, "response": out})
+    assert st == 200, body
+    assert json.loads(body)["result"] == 1.0
+    # tampered logits score lower
+    bad = json.loads(json.dumps(out))
+    for t in bad["tokenData"]:
+        for l in t["logits"]:
+            l["logit"] *= 1.5
+    st, body, _ = _post(port, "/verify_completion", {"request": req, "response": bad})
+    assert st == 200 and json.loads(body)["result"] < 0.95
+    # the CPU oracle verifies the HTTP completion like fillCtx (t-LogitComparer.cpp:41-79 gate)
+    orc = oracle_from_gguf(buf, n_ctx=64)
+    orc.decode(_prompt_ids(req["prompt"]))
+    agg = R.MetricsAggregator()
+    sims, score = [], None
+    for t in toks:
+        claimed = [(l["id"], l["logit"]) for l in t["logits"]]
+        lg = orc.decode_one(t["id"])
+        mine = sorted(R.gather(lg, sorted({i for i, _ in claimed})), key=lambda x: -x[1])
+        score = agg.push_and_verify([R.compare(claimed, mine)])
+        sims.append(R.logit_similarity(claimed, mine))
+    assert score >= 0.95 and float(np.mean(sims)) >= 0.98, (score, np.mean(sims))
+    # protocol errors (HttpServerMain.cpp:305-309, :350-354)
+    assert _post(port, "/complete", None, method="GET")[0] == 400
+    assert _post(port, "/nowhere", req)[0] == 404
+    assert _post(port, "/complete", "{not json")[0] == 500
+    assert _post(port, "/complete", {"max_tokens": 3})[0] == 500          # "prompt" is required
+    # the server keeps serving after errors
+    st, body, _ = _post(port, "/complete", dict(req, max_tokens=2))
+    assert st == 200 and len(json.loads(body)["tokenData"]) == 2
