@@ -2,7 +2,10 @@
 // (server/code/http/HttpServerMain.cpp: /complete and /verify_completion bodies).  The
 // reference uses nlohmann::json, which is not in this image.  Numbers are doubles.  A float
 // logit is written with 9 significant digits, which parses back to the same float: the
-// verify round trip depends on that.
+// verify round trip depends on that.  Strings that are not valid UTF-8 (a byte-fallback token
+// such as <0xE2> on its own) are written with U+FFFD for each maximal invalid subpart, the
+// Unicode-recommended practice (and Python's errors="replace").  nlohmann's default dump
+// throws on them instead, which ends the reference's request.
 #pragma once
 #include <cmath>
 #include <cstdio>
@@ -197,9 +200,36 @@ struct Parser {
     }
 };
 
+// Length of the valid UTF-8 sequence at s[i], or -(bytes of its maximal invalid subpart).
+inline int utf8_seq(const std::string& s, size_t i) {
+    const unsigned char b = (unsigned char)s[i];
+    if (b < 0x80) return 1;
+    int n;
+    unsigned char lo = 0x80, hi = 0xBF;
+    if (b >= 0xC2 && b <= 0xDF) n = 2;
+    else if (b >= 0xE0 && b <= 0xEF) { n = 3; if (b == 0xE0) lo = 0xA0; if (b == 0xED) hi = 0x9F; }
+    else if (b >= 0xF0 && b <= 0xF4) { n = 4; if (b == 0xF0) lo = 0x90; if (b == 0xF4) hi = 0x8F; }
+    else return -1;
+    for (int k = 1; k < n; ++k) {
+        if (i + k >= s.size()) return -k;
+        const unsigned char c = (unsigned char)s[i + k];
+        if (c < (k == 1 ? lo : 0x80) || c > (k == 1 ? hi : 0xBF)) return -k;
+    }
+    return n;
+}
+
 inline void dump_str(std::string& o, const std::string& s) {
     o += '"';
-    for (unsigned char c : s) {
+    for (size_t i = 0; i < s.size();) {
+        const unsigned char c = (unsigned char)s[i];
+        if (c >= 0x80) {
+            const int n = utf8_seq(s, i);
+            if (n > 0) o.append(s, i, (size_t)n);
+            else o += "\xEF\xBF\xBD";
+            i += (size_t)(n > 0 ? n : -n);
+            continue;
+        }
+        ++i;
         switch (c) {
         case '"': o += "\\\""; break;
         case '\\': o += "\\\\"; break;

@@ -175,6 +175,15 @@ TEST_CASE_G("wire format", "cpu") {   // HttpServerMain.cpp:37-94, 259-288
     CHECK_THROWS(wire::toCompleteParams(bl::json::parse(R"({"max_tokens": 3})")));
     CHECK_THROWS(bl::json::parse("{\"prompt\": }"));
     CHECK_THROWS(bl::json::parse("[1, 2"));
+    // invalid UTF-8 (byte-fallback tokens) becomes U+FFFD per maximal subpart; ids/logits intact
+    const std::string fffd = "\xef\xbf\xbd";
+    auto enc = [](std::string s) { bl::json::Value v = bl::json::Value::string(std::move(s)); return bl::json::parse(bl::json::dump(v)).as_string(); };
+    CHECK(enc("\xe2") == fffd);
+    CHECK(enc("a\xe2\x96") == "a" + fffd);                 // truncated 3-byte sequence: one U+FFFD
+    CHECK(enc("\xe2\x96\x81") == "\xe2\x96\x81");          // complete: kept
+    CHECK(enc("\xc0\xaf") == fffd + fffd);                 // overlong lead: each byte invalid
+    CHECK(enc("\xed\xa0\x80") == fffd + fffd + fffd);      // surrogate: 0xA0 outside ED's range
+    CHECK(enc("\xf0\x9f\x98\x80x\xff") == "\xf0\x9f\x98\x80x" + fffd);
     CHECK((float)bl::json::parse(wire::verifyBody(0.975f)).at("result").as_number() == 0.975f);
 }
 

@@ -77,6 +77,15 @@ def _prompt_ids(text):
     return [1] + [3 + b for b in ("▁" + text.replace(" ", "▁")).encode()]
 
 
+def _piece(tid):
+    """Vocab::tokenToString for the synthetic vocabulary (synthetic.vocab_tokens)."""
+    if tid < 3:
+        return {0: "\u2585", 1: "<s>", 2: "</s>"}[tid].encode()   # unknown prints U+2585
+    if tid < 259:
+        return bytes([tid - 3])
+    return (" t%d" % (tid - 259)).encode()
+
+
 @pytest.fixture
 def served(tmp_path):
     cfg = synthetic.CONFIGS["tiny-q4_k_m"]
@@ -113,7 +122,10 @@ def test_http_complete_and_verify(served):
     out = json.loads(body)
     toks = out["tokenData"]
     assert len(toks) == 10
-    assert out["text"] == "".join(t["str"] for t in toks)
+    # token strings are raw vocabulary bytes; invalid UTF-8 is sent as U+FFFD (json.hpp)
+    raw = [_piece(t["id"]) for t in toks]
+    assert [t["str"] for t in toks] == [r.decode("utf-8", errors="replace") for r in raw]
+    assert out["text"] == b"".join(raw).decode("utf-8", errors="replace")
     for t in toks:
         lg = [l["logit"] for l in t["logits"]]
         assert len(lg) == 10 and lg == sorted(lg, reverse=True)
