@@ -518,6 +518,8 @@ void Ctx::enqueue_step(bool with_logits) {
             const QMat* mats[3] = {&L.wq, &L.wk, &L.wv};
             const int epis[3] = {EPI_ROPE_Q, EPI_ROPE_K, EPI_V};
             bool done[3] = {false, false, false};
+            GemvParams pend;             // the first type's launch, held back to pair it
+            bool have_pend = false;
             for (int a = 0; a < 3; ++a) {
                 if (done[a]) continue;
                 GemvParams pl = p;
@@ -535,8 +537,18 @@ void Ctx::enqueue_step(bool with_logits) {
                 }
                 params_finish(pl);
                 pl.stamps = stamp();
-                if (on()) launch_gemv(pl, ROLE_QKV, 0, stream);
+                if (have_pend) {   // second quant type: one mixed launch when the pair has a kernel
+                    have_pend = false;
+                    if (gemv_mix && gemv_mix_supported(pend.seg[0].A.type, pl.seg[0].A.type, ROLE_QKV)) {
+                        if (on()) launch_gemv_mix(pend, pl, ROLE_QKV, stream);
+                        continue;
+                    }
+                    if (on()) launch_gemv(pend, ROLE_QKV, 0, stream);
+                }
+                pend = pl;
+                have_pend = true;
             }
+            if (have_pend && on()) launch_gemv(pend, ROLE_QKV, 0, stream);
         }
         // ---- attention ----
         {

@@ -130,6 +130,7 @@ struct Ctx {
     static constexpr int kTokbRing = 256;
     static constexpr int kBatchRows = MMQ_NT > GEMM_NT ? MMQ_NT : GEMM_NT;
     bool mmq_ok = false;                // int8-MFMA GEMM for prompt chunks (all layers Q4_K / Q6_K)
+    bool gemv_mix = getenv("MI_NO_MIX") == nullptr;   // mixed-type Q/K/V in one launch
     int8_t* q8r_q = nullptr;            // Q8_K rows of one prompt chunk
     float* q8r_d = nullptr;
     int* q8r_bsum = nullptr;

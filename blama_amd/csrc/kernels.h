@@ -98,6 +98,10 @@ size_t gemv_smem_bytes(const GemvParams& p);
 // (hipExtLaunchKernel) -- the bench's in-kernel timing of one launch.
 void launch_gemv(const GemvParams& p, int role, int grid, hipStream_t s,
                  hipEvent_t ev_start = nullptr, hipEvent_t ev_stop = nullptr);
+// Two launches of different quant types over the same activation as one launch (QKV of
+// Q4_K_M / Q5_K_M layers with a Q6_K attn_v); gemv_mix_supported says whether the pair has one.
+bool gemv_mix_supported(int t1, int t2, int role);
+void launch_gemv_mix(const GemvParams& p1, const GemvParams& p2, int role, hipStream_t s);
 void init_kernel_attributes();   // once per device, before any graph capture
 int gemv_default_grid(const GemvParams& p, int role = ROLE_GENERIC);
 

@@ -562,7 +562,7 @@ __device__ __forceinline__ bool pro_load_rest(const GemvParams& P, ProRegs& R, i
 }
 
 __device__ __forceinline__ void pro_finish(const GemvParams& P, const ProRegs& R, char* smem, const SmemPlan& SP,
-                                           int pos, int ncell, int wg_u0, int wg_u1) {
+                                           int pos, int ncell, int wg_u0, int wg_u1, int bid) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int nwaves = blockDim.x >> 6;
@@ -603,11 +603,11 @@ __device__ __forceinline__ void pro_finish(const GemvParams& P, const ProRegs& R
         s = wave_sum63_d(s);
         if (lane == 63) red[wave] = s;
 #ifdef MI_STAMPS
-        if (P.stamps && threadIdx.x == 0) P.stamps[blockIdx.x * 8 + 5] = __builtin_amdgcn_s_memrealtime();
+        if (P.stamps && threadIdx.x == 0) P.stamps[bid * 8 + 5] = __builtin_amdgcn_s_memrealtime();
 #endif
         __syncthreads();
 #ifdef MI_STAMPS
-        if (P.stamps && threadIdx.x == 0) P.stamps[blockIdx.x * 8 + 6] = __builtin_amdgcn_s_memrealtime();
+        if (P.stamps && threadIdx.x == 0) P.stamps[bid * 8 + 6] = __builtin_amdgcn_s_memrealtime();
 #endif
         double tot = 0.0;
         for (int w = 0; w < nwaves; ++w) tot += red[w];
@@ -797,11 +797,15 @@ __device__ __forceinline__ void gemv_epilogue(const EpiConst& E, const EpiSeg& S
     }
 }
 
-// NW waves per workgroup, D-deep ring.  ROLE: 0 generic, 1 FFN gate/up (own
-// symbol: the bench's roofline kernel), 2 dual activation slot (MoE down).
-template <int T, int D, int NW, int DUAL, int ROLE>
-__global__ __launch_bounds__(NW * 64) void gemv_t(const float* __restrict__ kx0, const float* __restrict__ knw,
-                                                   const int* __restrict__ ktp, int kflags, const GemvParams Pk) {
+constexpr int kGemvParamVecs = (int)((sizeof(GemvParams) + 15) / 16);
+
+// The GEMV of one workgroup: workgroup `bid` of P.grid.  NW waves per workgroup, D-deep ring.
+// ROLE (template only, so the roofline kernel has its own symbol): 0 generic, 1 FFN gate/up.
+// DUAL: two activation slots (MoE down).
+template <int T, int D, int NW, int DUAL>
+__device__ __forceinline__ void gemv_body(const float* __restrict__ kx0, const float* __restrict__ knw,
+                                          const int* __restrict__ ktp, int kflags, const GemvParams& Pk,
+                                          u32x4* sparams, const int bid) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     using K = Kq<T>;
     static_assert(K::LPS == 8, "8 lanes per superblock");
@@ -812,13 +816,12 @@ __global__ __launch_bounds__(NW * 64) void gemv_t(const float* __restrict__ kx0,
     // fields straight from kernarg compiles to a chain of ~15 dependent scalar
     // loads (segment lookup, plane bases, ...), each a full memory latency, which
     // cost 5-10 us per launch before the first weight load was issued.
-    __shared__ __attribute__((aligned(16))) u32x4 sparams[(sizeof(GemvParams) + 15) / 16];
     ProRegs pr;
     pro_load_entry(pr, kx0, knw, ktp, (kflags & 0xFFFFF) >> 8, (kflags >> 20) & 1, (kflags >> 21) & 1, NW, wave,
                    lane);
     {
         const u32x4* src = reinterpret_cast<const u32x4*>(&Pk);
-        for (int i = threadIdx.x; i < (int)((sizeof(GemvParams) + 15) / 16); i += NW * 64) sparams[i] = src[i];
+        for (int i = threadIdx.x; i < kGemvParamVecs; i += NW * 64) sparams[i] = src[i];
         __syncthreads();
     }
     const GemvParams& P = *reinterpret_cast<const GemvParams*>(sparams);
@@ -836,7 +839,7 @@ __global__ __launch_bounds__(NW * 64) void gemv_t(const float* __restrict__ kx0,
     }
 #ifdef MI_STAMPS   // diagnostic build only (scripts/exp_gemv_stamps)
 #define MI_STAMP(k) \
-    if (P.stamps && threadIdx.x == 0) P.stamps[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime();
+    if (P.stamps && threadIdx.x == 0) P.stamps[bid * 8 + (k)] = __builtin_amdgcn_s_memrealtime();
 #else
 #define MI_STAMP(k)
 #endif
@@ -844,9 +847,9 @@ __global__ __launch_bounds__(NW * 64) void gemv_t(const float* __restrict__ kx0,
     // P.grid == gridDim.x (set by launch_gemv; reading gridDim costs a hidden-kernarg round trip)
     const int W = P.grid * NW;
     int u0, u1, wg_u0, wg_u1, dummy;
-    unit_range(P.total_units, W, blockIdx.x * NW + wave, u0, u1);
-    unit_range(P.total_units, P.grid, blockIdx.x, wg_u0, dummy);
-    unit_range(P.total_units, W, blockIdx.x * NW + NW - 1, dummy, wg_u1);
+    unit_range(P.total_units, W, bid * NW + wave, u0, u1);
+    unit_range(P.total_units, P.grid, bid, wg_u0, dummy);
+    unit_range(P.total_units, W, bid * NW + NW - 1, dummy, wg_u1);
     const int n_items = (u1 - u0) * cpr;
 
     struct Slot { typename K::Ld a, b; };
@@ -920,7 +923,7 @@ __global__ __launch_bounds__(NW * 64) void gemv_t(const float* __restrict__ kx0,
     MI_STAMP(1)
     const int pos = __builtin_amdgcn_readfirstlane(pr.tp.y);
     const int cell = __builtin_amdgcn_readfirstlane(pr.tp.z);
-    pro_finish(P, pr, smem, SP, pos, cell + 1, wg_u0, wg_u1);
+    pro_finish(P, pr, smem, SP, pos, cell + 1, wg_u0, wg_u1, bid);
     MI_STAMP(7)
     __syncthreads();
     MI_STAMP(2)
@@ -973,7 +976,29 @@ __global__ __launch_bounds__(NW * 64) void gemv_t(const float* __restrict__ kx0,
 #undef MI_STAMP
 }
 
+template <int T, int D, int NW, int DUAL, int ROLE>
+__global__ __launch_bounds__(NW * 64) void gemv_t(const float* __restrict__ kx0, const float* __restrict__ knw,
+                                                   const int* __restrict__ ktp, int kflags, const GemvParams Pk) {
+    __shared__ __attribute__((aligned(16))) u32x4 sparams[kGemvParamVecs];
+    gemv_body<T, D, NW, DUAL>(kx0, knw, ktp, kflags, Pk, sparams, blockIdx.x);
+}
+
+// Two quant types in one launch (the Q/K/V projections of a Q4_K_M / Q5_K_M layer whose
+// attn_v is Q6_K): workgroups [0, P1.grid) run the T1 matrices, the rest the T2 ones, each
+// half with its own unit split.  Saves one launch (its fixed entry/prologue cost) per such
+// layer.  Both halves consume the same activation (Q8_K of the RMS-normed residual).
+template <int T1, int T2, int D, int NW>
+__global__ __launch_bounds__(NW * 64) void gemv_mix_t(const float* __restrict__ kx0, const float* __restrict__ knw,
+                                                       const int* __restrict__ ktp, int kflags, const GemvParams P1,
+                                                       const GemvParams P2) {
+    __shared__ __attribute__((aligned(16))) u32x4 sparams[kGemvParamVecs];
+    const int g1 = P1.grid;
+    if ((int)blockIdx.x < g1) gemv_body<T1, D, NW, 0>(kx0, knw, ktp, kflags, P1, sparams, blockIdx.x);
+    else gemv_body<T2, D, NW, 0>(kx0, knw, ktp, kflags, P2, sparams, blockIdx.x - g1);
+}
+
 typedef void (*GemvFn)(const float*, const float*, const int*, int, const GemvParams);
+typedef void (*GemvMixFn)(const float*, const float*, const int*, int, const GemvParams, const GemvParams);
 
 // Kernel configurations: waves per workgroup NW and ring depth D (one
 // workgroup per CU).  MI_GEMV_CFG=n selects config n for every type
@@ -1034,6 +1059,7 @@ constexpr int kGemvDynLds = 160 * 1024 - (int)((sizeof(GemvParams) + 15) / 16 * 
 
 template <int T, int D> __global__ void gemm_t(const GemmParams P);
 static void gemm_attrs();
+static GemvMixFn gemv_mix_fn(int t1, int t2);
 
 void init_kernel_attributes() {
     gemm_attrs();
@@ -1044,6 +1070,9 @@ void init_kernel_attributes() {
                 for (int c = 0; c < kNumGemvCfgs; ++c)
                     MI_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(gemv_fn(r, t, nsl, c)),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, kGemvDynLds));
+    for (int t1 : {T_Q4_K, T_Q5_K})
+        MI_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(gemv_mix_fn(t1, T_Q6_K)),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, kGemvDynLds));
 }
 
 // Units one workgroup owns at most (its residual staging in LDS).
@@ -1060,9 +1089,8 @@ int gemv_default_grid(const GemvParams& p, int role) {
     return g < 1 ? 1 : (g > 256 ? 256 : g);
 }
 
-void launch_gemv(const GemvParams& p_in, int role, int grid, hipStream_t s, hipEvent_t ev_start,
-                 hipEvent_t ev_stop) {
-    GemvParams p = p_in;
+// Validates a launch and fixes its grid-dependent fields; returns the kernel configuration.
+static int gemv_prepare(GemvParams& p, int role, int grid) {
     if (p.K % 256 != 0) throw Error("gemv: K must be a multiple of 256");
     const int type = p.seg[0].A.type;
     for (int i = 0; i < p.nseg; ++i)
@@ -1079,23 +1107,75 @@ void launch_gemv(const GemvParams& p_in, int role, int grid, hipStream_t s, hipE
     for (int i = 0; i < p.nseg; ++i)
         if (p.seg[i].resid && (p.nseg != 1 || p.wg_units > kGemvCfgs[cfg].nw * 64))
             throw Error("gemv: residual launches must have one segment and <= 64*NW units per workgroup");
-    const size_t smem = gemv_smem_bytes(p);
-    if (smem > (size_t)kGemvDynLds) throw Error("gemv: activation too large for LDS");
-    GemvFn fn = gemv_fn(role, type, p.nslots, cfg);
-    if (!fn) throw Error("gemv: unsupported quant type");
-    const dim3 block(kGemvCfgs[cfg].nw * 64);
-    // leading (kernarg-preloaded) arguments: activation, norm weight, token position, K | flags
+    if (gemv_smem_bytes(p) > (size_t)kGemvDynLds) throw Error("gemv: activation too large for LDS");
+    return cfg;
+}
+
+// leading arguments: K | flags (activation kept in registers, RMSNorm prologue)
+static int gemv_kflags(const GemvParams& p, int cfg) {
     const int nb = p.K / 256;
     const bool regs = p.pro != PRO_ATTN && p.nslots == 1 && nb <= PRO_MAXB * kGemvCfgs[cfg].nw;
     const bool rms = p.pro == PRO_RMSNORM;
-    const int kflags = p.K | (regs ? 1 << 20 : 0) | (rms ? 1 << 21 : 0);
+    return p.K | (regs ? 1 << 20 : 0) | (rms ? 1 << 21 : 0);
+}
+
+void launch_gemv(const GemvParams& p_in, int role, int grid, hipStream_t s, hipEvent_t ev_start,
+                 hipEvent_t ev_stop) {
+    GemvParams p = p_in;
+    const int cfg = gemv_prepare(p, role, grid);
+    const int type = p.seg[0].A.type;
+    const size_t smem = gemv_smem_bytes(p);
+    GemvFn fn = gemv_fn(role, type, p.nslots, cfg);
+    if (!fn) throw Error("gemv: unsupported quant type");
+    const dim3 block(kGemvCfgs[cfg].nw * 64);
+    const int kflags = gemv_kflags(p, cfg);
     const float* kx0 = p.x[0];
-    const float* knw = rms ? p.norm_w : nullptr;
+    const float* knw = p.pro == PRO_RMSNORM ? p.norm_w : nullptr;
     const int* ktp = p.tokpos;
     if (ev_start || ev_stop)
-        hipExtLaunchKernelGGL(fn, dim3(grid), block, smem, s, ev_start, ev_stop, 0, kx0, knw, ktp, kflags, p);
+        hipExtLaunchKernelGGL(fn, dim3(p.grid), block, smem, s, ev_start, ev_stop, 0, kx0, knw, ktp, kflags, p);
     else
-        hipLaunchKernelGGL(fn, dim3(grid), block, smem, s, kx0, knw, ktp, kflags, p);
+        hipLaunchKernelGGL(fn, dim3(p.grid), block, smem, s, kx0, knw, ktp, kflags, p);
+    MI_HIP(hipGetLastError());
+}
+
+// Config 1 (8 waves, 4-deep ring) is the QKV role's; the pairs are the Q*_K_M layer mixes.
+static GemvMixFn gemv_mix_fn(int t1, int t2) {
+    if (t1 == T_Q4_K && t2 == T_Q6_K) return gemv_mix_t<T_Q4_K, T_Q6_K, 4, 8>;
+    if (t1 == T_Q5_K && t2 == T_Q6_K) return gemv_mix_t<T_Q5_K, T_Q6_K, 4, 8>;
+    return nullptr;
+}
+
+bool gemv_mix_supported(int t1, int t2, int role) {
+    return gemv_mix_fn(t1, t2) != nullptr && gemv_cfg_for(t1, role) == 1 && gemv_cfg_for(t2, role) == 1;
+}
+
+void launch_gemv_mix(const GemvParams& p1_in, const GemvParams& p2_in, int role, hipStream_t s) {
+    GemvParams p1 = p1_in, p2 = p2_in;
+    const int t1 = p1.seg[0].A.type, t2 = p2.seg[0].A.type;
+    GemvMixFn fn = gemv_mix_fn(t1, t2);
+    if (!fn || !gemv_mix_supported(t1, t2, role)) throw Error("gemv: unsupported type pair for a mixed launch");
+    if (p1.K != p2.K || p1.pro != p2.pro || p1.x[0] != p2.x[0] || p1.norm_w != p2.norm_w || p1.tokpos != p2.tokpos ||
+        p1.nslots != 1 || p2.nslots != 1)
+        throw Error("gemv: the halves of a mixed launch must share their activation");
+    // split the 256 workgroups in proportion to the bytes each half streams
+    auto bytes = [](const GemvParams& p) {
+        double b = 0;
+        for (int i = 0; i < p.nseg; ++i) b += (double)p.seg[i].A.rows * (p.K / block_elems(p.seg[i].A.type)) * block_bytes(p.seg[i].A.type);
+        return b;
+    };
+    const int total = gemv_default_grid(p1, role) + gemv_default_grid(p2, role) >= 256 ? 256 : 128;
+    const double b1 = bytes(p1), b2 = bytes(p2);
+    int g1 = (int)(total * b1 / (b1 + b2) + 0.5);
+    g1 = std::max(1, std::min(total - 1, std::min(g1, gemv_default_grid(p1, role))));
+    const int g2 = std::min(total - g1, gemv_default_grid(p2, role));
+    const int cfg = gemv_prepare(p1, role, g1);
+    gemv_prepare(p2, role, g2);
+    const size_t smem = std::max(gemv_smem_bytes(p1), gemv_smem_bytes(p2));
+    const dim3 block(kGemvCfgs[cfg].nw * 64);
+    const int kflags = gemv_kflags(p1, cfg);
+    const float* knw = p1.pro == PRO_RMSNORM ? p1.norm_w : nullptr;
+    hipLaunchKernelGGL(fn, dim3(p1.grid + p2.grid), block, smem, s, p1.x[0], knw, p1.tokpos, kflags, p1, p2);
     MI_HIP(hipGetLastError());
 }
 
@@ -1995,12 +2075,26 @@ __global__ __launch_bounds__(256) void attn_fused_kernel(const AttnParams P) {
     if (stp && threadIdx.x == 0) stp[0] = __builtin_amdgcn_s_memrealtime();
 #endif
     const int* tp = P.tokpos + 4 * tok;
-    const int ncell = min(tp[2] + 1, ATTN_SHORT), qpos = tp[1];
+    const int tp2 = tp[2], qpos = tp[1];
     const float* qrow = P.q + (long long)tok * P.n_head * HD;
     float* orow = P.part_o + (long long)tok * P.n_head * HD;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int L = lane % LPC, G = lane / LPC;
     const long long row_off = (long long)g * HD + L * 8;
+    constexpr int U = 4;
+    // The first chunk of K, V and cell positions is fetched at entry, before the cell count
+    // arrives, so the token-position, K and V round trips overlap instead of chaining.  Cells
+    // past the count are clamped to the cache and masked by select below, never by arithmetic.
+    u32x4 k0[U], v0[U];
+    int cp0[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int c = min(wave * CPW + u * 4 * CPW + G, P.n_ctx - 1);
+        k0[u] = *reinterpret_cast<const u32x4*>(P.kcache + (long long)c * P.kv_dim + row_off);
+        v0[u] = *reinterpret_cast<const u32x4*>(P.vcache + (long long)c * P.kv_dim + row_off);
+        cp0[u] = P.cell_pos[c];
+    }
+    const int ncell = min(tp2 + 1, ATTN_SHORT);
     float q[R][8];
 #pragma unroll
     for (int t = 0; t < R; ++t) {
@@ -2014,16 +2108,23 @@ __global__ __launch_bounds__(256) void attn_fused_kernel(const AttnParams P) {
     float mx[R];
 #pragma unroll
     for (int t = 0; t < R; ++t) mx[t] = -INFINITY;
-    constexpr int U = 4;
     for (int cb = wave * CPW; cb < ncell; cb += 4 * CPW * U) {
         u32x4 kk[U];
         int cpos[U];
+        if (cb == wave * CPW) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            int c = cb + u * 4 * CPW + G;
-            c = c < ncell ? c : ncell - 1;
-            kk[u] = *reinterpret_cast<const u32x4*>(P.kcache + (long long)c * P.kv_dim + row_off);
-            cpos[u] = P.cell_pos[c];
+            for (int u = 0; u < U; ++u) {
+                kk[u] = k0[u];
+                cpos[u] = cp0[u];
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                int c = cb + u * 4 * CPW + G;
+                c = c < ncell ? c : ncell - 1;
+                kk[u] = *reinterpret_cast<const u32x4*>(P.kcache + (long long)c * P.kv_dim + row_off);
+                cpos[u] = P.cell_pos[c];
+            }
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -2077,12 +2178,18 @@ __global__ __launch_bounds__(256) void attn_fused_kernel(const AttnParams P) {
     for (int cb = wave * CPW; cb < ncell; cb += 4 * CPW * U) {
         u32x4 vv[U];
         float pw[U][R];
+        const bool first = cb == wave * CPW;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             int c = cb + u * 4 * CPW + G;
             const bool in = c < ncell;
             c = in ? c : ncell - 1;
-            vv[u] = *reinterpret_cast<const u32x4*>(P.vcache + (long long)c * P.kv_dim + row_off);
+            if (first) {   // prefetched at entry; a cell past the count may hold non-finite bits
+                const u32x4 z = {0u, 0u, 0u, 0u};
+                vv[u] = in ? v0[u] : z;
+            } else {
+                vv[u] = *reinterpret_cast<const u32x4*>(P.vcache + (long long)c * P.kv_dim + row_off);
+            }
 #pragma unroll
             for (int t = 0; t < R; ++t) {
                 const float p = expf(sw[t][c] - gm[t]) * ginv[t];

@@ -14,9 +14,10 @@ import re
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# MI_ENGINE_LIB=stamps selects the diagnostic build (per-workgroup timestamps)
-LIB_PATH = os.path.join(_HERE, "libmi_engine_stamps.so" if os.environ.get("MI_ENGINE_LIB") == "stamps"
-                        else "libmi_engine.so")
+# MI_ENGINE_LIB=<name> loads libmi_engine_<name>.so instead: "stamps" is the diagnostic build
+# (per-workgroup timestamps), other names are A/B builds of an earlier revision (scripts/ab_build.sh)
+_VARIANT = os.environ.get("MI_ENGINE_LIB")
+LIB_PATH = os.path.join(_HERE, f"libmi_engine_{_VARIANT}.so" if _VARIANT else "libmi_engine.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "mi_engine.h")
 
 _lib = None

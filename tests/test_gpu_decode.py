@@ -269,3 +269,24 @@ def test_prefill_512_tokens_matches_oracle(gpu_lib):
     ref = oracle_from_gguf(buf, n_ctx=520).decode(prompt)
     assert _logits_close(a.logits(), ref)
     assert [int(i) for i in a.topk(10)[0]] == [i for i, _ in R.topk(ref, 10)]
+
+
+@pytest.mark.parametrize("name", ["tiny-q4_k_m", "tiny-q5_k_m"])
+def test_mixed_type_qkv_launch_bit_identical(gpu_lib, monkeypatch, name):
+    """Layers whose attn_v is Q6_K under a Q4_K/Q5_K attn_q/attn_k (use_more_bits layers: 2 and 3
+    of tiny-q4_k_m, 1 of tiny-q5_k_m) run Q/K/V as one mixed-type launch (gemv_mix_t).  Every
+    output row is the same per-row arithmetic as in the two separate launches (MI_NO_MIX=1), so
+    logits and the KV cache are bit-identical, step after step."""
+    cfg = synthetic.CONFIGS[name]
+    buf = synthetic.build_gguf(cfg, seed=21)
+    m = engine.Model(buf)
+    prompt = [int(t) for t in np.random.default_rng(8).integers(0, cfg.n_vocab, 6)]
+    monkeypatch.setenv("MI_NO_BATCH", "1")        # token-by-token decode graphs
+    a = engine.Context(m, n_ctx=64)
+    monkeypatch.setenv("MI_NO_MIX", "1")
+    b = engine.Context(m, n_ctx=64)
+    for t in prompt + [7, 9, 11]:
+        a.decode([t])
+        b.decode([t])
+        assert np.array_equal(a.logits(), b.logits())
+    assert a.state_get() == b.state_get()
