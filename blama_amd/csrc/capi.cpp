@@ -8,6 +8,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstring>
 #include <vector>
 
@@ -437,6 +438,37 @@ int32_t mi_op_topk(int32_t device, const float* logits, int32_t n, int32_t k, in
         MI_HIP(hipMemcpy(hv.data(), dv.p, TOPK_MAX * 4, hipMemcpyDeviceToHost));
         for (int i = 0; i < k; ++i) { ids[i] = hi[i]; vals[i] = hv[i]; }
         return k;
+    }
+    MI_TRY(-1)
+}
+
+int32_t mi_op_attention(int32_t device, int32_t n_head, int32_t n_head_kv, int32_t head_dim, int32_t n_cells,
+                        const float* q, const uint16_t* k_f16, const uint16_t* v_f16, const int32_t* cell_pos,
+                        int32_t pos, float* out) {
+    try {
+        if (n_head <= 0 || n_head_kv <= 0 || n_head % n_head_kv || n_cells <= 0 || head_dim <= 0)
+            throw Error("attention: bad shape");
+        MI_HIP(hipSetDevice(device));
+        const int kv_dim = n_head_kv * head_dim, d = n_head * head_dim;
+        const size_t kvb = (size_t)n_cells * kv_dim * sizeof(uint16_t);
+        DevBuf dq(d * sizeof(float)), dk(kvb), dv(kvb), dcp(n_cells * sizeof(int)), dtp(4 * sizeof(int));
+        DevBuf dsc((size_t)n_head * n_cells * sizeof(float)), dsm((size_t)ATTN_SMAX * n_head * sizeof(float));
+        DevBuf dpo((size_t)ATTN_SMAX * d * sizeof(float)), dout(d * sizeof(float));
+        MI_HIP(hipMemcpy(dq.p, q, d * sizeof(float), hipMemcpyHostToDevice));
+        MI_HIP(hipMemcpy(dk.p, k_f16, kvb, hipMemcpyHostToDevice));
+        MI_HIP(hipMemcpy(dv.p, v_f16, kvb, hipMemcpyHostToDevice));
+        MI_HIP(hipMemcpy(dcp.p, cell_pos, n_cells * sizeof(int), hipMemcpyHostToDevice));
+        const int tp[4] = {0, pos, n_cells - 1, 0};   // {token, query position, last cell}
+        MI_HIP(hipMemcpy(dtp.p, tp, sizeof tp, hipMemcpyHostToDevice));
+        AttnParams a{dq.as<float>(), dk.as<__half>(), dv.as<__half>(), dtp.as<int>(), dcp.as<int>(),
+                     dsc.as<float>(), dsm.as<float>(), dpo.as<float>(), n_head, n_head_kv, head_dim, kv_dim,
+                     n_cells, 1.0f / std::sqrt((float)head_dim)};
+        a.fused = n_cells <= ATTN_SHORT ? 1 : 0;   // the decode graph's choice for this cell count
+        launch_attn(a, nullptr);
+        launch_attn_combine(AttnPartials{dpo.as<float>(), n_head, head_dim}, dtp.as<int>(), dout.as<float>(), nullptr);
+        MI_HIP(hipDeviceSynchronize());
+        MI_HIP(hipMemcpy(out, dout.p, d * sizeof(float), hipMemcpyDeviceToHost));
+        return 0;
     }
     MI_TRY(-1)
 }

@@ -85,6 +85,8 @@ _SIGS = {
     "mi_op_dequant": (C.c_int32, [C.c_int32, C.c_int32, _P, C.c_int32, C.c_int32, _P]),
     "mi_op_quantize_q8_K": (C.c_int32, [C.c_int32, _P, C.c_int32, _P, _P, _P]),
     "mi_op_topk": (C.c_int32, [C.c_int32, _P, C.c_int32, C.c_int32, _P, _P]),
+    "mi_op_attention": (C.c_int32, [C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _P, _P, _P, _P,
+                                    C.c_int32, _P]),
     "mi_op_gemv_bench": (C.c_int32, [C.c_int32, C.c_int32, _P, C.c_int32, C.c_int32, C.c_int32,
                                      C.POINTER(C.c_float)]),
 }
@@ -337,3 +339,19 @@ def op_topk(logits: np.ndarray, k: int, device: int = 0):
     vals = np.empty(k, np.float32)
     _check(lib().mi_op_topk(device, _ptr(logits), logits.size, k, _ptr(ids), _ptr(vals)), "op_topk")
     return ids, vals
+
+
+def op_attention(q: np.ndarray, k16: np.ndarray, v16: np.ndarray, n_head_kv: int, cell_pos=None, pos=None,
+                 device: int = 0) -> np.ndarray:
+    """q: (n_head, hd) f32; k16/v16: (n_cells, n_head_kv*hd) f16 -> (n_head, hd) f32."""
+    q = np.ascontiguousarray(q, np.float32)
+    n_head, hd = q.shape
+    k16 = np.ascontiguousarray(k16, np.float16)
+    v16 = np.ascontiguousarray(v16, np.float16)
+    n = k16.shape[0]
+    cp = np.ascontiguousarray(np.arange(n) if cell_pos is None else cell_pos, np.int32)
+    pos = n - 1 if pos is None else pos
+    out = np.empty(n_head * hd, np.float32)
+    _check(lib().mi_op_attention(device, n_head, n_head_kv, hd, n, _ptr(q), _ptr(k16), _ptr(v16), _ptr(cp), pos,
+                                 _ptr(out)), "op_attention")
+    return out.reshape(n_head, hd)

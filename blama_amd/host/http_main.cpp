@@ -17,12 +17,15 @@
 // - A body that is not valid JSON, or a request that throws on the worker, gets a 500 with
 //   the message in the body.  In the reference the exception ends the coroutine.
 // - /chat/completions and /chat/verify_completion return 501: chat templating is out of scope.
+// - A malformed request head or Content-Length gets a 400, a body over 64 MB a 413.
 #include <arpa/inet.h>
 #include <netinet/in.h>
 #include <signal.h>
 #include <sys/socket.h>
 #include <unistd.h>
 
+#include <algorithm>
+#include <charconv>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -46,19 +49,24 @@ struct Request {
     std::string method, target, body;
 };
 
-bool readRequest(int fd, Request& req) {
+// Bodies above this are refused with 413 (the reference's Beast parser has its own limit).
+constexpr size_t kMaxBody = 64u << 20;
+
+enum class ReadStatus { Ok, Closed, BadRequest, TooLarge };
+
+ReadStatus readRequest(int fd, Request& req) {
     std::string buf;
     char chunk[65536];
     size_t hdrEnd = std::string::npos;
     while ((hdrEnd = buf.find("\r\n\r\n")) == std::string::npos) {
         const ssize_t n = ::recv(fd, chunk, sizeof chunk, 0);
-        if (n <= 0) return false;
+        if (n <= 0) return ReadStatus::Closed;
         buf.append(chunk, (size_t)n);
-        if (buf.size() > (64u << 20)) return false;
+        if (buf.size() > (64u << 10) && buf.find("\r\n\r\n") == std::string::npos) return ReadStatus::TooLarge;
     }
     const std::string head = buf.substr(0, hdrEnd);
     const size_t sp1 = head.find(' '), sp2 = head.find(' ', sp1 + 1);
-    if (sp1 == std::string::npos || sp2 == std::string::npos) return false;
+    if (sp1 == std::string::npos || sp2 == std::string::npos) return ReadStatus::BadRequest;
     req.method = head.substr(0, sp1);
     req.target = head.substr(sp1 + 1, sp2 - sp1 - 1);
     size_t clen = 0;
@@ -70,18 +78,28 @@ bool readRequest(int fd, Request& req) {
         if (colon != std::string::npos) {
             std::string key = line.substr(0, colon);
             for (auto& c : key) c = (char)std::tolower((unsigned char)c);
-            if (key == "content-length") clen = std::stoul(line.substr(colon + 1));
+            if (key == "content-length") {
+                // digits only (optional surrounding blanks); no sign, no overflow
+                size_t b = colon + 1, e = line.size();
+                while (b < e && (line[b] == ' ' || line[b] == '\t')) ++b;
+                while (e > b && (line[e - 1] == ' ' || line[e - 1] == '\t')) --e;
+                unsigned long long v = 0;
+                const auto r = std::from_chars(line.data() + b, line.data() + e, v, 10);
+                if (b == e || r.ec != std::errc() || r.ptr != line.data() + e) return ReadStatus::BadRequest;
+                if (v > kMaxBody) return ReadStatus::TooLarge;
+                clen = (size_t)v;
+            }
         }
         pos = next;
     }
     req.body = buf.substr(hdrEnd + 4);
     while (req.body.size() < clen) {
-        const ssize_t n = ::recv(fd, chunk, sizeof chunk, 0);
-        if (n <= 0) return false;
+        const ssize_t n = ::recv(fd, chunk, std::min(sizeof chunk, clen - req.body.size()), 0);
+        if (n <= 0) return ReadStatus::Closed;
         req.body.append(chunk, (size_t)n);
     }
     req.body.resize(clen);
-    return true;
+    return ReadStatus::Ok;
 }
 
 void writeAll(int fd, const std::string& s) {
@@ -104,12 +122,7 @@ void respond(int fd, int status, const char* reason, const std::string& body, bo
     writeAll(fd, r);
 }
 
-void handle(int fd, Server& server) {
-    Request req;
-    if (!readRequest(fd, req)) {
-        ::close(fd);
-        return;
-    }
+void handleRequest(int fd, Server& server, const Request& req) {
     try {
         if (req.method != "POST") {
             respond(fd, 400, "Bad Request", "", false);
@@ -137,6 +150,21 @@ void handle(int fd, Server& server) {
         }
     } catch (const std::exception& e) {
         respond(fd, 500, "Internal Server Error", e.what(), false);
+    }
+}
+
+// Runs on a detached thread: nothing may escape it (an escaping exception would terminate the
+// whole server).
+void handle(int fd, Server& server) noexcept {
+    try {
+        Request req;
+        switch (readRequest(fd, req)) {
+        case ReadStatus::Ok: handleRequest(fd, server, req); break;
+        case ReadStatus::BadRequest: respond(fd, 400, "Bad Request", "malformed request head", false); break;
+        case ReadStatus::TooLarge: respond(fd, 413, "Payload Too Large", "", false); break;
+        case ReadStatus::Closed: break;
+        }
+    } catch (...) {
     }
     ::shutdown(fd, SHUT_WR);
     ::close(fd);

@@ -85,6 +85,8 @@ namespace detail {
 struct Parser {
     std::string_view s;
     size_t i = 0;
+    int depth = 0;
+    static constexpr int kMaxDepth = 256;   // nesting bound: no stack overflow on "[[[[..."
     [[noreturn]] void fail(const char* what) {
         throw std::runtime_error(std::string("json parse error: ") + what + " at " + std::to_string(i));
     }
@@ -152,10 +154,34 @@ struct Parser {
         ++i;
         return o;
     }
+    // A JSON number (RFC 8259 grammar: no nan/inf/hex/leading '+'), finite after conversion.
+    Value number() {
+        const size_t b = i;
+        if (i < s.size() && s[i] == '-') ++i;
+        auto digits = [&] { size_t k = i; while (i < s.size() && s[i] >= '0' && s[i] <= '9') ++i; return i - k; };
+        if (i < s.size() && s[i] == '0') ++i;
+        else if (digits() == 0) fail("bad value");
+        if (i < s.size() && s[i] == '.') { ++i; if (digits() == 0) fail("bad number"); }
+        if (i < s.size() && (s[i] == 'e' || s[i] == 'E')) {
+            ++i;
+            if (i < s.size() && (s[i] == '+' || s[i] == '-')) ++i;
+            if (digits() == 0) fail("bad number");
+        }
+        const std::string tok(s.substr(b, i - b));
+        const double d = std::strtod(tok.c_str(), nullptr);
+        if (!std::isfinite(d)) fail("number out of range");
+        return Value::number(d);
+    }
+    struct DepthGuard {
+        Parser& p;
+        explicit DepthGuard(Parser& q) : p(q) { if (++p.depth > kMaxDepth) p.fail("nesting too deep"); }
+        ~DepthGuard() { --p.depth; }
+    };
     Value val() {
         ws();
         if (i >= s.size()) fail("unexpected end");
         const char c = s[i];
+        DepthGuard guard(*this);
         if (c == '{') {
             ++i;
             Value o = Value::object();
@@ -191,12 +217,7 @@ struct Parser {
         if (lit("true")) { Value v; v.kind = Value::Kind::Bool; v.b = true; return v; }
         if (lit("false")) { Value v; v.kind = Value::Kind::Bool; return v; }
         if (lit("null")) return Value();
-        const char* b = s.data() + i;
-        char* e = nullptr;
-        const double d = std::strtod(b, &e);
-        if (e == b) fail("bad value");
-        i += (size_t)(e - b);
-        return Value::number(d);
+        return number();
     }
 };
 

@@ -344,8 +344,12 @@ Token Sampler::applyChain(std::vector<Candidate>& cur) {
 
 Token Sampler::sample(mi_ctx* ctx) {
     std::vector<Candidate> cur;
+    // The GPU top-k may stand in for the vocabulary only when nothing before top_k in the chain
+    // (logit_bias, penalties: Sampler.cpp:30-41) can move a token across the top-k boundary.
+    const auto& rp = m_params.repetitionPenalty;
+    const bool penalties = rp.numTokens != 0 && !(rp.repeat == 1.0f && rp.freq == 0.0f && rp.present == 0.0f);
     if (m_params.topK > 0 && m_params.topK <= 64 && m_params.samplerSequence.size() &&
-        m_params.samplerSequence[0] == SamplingType::Top_K) {
+        m_params.samplerSequence[0] == SamplingType::Top_K && m_params.logitBias.empty() && !penalties) {
         const int k = m_params.topK;
         std::vector<int32_t> ids(k);
         std::vector<float> lg(k);
@@ -634,6 +638,9 @@ float kl_to(const std::unordered_map<Token, float>& P, const std::unordered_map<
 }  // namespace
 
 ComparisonMetrics LogitComparer::compare(const TokenDataVector& a, const TokenDataVector& b) {
+    // the reference reads a[0]/b[0] unchecked (LogitComparer.cpp:39-55); this server faces the
+    // network, so an empty list is an error, not undefined behaviour
+    if (a.empty() || b.empty()) throw std::runtime_error("LogitComparer: empty logits");
     ComparisonMetrics m;
     m.top1Match = a[0].token == b[0].token ? 1.0f : 0.0f;
     const size_t n = std::min(a.size(), b.size());

@@ -138,9 +138,11 @@ public:
     };
     Sampler(Model& model, const Params& params);
 
-    // Samples from the context's last logits.  The chain runs on the engine's sorted top-k
-    // (k = max(topK, 64 cap)); the reference chain's first stage is top_k(topK), so both see
-    // the same candidate set (ties broken by id, which std::sort leaves unspecified).
+    // Samples from the context's last logits.  With no logit bias and no active penalty, the
+    // chain's first stage is top_k(topK) (topK <= 64), so the engine's sorted top-k is the same
+    // candidate set (ties broken by id, which std::sort leaves unspecified).  Otherwise bias and
+    // penalties can move tokens across the top-k boundary, so the chain runs on the full
+    // vocabulary, as the reference's does (Sampler.cpp:30-41).
     Token sample(mi_ctx* ctx);
     void accept(Token id, bool acceptGrammar);
     void reset();

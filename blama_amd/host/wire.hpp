@@ -16,6 +16,23 @@ namespace bl::llama::server::wire {
 
 using json::Value;
 
+// Numbers come from the network: every conversion is range-checked (the parser already rejects
+// nan/inf).  Integers must be integral and within [INT32_MIN, UINT32_MAX]; a negative value
+// wraps as nlohmann's get<uint32_t> (a static_cast) would.
+inline uint32_t to_u32(const Value& v, const char* what) {
+    const double d = v.as_number();
+    if (d != std::floor(d) || d < -2147483648.0 || d > 4294967295.0)
+        throw std::runtime_error(std::string("json: ") + what + " is not a 32-bit integer");
+    return (uint32_t)(int64_t)d;
+}
+inline float to_f32(const Value& v, const char* what) {
+    const double d = v.as_number();
+    if (!(std::fabs(d) <= 3.4028234663852886e38)) throw std::runtime_error(std::string("json: ") + what + " out of float range");
+    return (float)d;
+}
+// Claimed top-k lists per token: the verifier gathers at most this many ids (mi_gather).
+constexpr size_t kMaxClaimedLogits = 4096;
+
 inline Value toJson(const Server::CompleteReponse& gen) {
     Value arr = Value::array();
     for (const auto& g : gen) {
@@ -43,12 +60,13 @@ inline Server::CompleteReponse toCompleteResponse(const Value& j) {
     for (const Value& jt : toks.arr) {
         auto& g = gen.emplace_back();
         g.tokenStr = jt.at("str").as_string();
-        g.tokenId = (uint32_t)(int64_t)jt.at("id").as_number();
+        g.tokenId = to_u32(jt.at("id"), "id");
         const Value& jl = jt.at("logits");
         if (!jl.is_array()) throw std::runtime_error("json: logits is not an array");
+        if (jl.arr.empty() || jl.arr.size() > kMaxClaimedLogits)
+            throw std::runtime_error("json: logits must hold 1.." + std::to_string(kMaxClaimedLogits) + " entries");
         g.logits.reserve(jl.arr.size());
-        for (const Value& e : jl.arr)
-            g.logits.push_back({(uint32_t)(int64_t)e.at("id").as_number(), (float)e.at("logit").as_number()});
+        for (const Value& e : jl.arr) g.logits.push_back({to_u32(e.at("id"), "id"), to_f32(e.at("logit"), "logit")});
     }
     return gen;
 }
@@ -57,11 +75,11 @@ inline Server::CompleteRequestParams toCompleteParams(const Value& j) {
     Server::CompleteRequestParams p;
     if (!j.is_object()) throw std::runtime_error("json: request is not an object");
     p.prompt = j.at("prompt").as_string();
-    if (auto* v = j.find("max_tokens")) p.maxTokens = (uint32_t)(int64_t)v->as_number();
-    if (auto* v = j.find("seed")) p.seed = (uint32_t)(int64_t)v->as_number();
+    if (auto* v = j.find("max_tokens")) p.maxTokens = to_u32(*v, "max_tokens");
+    if (auto* v = j.find("seed")) p.seed = to_u32(*v, "seed");
     if (auto* v = j.find("suffix")) p.suffix = v->as_string();
-    if (auto* v = j.find("temp")) p.temperature = (float)v->as_number();
-    if (auto* v = j.find("top_p")) p.topP = (float)v->as_number();
+    if (auto* v = j.find("temp")) p.temperature = to_f32(*v, "temp");
+    if (auto* v = j.find("top_p")) p.topP = to_f32(*v, "top_p");
     return p;
 }
 

@@ -334,19 +334,30 @@ def _fill_structured(cfg, seed, name, t, view, P):
     be, bb = gguf.GGML_BLOCK[t]
     row_b = d // be * bb
     rows = view.reshape(V, row_b)
-    rng = _rng(seed, name)
     CH = 2048
     ns = int(P["nsucc"])
-    for a in range(0, V, CH):
+
+    def chunk(a):
         b = min(V, a + CH)
         if name == "token_embd.weight":
             X = _token_dirs(seed, a, b, V, d) * np.float32(P["embd"])
         else:
+            # chunk 0 draws from the tensor's own stream (as every small-vocab model always
+            # did); later chunks from streams of their own, so chunks fill in parallel
+            rng = _rng(seed, name) if a == 0 else _rng(seed, f"{name}:{a}")
             X = rng.standard_normal((b - a, d), dtype=np.float32) * np.float32(P["base"])
             Bw = _token_dirs(seed, a - ns, b, V, d)
             for k in range(1, ns + 1):
                 X += np.float32(P["alpha"] / np.sqrt(k)) * Bw[ns - k:ns - k + (b - a)]
         rows[a:b] = quantize_rows(X, t).reshape(b - a, row_b)
+
+    starts = list(range(0, V, CH))
+    if len(starts) == 1:
+        chunk(0)
+        return
+    from concurrent.futures import ThreadPoolExecutor   # numpy releases the GIL in these ops
+    with ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as ex:
+        list(ex.map(chunk, starts))
 
 
 def vocab_tokens(n_vocab: int):

@@ -140,6 +140,12 @@ int32_t mi_op_dequant(int32_t device, int32_t type, const void* raw_blocks, int3
 int32_t mi_op_quantize_q8_K(int32_t device, const float* x, int32_t K, int8_t* qs, float* d,
                             int32_t* bsums);
 int32_t mi_op_topk(int32_t device, const float* logits, int32_t n, int32_t k, int32_t* ids, float* vals);
+/* One decode step's attention (KQ -> soft_max -> KQV, Session.cpp:388's llama_decode inner
+ * graph, flash_attn=false) of n_head f32 query heads over n_cells cells of an f16 K/V cache
+ * [n_cells][n_head_kv*head_dim]; cells whose cell_pos > pos are masked.  out: [n_head*head_dim]. */
+int32_t mi_op_attention(int32_t device, int32_t n_head, int32_t n_head_kv, int32_t head_dim, int32_t n_cells,
+                        const float* q, const uint16_t* k_f16, const uint16_t* v_f16, const int32_t* cell_pos,
+                        int32_t pos, float* out);
 /* Median device time (us) of `iters` launches of the GEMV above (micro-benchmark). */
 int32_t mi_op_gemv_bench(int32_t device, int32_t type, const void* raw_blocks, int32_t rows, int32_t K,
                          int32_t iters, float* median_us);

@@ -128,11 +128,13 @@ static void scale_min_k4(int j, const uint8_t* q, uint8_t* d, uint8_t* m) {
 /* ORC_ALT=1: sum the 8 float lanes in reverse order -- a second, equally valid
  * fp32 accumulation order, used to measure how far two correct implementations
  * drift apart on a given model (test infrastructure only) */
+static int g_alt = -1;
 static int alt_order(void) {
-    static int on = -1;
-    if (on < 0) on = getenv("ORC_ALT") != NULL;
-    return on;
+    if (g_alt < 0) g_alt = getenv("ORC_ALT") != NULL;
+    return g_alt;
 }
+/* switch the accumulation order in-process (tests measure the algorithm's own noise floor) */
+void orc_set_alt(int on) { g_alt = on ? 1 : 0; }
 static float lane_sum(const float* sums, float init) {
     float s = init;
     if (alt_order()) for (int l = 7; l >= 0; --l) s += sums[l];

@@ -37,6 +37,7 @@ def lib():
         L.orc_decode.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
         L.orc_kv_clear.argtypes = [C.c_void_p]
         L.orc_n_threads.restype = C.c_int
+        L.orc_set_alt.argtypes = [C.c_int]
         _lib = L
     return _lib
 
@@ -80,9 +81,15 @@ class Model:
             ne = list(t.shape) + [1, 1]
             lib().orc_set_tensor(self.h, name.encode(), t.type, data.ctypes.data, ne[0], ne[1], ne[2])
 
-    def decode_one(self, token: int) -> np.ndarray:
+    def decode_one(self, token: int, alt: bool = False) -> np.ndarray:
+        """alt: the same algorithm with the 8 float lanes of every k-quant dot summed in the
+        reverse order -- an equally valid fp32 order (measures the CPU path's own noise floor)."""
         out = np.empty(self.hp.n_vocab, np.float32)
-        rc = lib().orc_decode(self.h, int(token), out.ctypes.data)
+        lib().orc_set_alt(1 if alt else 0)
+        try:
+            rc = lib().orc_decode(self.h, int(token), out.ctypes.data)
+        finally:
+            lib().orc_set_alt(0)
         if rc != 0:
             raise RuntimeError("orc_decode: no KV space")
         return out

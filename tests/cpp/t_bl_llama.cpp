@@ -5,6 +5,7 @@
 //
 // usage: t_bl_llama [cpu] [gpu] --model=<gguf> --vocab=<gguf> --out=<file>
 #include "llama.hpp"
+#include "mi_engine.h"
 #include "minitest.hpp"
 #include "server.hpp"
 #include "wire.hpp"
@@ -140,7 +141,6 @@ TEST_CASE_G("wire format", "cpu") {   // HttpServerMain.cpp:37-94, 259-288
     Server::CompleteReponse gen;
     gen.push_back({" he said \"hi\"\n\t\x01", 301, {{301, 17.25f}, {7, -0.1f}, {1234567, 3.14159274f}}});
     gen.push_back({"\xc3\xa9\xe2\x82\xac", 77, {{77, 1e-30f}, {5, -1.17549435e-38f}, {9, 0.333333343f}}});
-    gen.push_back({"", 0, {}});
     const std::string body = wire::completeBody(gen);
     const auto j = bl::json::parse(body);
     CHECK(j.at("text").as_string() == gen[0].tokenStr + gen[1].tokenStr);
@@ -185,6 +185,22 @@ TEST_CASE_G("wire format", "cpu") {   // HttpServerMain.cpp:37-94, 259-288
     CHECK(enc("\xed\xa0\x80") == fffd + fffd + fffd);      // surrogate: 0xA0 outside ED's range
     CHECK(enc("\xf0\x9f\x98\x80x\xff") == "\xf0\x9f\x98\x80x" + fffd);
     CHECK((float)bl::json::parse(wire::verifyBody(0.975f)).at("result").as_number() == 0.975f);
+    // network-facing validation: empty or oversized claimed logit lists, non-JSON numbers,
+    // out-of-range integers, deep nesting
+    CHECK_THROWS(wire::toCompleteResponse(bl::json::parse(R"({"tokenData":[{"str":"","id":0,"logits":[]}]})")));
+    CHECK_THROWS(wire::toCompleteParams(bl::json::parse(R"({"prompt":"x","seed":-1e300})")));
+    CHECK_THROWS(wire::toCompleteParams(bl::json::parse(R"({"prompt":"x","max_tokens":1.5})")));
+    CHECK_THROWS(wire::toCompleteParams(bl::json::parse(R"({"prompt":"x","temp":1e300})")));
+    CHECK(wire::toCompleteParams(bl::json::parse(R"({"prompt":"x","seed":4294967295})")).seed == 4294967295u);
+    CHECK_THROWS(bl::json::parse("nan"));
+    CHECK_THROWS(bl::json::parse("[inf]"));
+    CHECK_THROWS(bl::json::parse("0x10"));
+    CHECK_THROWS(bl::json::parse("1e999"));
+    CHECK_THROWS(bl::json::parse("+1"));
+    CHECK(bl::json::parse("-0.5e-3").as_number() == -0.5e-3);
+    CHECK_THROWS(bl::json::parse(std::string(100000, '[')));
+    CHECK(bl::json::parse(std::string(200, '[') + std::string(200, ']')).is_array());
+    CHECK_THROWS(LogitComparer::compare({}, {{1, 1.0f}}));
 }
 
 // ---------------------------------------------------------------- GPU ----
@@ -239,6 +255,33 @@ TEST_CASE_G("session", "gpu") {   // t-integration.cpp:124-250
         CHECK_THROWS_WITH(inst.startSession({}), "Session is already started. Stop it to start a new one.");
         inst.stopSession();
     }
+}
+
+TEST_CASE_G("sampler bias beyond top-k", "gpu") {   // Sampler.cpp:30-41: bias before top_k
+    Model model(g_model, {});
+    Instance inst(model, {});
+    REQUIRE(mi_decode(inst.mctx(), kPrompt.data(), (int32_t)kPrompt.size(), MI_OUT_LAST) == 0);
+    const float* lg = mi_logits(inst.mctx(), -1);
+    REQUIRE(lg != nullptr);
+    const int32_t n = mi_model_n_vocab(model.mmodel());
+    Token low = 0;
+    for (int32_t i = 1; i < n; ++i)
+        if (lg[i] < lg[low]) low = i;          // the lowest-ranked token: far outside the top 40
+    Sampler::Params p;
+    p.temp = 0.0f;                              // greedy
+    p.logitBias = {{low, 1e4f}};
+    Sampler s(model, p);
+    CHECK(s.sample(inst.mctx()) == low);        // the bias lifts it over every other token
+    Sampler::Params q;
+    q.temp = 0.0f;
+    Sampler plain(model, q);
+    Token top = plain.sample(inst.mctx());
+    q.repetitionPenalty.repeat = 1e6f;          // penalise the top token out of first place
+    q.repetitionPenalty.numTokens = 64;
+    Sampler pen(model, q);
+    pen.accept(top, false);
+    const Token second = pen.sample(inst.mctx());
+    CHECK(second != top);
 }
 
 TEST_CASE_G("filling ctx", "gpu") {   // t-integration.cpp:219-248: bit-identical verification

@@ -1,0 +1,144 @@
+"""Oracle parity of every shipped kernel instantiation at the BASELINE models' real widths.
+
+The small configs of test_gpu_decode.py all have n_embd 256 with GQA, so they never run the
+instantiations the benchmarks run.  These tests build full-width, reduced-depth synthetic
+models (2 layers; real n_embd, heads, head_dim, n_ff, vocabulary and Q*_K_M tensor mix) and
+compare the HIP engine with the C restatement of the ggml CPU path (oracle/ggml_cpu.c):
+
+  Llama-2-7B Q4_K_M   R=1, hd=128: attn_fused_kernel<1,16>, split attention past 512 cells,
+                      the mixed Q4_K/Q6_K QKV launch (layer 1 is a use_more_bits layer),
+                      16-wave FFN gate/up over 11008 rows, Q6_K output over 32000 rows
+  Llama-3-8B Q6_K     R=4, hd=128, V=128256 (the top-k over 126 blocks)
+  Mixtral Q5_K_M      8 experts (so attn_k/attn_v are Q8_0, llama_tensor_get_type's
+                      8-expert rule), top-2 routing, R=4; n_ff cut to 1024 to bound the file
+  TinyLlama Q8_0      R=8, hd=64, Q8_0 everywhere
+
+Tolerance.  At these widths the CPU algorithm is not stable to its own fp32 summation order:
+the C oracle run with the 8 float lanes of every k-quant dot summed in the reverse order (an
+equally valid order; ggml's AVX2 and generic paths differ in exactly this way) moves the
+logits by up to 6.6e-2 x rms (max) and 1.4e-2 x rms (L2) on these models (measured over 11
+steps x 3 models; profiles/r02_fullwidth_floor.txt).  The cause is the Q8_K / Q8_0
+re-quantisation of every GEMV input: a last-bit difference flips an activation quantum, and
+the flips compound through the layers.  The element-wise 2e-3 of the small configs is below
+that floor, so here each step must satisfy
+  * max|dlogit| <= TOL_MAX x rms and ||dlogit||_2 <= TOL_L2 x ||logit||_2 (about twice the
+    floor), and, for k-quant models, the run's mean L2 error within twice the live floor
+    (the same oracle in the reversed order, decoded alongside);
+  * top-10 ids identical up to near ties: the GPU's rank-i id, scored by the oracle, is within
+    2 max|dlogit| of the oracle's rank-i logit;
+and the run must pass the reference's acceptance gate (t-LogitComparer.cpp:76-78: aggregate
+score >= 0.95, mean logitSimilarity >= 0.98, top-1 match on every step).  The kernels' own
+arithmetic is checked without this chaos at op level (test_gpu_ops.py: GEMV at these shapes,
+attention at these head shapes)."""
+import numpy as np
+import pytest
+
+import ggml_cpu
+import ggml_ref as R
+from blama_amd import engine, synthetic
+
+pytestmark = pytest.mark.gpu
+
+TOL_MAX = 0.12
+TOL_L2 = 0.03
+
+FULL = {
+    "llama2-7b-q4_k_m": dict(n_layer=2),
+    "llama3-8b-q6_k": dict(n_layer=2),
+    "mixtral-8x7b-q5_k_m": dict(n_layer=2, n_ff=1024),
+    "tinyllama-1.1b-q8_0": dict(n_layer=2),
+}
+
+_cache = {}
+
+
+def full_model(name):
+    """(cfg, gguf image, engine model) -- built once per test session."""
+    if name not in _cache:
+        cfg = synthetic.small_config(name, **FULL[name])
+        buf = synthetic.build_gguf(cfg, seed=3)
+        _cache[name] = (cfg, buf, engine.Model(buf))
+    return _cache[name]
+
+
+def _err(got, ref):
+    d = np.abs(got.astype(np.float64) - ref)
+    rms = float(np.sqrt(np.mean(ref ** 2)))
+    return float(d.max()), float(d.max()) / rms, float(np.sqrt(np.mean(d ** 2))) / rms
+
+
+def _check_run(name, ctx, orc, prompt, steps, rng):
+    """Decode `prompt` then `steps` tokens on the engine, the oracle and the oracle in the
+    reversed lane order; check every distribution."""
+    cfg = _cache[name][0]
+    assert ctx.decode(prompt) == 0
+    alt = ggml_cpu.Model(_cache[name][1], n_ctx=orc.n_ctx)
+    for t in prompt:
+        ref = orc.decode_one(t).astype(np.float64)
+        ref_alt = alt.decode_one(t, alt=True)
+    agg = R.MetricsAggregator()
+    sims, top1, l2s, alt_l2s = [], [], [], []
+    score = None
+    try:
+        for s in range(steps + 1):
+            got = ctx.logits()
+            ids, vals = ctx.topk(10)
+            dmax, rmax, rl2 = _err(got, ref)
+            _, amax, al2 = _err(ref_alt, ref)
+            l2s.append(rl2)
+            alt_l2s.append(al2)
+            print(f"{name} step {s} cells {ctx.n_cells}: max/rms {rmax:.1e} l2 {rl2:.1e} "
+                  f"(cpu reorder floor: max {amax:.1e} l2 {al2:.1e})")
+            assert rmax <= TOL_MAX and rl2 <= TOL_L2, (name, s, rmax, rl2)
+            ref_sorted = np.sort(ref)[::-1][:10]
+            assert len(set(int(i) for i in ids)) == 10
+            assert np.all(np.abs(ref[ids.astype(np.int64)] - ref_sorted) <= 2 * dmax + 1e-6), (name, s)
+            a = [(int(i), float(v)) for i, v in zip(ids, vals)]
+            b = R.gather(ref.astype(np.float32), [i for i, _ in a])
+            cm = R.compare(a, b)
+            top1.append(cm.top1Match)
+            score = agg.push_and_verify([cm])
+            sims.append(R.logit_similarity(a, b))
+            if s == steps:
+                break
+            # follow the model's own preference most of the time (a realistic trajectory)
+            t = int(ids[0]) if rng.random() < 0.7 else int(rng.integers(0, cfg.n_vocab))
+            assert ctx.decode([t]) == 0
+            ref = orc.decode_one(t).astype(np.float64)
+            ref_alt = alt.decode_one(t, alt=True)
+    finally:
+        alt.close()
+    if max(alt_l2s) > 0:   # the reorder does not touch Q8_0 dots (one float sum per block)
+        assert np.mean(l2s) <= 2 * np.mean(alt_l2s) + 2e-3, (np.mean(l2s), np.mean(alt_l2s))
+    assert score >= 0.95 and float(np.mean(sims)) >= 0.98 and min(top1) == 1.0, (score, np.mean(sims))
+
+
+@pytest.mark.parametrize("name", list(FULL))
+def test_fullwidth_decode_matches_oracle(gpu_lib, name):
+    cfg, buf, m = full_model(name)
+    ctx = engine.Context(m, n_ctx=64)
+    orc = ggml_cpu.Model(buf, n_ctx=64)
+    rng = np.random.default_rng(11)
+    prompt = [int(t) for t in rng.integers(0, cfg.n_vocab, 12)]
+    try:
+        _check_run(name, ctx, orc, prompt, steps=10, rng=rng)
+    finally:
+        ctx.close()
+        orc.close()
+
+
+def test_fullwidth_7b_crosses_512_cells(gpu_lib):
+    """hd=128 past ATTN_SHORT: a 508-token prompt (batched ingestion), then decode steps over
+    cells 509..518, switching from the fused attention graph to the split one at 512."""
+    name = "llama2-7b-q4_k_m"
+    cfg, buf, m = full_model(name)
+    ctx = engine.Context(m, n_ctx=600)
+    orc = ggml_cpu.Model(buf, n_ctx=600)
+    rng = np.random.default_rng(12)
+    prompt = [int(t) for t in rng.integers(0, cfg.n_vocab, 508)]
+    try:
+        _check_run(name, ctx, orc, prompt, steps=10, rng=rng)
+        assert ctx.n_cells == 518
+    finally:
+        ctx.close()
+        orc.close()

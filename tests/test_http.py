@@ -88,7 +88,10 @@ def _piece(tid):
 
 @pytest.fixture
 def served(tmp_path):
-    cfg = synthetic.CONFIGS["tiny-q4_k_m"]
+    yield from _serve(tmp_path, synthetic.CONFIGS["tiny-q4_k_m"])
+
+
+def _serve(tmp_path, cfg):
     buf = synthetic.build_gguf(cfg, seed=5)
     path = str(tmp_path / "model.gguf")
     buf.tofile(path)
@@ -160,3 +163,42 @@ def test_http_complete_and_verify(served):
     # the server keeps serving after errors
     st, body, _ = _post(port, "/complete", dict(req, max_tokens=2))
     assert st == 200 and len(json.loads(body)["tokenData"]) == 2
+
+
+@pytest.fixture
+def served_tinyllama(tmp_path):
+    """BASELINE configs[0]: a TinyLlama-1.1B-shaped Q8_0 model (real width, heads 32/4,
+    n_ff 5632, V 32000; 2 layers instead of 22 to bound the file)."""
+    yield from _serve(tmp_path, synthetic.small_config("tinyllama-1.1b-q8_0", n_layer=2))
+
+
+@pytest.mark.gpu
+def test_http_tinyllama_complete_32_verified_by_oracle(served_tinyllama):
+    """/complete of 32 tokens on the TinyLlama-shaped Q8_0 model, then the C restatement of the
+    CPU path verifies the completion as Session::fillCtx would (Session.cpp:231-282) under the
+    reference's gate (t-LogitComparer.cpp:76-78), and the server's own /verify_completion of it
+    scores exactly 1."""
+    import ggml_cpu
+    port, buf = served_tinyllama
+    req = {"prompt": "the quick brown fox", "max_tokens": 32, "seed": 3, "temp": 0.8, "top_p": 0.95}
+    st, body, _ = _post(port, "/complete", req)
+    assert st == 200, body
+    out = json.loads(body)
+    toks = out["tokenData"]
+    assert len(toks) == 32
+    st, vbody, _ = _post(port, "/verify_completion", {"request": req, "response": out})
+    assert st == 200 and json.loads(vbody)["result"] == 1.0
+    orc = ggml_cpu.Model(buf, n_ctx=128)
+    orc.decode(_prompt_ids(req["prompt"]))
+    agg = R.MetricsAggregator()
+    sims, top1, score = [], [], None
+    for t in toks:
+        claimed = [(l["id"], l["logit"]) for l in t["logits"]]
+        lg = orc.decode_one(t["id"])
+        mine = sorted(R.gather(lg, sorted({i for i, _ in claimed})), key=lambda x: -x[1])
+        cm = R.compare(claimed, mine)
+        top1.append(cm.top1Match)
+        score = agg.push_and_verify([cm])
+        sims.append(R.logit_similarity(claimed, mine))
+    orc.close()
+    assert score >= 0.95 and float(np.mean(sims)) >= 0.98 and min(top1) == 1.0, (score, np.mean(sims))
