@@ -43,22 +43,39 @@ def broadcast_bytes(t, dist, src: int = 0, chunk_bytes: int = DEFAULT_CHUNK, gro
     return k
 
 
+def _check_sizes(nbytes: int, rank: int, dist, group, device) -> None:
+    """Every rank learns every rank's arena size, so a mismatch raises on ALL ranks together
+    (raising only where the size differs would leave the others blocked in the broadcast)."""
+    import torch
+    world = dist.get_world_size(group)
+    mine = torch.tensor([nbytes], dtype=torch.int64, device=device)
+    sizes = [torch.zeros(1, dtype=torch.int64, device=device) for _ in range(world)]
+    dist.all_gather(sizes, mine, group=group)
+    got = [int(x.item()) for x in sizes]
+    if len(set(got)) != 1:
+        raise engine.EngineError(f"replica arena sizes differ across ranks: {got} (rank {rank})")
+
+
+def _src_rank(dist, group) -> int:
+    """The global rank of the group's first member: the replica that parsed the GGUF."""
+    return 0 if group is None else dist.get_global_rank(group, 0)
+
+
 def load_replicated(source, rank: int, local_rank: int, dist, header=None,
                     chunk_bytes: int = DEFAULT_CHUNK, group=None) -> "engine.Model":
     """Load one replica per rank.  ``source`` (path or GGUF image) must hold the
-    tensor data on rank 0; other ranks only need the header (``header`` if
+    tensor data on the group's first rank; other ranks only need the header (``header`` if
     given, else ``source``).  Collective: every rank of ``group`` must call it."""
     import torch
-    if rank == 0:
+    src = _src_rank(dist, group)
+    if rank == src:
         model = engine.Model(source, device=local_rank)
     else:
         model = engine.Model(header if header is not None else source, device=local_rank, no_upload=True)
     ptr, nbytes = model.arena
-    sizes = torch.tensor([nbytes], dtype=torch.int64, device=f"cuda:{local_rank}")
-    dist.all_reduce(sizes, op=dist.ReduceOp.MAX)
-    if int(sizes.item()) != nbytes:
-        raise engine.EngineError(f"replica arena size mismatch on rank {rank}: {nbytes} vs {int(sizes.item())}")
-    torch.cuda.synchronize(local_rank)        # rank 0's repack is complete before its bytes are sent
-    broadcast_bytes(arena_tensor(model, local_rank), dist, 0, chunk_bytes, group)
+    dev = "cpu" if dist.get_backend(group) == "gloo" else f"cuda:{local_rank}"
+    _check_sizes(nbytes, rank, dist, group, dev)
+    torch.cuda.synchronize(local_rank)        # the source's repack is complete before its bytes are sent
+    broadcast_bytes(arena_tensor(model, local_rank), dist, src, chunk_bytes, group)
     torch.cuda.synchronize(local_rank)
     return model
