@@ -36,7 +36,7 @@ inline bool is_quant(int t) { return t == T_Q8_0 || t == T_Q4_K || t == T_Q5_K |
 //   Q5_K: p0 qs[128]  p1 qh[32]  p2 hdr[16]
 //   Q6_K: p0 ql[128]  p1 qh[64]  p2 i8 scales[16]  p3 f16 d
 //   Q8_0: p0 qs[256]  p1 f16 d[8]
-constexpr int kPlanePadSb = 8;   // tail padding (superblocks) after every plane
+constexpr int kPlanePadSb = 16;  // tail padding (superblocks) after every plane (ring GEMV over-reads)
 inline int plane_count(int t) {
     switch (t) { case T_Q4_K: return 2; case T_Q5_K: return 3; case T_Q6_K: return 4;
                  case T_Q8_0: return 2; default: return 0; }

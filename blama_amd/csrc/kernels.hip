@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
 #include <cstdlib>
+#include <cstring>
 
 namespace mi {
 
@@ -217,7 +218,11 @@ template <> struct Kq<T_Q4_K> {
     __device__ static Ld load(const uint8_t* const* rp, int sb, int j) {
         Ld l;
         l.qs = ldg16(rp[0] + sb * 128 + j * 16);
+#ifdef MI_EXP_NOHDR   // bandwidth experiment only (wrong numerics): no header loads
+        l.hdr = u32x4{0x3c003c00u, 0x01010101u, 0x01010101u, 0x01010101u};
+#else
         l.hdr = ldg16(rp[1] + sb * 16);
+#endif
         return l;
     }
     // the activation slice lane (sb, j) needs -- identical for every row
@@ -561,6 +566,9 @@ __device__ __forceinline__ bool pro_load_rest(const GemvParams& P, ProRegs& R, i
     return any;
 }
 
+// RAW_BARRIER: LDS-DMA is in flight (gemv_ring_body), so the reduction's barrier must not
+// wait vmcnt(0) (see lds_barrier).
+template <bool RAW_BARRIER>
 __device__ __forceinline__ void pro_finish(const GemvParams& P, const ProRegs& R, char* smem, const SmemPlan& SP,
                                            int pos, int ncell, int wg_u0, int wg_u1, int bid) {
     const int tid = threadIdx.x, lane = tid & 63;
@@ -605,7 +613,12 @@ __device__ __forceinline__ void pro_finish(const GemvParams& P, const ProRegs& R
 #ifdef MI_STAMPS
         if (P.stamps && threadIdx.x == 0) P.stamps[bid * 8 + 5] = __builtin_amdgcn_s_memrealtime();
 #endif
-        __syncthreads();
+        if (RAW_BARRIER) {
+            __builtin_amdgcn_s_waitcnt((0xF) | (0x3 << 14) | (0x7 << 4));   // lgkmcnt(0) only
+            __builtin_amdgcn_s_barrier();
+        } else {
+            __syncthreads();
+        }
 #ifdef MI_STAMPS
         if (P.stamps && threadIdx.x == 0) P.stamps[bid * 8 + 6] = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -923,7 +936,7 @@ __device__ __forceinline__ void gemv_body(const float* __restrict__ kx0, const f
     MI_STAMP(1)
     const int pos = __builtin_amdgcn_readfirstlane(pr.tp.y);
     const int cell = __builtin_amdgcn_readfirstlane(pr.tp.z);
-    pro_finish(P, pr, smem, SP, pos, cell + 1, wg_u0, wg_u1, bid);
+    pro_finish<false>(P, pr, smem, SP, pos, cell + 1, wg_u0, wg_u1, bid);
     MI_STAMP(7)
     __syncthreads();
     MI_STAMP(2)
@@ -997,6 +1010,798 @@ __global__ __launch_bounds__(NW * 64) void gemv_mix_t(const float* __restrict__ 
     else gemv_body<T2, D, NW, 0>(kx0, knw, ktp, kflags, P2, sparams, blockIdx.x - g1);
 }
 
+// ---------------------------------------------------------------------------
+// The GEMV with its weight stream staged through LDS by LDS-DMA (global_load_lds).
+//
+// gemv_body keeps its in-flight weights in registers: D-1 items per wave, which at the
+// register budget of its prologue is ~50 KB per CU, ~2 us of the CU's share of HBM
+// bandwidth -- less than the prologue (activation arrival, RMSNorm, Q8_K quantisation) takes,
+// so HBM idles until the prologue is done.  Here every wave owns a private ring of D item
+// slots in LDS, filled by global_load_lds: ~110 KB in flight per CU from the moment the
+// prologue starts, no VGPRs held, and no cross-wave synchronisation in the stream (a wave
+// only ever reads the slots it filled itself, so its own vmcnt orders it).
+// An item is one 8-superblock chunk of the unit's two rows, every plane (Rq<T>::ROW bytes a
+// row); the LDS image is lane-linear per plane, so the consumer's reads are the register
+// ring's loads with an LDS base.
+// ---------------------------------------------------------------------------
+// One LDS-DMA of 16 bytes a lane (global_load_lds_dwordx4, non-temporal: decode weights are
+// read once).  Inline asm, not __builtin_amdgcn_global_load_lds: with the builtin, hipcc
+// (ROCm 7.2) tail-merges an exec-masked DMA (the 8-lane header planes) with the full-wave one
+// after it into ONE instruction whose M0 comes from v_readfirstlane of a per-lane select --
+// the wrong LDS base for every lane outside the first (found by the GEMV op tests).  M0 is
+// written and restored inside the statement (it is compiler-reserved); hipcc does not count
+// these loads, the ring's wait_vm() does.
+__device__ __forceinline__ void gl16(const uint8_t* g, char* l) {
+    const unsigned la = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)l;
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(g), "s"(la) : "memory");
+}
+// s_waitcnt vmcnt(N) and nothing else (expcnt 7, lgkmcnt 15 = no wait)
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+    static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+    __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+}
+// workgroup barrier that leaves LDS-DMA in flight: this wave's LDS accesses complete (the
+// data other waves read after the barrier), then s_barrier; __syncthreads() would also wait
+// vmcnt(0), draining every wave's ring.
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_s_waitcnt((0xF) | (0x3 << 14) | (0x7 << 4) | (0x0 << 8));   // lgkmcnt(0)
+    __builtin_amdgcn_s_barrier();
+}
+
+template <int T> struct Rq;
+template <> struct Rq<T_Q4_K> {   // qs 8x128 | hdr 8x16
+    static constexpr int ROW = 1152, G = 2;
+    __device__ static int glds(const uint8_t* const* rp, int sb0, char* d, int lane) {
+        gl16(rp[0] + sb0 * 128 + lane * 16, d);
+        if (lane < 8) gl16(rp[1] + (sb0 + lane) * 16, d + 1024);
+        return 0;
+    }
+    __device__ static Kq<T_Q4_K>::Ld lds(const char* s, int sbl, int j, int) {
+        Kq<T_Q4_K>::Ld l;
+        l.qs = *reinterpret_cast<const u32x4*>(s + sbl * 128 + j * 16);
+        l.hdr = *reinterpret_cast<const u32x4*>(s + 1024 + sbl * 16);
+        return l;
+    }
+};
+template <> struct Rq<T_Q5_K> {   // qs 8x128 | qh 8x32 | hdr 8x16
+    static constexpr int ROW = 1408, G = 3;
+    __device__ static int glds(const uint8_t* const* rp, int sb0, char* d, int lane) {
+        gl16(rp[0] + sb0 * 128 + lane * 16, d);
+        if (lane < 16) gl16(rp[1] + sb0 * 32 + lane * 16, d + 1024);
+        if (lane < 8) gl16(rp[2] + (sb0 + lane) * 16, d + 1280);
+        return 0;
+    }
+    __device__ static Kq<T_Q5_K>::Ld lds(const char* s, int sbl, int j, int) {
+        Kq<T_Q5_K>::Ld l;
+        l.qs = *reinterpret_cast<const u32x4*>(s + sbl * 128 + j * 16);
+        l.qh = *reinterpret_cast<const u32x4*>(s + 1024 + sbl * 32 + (j & 1) * 16);
+        l.hdr = *reinterpret_cast<const u32x4*>(s + 1280 + sbl * 16);
+        return l;
+    }
+};
+template <> struct Rq<T_Q6_K> {   // ql 8x128 | qh 8x64 | scales 8x16 | d: 32 B holding 8x2
+    static constexpr int ROW = 1696, G = 4;
+    // The d plane has 2 bytes a superblock, so a chunk's 16 bytes need not be 16-B aligned: two
+    // lanes fetch the 32 aligned bytes around them; returns the chunk's offset within those.
+    __device__ static int glds(const uint8_t* const* rp, int sb0, char* d, int lane) {
+        gl16(rp[0] + sb0 * 128 + lane * 16, d);
+        if (lane < 32) gl16(rp[1] + sb0 * 64 + lane * 16, d + 1024);
+        if (lane < 8) gl16(rp[2] + (sb0 + lane) * 16, d + 1536);
+        const uint8_t* dp = rp[3] + sb0 * 2;
+        const uint8_t* da = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(dp) & ~(uintptr_t)15);
+        if (lane < 2) gl16(da + lane * 16, d + 1664);
+        return (int)(dp - da);
+    }
+    __device__ static Kq<T_Q6_K>::Ld lds(const char* s, int sbl, int j, int doff) {
+        typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+        Kq<T_Q6_K>::Ld l;
+        const int h = j >> 2, half = j & 1;
+        l.ql = *reinterpret_cast<const u32x4*>(s + sbl * 128 + j * 16);
+        l.qh = *reinterpret_cast<const u32x4*>(s + 1024 + sbl * 64 + 32 * h + 16 * half);
+        const u32x2 sc = *reinterpret_cast<const u32x2*>(s + 1536 + sbl * 16 + h * 8);
+        l.sc0 = sc.x;
+        l.sc1 = sc.y;
+        l.d = *reinterpret_cast<const unsigned short*>(s + 1664 + doff + sbl * 2);
+        return l;
+    }
+};
+template <> struct Rq<T_Q8_0> {   // qs 8x256 | d 8x16
+    static constexpr int ROW = 2176, G = 3;
+    __device__ static int glds(const uint8_t* const* rp, int sb0, char* d, int lane) {
+        gl16(rp[0] + sb0 * 256 + lane * 16, d);
+        gl16(rp[0] + sb0 * 256 + 1024 + lane * 16, d + 1024);
+        if (lane < 8) gl16(rp[1] + (sb0 + lane) * 16, d + 2048);
+        return 0;
+    }
+    __device__ static Kq<T_Q8_0>::Ld lds(const char* s, int sbl, int j, int) {
+        Kq<T_Q8_0>::Ld l;
+        l.q0 = *reinterpret_cast<const u32x4*>(s + sbl * 256 + j * 32);
+        l.q1 = *reinterpret_cast<const u32x4*>(s + sbl * 256 + j * 32 + 16);
+        l.d = *reinterpret_cast<const unsigned short*>(s + 2048 + sbl * 16 + j * 2);
+        return l;
+    }
+};
+
+// LDS ring depth per type at 8 waves (ring = 8 x D x 2 x ROW bytes, ~105-113 KB)
+template <int T> struct RingD;
+template <> struct RingD<T_Q4_K> { static constexpr int D = 6; };
+template <> struct RingD<T_Q5_K> { static constexpr int D = 5; };
+template <> struct RingD<T_Q6_K> { static constexpr int D = 4; };
+template <> struct RingD<T_Q8_0> { static constexpr int D = 3; };
+constexpr int RING_NW = 8;
+__host__ __device__ inline int ring_bytes(int t) {
+    switch (t) {
+    case T_Q4_K: return RING_NW * 6 * 2 * 1152;
+    case T_Q5_K: return RING_NW * 5 * 2 * 1408;
+    case T_Q6_K: return RING_NW * 4 * 2 * 1696;
+    case T_Q8_0: return RING_NW * 3 * 2 * 2176;
+    default: return 0;
+    }
+}
+
+template <int T, int DUAL>
+__device__ __forceinline__ void gemv_ring_body(const float* __restrict__ kx0, const float* __restrict__ knw,
+                                               const int* __restrict__ ktp, int kflags, const GemvParams& Pk,
+                                               u32x4* sparams, const int bid) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    using K = Kq<T>;
+    using RQ = Rq<T>;
+    constexpr int NW = RING_NW, D = RingD<T>::D, ITEM = 2 * RQ::ROW, GI = 2 * RQ::G;
+    static_assert((D - 1) * GI < 64, "in-flight LDS-DMA count must fit vmcnt");
+    static_assert(D <= 8, "8 bits of slot offsets per slot in 64");
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    ProRegs pr;
+    pro_load_entry(pr, kx0, knw, ktp, (kflags & 0xFFFFF) >> 8, (kflags >> 20) & 1, (kflags >> 21) & 1, NW, wave,
+                   lane);
+    {
+        const u32x4* src = reinterpret_cast<const u32x4*>(&Pk);
+        for (int i = threadIdx.x; i < kGemvParamVecs; i += NW * 64) sparams[i] = src[i];
+        __syncthreads();   // no LDS-DMA in flight yet: waits for the parameters (and x) only
+    }
+    const GemvParams& P = *reinterpret_cast<const GemvParams*>(sparams);
+#ifdef MI_STAMPS   // diagnostic build only (scripts/timeline.py)
+#define MI_STAMP(k) \
+    if (P.stamps && threadIdx.x == 0) P.stamps[bid * 8 + (k)] = __builtin_amdgcn_s_memrealtime();
+#else
+#define MI_STAMP(k)
+#endif
+    MI_STAMP(0)
+    const int sbl = lane >> 3, j = lane & 7;
+    const SmemPlan SP = smem_plan(P);
+    char* const ring = smem + ((SP.total + 15) & ~15) + wave * (D * ITEM);
+    const int nb = P.K >> 8;
+    const int cpr = (nb + 7) >> 3;   // chunks per row
+    int e0 = 0, e1 = 0;
+    float w0 = 0.0f, w1 = 0.0f;
+    if (P.sel) {
+        e0 = __builtin_amdgcn_readfirstlane(gptr(P.sel)[0]);
+        e1 = __builtin_amdgcn_readfirstlane(gptr(P.sel)[1]);
+        w0 = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(gptr(P.selw)[0])));
+        w1 = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(gptr(P.selw)[1])));
+    }
+    const int W = P.grid * NW;
+    int u0, u1, wg_u0, wg_u1, dummy;
+    unit_range(P.total_units, W, bid * NW + wave, u0, u1);
+    unit_range(P.total_units, P.grid, bid, wg_u0, dummy);
+    unit_range(P.total_units, W, bid * NW + NW - 1, dummy, wg_u1);
+    const int n_items = (u1 - u0) * cpr;
+
+    int iu = u0, ic = 0, islot = 0;
+    unsigned long long doffs = 0;   // per ring slot: the A and B rows' Rq::glds offsets (4 bits each)
+    const uint8_t* pa[4] = {nullptr, nullptr, nullptr, nullptr};
+    const uint8_t* pb[4] = {nullptr, nullptr, nullptr, nullptr};
+    int fast_end = 0, step_rows = 0;
+    auto bases = [&](int u) {
+        const UnitRef c = unit_ref(P, u);
+        const GemvSeg& S = P.seg[c.si];
+        const QMat& MB = S.pair == PAIR_ADJ ? S.A : S.B;
+        const long long ea = S.expA == 0 ? e0 : S.expA == 1 ? e1 : 0;
+        const long long eb = S.expB == 0 ? e0 : S.expB == 1 ? e1 : 0;
+        const long long rb = c.hasB ? c.rb : c.ra;   // odd tail: re-read row A, result unused
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            pa[i] = rfl_ptr(S.A.p[i] + ea * S.A.expert_stride[i] + c.ra * nb * PlaneBytes<T>::b[i]);
+            pb[i] = rfl_ptr(MB.p[i] + eb * MB.expert_stride[i] + rb * nb * PlaneBytes<T>::b[i]);
+        }
+        const int pair = __builtin_amdgcn_readfirstlane(S.pair);
+        const int end = __builtin_amdgcn_readfirstlane(S.unit0 + S.units);
+        const int rows = __builtin_amdgcn_readfirstlane(S.A.rows);
+        step_rows = pair == PAIR_ADJ ? 2 : 1;
+        fast_end = (pair == PAIR_ADJ && (rows & 1)) ? end - 1 : end;
+    };
+    auto next_unit = [&](int u) {
+        if (u < fast_end) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const long long d = (long long)step_rows * nb * PlaneBytes<T>::b[i];
+                pa[i] += d;
+                pb[i] += d;
+            }
+        } else {
+            bases(u);
+        }
+    };
+    bases(u0 < P.total_units ? u0 : P.total_units - 1);
+    // Issue the next item into the next ring slot.  Past the end of its range a wave keeps
+    // issuing the last item again (cache hits into a free slot), so every step issues exactly
+    // GI LDS-DMA instructions and the counted vmcnt waits stay exact.
+    auto issue = [&]() {
+        char* slot = ring + islot * ITEM;
+        const unsigned oa = (unsigned)RQ::glds(pa, ic * 8, slot, lane);
+        const unsigned ob = (unsigned)RQ::glds(pb, ic * 8, slot + RQ::ROW, lane);
+        doffs = (doffs & ~(0xFFull << (8 * islot))) | ((unsigned long long)(oa | (ob << 4)) << (8 * islot));
+        islot = islot + 1 == D ? 0 : islot + 1;
+        if (iu < u1) {
+            if (++ic == cpr) {
+                if (iu + 1 < u1) {
+                    ic = 0;
+                    ++iu;
+                    next_unit(iu);
+                } else {
+                    ic = cpr - 1;   // park on the last item
+                    iu = u1;
+                }
+            }
+        }
+    };
+    pro_load_rest(P, pr, nb, NW, wave, lane, wg_u0, wg_u1);
+    // Every ordinary load the prologue consumes has landed before the first LDS-DMA: hipcc does
+    // not count the asm DMAs, so a wait it placed later for one of those loads would count
+    // them as younger loads and drain the ring's prefill.  The builtin (not asm) tells hipcc.
+    wait_vm<0>();
+#pragma unroll
+    for (int k = 0; k < D - 1; ++k) issue();
+    MI_STAMP(1)
+    const int pos = __builtin_amdgcn_readfirstlane(pr.tp.y);
+    const int cell = __builtin_amdgcn_readfirstlane(pr.tp.z);
+    pro_finish<true>(P, pr, smem, SP, pos, cell + 1, wg_u0, wg_u1, bid);
+    MI_STAMP(7)
+    lds_barrier();
+    MI_STAMP(2)
+    const float* rope = reinterpret_cast<const float*>(smem + SP.rope_off);
+    const float* rs = reinterpret_cast<const float*>(smem + SP.resid_off);
+    const Act a0 = act_view(smem, SP.L, 0);
+    const Act a1 = act_view(smem, SP.L, DUAL ? 1 : 0);
+
+    int cu = u0, cc = 0, cslot = 0;
+    float accA = 0.0f, accB = 0.0f;
+    const EpiConst EC = epi_const(P);
+    EpiSeg cseg = epi_seg(P, u0 < P.total_units ? u0 : P.total_units - 1);
+    for (int it = 0; it < n_items; ++it) {
+        issue();
+        wait_vm<(D - 1) * GI>();   // this item's GI transfers have landed (D-1 items stay in flight)
+        const char* slot = ring + cslot * ITEM;
+        const unsigned off = (unsigned)(doffs >> (8 * cslot)) & 0xFFu;
+        cslot = cslot + 1 == D ? 0 : cslot + 1;
+        const typename K::Ld la = RQ::lds(slot, sbl, j, (int)(off & 0xF));
+        const typename K::Ld lb = RQ::lds(slot + RQ::ROW, sbl, j, (int)(off >> 4));
+        const int sb = cc * 8 + sbl;
+        const bool lv = sb < nb;
+        const int sbc = lv ? sb : nb - 1;
+        const typename K::AR arA = K::act(a0, sbc, j);
+        const float pa_ = K::dot(la, arA, j);
+        float pb_;
+        if (DUAL) {
+            const typename K::AR arB = K::act(a1, sbc, j);
+            pb_ = K::dot(lb, arB, j);
+        } else {
+            pb_ = K::dot(lb, arA, j);
+        }
+        accA += lv ? pa_ : 0.0f;
+        accB += lv ? pb_ : 0.0f;
+        if (++cc == cpr) {
+            const float yA = wave_sum63(accA);
+            const float yB = wave_sum63(accB);
+            if (cu >= cseg.end) cseg = epi_seg(P, cu);   // segment change (rare)
+            if (lane == 63) {
+                const int i = cu - wg_u0;
+                gemv_epilogue(EC, cseg, cu, rope, rs[2 * i], rs[2 * i + 1], w0, w1, pos, cell, yA, yB);
+            }
+            accA = accB = 0.0f;
+            cc = 0;
+            ++cu;
+        }
+        if (it == 0) { MI_STAMP(3) }
+    }
+    MI_STAMP(4)
+    wait_vm<0>();   // the parked transfers land before the wave (and its LDS) retires
+#undef MI_STAMP
+}
+
+template <int T, int DUAL, int ROLE>
+__global__ __launch_bounds__(RING_NW * 64) void gemv_r(const float* __restrict__ kx0, const float* __restrict__ knw,
+                                                        const int* __restrict__ ktp, int kflags, const GemvParams Pk) {
+    __shared__ __attribute__((aligned(16))) u32x4 sparams[kGemvParamVecs];
+    gemv_ring_body<T, DUAL>(kx0, knw, ktp, kflags, Pk, sparams, blockIdx.x);
+}
+
+template <int T1, int T2>
+__global__ __launch_bounds__(RING_NW * 64) void gemv_r_mix(const float* __restrict__ kx0, const float* __restrict__ knw,
+                                                            const int* __restrict__ ktp, int kflags, const GemvParams P1,
+                                                            const GemvParams P2) {
+    __shared__ __attribute__((aligned(16))) u32x4 sparams[kGemvParamVecs];
+    if ((int)blockIdx.x < P1.grid) gemv_ring_body<T1, 0>(kx0, knw, ktp, kflags, P1, sparams, blockIdx.x);
+    else gemv_ring_body<T2, 0>(kx0, knw, ktp, kflags, P2, sparams, blockIdx.x - P1.grid);
+}
+
+// ---------------------------------------------------------------------------
+// The K-split GEMV (gemv_k): the decode GEMV without a workgroup-wide prologue.
+//
+// gemv_body / gemv_ring_body quantise the whole activation into LDS before any wave can
+// consume a weight: x arrives, RMSNorm (a workgroup reduction), Q8_K of every block, a
+// barrier -- 4-6 us per launch during which the weight stream is throttled (the stamp
+// timelines of profiles/r02_timeline_*.txt).  Here the waves of a workgroup split K instead:
+// G = ceil(K/2048) groups of m waves; group g streams superblocks [8g, 8g+8) of every unit the
+// workgroup owns, so each lane needs the activation of ONE 32-element slice only, for the
+// whole launch.  Every wave builds that slice itself, in registers:
+//   RMSNorm   each wave sums the squares of the full x (the same double sum in every wave, so
+//             every wave gets the bit-identical scale) -- no barrier;
+//   Q8_K      the 8 lanes of a superblock reduce its amax (and the sign of its first
+//             maximal element, ggml's tie rule) by DPP; each lane quantises its own 32 values
+//             and forms its own two 16-element bsums, exactly as quantize_row_q8_K_ref;
+//   Q8_0      a lane owns a whole 32-block (quantize_row_q8_0's x86 form), no reduction.
+// The weight ring is issued right after the parameter block arrives and the slice math runs
+// while it is in flight.  A unit's G chunk partials meet in LDS and are added in chunk order
+// (deterministic) by the epilogue threads after one barrier at the end.
+// ---------------------------------------------------------------------------
+template <int T> struct KAct;
+// Q8_K element positions of lane j within its superblock (Kq<T>::act's slices): two runs of 16
+__device__ __forceinline__ int kpos_lo_q45(int j) { return 64 * (j >> 1) + 16 * (j & 1); }
+__device__ __forceinline__ int kpos_lo_q6(int j) { return 128 * (j >> 2) + 32 * ((j >> 1) & 1) + 16 * (j & 1); }
+
+// max over the 8 lanes of a lane group (lanes 8k..8k+7), every lane gets it
+__device__ __forceinline__ float max8(float v) {
+    v = fmaxf(v, __int_as_float(dpp_i<0xB1, 0xf>(__float_as_int(v))));   // quad_perm [1,0,3,2]
+    v = fmaxf(v, __int_as_float(dpp_i<0x4E, 0xf>(__float_as_int(v))));   // quad_perm [2,3,0,1]
+    v = fmaxf(v, __int_as_float(dpp_i<0x141, 0xf>(__float_as_int(v))));  // row_half_mirror
+    return v;
+}
+__device__ __forceinline__ int min8(int v) {
+    v = min(v, dpp_i<0xB1, 0xf>(v));
+    v = min(v, dpp_i<0x4E, 0xf>(v));
+    v = min(v, dpp_i<0x141, 0xf>(v));
+    return v;
+}
+
+// quantize_row_q8_K_ref on one 256-block held as 32 values per lane by 8 lanes: lo[16] are
+// elements plo..plo+15 and hi[16] elements phi..phi+15 (plo < phi).  Returns this lane's
+// packed int8 values and bsums, and the block's d.
+__device__ __forceinline__ void q8k_slice(const float lo[16], const float hi[16], int plo, int phi, i32x4& alo,
+                                          i32x4& ahi, int& bs_lo, int& bs_hi, float& dx) {
+    float am = 0.0f;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) am = fmaxf(am, fmaxf(fabsf(lo[e]), fabsf(hi[e])));
+    const float amax = max8(am);
+    int q[32];
+    if (amax == 0.0f) {
+#pragma unroll
+        for (int e = 0; e < 32; ++e) q[e] = 0;
+        dx = 0.0f;
+    } else {
+        // the signed value at the FIRST index whose |x| is the maximum: key = 2*index + sign
+        int key = 1 << 20;
+#pragma unroll
+        for (int e = 15; e >= 0; --e)
+            if (fabsf(hi[e]) == amax) key = 2 * (phi + e) + (hi[e] < 0.0f ? 1 : 0);
+#pragma unroll
+        for (int e = 15; e >= 0; --e)
+            if (fabsf(lo[e]) == amax) key = 2 * (plo + e) + (lo[e] < 0.0f ? 1 : 0);
+        key = min8(key);
+        const float mx = (key & 1) ? -amax : amax;
+        const float iscale = -127.0f / mx;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            q[e] = min(127, (int)rintf(iscale * lo[e]));
+            q[16 + e] = min(127, (int)rintf(iscale * hi[e]));
+        }
+        dx = 1.0f / iscale;
+    }
+    int sl = 0, sh = 0;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+        sl += q[e];
+        sh += q[16 + e];
+    }
+    bs_lo = sl;
+    bs_hi = sh;
+    int pk[8];
+#pragma unroll
+    for (int w = 0; w < 8; ++w)
+        pk[w] = (q[4 * w] & 0xFF) | ((q[4 * w + 1] & 0xFF) << 8) | ((q[4 * w + 2] & 0xFF) << 16) | ((q[4 * w + 3] & 0xFF) << 24);
+    alo = i32x4{pk[0], pk[1], pk[2], pk[3]};
+    ahi = i32x4{pk[4], pk[5], pk[6], pk[7]};
+}
+
+template <> struct KAct<T_Q4_K> {
+    __device__ static void pos(int j, int& lo, int& hi) { lo = kpos_lo_q45(j); hi = lo + 32; }
+    __device__ static Kq<T_Q4_K>::AR quant(const float lo[16], const float hi[16], int j) {
+        int plo, phi;
+        pos(j, plo, phi);
+        Kq<T_Q4_K>::AR r;
+        q8k_slice(lo, hi, plo, phi, r.alo, r.ahi, r.bs_lo, r.bs_hi, r.dx);
+        return r;
+    }
+};
+template <> struct KAct<T_Q5_K> {
+    __device__ static void pos(int j, int& lo, int& hi) { KAct<T_Q4_K>::pos(j, lo, hi); }
+    __device__ static Kq<T_Q5_K>::AR quant(const float lo[16], const float hi[16], int j) {
+        return KAct<T_Q4_K>::quant(lo, hi, j);
+    }
+};
+template <> struct KAct<T_Q6_K> {
+    __device__ static void pos(int j, int& lo, int& hi) { lo = kpos_lo_q6(j); hi = lo + 64; }
+    __device__ static Kq<T_Q6_K>::AR quant(const float lo[16], const float hi[16], int j) {
+        int plo, phi;
+        pos(j, plo, phi);
+        Kq<T_Q6_K>::AR r;
+        q8k_slice(lo, hi, plo, phi, r.alo, r.ahi, r.bs_lo, r.bs_hi, r.dx);
+        return r;
+    }
+};
+template <> struct KAct<T_Q8_0> {   // lane j: elements 32j..32j+31 = one Q8_0 block
+    __device__ static void pos(int j, int& lo, int& hi) { lo = 32 * j; hi = lo + 16; }
+    __device__ static Kq<T_Q8_0>::AR quant(const float lo[16], const float hi[16], int) {
+        float am = 0.0f;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) am = fmaxf(am, fmaxf(fabsf(lo[e]), fabsf(hi[e])));
+        const float d = am / 127.0f;
+        const float id = am != 0.0f ? 127.0f / am : 0.0f;
+        int pk[8];
+#pragma unroll
+        for (int w = 0; w < 8; ++w) {
+            const float* src = w < 4 ? lo + 4 * w : hi + 4 * (w - 4);
+            int q0 = (int)rintf(src[0] * id), q1 = (int)rintf(src[1] * id), q2 = (int)rintf(src[2] * id),
+                q3 = (int)rintf(src[3] * id);
+            pk[w] = (q0 & 0xFF) | ((q1 & 0xFF) << 8) | ((q2 & 0xFF) << 16) | ((q3 & 0xFF) << 24);
+        }
+        Kq<T_Q8_0>::AR r;
+        r.a0 = i32x4{pk[0], pk[1], pk[2], pk[3]};
+        r.a1 = i32x4{pk[4], pk[5], pk[6], pk[7]};
+        r.d0 = __half2float(__float2half_rn(d));
+        return r;
+    }
+};
+
+// K-split geometry: G chunk groups of m waves, NW = G*m <= 8 (two waves a SIMD: the
+// prologue's x slices and the ring need the 256-VGPR budget)
+__host__ __device__ inline int gemv_k_groups(int K) { return (K / 256 + 7) / 8; }
+__host__ __device__ inline int gemv_k_waves(int K) {
+    const int G = gemv_k_groups(K);
+    return G * (8 / G);
+}
+template <int T> struct KRingD { static constexpr int D = 4; };   // register ring depth
+
+// LDS: [params copy (static)] [rope table | resid | partials[wg_units][G] float2]
+struct KPlan { int rope_off, resid_off, part_off, total; };
+__host__ __device__ inline KPlan kplan(const GemvParams& p) {
+    KPlan k;
+    k.rope_off = 0;
+    k.resid_off = ((p.n_rot / 2) * 8 + 15) / 16 * 16;
+    k.part_off = k.resid_off + ((p.wg_units * 2 * 4 + 15) / 16) * 16;
+    k.total = k.part_off + p.wg_units * gemv_k_groups(p.K) * 8;
+    k.total = (k.total + 15) & ~15;   // then [16] doubles of RMSNorm shares (the kernel's red[])
+    return k;
+}
+
+__device__ __forceinline__ void k_load_slice(const float* __restrict__ p, int e0, int e1, float lo[16], float hi[16]) {
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+        const f32x4 a = *gptr(reinterpret_cast<const f32x4*>(p + e0) + v);
+        const f32x4 b = *gptr(reinterpret_cast<const f32x4*>(p + e1) + v);
+        lo[4 * v] = a.x; lo[4 * v + 1] = a.y; lo[4 * v + 2] = a.z; lo[4 * v + 3] = a.w;
+        hi[4 * v] = b.x; hi[4 * v + 1] = b.y; hi[4 * v + 2] = b.z; hi[4 * v + 3] = b.w;
+    }
+}
+
+// This wave's share of ggml_compute_forward_rms_norm_f32's sum of squares: float4 i of x for
+// i = lane + 64*(wave + NW*r); KX_PART float4 a lane are loaded at kernel entry (K <= 8192 at 8
+// waves), the rest (larger K) after.  The shares meet in LDS in wave order.
+constexpr int KX_PART = 4;
+
+// kflags: K (bits 0-19) | RMSNorm prologue (21) | attention-combine prologue (22); for the
+// attention prologue kx0 is split 0 of the attention partials.
+template <int T, int D, int DUAL>
+__device__ __forceinline__ void gemv_k_body(const float* __restrict__ kx0, const float* __restrict__ knw,
+                                            const int* __restrict__ ktp, int kflags, const GemvParams& Pk,
+                                            u32x4* sparams, const int bid) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    using K = Kq<T>;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int NW = blockDim.x >> 6;
+    const int Kdim = kflags & 0xFFFFF;
+    const int nb = Kdim >> 8;
+    const int G = (nb + 7) >> 3;
+    const int m = NW / G;
+    const int g = wave / m, wk = wave - g * m;
+    const int sbl = lane >> 3, j = lane & 7;
+    const int sb = 8 * g + sbl;
+    const bool lv = sb < nb;
+    const bool rms = (kflags >> 21) & 1;
+    const bool attn_pro = (kflags >> 22) & 1;
+    int plo, phi;
+    KAct<T>::pos(j, plo, phi);
+    const int xe0 = (lv ? sb : 0) * 256 + plo, xe1 = (lv ? sb : 0) * 256 + phi;
+    // ---- entry: loads that need only the direct arguments (this lane's activation slice of
+    // slot 0, its norm weights, this wave's share of the RMSNorm sum, the token position) and
+    // the parameter block: one round trip for all of them
+    float xlo[16], xhi[16], wlo[16], whi[16];
+    k_load_slice(kx0, xe0, xe1, xlo, xhi);
+    if (rms) k_load_slice(knw, xe0, xe1, wlo, whi);
+    f32x4 xr[KX_PART];
+    const int n4 = Kdim / 4;
+    if (rms) {
+        const auto x4 = gptr(reinterpret_cast<const f32x4*>(kx0));
+#pragma unroll
+        for (int r = 0; r < KX_PART; ++r) {
+            const int i = lane + 64 * (wave + NW * r);
+            xr[r] = i < n4 ? x4[i] : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+    }
+    const i32x4 tp = ktp ? *gptr(reinterpret_cast<const i32x4*>(ktp)) : i32x4{0, 0, 0, 0};
+    {
+        const u32x4* src = reinterpret_cast<const u32x4*>(&Pk);
+        for (int i = threadIdx.x; i < kGemvParamVecs; i += blockDim.x) sparams[i] = src[i];
+        __syncthreads();
+    }
+    const GemvParams& P = *reinterpret_cast<const GemvParams*>(sparams);
+#ifdef MI_STAMPS   // diagnostic build only (scripts/timeline.py)
+#define MI_STAMP(k) \
+    if (P.stamps && threadIdx.x == 0) P.stamps[bid * 8 + (k)] = __builtin_amdgcn_s_memrealtime();
+#else
+#define MI_STAMP(k)
+#endif
+    MI_STAMP(0)
+    const KPlan KP = kplan(P);
+    double* red = reinterpret_cast<double*>(smem + KP.total);   // [NW] RMSNorm shares
+    int e0 = 0, e1 = 0;
+    float w0 = 0.0f, w1 = 0.0f;
+    if (P.sel) {   // MoE: the experts decide the weight addresses
+        e0 = __builtin_amdgcn_readfirstlane(gptr(P.sel)[0]);
+        e1 = __builtin_amdgcn_readfirstlane(gptr(P.sel)[1]);
+        w0 = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(gptr(P.selw)[0])));
+        w1 = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(gptr(P.selw)[1])));
+    }
+    int wg_u0, wg_u1;
+    unit_range(P.total_units, P.grid, bid, wg_u0, wg_u1);
+    const int nwu = wg_u1 - wg_u0;
+    const int u0 = wg_u0 + (int)(((unsigned)nwu * (unsigned)wk) / (unsigned)m);
+    const int u1 = wg_u0 + (int)(((unsigned)nwu * (unsigned)(wk + 1)) / (unsigned)m);
+    const int n_items = u1 - u0;
+    // attention splits past the first (contexts over ATTN_SHORT cells): added in split order
+    // before the prefetch -- a load issued behind it would wait for all of it
+    if (attn_pro) {
+        int chunk_, nsplit;
+        attn_split(__builtin_amdgcn_readfirstlane(tp.z) + 1, chunk_, nsplit);
+        const AttnPartials& A = P.attn;
+        for (int s = 1; s < nsplit; ++s) {
+            float lo[16], hi[16];
+            k_load_slice(A.o + (long long)s * A.n_head * A.head_dim, xe0, xe1, lo, hi);
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                xlo[e] += lo[e];
+                xhi[e] += hi[e];
+            }
+        }
+    }
+    // the other inputs of the prologue, issued before the prefetch, consumed after it
+    float ylo[16], yhi[16];
+    if (DUAL) k_load_slice(P.x[1], xe0, xe1, ylo, yhi);
+    const bool rope_wave = P.n_rot > 0 && wave == NW - 1;
+    float ff0 = 1.0f, ff1 = 1.0f;
+    if (rope_wave && P.freq_factors) {
+        if (lane < P.n_rot / 2) ff0 = gptr(P.freq_factors)[lane];
+        if (lane + 64 < P.n_rot / 2) ff1 = gptr(P.freq_factors)[lane + 64];
+    }
+    // this wave's RMSNorm share (its x arrived with the parameter block)
+    if (rms) {
+        double sacc = 0.0;
+#pragma unroll
+        for (int r = 0; r < KX_PART; ++r) {
+            const f32x4 v = xr[r];
+            sacc += (double)(v.x * v.x);
+            sacc += (double)(v.y * v.y);
+            sacc += (double)(v.z * v.z);
+            sacc += (double)(v.w * v.w);
+        }
+        sacc = wave_sum63_d(sacc);
+        if (lane == 63) red[wave] = sacc;
+    }
+
+    // ---- the weight prefetch
+    struct Slot { typename K::Ld a, b; };
+    Slot ring[D];
+    int iu = u0;
+    const uint8_t* pa[4] = {nullptr, nullptr, nullptr, nullptr};
+    const uint8_t* pb[4] = {nullptr, nullptr, nullptr, nullptr};
+    int fast_end = 0, step_rows = 0;
+    auto bases = [&](int u) {
+        const UnitRef c = unit_ref(P, u);
+        const GemvSeg& S = P.seg[c.si];
+        const QMat& MB = S.pair == PAIR_ADJ ? S.A : S.B;
+        const long long ea = S.expA == 0 ? e0 : S.expA == 1 ? e1 : 0;
+        const long long eb = S.expB == 0 ? e0 : S.expB == 1 ? e1 : 0;
+        const long long rb = c.hasB ? c.rb : c.ra;   // odd tail: re-read row A, result unused
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            pa[i] = rfl_ptr(S.A.p[i] + ea * S.A.expert_stride[i] + c.ra * nb * PlaneBytes<T>::b[i]);
+            pb[i] = rfl_ptr(MB.p[i] + eb * MB.expert_stride[i] + rb * nb * PlaneBytes<T>::b[i]);
+        }
+        const int pair = __builtin_amdgcn_readfirstlane(S.pair);
+        const int end = __builtin_amdgcn_readfirstlane(S.unit0 + S.units);
+        const int rows = __builtin_amdgcn_readfirstlane(S.A.rows);
+        step_rows = pair == PAIR_ADJ ? 2 : 1;
+        fast_end = (pair == PAIR_ADJ && (rows & 1)) ? end - 1 : end;
+    };
+    auto next_unit = [&](int u) {
+        if (u < fast_end) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const long long d = (long long)step_rows * nb * PlaneBytes<T>::b[i];
+                pa[i] += d;
+                pb[i] += d;
+            }
+        } else {
+            bases(u);
+        }
+    };
+    bases(u0 < P.total_units ? u0 : P.total_units - 1);
+    // past the end of its range a wave re-issues its last item (cache hits) so every ring step
+    // issues the same loads and hipcc's vmcnt bookkeeping stays exact
+    const int sbi = lv ? sb : nb - 1;
+    auto issue = [&](Slot& S) {
+        S.a = K::load(pa, sbi, j);
+        S.b = K::load(pb, sbi, j);
+        if (iu + 1 < u1) next_unit(++iu);
+    };
+#pragma unroll
+    for (int k = 0; k < D - 1; ++k) issue(ring[k]);
+    MI_STAMP(1)
+    // residual values of this workgroup's units: needed only by the epilogue threads
+    float ra = 0.0f, rbv = 0.0f;
+    const bool has_resid = P.seg[0].resid && (int)threadIdx.x < nwu;
+    if (has_resid) {
+        const GemvSeg& S0 = P.seg[0];
+        const long long lu = wg_u0 + threadIdx.x;
+        if (S0.pair == PAIR_ADJ) {
+            ra = gptr(S0.resid)[2 * lu];
+            rbv = gptr(S0.resid)[2 * lu + 1 < S0.A.rows ? 2 * lu + 1 : 2 * lu];
+        } else {
+            ra = gptr(S0.resid)[lu];
+            rbv = gptr(S0.resid)[lu];
+        }
+    }
+    // ---- the activation slice, while the prefetch is in flight
+    typename K::AR arA, arB;
+    {
+        if (rms) {
+            __syncthreads();   // every wave's RMSNorm share is in LDS (loads stay in flight)
+            double tot = 0.0;
+            for (int w = 0; w < NW; ++w) tot += red[w];
+            if (n4 > 64 * NW * KX_PART) {   // K > 8192 at 8 waves: the rest of the sum (rare)
+                const auto x4 = gptr(reinterpret_cast<const f32x4*>(kx0));
+                double sacc = 0.0;
+                for (int i = lane + 64 * NW * KX_PART; i < n4; i += 64) {
+                    const f32x4 v = x4[i];
+                    sacc += (double)(v.x * v.x);
+                    sacc += (double)(v.y * v.y);
+                    sacc += (double)(v.z * v.z);
+                    sacc += (double)(v.w * v.w);
+                }
+                sacc = wave_sum63_d(sacc);
+                const long long b = __double_as_longlong(sacc);
+                const int lo = __builtin_amdgcn_readlane((int)b, 63), hi = __builtin_amdgcn_readlane((int)(b >> 32), 63);
+                tot += __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+            }
+            const float mean = (float)(tot / (double)Kdim);
+            const float scale = 1.0f / sqrtf(mean + P.eps);
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                xlo[e] = (xlo[e] * scale) * wlo[e];   // ggml_vec_scale_f32 then ggml_mul
+                xhi[e] = (xhi[e] * scale) * whi[e];
+            }
+        }
+        if (!lv) {
+#pragma unroll
+            for (int e = 0; e < 16; ++e) xlo[e] = xhi[e] = 0.0f;
+        }
+        arA = KAct<T>::quant(xlo, xhi, j);
+        if (DUAL) {
+            if (!lv) {
+#pragma unroll
+                for (int e = 0; e < 16; ++e) ylo[e] = yhi[e] = 0.0f;
+            }
+            arB = KAct<T>::quant(ylo, yhi, j);
+        } else {
+            arB = arA;
+        }
+    }
+    const int pos = __builtin_amdgcn_readfirstlane(tp.y);
+    const int cell = __builtin_amdgcn_readfirstlane(tp.z);
+    float* rope = reinterpret_cast<float*>(smem + KP.rope_off);
+    float* rs = reinterpret_cast<float*>(smem + KP.resid_off);
+    float2* part = reinterpret_cast<float2*>(smem + KP.part_off);
+    if (rope_wave) {   // ggml_rope_cache_init for this token's position (the epilogue reads it)
+        for (int i = lane; i < P.n_rot / 2; i += 64) {
+            float theta = (float)pos;
+            for (int k = 0; k < i; ++k) theta = theta * P.theta_scale;
+            const float ff = i < 64 ? ff0 : ff1;
+            const float th = P.freq_scale * (theta / ff);
+            rope[2 * i] = cosf(th);
+            rope[2 * i + 1] = sinf(th);
+        }
+    }
+    MI_STAMP(7)
+    // ---- the stream: one item (this chunk of one unit's two rows) per unit
+    int cu = u0;
+    auto consume = [&](const Slot& S) {
+        const float pa_ = K::dot(S.a, arA, j);
+        const float pb_ = K::dot(S.b, arB, j);
+        const float yA = wave_sum63(lv ? pa_ : 0.0f);
+        const float yB = wave_sum63(lv ? pb_ : 0.0f);
+        if (lane == 63) part[(cu - wg_u0) * G + g] = make_float2(yA, yB);
+        ++cu;
+    };
+    for (int base = 0; base < n_items; base += D) {
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+            issue(ring[(k + D - 1) % D]);
+            if (base + k < n_items) consume(ring[k]);
+        }
+        if (base == 0) { MI_STAMP(3) }
+    }
+    if (has_resid) {
+        rs[2 * threadIdx.x] = ra;
+        rs[2 * threadIdx.x + 1] = rbv;
+    }
+    __syncthreads();
+    MI_STAMP(2)
+    // ---- epilogue: one thread per unit adds its G chunk partials in chunk order
+    const EpiConst EC = epi_const(P);
+    for (int i = threadIdx.x; i < nwu; i += blockDim.x) {
+        const int u = wg_u0 + i;
+        float yA = 0.0f, yB = 0.0f;
+        for (int q = 0; q < G; ++q) {
+            const float2 v = part[i * G + q];
+            yA += v.x;
+            yB += v.y;
+        }
+        int si = 0;
+        while (si + 1 < P.nseg && u >= P.seg[si + 1].unit0) ++si;
+        const GemvSeg& S = P.seg[si];
+        EpiSeg es;
+        es.out = S.out;
+        es.epi = S.epi;
+        es.pair = S.pair;
+        es.unit0 = S.unit0;
+        es.end = S.unit0 + S.units;
+        es.rows = S.A.rows;
+        gemv_epilogue(EC, es, u, rope, rs[2 * i], rs[2 * i + 1], w0, w1, pos, cell, yA, yB);
+    }
+    MI_STAMP(4)
+#undef MI_STAMP
+}
+
+template <int T, int DUAL, int ROLE>
+__global__ __launch_bounds__(512) void gemv_k(const float* __restrict__ kx0, const float* __restrict__ knw,
+                                               const int* __restrict__ ktp, int kflags, const GemvParams Pk) {
+    __shared__ __attribute__((aligned(16))) u32x4 sparams[kGemvParamVecs];
+    gemv_k_body<T, KRingD<T>::D, DUAL>(kx0, knw, ktp, kflags, Pk, sparams, blockIdx.x);
+}
+
+template <int T1, int T2>
+__global__ __launch_bounds__(512) void gemv_k_mix(const float* __restrict__ kx0, const float* __restrict__ knw,
+                                                   const int* __restrict__ ktp, int kflags, const GemvParams P1,
+                                                   const GemvParams P2) {
+    __shared__ __attribute__((aligned(16))) u32x4 sparams[kGemvParamVecs];
+    if ((int)blockIdx.x < P1.grid) gemv_k_body<T1, KRingD<T1>::D, 0>(kx0, knw, ktp, kflags, P1, sparams, blockIdx.x);
+    else gemv_k_body<T2, KRingD<T2>::D, 0>(kx0, knw, ktp, kflags, P2, sparams, blockIdx.x - P1.grid);
+}
+
 typedef void (*GemvFn)(const float*, const float*, const int*, int, const GemvParams);
 typedef void (*GemvMixFn)(const float*, const float*, const int*, int, const GemvParams, const GemvParams);
 
@@ -1061,35 +1866,107 @@ template <int T, int D> __global__ void gemm_t(const GemmParams P);
 static void gemm_attrs();
 static GemvMixFn gemv_mix_fn(int t1, int t2);
 
+// Decode GEMV implementation: MI_GEMV=k (default: the K-split gemv_k), ring (the LDS-DMA ring
+// gemv_r), reg (the register ring gemv_t with a workgroup prologue) -- A/B switches.
+enum GemvImpl { GEMV_REG = 0, GEMV_RING = 1, GEMV_KSPLIT = 2 };
+static int gemv_impl() {
+    static const int impl = [] {
+        const char* e = getenv("MI_GEMV");
+        if (getenv("MI_GEMV_REG")) return (int)GEMV_REG;
+        if (!e || !*e || !strcmp(e, "k")) return (int)GEMV_KSPLIT;
+        if (!strcmp(e, "ring")) return (int)GEMV_RING;
+        return (int)GEMV_REG;
+    }();
+    return impl;
+}
+static bool gemv_ring_on() { return gemv_impl() == GEMV_RING; }
+static bool gemv_k_on(int K) { return gemv_impl() == GEMV_KSPLIT && gemv_k_groups(K) <= 8; }
+
+template <int DUAL, int ROLE>
+static GemvFn gemv_k_fn_t(int type) {
+    switch (type) {
+    case T_Q4_K: return gemv_k<T_Q4_K, DUAL, ROLE>;
+    case T_Q5_K: return gemv_k<T_Q5_K, DUAL, ROLE>;
+    case T_Q6_K: return gemv_k<T_Q6_K, DUAL, ROLE>;
+    case T_Q8_0: return gemv_k<T_Q8_0, DUAL, ROLE>;
+    default: return nullptr;
+    }
+}
+static GemvFn gemv_k_fn(int role, int type, int nslots) {
+    if (nslots > 1) return gemv_k_fn_t<1, 2>(type);
+    return role == ROLE_FFN_UP ? gemv_k_fn_t<0, 1>(type) : gemv_k_fn_t<0, 0>(type);
+}
+static GemvMixFn gemv_k_mix_fn(int t1, int t2) {
+    if (t1 == T_Q4_K && t2 == T_Q6_K) return gemv_k_mix<T_Q4_K, T_Q6_K>;
+    if (t1 == T_Q5_K && t2 == T_Q6_K) return gemv_k_mix<T_Q5_K, T_Q6_K>;
+    return nullptr;
+}
+
+template <int DUAL, int ROLE>
+static GemvFn gemv_r_fn_t(int type) {
+    switch (type) {
+    case T_Q4_K: return gemv_r<T_Q4_K, DUAL, ROLE>;
+    case T_Q5_K: return gemv_r<T_Q5_K, DUAL, ROLE>;
+    case T_Q6_K: return gemv_r<T_Q6_K, DUAL, ROLE>;
+    case T_Q8_0: return gemv_r<T_Q8_0, DUAL, ROLE>;
+    default: return nullptr;
+    }
+}
+static GemvFn gemv_r_fn(int role, int type, int nslots) {
+    if (nslots > 1) return gemv_r_fn_t<1, 2>(type);
+    return role == ROLE_FFN_UP ? gemv_r_fn_t<0, 1>(type) : gemv_r_fn_t<0, 0>(type);
+}
+static GemvMixFn gemv_r_mix_fn(int t1, int t2) {
+    if (t1 == T_Q4_K && t2 == T_Q6_K) return gemv_r_mix<T_Q4_K, T_Q6_K>;
+    if (t1 == T_Q5_K && t2 == T_Q6_K) return gemv_r_mix<T_Q5_K, T_Q6_K>;
+    return nullptr;
+}
+
 void init_kernel_attributes() {
     gemm_attrs();
     const int types[4] = {T_Q4_K, T_Q5_K, T_Q6_K, T_Q8_0};
     for (int r : {ROLE_GENERIC, ROLE_FFN_UP})
         for (int t : types)
-            for (int nsl = 1; nsl <= 2; ++nsl)
+            for (int nsl = 1; nsl <= 2; ++nsl) {
                 for (int c = 0; c < kNumGemvCfgs; ++c)
                     MI_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(gemv_fn(r, t, nsl, c)),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, kGemvDynLds));
-    for (int t1 : {T_Q4_K, T_Q5_K})
+                MI_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(gemv_r_fn(r, t, nsl)),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, kGemvDynLds));
+            }
+    for (int t1 : {T_Q4_K, T_Q5_K}) {
         MI_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(gemv_mix_fn(t1, T_Q6_K)),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, kGemvDynLds));
+        MI_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(gemv_r_mix_fn(t1, T_Q6_K)),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, kGemvDynLds));
+    }
 }
 
 // Units one workgroup owns at most (its residual staging in LDS).
 static int wg_units_max(int total_units, int grid) { return (total_units + grid - 1) / grid + 1; }
 
 size_t gemv_smem_bytes(const GemvParams& p) { return (size_t)smem_plan(p).total; }
+// the LDS-DMA ring kernel: prologue plan, then the rings
+static size_t gemv_r_smem_bytes(const GemvParams& p) {
+    return (((size_t)smem_plan(p).total + 15) & ~(size_t)15) + (size_t)ring_bytes(p.seg[0].A.type);
+}
+
+static int gemv_waves(int type, int role, int K) {
+    if (gemv_k_on(K)) return gemv_k_waves(K);
+    return gemv_ring_on() ? RING_NW : kGemvCfgs[gemv_cfg_for(type, role)].nw;
+}
 
 int gemv_default_grid(const GemvParams& p, int role) {
-    // One workgroup per CU (256 CUs): the per-workgroup prologue (activation
-    // quantisation) is paid once per CU.  Small launches use fewer workgroups
-    // so that every wave still gets a unit.
-    const int nw = kGemvCfgs[gemv_cfg_for(p.seg[0].A.type, role)].nw;
-    const int g = (p.total_units + nw - 1) / nw;
+    // One workgroup per CU (256 CUs).  Small launches use fewer workgroups so that every
+    // wave (of a K group, for gemv_k) still gets a unit.
+    int per = gemv_waves(p.seg[0].A.type, role, p.K);
+    if (gemv_k_on(p.K)) per /= gemv_k_groups(p.K);
+    const int g = (p.total_units + per - 1) / per;
     return g < 1 ? 1 : (g > 256 ? 256 : g);
 }
 
-// Validates a launch and fixes its grid-dependent fields; returns the kernel configuration.
+// Validates a launch and fixes its grid-dependent fields; returns the kernel configuration
+// (register ring), -1 (LDS-DMA ring) or -2 (K-split).
 static int gemv_prepare(GemvParams& p, int role, int grid) {
     if (p.K % 256 != 0) throw Error("gemv: K must be a multiple of 256");
     const int type = p.seg[0].A.type;
@@ -1098,38 +1975,61 @@ static int gemv_prepare(GemvParams& p, int role, int grid) {
             throw Error("gemv: all matrices of one launch must share a quant type");
     if (p.pro == PRO_ATTN && (p.attn.n_head * p.attn.head_dim != p.K || p.attn.head_dim % 4 != 0))
         throw Error("gemv: attention combine needs K == n_head*head_dim");
-    const int cfg = gemv_cfg_for(type, role);
+    const bool kk = gemv_k_on(p.K);
+    const int cfg = kk ? -2 : gemv_ring_on() ? -1 : gemv_cfg_for(type, role);
+    const int nw = gemv_waves(type, role, p.K);
     if (grid <= 0) grid = gemv_default_grid(p, role);
-    if ((long long)p.total_units * grid * kGemvCfgs[cfg].nw >= (1LL << 32))
+    if ((long long)p.total_units * grid * nw >= (1LL << 32))
         throw Error("gemv: too many units for the 32-bit unit split");
     p.wg_units = wg_units_max(p.total_units, grid);
     p.grid = grid;
     for (int i = 0; i < p.nseg; ++i)
-        if (p.seg[i].resid && (p.nseg != 1 || p.wg_units > kGemvCfgs[cfg].nw * 64))
+        if (p.seg[i].resid && (p.nseg != 1 || p.wg_units > nw * 64))
             throw Error("gemv: residual launches must have one segment and <= 64*NW units per workgroup");
-    if (gemv_smem_bytes(p) > (size_t)kGemvDynLds) throw Error("gemv: activation too large for LDS");
+    const size_t lds = kk ? (size_t)kplan(p).total : cfg < 0 ? gemv_r_smem_bytes(p) : gemv_smem_bytes(p);
+    if (lds > (size_t)kGemvDynLds) throw Error("gemv: activation too large for LDS");
     return cfg;
 }
 
 // leading arguments: K | flags (activation kept in registers, RMSNorm prologue)
-static int gemv_kflags(const GemvParams& p, int cfg) {
+static int gemv_kflags(const GemvParams& p, int nw) {
     const int nb = p.K / 256;
-    const bool regs = p.pro != PRO_ATTN && p.nslots == 1 && nb <= PRO_MAXB * kGemvCfgs[cfg].nw;
+    const bool regs = p.pro != PRO_ATTN && p.nslots == 1 && nb <= PRO_MAXB * nw;
     const bool rms = p.pro == PRO_RMSNORM;
     return p.K | (regs ? 1 << 20 : 0) | (rms ? 1 << 21 : 0);
 }
+
+// gemv_k's leading arguments: K | RMSNorm (bit 21) | attention combine (bit 22); kx0 is the
+// activation, or split 0 of the attention partials
+static int gemv_k_kflags(const GemvParams& p) {
+    return p.K | (p.pro == PRO_RMSNORM ? 1 << 21 : 0) | (p.pro == PRO_ATTN ? 1 << 22 : 0);
+}
+static const float* gemv_k_x0(const GemvParams& p) { return p.pro == PRO_ATTN ? p.attn.o : p.x[0]; }
 
 void launch_gemv(const GemvParams& p_in, int role, int grid, hipStream_t s, hipEvent_t ev_start,
                  hipEvent_t ev_stop) {
     GemvParams p = p_in;
     const int cfg = gemv_prepare(p, role, grid);
     const int type = p.seg[0].A.type;
-    const size_t smem = gemv_smem_bytes(p);
-    GemvFn fn = gemv_fn(role, type, p.nslots, cfg);
-    if (!fn) throw Error("gemv: unsupported quant type");
-    const dim3 block(kGemvCfgs[cfg].nw * 64);
-    const int kflags = gemv_kflags(p, cfg);
+    GemvFn fn;
+    size_t smem;
+    int nw, kflags;
     const float* kx0 = p.x[0];
+    if (cfg == -2) {
+        fn = gemv_k_fn(role, type, p.nslots);
+        smem = (size_t)kplan(p).total + 16 * sizeof(double);
+        nw = gemv_k_waves(p.K);
+        kflags = gemv_k_kflags(p);
+        kx0 = gemv_k_x0(p);
+    } else {
+        const bool ring = cfg < 0;
+        smem = ring ? gemv_r_smem_bytes(p) : gemv_smem_bytes(p);
+        fn = ring ? gemv_r_fn(role, type, p.nslots) : gemv_fn(role, type, p.nslots, cfg);
+        nw = ring ? RING_NW : kGemvCfgs[cfg].nw;
+        kflags = gemv_kflags(p, nw);
+    }
+    if (!fn) throw Error("gemv: unsupported quant type");
+    const dim3 block(nw * 64);
     const float* knw = p.pro == PRO_RMSNORM ? p.norm_w : nullptr;
     const int* ktp = p.tokpos;
     if (ev_start || ev_stop)
@@ -1147,13 +2047,17 @@ static GemvMixFn gemv_mix_fn(int t1, int t2) {
 }
 
 bool gemv_mix_supported(int t1, int t2, int role) {
+    if (gemv_impl() == GEMV_KSPLIT) return gemv_k_mix_fn(t1, t2) != nullptr;
+    if (gemv_ring_on()) return gemv_r_mix_fn(t1, t2) != nullptr;
     return gemv_mix_fn(t1, t2) != nullptr && gemv_cfg_for(t1, role) == 1 && gemv_cfg_for(t2, role) == 1;
 }
 
 void launch_gemv_mix(const GemvParams& p1_in, const GemvParams& p2_in, int role, hipStream_t s) {
     GemvParams p1 = p1_in, p2 = p2_in;
     const int t1 = p1.seg[0].A.type, t2 = p2.seg[0].A.type;
-    GemvMixFn fn = gemv_mix_fn(t1, t2);
+    const bool ring = gemv_ring_on();
+    const bool kk = gemv_k_on(p1.K);
+    GemvMixFn fn = kk ? gemv_k_mix_fn(t1, t2) : ring ? gemv_r_mix_fn(t1, t2) : gemv_mix_fn(t1, t2);
     if (!fn || !gemv_mix_supported(t1, t2, role)) throw Error("gemv: unsupported type pair for a mixed launch");
     if (p1.K != p2.K || p1.pro != p2.pro || p1.x[0] != p2.x[0] || p1.norm_w != p2.norm_w || p1.tokpos != p2.tokpos ||
         p1.nslots != 1 || p2.nslots != 1)
@@ -1171,11 +2075,23 @@ void launch_gemv_mix(const GemvParams& p1_in, const GemvParams& p2_in, int role,
     const int g2 = std::min(total - g1, gemv_default_grid(p2, role));
     const int cfg = gemv_prepare(p1, role, g1);
     gemv_prepare(p2, role, g2);
-    const size_t smem = std::max(gemv_smem_bytes(p1), gemv_smem_bytes(p2));
-    const dim3 block(kGemvCfgs[cfg].nw * 64);
-    const int kflags = gemv_kflags(p1, cfg);
+    size_t smem;
+    int nw, kflags;
+    const float* kx0 = p1.x[0];
+    if (kk) {
+        smem = (size_t)std::max(kplan(p1).total, kplan(p2).total) + 16 * sizeof(double);
+        nw = gemv_k_waves(p1.K);
+        kflags = gemv_k_kflags(p1);
+        kx0 = gemv_k_x0(p1);
+    } else {
+        smem = ring ? std::max(gemv_r_smem_bytes(p1), gemv_r_smem_bytes(p2))
+                    : std::max(gemv_smem_bytes(p1), gemv_smem_bytes(p2));
+        nw = ring ? RING_NW : kGemvCfgs[cfg].nw;
+        kflags = gemv_kflags(p1, nw);
+    }
+    const dim3 block(nw * 64);
     const float* knw = p1.pro == PRO_RMSNORM ? p1.norm_w : nullptr;
-    hipLaunchKernelGGL(fn, dim3(p1.grid + p2.grid), block, smem, s, p1.x[0], knw, p1.tokpos, kflags, p1, p2);
+    hipLaunchKernelGGL(fn, dim3(p1.grid + p2.grid), block, smem, s, kx0, knw, p1.tokpos, kflags, p1, p2);
     MI_HIP(hipGetLastError());
 }
 
