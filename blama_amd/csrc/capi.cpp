@@ -165,8 +165,8 @@ uint32_t mi_n_batch(const mi_ctx* c) { return c ? c->impl->n_batch : 0; }
 int32_t mi_decode(mi_ctx* c, const int32_t* tokens, int32_t n, int32_t out_mode) {
     try {
         if (!c || !tokens) throw Error("null argument");
-        if (out_mode != MI_OUT_LAST) throw Error("decode: only MI_OUT_LAST is implemented");
-        return c->impl->decode(tokens, n);
+        if (out_mode != MI_OUT_LAST && out_mode != MI_OUT_ALL) throw Error("decode: out_mode must be MI_OUT_LAST or MI_OUT_ALL");
+        return c->impl->decode(tokens, n, out_mode == MI_OUT_ALL);
     }
     MI_TRY(-1)
 }
@@ -174,8 +174,7 @@ int32_t mi_decode(mi_ctx* c, const int32_t* tokens, int32_t n, int32_t out_mode)
 int32_t mi_topk(mi_ctx* c, int32_t row, int32_t k, int32_t* ids, float* logits) {
     try {
         if (!c || !ids || !logits) throw Error("null argument");
-        if (row != -1 && row != 0) throw Error("topk: only the last output row is kept");
-        return c->impl->topk(k, ids, logits);
+        return c->impl->topk(row, k, ids, logits);
     }
     MI_TRY(-1)
 }
@@ -183,8 +182,7 @@ int32_t mi_topk(mi_ctx* c, int32_t row, int32_t k, int32_t* ids, float* logits) 
 int32_t mi_gather(mi_ctx* c, int32_t row, const int32_t* ids, int32_t n, float* out) {
     try {
         if (!c || (n > 0 && (!ids || !out))) throw Error("null argument");
-        if (row != -1 && row != 0) throw Error("gather: only the last output row is kept");
-        return c->impl->gather(ids, n, out);
+        return c->impl->gather(row, ids, n, out);
     }
     MI_TRY(-1)
 }
@@ -192,8 +190,7 @@ int32_t mi_gather(mi_ctx* c, int32_t row, const int32_t* ids, int32_t n, float* 
 const float* mi_logits(mi_ctx* c, int32_t row) {
     try {
         if (!c) throw Error("null ctx");
-        if (row != -1 && row != 0) throw Error("logits: only the last output row is kept");
-        return c->impl->logits_host();
+        return c->impl->logits_host(row);
     }
     MI_TRY(nullptr)
 }

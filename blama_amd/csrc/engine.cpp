@@ -413,6 +413,18 @@ Ctx::Ctx(Model* model, uint32_t nctx, uint32_t nbatch, uint32_t nubatch) : m(mod
         MI_HIP(hipMalloc(&q8r_q, (size_t)MMQ_NT * kmax));
         MI_HIP(hipMalloc(&q8r_d, (size_t)MMQ_NT * (kmax / 256) * sizeof(float)));
         MI_HIP(hipMalloc(&q8r_bsum, (size_t)MMQ_NT * (kmax / 16) * sizeof(int)));
+        // physical batches on mmq32: every layer matrix Q4_K / Q6_K (the output head too for
+        // batched logits of every token)
+        if (mmq_ok) {
+            for (const Layer& L : m->layers)
+                for (const QMat* q : {&L.wq, &L.wk, &L.wv, &L.wo, &L.gate, &L.up, &L.down})
+                    mmq_ok = mmq_ok && mmq32_supported(q->type);
+            out_mmq = mmq_ok && mmq32_supported(m->output.type);
+            MI_HIP(hipMalloc(&ub_q, (size_t)UB_MAX * kmax));
+            MI_HIP(hipMalloc(&ub_dT, (size_t)UB_MAX * (kmax / 256) * sizeof(float)));
+            MI_HIP(hipMalloc(&ub_bsb, (size_t)UB_MAX * (kmax / 256) * 16));
+            MI_HIP(hipMalloc(&ub_rope, (size_t)UB_MAX * std::max(1, hp.n_rot / 2) * sizeof(float2)));
+        }
     }
     MI_HIP(hipMalloc(&attn_smax, (size_t)ATTN_SMAX * hp.n_head * sizeof(float)));
     MI_HIP(hipMalloc(&attn_scores, (size_t)hp.n_head * n_ctx * sizeof(float)));
@@ -447,7 +459,8 @@ Ctx::~Ctx() {
                     (void*)topk_vals, (void*)sel, (void*)selw, (void*)gather_ids, (void*)gather_out,
                     (void*)cell_delta, (void*)move_src, (void*)part_o, (void*)attn_smax, (void*)attn_scores, (void*)stamps,
                     (void*)xb, (void*)qb, (void*)attnb, (void*)hb, (void*)tokpos_b, (void*)q8r_q,
-                    (void*)q8r_d, (void*)q8r_bsum})
+                    (void*)q8r_d, (void*)q8r_bsum, (void*)ub_q, (void*)ub_dT, (void*)ub_bsb, (void*)ub_rope,
+                    (void*)logits_all})
         if (p) hipFree(p);
     for (void* p : {(void*)h_tokpos, (void*)h_topk_ids, (void*)h_topk_vals, (void*)h_logits, (void*)h_gather,
                     (void*)h_tokpos_b})
@@ -817,20 +830,164 @@ void Ctx::decode_batch(const int32_t* tokens, int n) {
     logits_valid = true;
 }
 
-int Ctx::decode(const int32_t* tokens, int n) {
+ActQ8 Ctx::ub_act(int K, int ntok) const {
+    ActQ8 a;
+    a.q = ub_q;
+    a.dT = ub_dT;
+    a.bsb = ub_bsb;
+    a.K = K;
+    a.ntok = ntok;
+    a.npad = (ntok + 31) / 32 * 32;
+    return a;
+}
+
+// Prompt ingestion / batched verification in physical batches of up to UB_MAX tokens on the
+// int8-MFMA GEMM (mmq.hip): per layer every weight matrix is streamed once per batch; each
+// activation is quantised to Q8_K once (RMSNorm fused) and shared by the matrices that read it.
+// `all`: the output head runs over every token (rows of logits_all), else over the last one.
+void Ctx::decode_ubatch(const int32_t* tokens, int n, bool all) {
+    const HParams& hp = m->hp;
+    const float theta_scale = std::pow(hp.rope_base, -2.0f / (float)hp.n_rot);
+    const float kq_scale = 1.0f / std::sqrt((float)hp.head_dim);
+    for (int c0 = 0; c0 < n; c0 += UB_MAX) {
+        const int nt = std::min(UB_MAX, n - c0);
+        const long long slot = tokb_slot++ % kTokbRing;
+        if (slot == 0 && tokb_slot > 1) MI_HIP(hipStreamSynchronize(stream));
+        int* hpos = h_tokpos_b + slot * kBatchRows * 4;
+        for (int t = 0; t < nt; ++t) {
+            const int pos = pos_max + 1, cell = n_cells;
+            hpos[t * 4 + 0] = tokens[c0 + t];
+            hpos[t * 4 + 1] = pos;
+            hpos[t * 4 + 2] = cell;
+            hpos[t * 4 + 3] = 0;
+            h_cell_pos[cell] = pos;
+            n_cells++;
+            pos_max = pos;
+        }
+        MI_HIP(hipMemcpyAsync(tokpos_b, hpos, nt * 4 * sizeof(int), hipMemcpyHostToDevice, stream));
+        EmbedParams ep{m->tok_embd, tokpos_b, xb, hp.n_embd};
+        launch_embed_multi(ep, nt, stream);
+        launch_rope_table(tokpos_b, nt, hp.n_rot, theta_scale, hp.freq_scale, m->rope_freqs, ub_rope, stream);
+        const ActQ8 a_embd = ub_act(hp.n_embd, nt), a_ff = ub_act(hp.n_ff, nt);
+        for (int l = 0; l < hp.n_layer; ++l) {
+            const Layer& L = m->layers[l];
+            __half* kl = kcache + (size_t)l * n_ctx * kv_dim;
+            __half* vl = vcache + (size_t)l * n_ctx * kv_dim;
+            GemmParams b;
+            std::memset(&b, 0, sizeof(b));
+            b.ntok = nt;
+            b.tokpos = tokpos_b;
+            b.cell_pos = cell_pos;
+            b.head_dim = hp.head_dim;
+            b.n_rot = hp.n_rot;
+            b.kcache = kl;
+            b.vcache = vl;
+            b.kv_dim = kv_dim;
+            b.K = hp.n_embd;
+            b.out_stride = hp.n_embd;
+            // Q / K / V (+ RoPE, KV append) over one quantisation of rms_norm(x) * attn_norm
+            launch_quant_act(xb, hp.n_embd, L.attn_norm, hp.eps, a_embd, stream);
+            const QMat* mats[3] = {&L.wq, &L.wk, &L.wv};
+            const int epis[3] = {EPI_ROPE_Q, EPI_ROPE_K, EPI_V};
+            for (int i = 0; i < 3; ++i) {
+                GemmParams p = b;
+                p.A = *mats[i];
+                p.pair = PAIR_ADJ;
+                p.epi = epis[i];
+                p.out = qb;
+                launch_mmq32(p, a_embd, ub_rope, stream);
+            }
+            AttnParams a{qb, kl, vl, tokpos_b, cell_pos, attn_scores, attn_smax, attnb, hp.n_head, hp.n_head_kv,
+                         hp.head_dim, kv_dim, (int)n_ctx, kq_scale};
+            launch_attn_multi(a, nt, attnb, stream);
+            {   // output projection + residual
+                launch_quant_act(attnb, hp.n_embd, nullptr, hp.eps, a_embd, stream);
+                GemmParams p = b;
+                p.A = L.wo;
+                p.pair = PAIR_ADJ;
+                p.epi = EPI_ADD;
+                p.out = xb;
+                p.resid = xb;
+                launch_mmq32(p, a_embd, ub_rope, stream);
+            }
+            {   // FFN gate/up + SwiGLU
+                launch_quant_act(xb, hp.n_embd, L.ffn_norm, hp.eps, a_embd, stream);
+                GemmParams p = b;
+                p.A = L.gate;
+                p.B = L.up;
+                p.pair = PAIR_AB;
+                p.epi = EPI_SWIGLU;
+                p.out = hb;
+                p.out_stride = hp.n_ff;
+                launch_mmq32(p, a_embd, ub_rope, stream);
+            }
+            {   // FFN down + residual
+                launch_quant_act(hb, hp.n_ff, nullptr, hp.eps, a_ff, stream);
+                GemmParams p = b;
+                p.A = L.down;
+                p.pair = PAIR_ADJ;
+                p.epi = EPI_ADD;
+                p.K = hp.n_ff;
+                p.out = xb;
+                p.resid = xb;
+                launch_mmq32(p, a_ff, ub_rope, stream);
+            }
+        }
+        if (all) {   // final norm + output head over every token of the batch
+            launch_quant_act(xb, hp.n_embd, m->output_norm, hp.eps, a_embd, stream);
+            GemmParams p;
+            std::memset(&p, 0, sizeof(p));
+            p.A = m->output;
+            p.pair = PAIR_ADJ;
+            p.epi = EPI_STORE;
+            p.K = hp.n_embd;
+            p.ntok = nt;
+            p.tokpos = tokpos_b;
+            p.out = logits_all + (size_t)c0 * hp.n_vocab;
+            p.out_stride = hp.n_vocab;
+            launch_mmq32(p, a_embd, ub_rope, stream);
+            if (c0 + nt == n) {   // the last row also feeds `logits` and the mapped top-k
+                MI_HIP(hipMemcpyAsync(logits, logits_all + (size_t)(n - 1) * hp.n_vocab, (size_t)hp.n_vocab * sizeof(float),
+                                      hipMemcpyDeviceToDevice, stream));
+                TopkParams tp{logits, hp.n_vocab, cand, topk_ids, topk_vals, d_h_topk_ids, d_h_topk_vals};
+                launch_topk(tp, stream);
+            }
+        } else if (c0 + nt == n) {
+            enqueue_output(xb + (size_t)(nt - 1) * hp.n_embd, nullptr);
+        }
+    }
+    logits_valid = true;
+}
+
+int Ctx::decode(const int32_t* tokens, int n, bool all) {
     MI_HIP(hipSetDevice(device));
     if (n <= 0) throw Error("decode: empty batch");
     for (int i = 0; i < n; ++i)
         if (tokens[i] < 0 || tokens[i] >= m->hp.n_vocab) throw Error("decode: token id out of range");
     if (n_cells + n > (int)n_ctx) return 1;   // no KV slot (llama_decode returns 1)
+    if (all && n > (int)n_batch) throw Error("decode: MI_OUT_ALL takes at most n_batch tokens");
+    out_rows = 0;
+    topk_row = -1;
+    if (all && logits_all_cap < n) {   // every token's logits: [n_batch][n_vocab], allocated once
+        if (logits_all) MI_HIP(hipFree(logits_all));
+        logits_all = nullptr;
+        MI_HIP(hipMalloc(&logits_all, (size_t)n_batch * m->hp.n_vocab * sizeof(float)));
+        logits_all_cap = (int)n_batch;
+    }
     // prompt ingestion through the batched GEMM when the context stays within the fused
     // attention's reach (dense models; MI_NO_BATCH=1 forces token-by-token decode)
-    if (n >= 2 && batch_ok && n_cells + n <= ATTN_SHORT && prof_layer < 0) {
+    const bool fits = n >= 2 && batch_ok && n_cells + n <= ATTN_SHORT && prof_layer < 0;
+    if (fits && mmq_ok && (!all || out_mmq)) {
+        decode_ubatch(tokens, n, all);
+        if (all) out_rows = n;
+        return 0;
+    }
+    if (fits && !all) {
         decode_batch(tokens, n);
         return 0;
     }
     for (int i = 0; i < n; ++i) {
-        const bool last = i == n - 1;
+        const bool last = i == n - 1 || all;
         const int pos = pos_max + 1, cell = n_cells;
         attn_fused = cell + 1 <= ATTN_SHORT ? 1 : 0;   // this step attends over cell + 1 cells
         const long long slot = tok_slot++ % kTokRing;
@@ -864,10 +1021,14 @@ int Ctx::decode(const int32_t* tokens, int n) {
             if (!g) g = build_graph(last, -1);
             MI_HIP(hipGraphLaunch(g, stream));
         }
+        if (all)   // this token's logits -> row i
+            MI_HIP(hipMemcpyAsync(logits_all + (size_t)i * m->hp.n_vocab, logits, (size_t)m->hp.n_vocab * sizeof(float),
+                                  hipMemcpyDeviceToDevice, stream));
         h_cell_pos[cell] = pos;
         n_cells++;
         pos_max = pos;
     }
+    if (all) out_rows = n;
     logits_valid = true;
     return 0;
 }
@@ -877,9 +1038,24 @@ void Ctx::sync() {
     MI_HIP(hipStreamSynchronize(stream));
 }
 
-int Ctx::topk(int k, int32_t* ids, float* vals) {
+const float* Ctx::out_row(int row) const {
+    if (row == -1) return logits;
+    if (row < 0 || row >= std::max(out_rows, 1)) throw Error("output row out of range");
+    if (out_rows == 0) return logits;   // MI_OUT_LAST: row 0 is the last token's
+    return logits_all + (size_t)row * m->hp.n_vocab;
+}
+
+int Ctx::topk(int row, int k, int32_t* ids, float* vals) {
     if (!logits_valid) throw Error("no logits: decode a token first");
     if (k < 0 || k > TOPK_MAX) throw Error("topk: k must be in [0, 64]");
+    if (out_rows > 0 && row == out_rows - 1) row = -1;   // the last row's top-k is already computed
+    const float* src = out_row(row);
+    if (src != logits || topk_row != -1) {   // another row than the mapped buffers hold
+        MI_HIP(hipSetDevice(device));
+        TopkParams tp{src, m->hp.n_vocab, cand, topk_ids, topk_vals, d_h_topk_ids, d_h_topk_vals};
+        launch_topk(tp, stream);
+        topk_row = src == logits ? -1 : row;
+    }
     sync();
     for (int i = 0; i < k; ++i) {
         ids[i] = h_topk_ids[i];
@@ -888,25 +1064,27 @@ int Ctx::topk(int k, int32_t* ids, float* vals) {
     return k;
 }
 
-int Ctx::gather(const int32_t* ids, int n, float* out) {
+int Ctx::gather(int row, const int32_t* ids, int n, float* out) {
     if (!logits_valid) throw Error("no logits: decode a token first");
+    const float* src = out_row(row);
     if (n < 0 || n > 4096) throw Error("gather: n must be in [0, 4096]");
     for (int i = 0; i < n; ++i)
         if (ids[i] < 0 || ids[i] >= m->hp.n_vocab) throw Error("gather: id out of range");
     if (n == 0) return 0;
     MI_HIP(hipSetDevice(device));
     MI_HIP(hipMemcpyAsync(gather_ids, ids, n * sizeof(int), hipMemcpyHostToDevice, stream));
-    launch_gather(logits, gather_ids, n, gather_out, stream);
+    launch_gather(src, gather_ids, n, gather_out, stream);
     MI_HIP(hipMemcpyAsync(h_gather, gather_out, n * sizeof(float), hipMemcpyDeviceToHost, stream));
     sync();
     std::memcpy(out, h_gather, n * sizeof(float));
     return n;
 }
 
-const float* Ctx::logits_host() {
+const float* Ctx::logits_host(int row) {
     if (!logits_valid) throw Error("no logits: decode a token first");
+    const float* src = out_row(row);
     MI_HIP(hipSetDevice(device));
-    MI_HIP(hipMemcpyAsync(h_logits, logits, (size_t)m->hp.n_vocab * sizeof(float), hipMemcpyDeviceToHost, stream));
+    MI_HIP(hipMemcpyAsync(h_logits, src, (size_t)m->hp.n_vocab * sizeof(float), hipMemcpyDeviceToHost, stream));
     sync();
     return h_logits;
 }

@@ -128,8 +128,19 @@ struct Ctx {
     int* h_tokpos_b = nullptr;          // pinned ring [kTokbRing][GEMM_NT][4]
     long long tokb_slot = 0;
     static constexpr int kTokbRing = 256;
-    static constexpr int kBatchRows = MMQ_NT > GEMM_NT ? MMQ_NT : GEMM_NT;
+    static constexpr int kBatchRows = UB_MAX;
     bool mmq_ok = false;                // int8-MFMA GEMM for prompt chunks (all layers Q4_K / Q6_K)
+    // physical batches of up to UB_MAX tokens on mmq32 (mmq.hip): activations, rope table
+    int8_t* ub_q = nullptr;             // Q8_K rows [UB_MAX][kmax]
+    float* ub_dT = nullptr;             // [kmax/256][UB_MAX]
+    int8_t* ub_bsb = nullptr;           // [UB_MAX][kmax/256][16]
+    float2* ub_rope = nullptr;          // [UB_MAX][n_rot/2]
+    bool out_mmq = false;               // the output head is mmq32-capable (batched logits of every token)
+    // MI_OUT_ALL: logits of every token of the last decode call, [out_rows][n_vocab]
+    float* logits_all = nullptr;
+    int logits_all_cap = 0;
+    int out_rows = 0;                   // rows of logits_all valid (0: the last decode was MI_OUT_LAST)
+    int topk_row = -1;                  // output row the mapped top-k buffers hold (-1: the last token)
     bool gemv_mix = getenv("MI_NO_MIX") == nullptr;   // mixed-type Q/K/V in one launch
     int8_t* q8r_q = nullptr;            // Q8_K rows of one prompt chunk
     float* q8r_d = nullptr;
@@ -178,13 +189,16 @@ struct Ctx {
     void enqueue_step(bool with_logits);
     void enqueue_output(const float* xrow, unsigned long long* stamps_slab);
     void decode_batch(const int32_t* tokens, int n);
+    void decode_ubatch(const int32_t* tokens, int n, bool all);
+    ActQ8 ub_act(int K, int ntok) const;
+    const float* out_row(int row) const;   // device logits of output row `row` (-1: the last)
     hipGraphExec_t build_graph(bool with_logits, int seg);
     void invalidate_graphs();
-    int decode(const int32_t* tokens, int n);
+    int decode(const int32_t* tokens, int n, bool all = false);
     void sync();
-    int topk(int k, int32_t* ids, float* vals);
-    int gather(const int32_t* ids, int n, float* out);
-    const float* logits_host();
+    int topk(int row, int k, int32_t* ids, float* vals);
+    int gather(int row, const int32_t* ids, int n, float* out);
+    const float* logits_host(int row);
     void kv_clear();
     int kv_seq_rm(int p0, int p1);
     int kv_seq_shift(int p0, int p1, int delta, int div);

@@ -246,4 +246,24 @@ bool mmq_supported(int type);
 // GemmParams as for launch_gemm (ntok <= MMQ_NT; pro/x/norm ignored: the activations are `act`)
 void launch_gemm_mmq(const GemmParams& p, const Q8Rows& act, hipStream_t s);
 
+// ---- int8-MFMA GEMM over a physical batch of up to UB_MAX tokens (mmq.hip) ----
+// Prompt ingestion and batched verification: activations quantised to Q8_K once per matrix
+// input (launch_quant_act), then v_mfma_i32_32x32x32_i8 per sub-block (launch_mmq32).
+constexpr int UB_MAX = 512;    // n_ubatch (reference Instance.hpp:24)
+struct ActQ8 {
+    int8_t* q;                 // [npad][K]
+    float* dT;                 // [K/256][npad]  (Q8_K d, token-minor)
+    int8_t* bsb;               // [npad][K/256][16]: sub-block bsums as 64*hi + lo (bytes 0-7 hi, 8-15 lo)
+    int K;
+    int ntok, npad;            // tokens; rows allocated (ntok rounded up to 32, <= UB_MAX)
+};
+void launch_quant_act(const float* x, int x_stride, const float* norm_w, float eps, const ActQ8& a, hipStream_t s);
+// ggml_rope_cache_init per token of the batch: out [ntok][n_rot/2] (cos, sin)
+void launch_rope_table(const int* tokpos, int ntok, int n_rot, float theta_scale, float freq_scale,
+                       const float* freq_factors, float2* out, hipStream_t s);
+bool mmq32_supported(int type);
+// GemmParams: A (B = up for PAIR_AB / EPI_SWIGLU), epi, K, out/out_stride, resid, tokpos [ntok][4],
+// RoPE fields (rope table from launch_rope_table), caches; the tokens are act's.
+void launch_mmq32(const GemmParams& p, const ActQ8& act, const float2* rope, hipStream_t s);
+
 }  // namespace mi

@@ -1,0 +1,405 @@
+// Prompt ingestion / batched verification on gfx950 int8 MFMA: the quantised GEMM of a
+// physical batch of up to UB_MAX tokens (n_ubatch, reference Instance.hpp:24).
+//
+// The arithmetic is ggml b5187's CPU mul_mat for these types: the activation rows are
+// quantised to Q8_K exactly as quantize_row_q8_K_ref (one row per token, as the CPU graph
+// does for src1), and every weight row x activation row product is
+//   Q4_K  sum_sb [ d_x d_y * sum_j sc_j * dot_j  -  dmin_x d_y * sum_j m_j * bsum_j ]
+//   Q6_K  sum_sb [ d_x d_y * sum_g sc_g * dot_g ]                  (vec_dot_q*_K_q8_K)
+// with the sub-block dots dot_j (32 elements; Q6_K: 16-element groups g) and the min terms
+// computed EXACTLY in int32 by v_mfma_i32_32x32x32_i8, one MFMA per sub-block.  Only the
+// fp32 sum across superblocks runs in another order than the CPU's.
+//
+// Geometry.  A wave computes a 32x32 D tile per MFMA, D[token][weight row]:
+//   A operand = activations: lane l holds token l&31, k-half l>>5 (16 int8)
+//   B operand = weights:     lane l holds weight row l&31, the same k-half
+//   D: lane l, register r  = token (r&3) + 8(r>>2) + 4(l>>5), weight row l&31
+// (the k order inside an MFMA does not matter: A and B share it; scripts/exp_mfma_layout.cpp
+// checks the D map).  So every lane owns ONE weight row: its sub-block scales and mins are
+// per-lane scalars, and the scale multiply is one v_mad per result.
+// A workgroup is 4 waves over one tile of 32 weight rows (16 gate/up pairs for SwiGLU) x 128
+// tokens; the waves split the superblocks, and their partial sums meet in LDS in wave order
+// (deterministic), after which wave w runs the epilogue of token tile w.  The 4 token groups
+// of a row tile are placed on one XCD (blockIdx % 8), so their weight reads share its L2.
+#include "kernels.h"
+#include <hip/hip_runtime.h>
+
+namespace mi {
+namespace mmq {
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v16i __attribute__((ext_vector_type(16)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <typename T>
+__device__ __forceinline__ const __attribute__((address_space(1))) T* gp(const T* p) {
+    return (const __attribute__((address_space(1))) T*)(p);
+}
+__device__ __forceinline__ float h2f(uint32_t bits) {
+    return __half2float(__ushort_as_half(static_cast<unsigned short>(bits & 0xFFFFu)));
+}
+template <int CTRL, int RMASK>
+__device__ __forceinline__ int dpp_i(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, CTRL, RMASK, 0xf, false);
+}
+template <int CTRL, int RMASK>
+__device__ __forceinline__ double dpp_d(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = dpp_i<CTRL, RMASK>((int)b), hi = dpp_i<CTRL, RMASK>((int)(b >> 32));
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+// full-wave double sum (fixed order), total in lane 63
+__device__ __forceinline__ double wave_sum63_d(double v) {
+    v += dpp_d<0x111, 0xf>(v);
+    v += dpp_d<0x112, 0xf>(v);
+    v += dpp_d<0x114, 0xf>(v);
+    v += dpp_d<0x118, 0xf>(v);
+    v += dpp_d<0x142, 0xa>(v);
+    v += dpp_d<0x143, 0xc>(v);
+    return v;
+}
+__device__ __forceinline__ float wave_max_pos(float v) {
+#define MX(ctrl, rm) v = fmaxf(v, __int_as_float(dpp_i<ctrl, rm>(__float_as_int(v))))
+    MX(0x111, 0xf); MX(0x112, 0xf); MX(0x114, 0xf); MX(0x118, 0xf); MX(0x142, 0xa); MX(0x143, 0xc);
+#undef MX
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+
+// ---------------------------------------------------------------------------
+// Activation rows -> Q8_K (quantize_row_q8_K_ref), one workgroup per token row.
+// Writes q [npad][K], d transposed [nb][npad] (4 consecutive tokens = one 16-B load in the
+// GEMM), and per superblock the 8 sub-block bsums split as 64*hi + lo (hi = floor(b/64),
+// lo in 0..63): bytes 0-7 hi_j, 8-15 lo_j -- the int8 A operand of the MFMA that forms
+// sum_j m_j*bsum_j = 64*sum m_j hi_j + sum m_j lo_j exactly.  Rows ntok..npad-1 are zero.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void quant_act_kernel(const float* x, int x_stride, const float* norm_w,
+                                                        float eps, ActQ8 a) {
+    const int t = blockIdx.x;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int nb = a.K >> 8;
+    __shared__ double red[4];
+    int8_t* q = a.q + (long long)t * a.K;
+    int8_t* bsb = a.bsb + (long long)t * nb * 16;
+    if (t >= a.ntok) {
+        for (int i = threadIdx.x; i < a.K / 4; i += 256) reinterpret_cast<int*>(q)[i] = 0;
+        for (int i = threadIdx.x; i < nb; i += 256) a.dT[(long long)i * a.npad + t] = 0.0f;
+        for (int i = threadIdx.x; i < nb * 4; i += 256) reinterpret_cast<int*>(bsb)[i] = 0;
+        return;
+    }
+    const f32x4* x4 = reinterpret_cast<const f32x4*>(x + (long long)t * x_stride);
+    float scale = 1.0f;
+    if (norm_w) {   // ggml_compute_forward_rms_norm_f32: sum of squares in double
+        double sacc = 0.0;
+        for (int blk = wave; blk < nb; blk += 4) {
+            const f32x4 v = x4[blk * 64 + lane];
+            sacc += (double)(v.x * v.x);
+            sacc += (double)(v.y * v.y);
+            sacc += (double)(v.z * v.z);
+            sacc += (double)(v.w * v.w);
+        }
+        sacc = wave_sum63_d(sacc);
+        if (lane == 63) red[wave] = sacc;
+        __syncthreads();
+        const double tot = ((red[0] + red[1]) + red[2]) + red[3];
+        scale = 1.0f / sqrtf((float)(tot / (double)a.K) + eps);
+    }
+    const f32x4* w4 = reinterpret_cast<const f32x4*>(norm_w);
+    for (int blk = wave; blk < nb; blk += 4) {
+        const f32x4 xv = x4[blk * 64 + lane];
+        float v[4] = {xv.x, xv.y, xv.z, xv.w};
+        if (norm_w) {
+            const f32x4 w = w4[blk * 64 + lane];
+            v[0] = (v[0] * scale) * w.x;   // ggml_vec_scale_f32, then ggml_mul
+            v[1] = (v[1] * scale) * w.y;
+            v[2] = (v[2] * scale) * w.z;
+            v[3] = (v[3] * scale) * w.w;
+        }
+        const float a0 = fabsf(v[0]), a1 = fabsf(v[1]), a2 = fabsf(v[2]), a3 = fabsf(v[3]);
+        const float amax = wave_max_pos(fmaxf(fmaxf(a0, a1), fmaxf(a2, a3)));
+        int qv[4];
+        float d;
+        if (amax == 0.0f) {
+            qv[0] = qv[1] = qv[2] = qv[3] = 0;
+            d = 0.0f;
+        } else {   // max = the signed value at the FIRST index whose |x| is the maximum
+            const int e = a0 == amax ? 0 : a1 == amax ? 1 : a2 == amax ? 2 : a3 == amax ? 3 : 4;
+            const float mine = e == 0 ? v[0] : e == 1 ? v[1] : e == 2 ? v[2] : v[3];
+            const unsigned long long m = __ballot(e < 4);
+            const int src = __builtin_ctzll(m);
+            const float mx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mine), src));
+            const float iscale = -127.0f / mx;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) qv[k] = min(127, (int)rintf(iscale * v[k]));
+            d = 1.0f / iscale;
+        }
+        reinterpret_cast<int*>(q + blk * 256)[lane] =
+            (qv[0] & 0xFF) | ((qv[1] & 0xFF) << 8) | ((qv[2] & 0xFF) << 16) | ((qv[3] & 0xFF) << 24);
+        // the 32-element sub-block sums: lanes 8j..8j+7
+        int sm = (qv[0] + qv[1]) + (qv[2] + qv[3]);
+        sm += dpp_i<0xB1, 0xf>(sm);    // quad_perm [1,0,3,2]
+        sm += dpp_i<0x4E, 0xf>(sm);    // quad_perm [2,3,0,1]
+        sm += __shfl_xor(sm, 4, 64);   // the two quads of a sub-block
+        if ((lane & 7) == 0) {
+            const int j = lane >> 3;
+            bsb[blk * 16 + j] = (int8_t)(sm >> 6);          // floor(b/64), -64..63
+            bsb[blk * 16 + 8 + j] = (int8_t)(sm & 63);      // b - 64*floor(b/64), 0..63
+        }
+        if (lane == 0) a.dT[(long long)blk * a.npad + t] = d;
+    }
+}
+
+// ggml_rope_cache_init (rope NORM) for every token of the batch: theta iterated from the
+// position as the CPU does, table [ntok][n_rot/2] of (cos, sin).
+__global__ void rope_table_kernel(const int* tokpos, int ntok, int n_rot, float theta_scale, float freq_scale,
+                                  const float* freq_factors, float2* out) {
+    const int t = blockIdx.x;
+    if (t >= ntok) return;
+    const int pos = tokpos[t * 4 + 1];
+    for (int i = threadIdx.x; i < n_rot / 2; i += blockDim.x) {
+        float theta = (float)pos;
+        for (int k = 0; k < i; ++k) theta = theta * theta_scale;
+        const float ff = freq_factors ? freq_factors[i] : 1.0f;
+        const float th = freq_scale * (theta / ff);
+        out[(long long)t * (n_rot / 2) + i] = make_float2(cosf(th), sinf(th));
+    }
+}
+
+__device__ __forceinline__ float silu(float x) { return x / (1.0f + expf(-x)); }
+
+__device__ __forceinline__ v16i mfma(v4i a, v4i b) {
+    const v16i z = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    return __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b, z, 0, 0, 0);
+}
+
+constexpr int TT = 4;   // token tiles (of 32) per workgroup
+constexpr int KS = 4;   // waves = superblock splits
+
+// get_scale_min_k4 for the 8 sub-blocks of a Q4_K header {d, dmin, scales[12]}
+__device__ __forceinline__ void q4k_scales(const u32x4 hd, int sc[8], int mn[8]) {
+    const unsigned Y = hd.y, Z = hd.z, W = hd.w;   // bytes 0-3, 4-7, 8-11 of scales[12]
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        sc[j] = (Y >> (8 * j)) & 63;
+        mn[j] = (Z >> (8 * j)) & 63;
+        sc[4 + j] = ((W >> (8 * j)) & 0xF) | (((Y >> (8 * j + 6)) & 3) << 4);
+        mn[4 + j] = ((W >> (8 * j + 4)) & 0xF) | (((Z >> (8 * j + 6)) & 3) << 4);
+    }
+}
+
+template <int T, bool AB>
+__global__ __launch_bounds__(256, 2) void mmq32_t(const GemmParams P, const ActQ8 act, const float2* rope) {
+    __shared__ float red[KS][TT][16][64];   // 64 KiB: the waves' partial sums
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int col = lane & 31, h = lane >> 5;
+    const int nb = P.K >> 8;
+    const int ntg = (act.npad + 32 * TT - 1) / (32 * TT);
+    const int nrt = AB ? (P.A.rows + 15) / 16 : (P.A.rows + 31) / 32;
+    // blockIdx -> (row tile, token group): the token groups of a row tile on one XCD
+    const int b = blockIdx.x, xcd = b & 7, slot = b >> 3;
+    const int rt = (slot / ntg) * 8 + xcd, tg = slot % ntg;
+    if (rt >= nrt) return;
+    // this lane's weight row
+    const QMat& M = (AB && col >= 16) ? P.B : P.A;
+    const int row = AB ? rt * 16 + (col & 15) : rt * 32 + col;
+    const long long rl = row < M.rows ? row : M.rows - 1;   // tail lanes re-read a valid row
+    const int sb0 = nb * w / KS, sb1 = nb * (w + 1) / KS;
+    const int tok0 = tg * 32 * TT;
+    int ntt = (act.npad - tok0) / 32;
+    ntt = ntt > TT ? TT : ntt;
+
+    // token tiles outer (one 16-register accumulator live), superblocks inner; the weight
+    // fragments of a superblock are re-read per token tile (L1/L2 hits after the first)
+    for (int t = 0; t < ntt; ++t) {
+        float y[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) y[r] = 0.0f;
+        const int ta = tok0 + 32 * t + col;   // A-operand token of this lane
+        for (int sb = sb0; sb < sb1; ++sb) {
+            const long long wsb = rl * nb + sb;
+            const int8_t* aq = act.q + (long long)ta * P.K + sb * 256 + 16 * h;
+            const float* dT = act.dT + (long long)sb * act.npad + tok0 + 32 * t + 4 * h;
+            int S[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) S[r] = 0;
+            if (T == T_Q4_K) {
+                // qs[32p + l]: low nibble = sub-block 2p element l, high nibble = sub-block 2p+1
+                const u32x4 hd = *gp(reinterpret_cast<const u32x4*>(M.p[1] + wsb * 16));
+                int sc[8], mn[8];
+                q4k_scales(hd, sc, mn);
+#pragma unroll
+                for (int p = 0; p < 4; ++p) {
+                    const u32x4 wq = *gp(reinterpret_cast<const u32x4*>(M.p[0] + wsb * 128 + 32 * p + 16 * h));
+                    const v4i blo = v4i{(int)(wq.x & 0x0F0F0F0Fu), (int)(wq.y & 0x0F0F0F0Fu), (int)(wq.z & 0x0F0F0F0Fu),
+                                        (int)(wq.w & 0x0F0F0F0Fu)};
+                    const v4i bhi = v4i{(int)((wq.x >> 4) & 0x0F0F0F0Fu), (int)((wq.y >> 4) & 0x0F0F0F0Fu),
+                                        (int)((wq.z >> 4) & 0x0F0F0F0Fu), (int)((wq.w >> 4) & 0x0F0F0F0Fu)};
+                    const v4i a0 = *gp(reinterpret_cast<const v4i*>(aq + 64 * p));
+                    const v4i a1 = *gp(reinterpret_cast<const v4i*>(aq + 64 * p + 32));
+                    const v16i d0 = mfma(a0, blo);
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) S[r] += sc[2 * p] * d0[r];
+                    const v16i d1 = mfma(a1, bhi);
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) S[r] += sc[2 * p + 1] * d1[r];
+                }
+                // sum_j m_j*bsum_j: mins as int8 B operands, k 0-7 (against hi) / k 8-15 (against lo)
+                const int m03 = mn[0] | (mn[1] << 8) | (mn[2] << 16) | (mn[3] << 24);
+                const int m47 = mn[4] | (mn[5] << 8) | (mn[6] << 16) | (mn[7] << 24);
+                const v4i bm1 = h == 0 ? v4i{m03, m47, 0, 0} : v4i{0, 0, 0, 0};
+                const v4i bm2 = h == 0 ? v4i{0, 0, m03, m47} : v4i{0, 0, 0, 0};
+                const v4i ab = h == 0 ? *gp(reinterpret_cast<const v4i*>(act.bsb + ((long long)ta * nb + sb) * 16))
+                                      : v4i{0, 0, 0, 0};
+                const v16i x1 = mfma(ab, bm1);
+                const v16i x2 = mfma(ab, bm2);
+                const float dr = h2f(hd.x), dmr = h2f(hd.x >> 16);
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const f32x4 dx4 = *gp(reinterpret_cast<const f32x4*>(dT + 8 * g));
+                    const float dx[4] = {dx4.x, dx4.y, dx4.z, dx4.w};
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int r = 4 * g + i;
+                        const float d = dr * dx[i], dm = dmr * dx[i];
+                        y[r] += d * (float)S[r] - dm * (float)(64 * x1[r] + x2[r]);
+                    }
+                }
+            } else {   // Q6_K: ql[128] qh[64] scales[16] d
+                const u32x4 scw = *gp(reinterpret_cast<const u32x4*>(M.p[2] + wsb * 16));
+                const unsigned scv[4] = {scw.x, scw.y, scw.z, scw.w};
+#pragma unroll
+                for (int hf = 0; hf < 2; ++hf) {
+                    const u32x4 H = *gp(reinterpret_cast<const u32x4*>(M.p[1] + wsb * 64 + 32 * hf + 16 * h));
+#pragma unroll
+                    for (int c = 0; c < 2; ++c) {
+                        const u32x4 L = *gp(reinterpret_cast<const u32x4*>(M.p[0] + wsb * 128 + 64 * hf + 32 * c + 16 * h));
+#pragma unroll
+                        for (int nib = 0; nib < 2; ++nib) {
+                            // span (hf, qq): elements 128hf + 32qq + l; this lane's l = 16h + e
+                            const int qq = c + 2 * nib, s = 4 * hf + qq;
+                            const unsigned ls = 4 * nib, hs = 2 * qq;
+                            const unsigned lw[4] = {L.x, L.y, L.z, L.w}, hw[4] = {H.x, H.y, H.z, H.w};
+                            int v[4];
+#pragma unroll
+                            for (int k = 0; k < 4; ++k) {
+                                const unsigned u = ((lw[k] >> ls) & 0x0F0F0F0Fu) | (((hw[k] >> hs) & 0x03030303u) << 4);
+                                v[k] = (int)(((u | 0x80808080u) - 0x20202020u) ^ 0x80808080u);   // q - 32 per byte
+                            }
+                            const v4i bf = v4i{v[0], v[1], v[2], v[3]};
+                            const v4i z = {0, 0, 0, 0};
+                            const int is = 2 * s;   // the span's scale groups 2s (k-half 0), 2s+1 (k-half 1)
+                            const int g0 = (int)(signed char)((scv[is >> 2] >> (8 * (is & 3))) & 0xFF);
+                            const int g1 = (int)(signed char)((scv[is >> 2] >> (8 * (is & 3) + 8)) & 0xFF);
+                            const v4i a = *gp(reinterpret_cast<const v4i*>(aq + 32 * s));
+                            const v16i d0 = mfma(a, h == 0 ? bf : z);
+#pragma unroll
+                            for (int r = 0; r < 16; ++r) S[r] += g0 * d0[r];
+                            const v16i d1 = mfma(a, h == 1 ? bf : z);
+#pragma unroll
+                            for (int r = 0; r < 16; ++r) S[r] += g1 * d1[r];
+                        }
+                    }
+                }
+                const float dr = h2f(*gp(reinterpret_cast<const unsigned short*>(M.p[3] + wsb * 2)));
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const f32x4 dx4 = *gp(reinterpret_cast<const f32x4*>(dT + 8 * g));
+                    const float dx[4] = {dx4.x, dx4.y, dx4.z, dx4.w};
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) y[4 * g + i] += (dr * dx[i]) * (float)S[4 * g + i];
+                }
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) red[w][t][r][lane] = y[r];
+    }
+    // ---- the superblock splits meet in LDS, in wave order
+    __syncthreads();
+    const int t = w;   // this wave's epilogue: token tile w
+    if (t >= ntt) return;
+    float v[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = ((red[0][t][r][lane] + red[1][t][r][lane]) + red[2][t][r][lane]) + red[3][t][r][lane];
+    const int epi = P.epi;
+    const bool roped = epi == EPI_ROPE_Q || epi == EPI_ROPE_K;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int tok = tok0 + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const float pv = __shfl_xor(v[r], AB ? 16 : 1, 64);   // SwiGLU partner / RoPE partner
+        if (tok >= act.ntok) continue;
+        if (AB) {
+            if (col >= 16 || row >= P.A.rows) continue;
+            P.out[(long long)tok * P.out_stride + row] = silu(v[r]) * pv;   // silu(gate) * up
+            continue;
+        }
+        if (row >= P.A.rows) continue;
+        float o = v[r];
+        if (roped) {
+            const int i0 = row % P.head_dim;
+            if (i0 < P.n_rot) {
+                const float2 cs = rope[(long long)tok * (P.n_rot / 2) + i0 / 2];
+                o = (col & 1) ? pv * cs.y + v[r] * cs.x : v[r] * cs.x - pv * cs.y;
+            }
+        }
+        const int* tp = P.tokpos + tok * 4;
+        switch (epi) {
+        case EPI_STORE:
+        case EPI_ROPE_Q: P.out[(long long)tok * P.out_stride + row] = o; break;
+        case EPI_ADD: {
+            const long long i = (long long)tok * P.out_stride + row;
+            P.out[i] = o + P.resid[i];
+            break;
+        }
+        case EPI_ROPE_K: {
+            const int cell = tp[2];
+            P.kcache[(long long)cell * P.kv_dim + row] = __float2half_rn(o);
+            if (row == 0) P.cell_pos[cell] = tp[1];
+            break;
+        }
+        case EPI_V: P.vcache[(long long)tp[2] * P.kv_dim + row] = __float2half_rn(o); break;
+        default: break;
+        }
+    }
+}
+
+}  // namespace mmq
+
+void launch_quant_act(const float* x, int x_stride, const float* norm_w, float eps, const ActQ8& a, hipStream_t s) {
+    if (a.K % 256) throw Error("quant_act: K must be a multiple of 256");
+    if (a.npad % 32 || a.ntok > a.npad || a.npad > UB_MAX) throw Error("quant_act: bad token count");
+    hipLaunchKernelGGL(mmq::quant_act_kernel, dim3(a.npad), dim3(256), 0, s, x, x_stride, norm_w, eps, a);
+    MI_HIP(hipGetLastError());
+}
+
+void launch_rope_table(const int* tokpos, int ntok, int n_rot, float theta_scale, float freq_scale,
+                       const float* freq_factors, float2* out, hipStream_t s) {
+    if (ntok <= 0 || n_rot <= 0) return;
+    hipLaunchKernelGGL(mmq::rope_table_kernel, dim3(ntok), dim3(64), 0, s, tokpos, ntok, n_rot, theta_scale,
+                       freq_scale, freq_factors, out);
+    MI_HIP(hipGetLastError());
+}
+
+bool mmq32_supported(int type) { return type == T_Q4_K || type == T_Q6_K; }
+
+void launch_mmq32(const GemmParams& p, const ActQ8& act, const float2* rope, hipStream_t s) {
+    if (!mmq32_supported(p.A.type)) throw Error("mmq32: Q4_K / Q6_K only");
+    if (act.K != p.K || p.A.K != p.K) throw Error("mmq32: activation length differs from K");
+    const bool ab = p.pair == PAIR_AB;
+    if (ab && (p.B.type != p.A.type || p.B.rows != p.A.rows || p.epi != EPI_SWIGLU))
+        throw Error("mmq32: a pair launch is gate/up SwiGLU of one type");
+    if (!ab && p.epi == EPI_SWIGLU) throw Error("mmq32: SwiGLU needs a pair");
+    if ((p.epi == EPI_ROPE_Q || p.epi == EPI_ROPE_K) && (!rope || p.head_dim % 2 || p.n_rot > p.head_dim))
+        throw Error("mmq32: RoPE epilogue needs the rope table");
+    if (act.ntok < 1 || act.npad % 32 || act.npad > UB_MAX) throw Error("mmq32: bad token count");
+    const int ntg = (act.npad + 32 * mmq::TT - 1) / (32 * mmq::TT);
+    const int nrt = ab ? (p.A.rows + 15) / 16 : (p.A.rows + 31) / 32;
+    const int grid = (nrt + 7) / 8 * 8 * ntg;
+    decltype(&mmq::mmq32_t<T_Q4_K, false>) fn;
+    if (p.A.type == T_Q4_K) fn = ab ? mmq::mmq32_t<T_Q4_K, true> : mmq::mmq32_t<T_Q4_K, false>;
+    else fn = ab ? mmq::mmq32_t<T_Q6_K, true> : mmq::mmq32_t<T_Q6_K, false>;
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(256), 0, s, p, act, rope);
+    MI_HIP(hipGetLastError());
+}
+
+}  // namespace mi

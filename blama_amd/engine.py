@@ -223,28 +223,29 @@ class Context:
         except Exception:
             pass
 
-    def decode(self, tokens) -> int:
+    def decode(self, tokens, all_logits: bool = False) -> int:
+        """mi_decode; all_logits=True is MI_OUT_ALL (output row i = the distribution after token i)."""
         t = np.ascontiguousarray(tokens, dtype=np.int32)
-        rc = lib().mi_decode(self.h, t.ctypes.data_as(C.POINTER(C.c_int32)), t.size, 0)
+        rc = lib().mi_decode(self.h, t.ctypes.data_as(C.POINTER(C.c_int32)), t.size, 1 if all_logits else 0)
         _check(rc, "decode")
         return rc
 
-    def topk(self, k: int = 10):
+    def topk(self, k: int = 10, row: int = -1):
         ids = np.empty(k, np.int32)
         vals = np.empty(k, np.float32)
-        _check(lib().mi_topk(self.h, -1, k, ids.ctypes.data_as(C.POINTER(C.c_int32)),
+        _check(lib().mi_topk(self.h, row, k, ids.ctypes.data_as(C.POINTER(C.c_int32)),
                              vals.ctypes.data_as(C.POINTER(C.c_float))), "topk")
         return ids, vals
 
-    def gather(self, ids):
+    def gather(self, ids, row: int = -1):
         ids = np.ascontiguousarray(ids, dtype=np.int32)
         out = np.empty(ids.size, np.float32)
-        _check(lib().mi_gather(self.h, -1, ids.ctypes.data_as(C.POINTER(C.c_int32)), ids.size,
+        _check(lib().mi_gather(self.h, row, ids.ctypes.data_as(C.POINTER(C.c_int32)), ids.size,
                                out.ctypes.data_as(C.POINTER(C.c_float))), "gather")
         return out
 
-    def logits(self) -> np.ndarray:
-        p = lib().mi_logits(self.h, -1)
+    def logits(self, row: int = -1) -> np.ndarray:
+        p = lib().mi_logits(self.h, row)
         if not p:
             raise EngineError(f"logits: {last_error()}")
         return np.ctypeslib.as_array(p, shape=(self.model.n_vocab,)).copy()

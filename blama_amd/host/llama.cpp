@@ -1,5 +1,6 @@
 // bl::llama host surface on the MI355X engine (see llama.hpp for the mirrored reference files).
 #include "llama.hpp"
+#include <cstdlib>
 
 #include "mi_engine.h"
 
@@ -496,6 +497,33 @@ TokenPrediction Session::StreamGenerator::complete() {
 std::vector<TokenPrediction> Session::fillCtx(std::span<TokenPrediction> tokens) {
     std::vector<TokenPrediction> out;
     out.reserve(tokens.size());
+    // Batched verification: the reference pushes the claimed tokens one decode at a time
+    // (Session.cpp:231-244).  When no context shift or Self-Extend step can fall inside the
+    // run, the same tokens go through mi_decode(MI_OUT_ALL) in n_batch chunks and row i holds
+    // the distribution after token i -- what the i-th single-token decode leaves behind.
+    // BL_SERIAL_VERIFY=1 keeps the reference's per-token loop.
+    requireGenerating();
+    flushPendingState();
+    const uint32_t n = (uint32_t)tokens.size();
+    const uint32_t batch = mi_n_batch(m_ctx);
+    if (n > 0 && m_params.gaFactor == 1 && m_state.numPast + n < mi_n_ctx(m_ctx) && batch > 0 &&
+        getenv("BL_SERIAL_VERIFY") == nullptr) {
+        for (const TokenPrediction& t : tokens) m_sampler->accept(t.token, false);
+        for (uint32_t c0 = 0; c0 < n; c0 += batch) {
+            const uint32_t nc = std::min(batch, n - c0);
+            std::vector<Token> ids(nc);
+            for (uint32_t i = 0; i < nc; ++i) ids[i] = tokens[c0 + i].token;
+            if (mi_decode(m_ctx, ids.data(), (int32_t)nc, MI_OUT_ALL) != 0) BL_THROW("Failed to decode tokens");
+            m_state.numPast += nc;
+            for (uint32_t i = 0; i < nc; ++i) {
+                TokenPrediction r;
+                r.token = tokens[c0 + i].token;
+                r.logits = getLogitsFromCtx(tokens[c0 + i].logits, (int32_t)i);
+                out.push_back(std::move(r));
+            }
+        }
+        return out;
+    }
     for (const TokenPrediction& t : tokens) {
         pushPrompt({&t.token, 1}, {});
         TokenPrediction r;
@@ -523,7 +551,7 @@ TokenDataVector Session::getLogitsFromCtx(int32_t topK) {
     return r;
 }
 
-TokenDataVector Session::getLogitsFromCtx(const TokenDataVector& tokens) {
+TokenDataVector Session::getLogitsFromCtx(const TokenDataVector& tokens, int32_t row) {
     requireGenerating();
     flushPendingState();
     // the reference scans the vocabulary in id order keeping ids in `tokens`: each id once
@@ -533,7 +561,7 @@ TokenDataVector Session::getLogitsFromCtx(const TokenDataVector& tokens) {
     std::sort(ids.begin(), ids.end());
     ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
     std::vector<float> lg(ids.size());
-    if (!ids.empty() && mi_gather(m_ctx, -1, ids.data(), (int32_t)ids.size(), lg.data()) < 0)
+    if (!ids.empty() && mi_gather(m_ctx, row, ids.data(), (int32_t)ids.size(), lg.data()) < 0)
         BL_THROW("gather: " << last_error());
     TokenDataVector r(ids.size());
     for (size_t i = 0; i < ids.size(); ++i) r[i] = {ids[i], lg[i]};

@@ -212,7 +212,9 @@ private:
     void doDecode(std::span<const Token> tokens, Source src);
     void flushPendingState();
     TokenDataVector getLogitsFromCtx(int32_t topK);
-    TokenDataVector getLogitsFromCtx(const TokenDataVector& tokens);
+    // logits at `tokens`' ids of output row `row` (-1: the last token's; 0..n-1 after a batched
+    // fillCtx pass)
+    TokenDataVector getLogitsFromCtx(const TokenDataVector& tokens, int32_t row = -1);
     void requireGenerating() const;
 
     struct State {

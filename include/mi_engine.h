@@ -86,15 +86,20 @@ uint32_t mi_n_batch(const mi_ctx* ctx);   /* llama_n_batch (Session.cpp:381) */
 
 /* llama_decode(llama_batch_get_one(tokens, n)) (Session.cpp:388, Instance.cpp:115):
  * tokens take positions pos_max+1...; asynchronous on the context's stream.
- * out_mode 0 = logits of the last token only (llama_batch_get_one). */
+ * out_mode MI_OUT_LAST = logits of the last token only (llama_batch_get_one);
+ * MI_OUT_ALL = logits of every token (a batch with logits[i] = true for all i), n <= n_batch:
+ * output row i is the distribution after token i -- one batched pass in place of the
+ * per-token decodes of Session::fillCtx (Session.cpp:231-244). */
 #define MI_OUT_LAST 0
+#define MI_OUT_ALL 1
 int32_t mi_decode(mi_ctx* ctx, const int32_t* tokens, int32_t n, int32_t out_mode);
 
-/* Top-k of the last output row, sorted by logit descending then id ascending;
+/* Output rows: -1 = the last token's; 0..n-1 after an MI_OUT_ALL decode of n tokens (row 0 only
+ * after MI_OUT_LAST).  Top-k of an output row, sorted by logit descending then id ascending;
  * k <= 64.  Replaces fillLogits + std::sort + first 10 (Session.cpp:246-261) and
  * feeds the sampler chain's top_k(40) stage (Sampler.cpp:15-97).  Synchronises. */
 int32_t mi_topk(mi_ctx* ctx, int32_t row, int32_t k, int32_t* ids, float* logits);
-/* Logits of the last output row at the given ids (Session.cpp:263-282).  Synchronises. */
+/* Logits of an output row at the given ids (Session.cpp:263-282).  Synchronises. */
 int32_t mi_gather(mi_ctx* ctx, int32_t row, const int32_t* ids, int32_t n, float* out);
 /* Full-vocabulary escape hatch: llama_get_logits_ith(ctx, -1) (Session.cpp:24,
  * Sampler.cpp:111).  Context-owned; valid until the next decode.  Synchronises. */

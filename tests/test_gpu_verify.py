@@ -1,0 +1,100 @@
+"""Batched verification: mi_decode(..., MI_OUT_ALL) -- the logits after EVERY token of one
+call, in place of Session::fillCtx's one decode per claimed token
+(/root/reference/inference/code/llama/Session.cpp:231-244, 263-282).
+
+Each output row i is checked against the CPU oracle decoding the same tokens one at a time
+(element-wise within LOGIT_TOL x rms, identical top-10, the t-LogitComparer.cpp:76-78 gate),
+for the int8-MFMA batch path (Q4_K_M / Q6_K models: mmq32, the output head batched too) and
+for the per-token fallback (other quant types, MI_NO_BATCH=1), and the two paths against each
+other.  Row selection of mi_topk / mi_gather / mi_logits is exact against the row's logits."""
+import numpy as np
+import pytest
+
+import ggml_ref as R
+from blama_amd import engine, synthetic
+from util import oracle_from_gguf
+
+pytestmark = pytest.mark.gpu
+LOGIT_TOL = 2e-3
+
+
+def _close(got, ref, tol=LOGIT_TOL):
+    rms = float(np.sqrt(np.mean(ref.astype(np.float64) ** 2)))
+    return float(np.max(np.abs(got - ref))) <= tol * rms
+
+
+def _check_rows(ctx, buf, prompt, claimed, n_ctx):
+    orc = oracle_from_gguf(buf, n_ctx=n_ctx)
+    orc.decode(prompt)
+    agg = R.MetricsAggregator()
+    for i, t in enumerate(claimed):
+        ref = orc.decode_one(t)
+        got = ctx.logits(row=i)
+        assert _close(got, ref), f"row {i}"
+        ids, vals = ctx.topk(10, row=i)
+        assert [int(x) for x in ids] == [j for j, _ in R.topk(ref, 10)], f"row {i}"
+        assert np.array_equal(vals, got[ids])
+        g = ctx.gather(ids[::-1], row=i)
+        assert np.array_equal(g, got[ids[::-1]])
+        a = [(int(x), float(v)) for x, v in zip(ids, vals)]
+        cm = R.compare(a, R.gather(ref, [j for j, _ in a]))
+        assert cm.top1Match == 1.0
+        score = agg.push_and_verify([cm])
+    assert score >= 0.95
+
+
+@pytest.mark.parametrize("cfg_name", ["tiny-q4_k_m", "tiny-q6_k", "tiny-q5_k_m", "tiny-q8_0"])
+def test_out_all_matches_oracle(gpu_lib, cfg_name):
+    cfg = synthetic.CONFIGS[cfg_name]
+    buf = synthetic.build_gguf(cfg, seed=31)
+    m = engine.Model(buf)
+    rng = np.random.default_rng(9)
+    prompt = [int(t) for t in rng.integers(0, cfg.n_vocab, 7)]
+    claimed = [int(t) for t in rng.integers(0, cfg.n_vocab, 40)]
+    ctx = engine.Context(m, n_ctx=96)
+    ctx.decode(prompt)
+    ctx.decode(claimed, all_logits=True)
+    _check_rows(ctx, buf, prompt, claimed, 96)
+    # the last row is also row -1, and the next single-token step sees the whole batch's cache
+    assert np.array_equal(ctx.logits(), ctx.logits(row=len(claimed) - 1))
+    ids_last, _ = ctx.topk(10)
+    ids_row, _ = ctx.topk(10, row=len(claimed) - 1)
+    assert np.array_equal(ids_last, ids_row)
+
+
+def test_out_all_batch_vs_serial(gpu_lib, monkeypatch):
+    """The MFMA batch (one pass, output head as a GEMM) and the per-token fallback agree."""
+    cfg = synthetic.CONFIGS["tiny-q4_k_m"]
+    buf = synthetic.build_gguf(cfg, seed=33)
+    m = engine.Model(buf)
+    rng = np.random.default_rng(10)
+    prompt = [int(t) for t in rng.integers(0, cfg.n_vocab, 5)]
+    claimed = [int(t) for t in rng.integers(0, cfg.n_vocab, 33)]   # npad 64: a padded tile
+    a = engine.Context(m, n_ctx=64)
+    a.decode(prompt)
+    a.decode(claimed, all_logits=True)
+    monkeypatch.setenv("MI_NO_BATCH", "1")
+    b = engine.Context(m, n_ctx=64)
+    b.decode(prompt)
+    b.decode(claimed, all_logits=True)
+    # each path is within LOGIT_TOL of the oracle (test above), so within 2x of each other
+    for i in range(len(claimed)):
+        assert _close(a.logits(row=i), b.logits(row=i), 2 * LOGIT_TOL), i
+    for t in [5, 6]:   # caches written by the batch serve later steps
+        a.decode([t])
+        b.decode([t])
+        assert _close(a.logits(), b.logits(), 2 * LOGIT_TOL)
+
+
+def test_out_all_row_bounds(gpu_lib):
+    cfg = synthetic.CONFIGS["tiny-q4_k_m"]
+    m = engine.Model(synthetic.build_gguf(cfg, seed=35))
+    ctx = engine.Context(m, n_ctx=64)
+    ctx.decode([1, 2, 3], all_logits=True)
+    ctx.topk(5, row=2)
+    with pytest.raises(engine.EngineError):
+        ctx.topk(5, row=3)
+    ctx.decode([4])   # MI_OUT_LAST: only row 0 / -1 exist
+    ctx.topk(5, row=0)
+    with pytest.raises(engine.EngineError):
+        ctx.topk(5, row=1)
