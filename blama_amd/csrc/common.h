@@ -56,6 +56,10 @@ struct QMat {                // device view of one (expert of a) quantised matri
     int K;                   // input features (multiple of 256)
     int nb;                  // superblocks per row = K/256
     long long expert_stride[4];  // bytes between experts, per plane (0 if dense)
+    // Prompt-batch copy in MFMA-fragment order (mmq.hip, built per context on first use; null if
+    // none): [row tile of 32][superblock][tile bytes], for a gate/up pair on the gate matrix with
+    // 16 gate + 16 up rows per tile.
+    const uint8_t* sw;
 };
 
 struct Error : std::runtime_error { using std::runtime_error::runtime_error; };

@@ -140,10 +140,37 @@ const GgufTensor* Gguf::tensor(const std::string& name) const {
 
 // ================================================================= model ===
 Model::~Model() {
-    if (arena) {
-        hipSetDevice(device);
-        hipFree(arena);
+    if (arena || mmq_arena) hipSetDevice(device);
+    if (arena) hipFree(arena);
+    if (mmq_arena) hipFree(mmq_arena);
+}
+
+void Model::ensure_mmq_copies() {
+    std::lock_guard<std::mutex> lk(mmq_mu);
+    if (mmq_arena) return;
+    MI_HIP(hipSetDevice(device));
+    // every Q4_K / Q6_K projection (gate and up as one pair copy) and the output head
+    std::vector<std::pair<QMat*, QMat*>> todo;
+    for (Layer& L : layers) {
+        for (QMat* q : {&L.wq, &L.wk, &L.wv, &L.wo, &L.down})
+            if (mmq32_supported(q->type)) todo.push_back({q, nullptr});
+        if (mmq32_supported(L.gate.type) && L.up.type == L.gate.type) todo.push_back({&L.gate, &L.up});
     }
+    if (mmq32_supported(output.type)) todo.push_back({&output, nullptr});
+    size_t total = 0;
+    std::vector<size_t> offs;
+    for (auto& t : todo) {
+        offs.push_back(total);
+        total = (total + mmq32_copy_bytes(*t.first, t.second != nullptr) + 255) & ~size_t(255);
+    }
+    if (!total) return;
+    MI_HIP(hipMalloc(&mmq_arena, total));
+    mmq_bytes = total;
+    for (size_t i = 0; i < todo.size(); ++i) {
+        launch_mmq32_swizzle(*todo[i].first, todo[i].second, mmq_arena + offs[i], nullptr);
+        todo[i].first->sw = mmq_arena + offs[i];
+    }
+    MI_HIP(hipDeviceSynchronize());
 }
 
 const QMat* Model::find_qmat(const std::string&) const { return nullptr; }
@@ -420,6 +447,7 @@ Ctx::Ctx(Model* model, uint32_t nctx, uint32_t nbatch, uint32_t nubatch) : m(mod
                 for (const QMat* q : {&L.wq, &L.wk, &L.wv, &L.wo, &L.gate, &L.up, &L.down})
                     mmq_ok = mmq_ok && mmq32_supported(q->type);
             out_mmq = mmq_ok && mmq32_supported(m->output.type);
+            if (mmq_ok) m->ensure_mmq_copies();
             MI_HIP(hipMalloc(&ub_q, (size_t)UB_MAX * kmax));
             MI_HIP(hipMalloc(&ub_dT, (size_t)UB_MAX * (kmax / 256) * sizeof(float)));
             MI_HIP(hipMalloc(&ub_bsb, (size_t)UB_MAX * (kmax / 256) * 16));

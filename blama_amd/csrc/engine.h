@@ -1,6 +1,7 @@
 // Engine internals: GGUF parsing, the device-resident model and the decode
 // context.  The public surface is the C ABI in include/mi_engine.h.
 #pragma once
+#include <mutex>
 #include <cstdlib>
 #include "common.h"
 #include "kernels.h"
@@ -79,6 +80,13 @@ struct Model {
 
     uint8_t* arena = nullptr;
     size_t arena_bytes = 0;
+    // MFMA-order copies of the layer matrices and the output head for prompt batches (mmq32),
+    // built from the arena on the device the first time a context needs them (replicas build
+    // their own after the arena broadcast): one more weight-sized allocation, HBM for speed
+    uint8_t* mmq_arena = nullptr;
+    size_t mmq_bytes = 0;
+    std::mutex mmq_mu;
+    void ensure_mmq_copies();
     long long weight_bytes = 0;         // GGUF bytes streamed per token (all but tok_embd)
     long long type_bytes[32] = {0};
 

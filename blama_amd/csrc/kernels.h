@@ -251,9 +251,9 @@ void launch_gemm_mmq(const GemmParams& p, const Q8Rows& act, hipStream_t s);
 // input (launch_quant_act), then v_mfma_i32_32x32x32_i8 per sub-block (launch_mmq32).
 constexpr int UB_MAX = 512;    // n_ubatch (reference Instance.hpp:24)
 struct ActQ8 {
-    int8_t* q;                 // [npad][K]
+    int8_t* q;                 // [npad/32][K/256][8][64][16]: MFMA A fragments (mmq.hip quant_act_kernel)
     float* dT;                 // [K/256][npad]  (Q8_K d, token-minor)
-    int8_t* bsb;               // [npad][K/256][16]: sub-block bsums as 64*hi + lo (bytes 0-7 hi, 8-15 lo)
+    int8_t* bsb;               // [npad/32][K/256][32][16]: sub-block bsums as 64*hi + lo (bytes 0-7 hi, 8-15 lo)
     int K;
     int ntok, npad;            // tokens; rows allocated (ntok rounded up to 32, <= UB_MAX)
 };
@@ -262,6 +262,12 @@ void launch_quant_act(const float* x, int x_stride, const float* norm_w, float e
 void launch_rope_table(const int* tokpos, int ntok, int n_rot, float theta_scale, float freq_scale,
                        const float* freq_factors, float2* out, hipStream_t s);
 bool mmq32_supported(int type);
+// Bytes of one 32-row x superblock tile of the MFMA-order copy; total bytes of a copy of A
+// (pair = gate/up: A and B in one copy, 16 rows of each per tile).
+int mmq32_tile_bytes(int type);
+size_t mmq32_copy_bytes(const QMat& A, bool pair);
+// Builds the MFMA-order copy of A (and B for a pair) into dst from the planes.
+void launch_mmq32_swizzle(const QMat& A, const QMat* B, uint8_t* dst, hipStream_t s);
 // GemmParams: A (B = up for PAIR_AB / EPI_SWIGLU), epi, K, out/out_stride, resid, tokpos [ntok][4],
 // RoPE fields (rope table from launch_rope_table), caches; the tokens are act's.
 void launch_mmq32(const GemmParams& p, const ActQ8& act, const float2* rope, hipStream_t s);

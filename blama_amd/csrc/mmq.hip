@@ -16,13 +16,16 @@
 //   D: lane l, register r  = token (r&3) + 8(r>>2) + 4(l>>5), weight row l&31
 // (the k order inside an MFMA does not matter: A and B share it; scripts/exp_mfma_layout.cpp
 // checks the D map).  So every lane owns ONE weight row: its sub-block scales and mins are
-// per-lane scalars, and the scale multiply is one v_mad per result.
+// per-lane scalars, and the scale multiply is one full-rate v_mad_i32_i24 per result (|dot| < 2^17,
+// |scale| < 2^7: the 24-bit product is exact; a plain int multiply would be quarter-rate
+// v_mul_lo_u32).  The per-superblock float update is fused (fmaf): only fp32 rounding differs.
 // A workgroup is 4 waves over one tile of 32 weight rows (16 gate/up pairs for SwiGLU) x 128
 // tokens; the waves split the superblocks, and their partial sums meet in LDS in wave order
 // (deterministic), after which wave w runs the epilogue of token tile w.  The 4 token groups
 // of a row tile are placed on one XCD (blockIdx % 8), so their weight reads share its L2.
 #include "kernels.h"
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 
 namespace mi {
 namespace mmq {
@@ -68,8 +71,8 @@ __device__ __forceinline__ float wave_max_pos(float v) {
 
 // ---------------------------------------------------------------------------
 // Activation rows -> Q8_K (quantize_row_q8_K_ref), one workgroup per token row.
-// Writes q [npad][K], d transposed [nb][npad] (4 consecutive tokens = one 16-B load in the
-// GEMM), and per superblock the 8 sub-block bsums split as 64*hi + lo (hi = floor(b/64),
+// Writes q in MFMA-fragment order (below), d transposed [nb][npad] (4 consecutive tokens = one
+// 16-B load in the GEMM), and per superblock the 8 sub-block bsums split as 64*hi + lo (hi = floor(b/64),
 // lo in 0..63): bytes 0-7 hi_j, 8-15 lo_j -- the int8 A operand of the MFMA that forms
 // sum_j m_j*bsum_j = 64*sum m_j hi_j + sum m_j lo_j exactly.  Rows ntok..npad-1 are zero.
 // ---------------------------------------------------------------------------
@@ -79,12 +82,18 @@ __global__ __launch_bounds__(256) void quant_act_kernel(const float* x, int x_st
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int nb = a.K >> 8;
     __shared__ double red[4];
-    int8_t* q = a.q + (long long)t * a.K;
-    int8_t* bsb = a.bsb + (long long)t * nb * 16;
+    // MFMA-fragment order (one wave load = 1 KiB contiguous): q [tile][sb][j][h*32 + t%32][16 B],
+    // element 32j + 16h + e of superblock sb of token t at byte e; bsb [tile][sb][t%32][16 B]
+    const int tile = t >> 5, tr = t & 31;
+    const int fj = lane >> 3, fh = (lane >> 2) & 1, fw = lane & 3;   // this lane's 4 elements
+    int8_t* q = a.q + (long long)tile * nb * 8192 + fj * 1024 + (fh * 32 + tr) * 16 + 4 * fw;
+    int8_t* bsb = a.bsb + ((long long)tile * nb * 32 + tr) * 16;
     if (t >= a.ntok) {
-        for (int i = threadIdx.x; i < a.K / 4; i += 256) reinterpret_cast<int*>(q)[i] = 0;
-        for (int i = threadIdx.x; i < nb; i += 256) a.dT[(long long)i * a.npad + t] = 0.0f;
-        for (int i = threadIdx.x; i < nb * 4; i += 256) reinterpret_cast<int*>(bsb)[i] = 0;
+        for (int blk = wave; blk < nb; blk += 4) {
+            *reinterpret_cast<int*>(q + blk * 8192) = 0;
+            if (lane < 4) reinterpret_cast<int*>(bsb + blk * 512)[lane] = 0;
+            if (lane == 0) a.dT[(long long)blk * a.npad + t] = 0.0f;
+        }
         return;
     }
     const f32x4* x4 = reinterpret_cast<const f32x4*>(x + (long long)t * x_stride);
@@ -133,7 +142,7 @@ __global__ __launch_bounds__(256) void quant_act_kernel(const float* x, int x_st
             for (int k = 0; k < 4; ++k) qv[k] = min(127, (int)rintf(iscale * v[k]));
             d = 1.0f / iscale;
         }
-        reinterpret_cast<int*>(q + blk * 256)[lane] =
+        *reinterpret_cast<int*>(q + blk * 8192) =
             (qv[0] & 0xFF) | ((qv[1] & 0xFF) << 8) | ((qv[2] & 0xFF) << 16) | ((qv[3] & 0xFF) << 24);
         // the 32-element sub-block sums: lanes 8j..8j+7
         int sm = (qv[0] + qv[1]) + (qv[2] + qv[3]);
@@ -142,8 +151,8 @@ __global__ __launch_bounds__(256) void quant_act_kernel(const float* x, int x_st
         sm += __shfl_xor(sm, 4, 64);   // the two quads of a sub-block
         if ((lane & 7) == 0) {
             const int j = lane >> 3;
-            bsb[blk * 16 + j] = (int8_t)(sm >> 6);          // floor(b/64), -64..63
-            bsb[blk * 16 + 8 + j] = (int8_t)(sm & 63);      // b - 64*floor(b/64), 0..63
+            bsb[blk * 512 + j] = (int8_t)(sm >> 6);          // floor(b/64), -64..63
+            bsb[blk * 512 + 8 + j] = (int8_t)(sm & 63);      // b - 64*floor(b/64), 0..63
         }
         if (lane == 0) a.dT[(long long)blk * a.npad + t] = d;
     }
@@ -187,9 +196,59 @@ __device__ __forceinline__ void q4k_scales(const u32x4 hd, int sc[8], int mn[8])
     }
 }
 
-template <int T, bool AB>
-__global__ __launch_bounds__(256, 2) void mmq32_t(const GemmParams P, const ActQ8 act, const float2* rope) {
-    __shared__ float red[KS][TT][16][64];   // 64 KiB: the waves' partial sums
+// MFMA-order weight copy: one 32-row x superblock tile (lane = h*32 + c holds row c's bytes of
+// k-half h; rows of a gate/up pair tile: c < 16 gate row 16*rt + c, c >= 16 up row 16*rt + c - 16)
+//   Q4_K  [p 4][lane 64][16] qs bytes 32p + 16h.. | [c 32][16] header                       4608 B
+//   Q6_K  [hf 2][cc 2][lane 64][16] ql bytes 64hf + 32cc + 16h.. | [hf 2][lane 64][16] qh bytes
+//         32hf + 16h.. | [c 32][16] scales | [c 32][2] d                                     6720 B
+__host__ __device__ constexpr int mmq32_tile_bytes_d(int type) { return type == T_Q4_K ? 4608 : type == T_Q6_K ? 6720 : 0; }
+
+__global__ void swizzle_kernel(const QMat A, const QMat B, int pair, uint8_t* dst) {
+    const int nb = A.nb;
+    const long long tile = blockIdx.x;   // rt * nb + sb
+    const int rt = (int)(tile / nb), sb = (int)(tile % nb);
+    const int TB = mmq32_tile_bytes_d(A.type);
+    uint8_t* o = dst + tile * TB;
+    for (int off = threadIdx.x; off < TB; off += blockDim.x) {
+        int plane, c, byte;
+        if (A.type == T_Q4_K) {
+            if (off < 4096) {
+                const int p = off >> 10, ln = (off >> 4) & 63, e = off & 15;
+                plane = 0; c = ln & 31; byte = 32 * p + 16 * (ln >> 5) + e;
+            } else {
+                plane = 1; c = (off - 4096) >> 4; byte = (off - 4096) & 15;
+            }
+        } else {
+            if (off < 4096) {
+                const int f = off >> 10, ln = (off >> 4) & 63, e = off & 15;
+                plane = 0; c = ln & 31; byte = 64 * (f >> 1) + 32 * (f & 1) + 16 * (ln >> 5) + e;
+            } else if (off < 6144) {
+                const int f = (off - 4096) >> 10, ln = ((off - 4096) >> 4) & 63, e = off & 15;
+                plane = 1; c = ln & 31; byte = 32 * f + 16 * (ln >> 5) + e;
+            } else if (off < 6656) {
+                plane = 2; c = (off - 6144) >> 4; byte = (off - 6144) & 15;
+            } else {
+                plane = 3; c = (off - 6656) >> 1; byte = (off - 6656) & 1;
+            }
+        }
+        const QMat& M = (pair && c >= 16) ? B : A;
+        long long row = pair ? 16LL * rt + (c & 15) : 32LL * rt + c;
+        if (row >= M.rows) row = M.rows - 1;
+        const int pb = A.type == T_Q4_K ? (plane == 0 ? 128 : 16) : (plane == 0 ? 128 : plane == 1 ? 64 : plane == 2 ? 16 : 2);
+        o[off] = M.p[plane][(row * nb + sb) * pb + byte];
+    }
+}
+
+template <bool AB>
+__device__ __forceinline__ void mmq_epilogue(const GemmParams& P, const ActQ8& act, const float2* rope, int ttok0,
+                                             int lane, int row, const float v[16]);
+
+// KSPLIT 4: the 4 waves split the superblocks of all 4 token tiles (partials meet in LDS);
+// KSPLIT 1: wave w owns token tile w over all superblocks (no LDS; the 4 waves read the same
+// weight bytes, L1/L2 hits).  OCC: waves per SIMD the register budget is sized for.
+template <int T, bool AB, int KSPLIT, int OCC>
+__global__ __launch_bounds__(256, OCC) void mmq32_t(const GemmParams P, const ActQ8 act, const float2* rope) {
+    __shared__ float red[KSPLIT > 1 ? KS : 1][KSPLIT > 1 ? TT : 1][16][64];   // 64 KiB: partial sums
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int col = lane & 31, h = lane >> 5;
@@ -201,55 +260,53 @@ __global__ __launch_bounds__(256, 2) void mmq32_t(const GemmParams P, const ActQ
     const int rt = (slot / ntg) * 8 + xcd, tg = slot % ntg;
     if (rt >= nrt) return;
     // this lane's weight row
-    const QMat& M = (AB && col >= 16) ? P.B : P.A;
     const int row = AB ? rt * 16 + (col & 15) : rt * 32 + col;
-    const long long rl = row < M.rows ? row : M.rows - 1;   // tail lanes re-read a valid row
-    const int sb0 = nb * w / KS, sb1 = nb * (w + 1) / KS;
+    const int sb0 = KSPLIT > 1 ? nb * w / KS : 0, sb1 = KSPLIT > 1 ? nb * (w + 1) / KS : nb;
     const int tok0 = tg * 32 * TT;
     int ntt = (act.npad - tok0) / 32;
     ntt = ntt > TT ? TT : ntt;
+    const int t_begin = KSPLIT > 1 ? 0 : w, t_end = KSPLIT > 1 ? ntt : (w < ntt ? w + 1 : w);
 
     // token tiles outer (one 16-register accumulator live), superblocks inner; the weight
     // fragments of a superblock are re-read per token tile (L1/L2 hits after the first)
-    for (int t = 0; t < ntt; ++t) {
+    for (int t = t_begin; t < t_end; ++t) {
         float y[16];
 #pragma unroll
         for (int r = 0; r < 16; ++r) y[r] = 0.0f;
-        const int ta = tok0 + 32 * t + col;   // A-operand token of this lane
         for (int sb = sb0; sb < sb1; ++sb) {
-            const long long wsb = rl * nb + sb;
-            const int8_t* aq = act.q + (long long)ta * P.K + sb * 256 + 16 * h;
+            const int8_t* aq = act.q + ((long long)(tok0 / 32 + t) * nb + sb) * 8192 + lane * 16;
             const float* dT = act.dT + (long long)sb * act.npad + tok0 + 32 * t + 4 * h;
             int S[16];
 #pragma unroll
             for (int r = 0; r < 16; ++r) S[r] = 0;
+            const uint8_t* wt = P.A.sw + ((long long)rt * nb + sb) * mmq32_tile_bytes_d(T);
             if (T == T_Q4_K) {
                 // qs[32p + l]: low nibble = sub-block 2p element l, high nibble = sub-block 2p+1
-                const u32x4 hd = *gp(reinterpret_cast<const u32x4*>(M.p[1] + wsb * 16));
+                const u32x4 hd = *gp(reinterpret_cast<const u32x4*>(wt + 4096 + col * 16));
                 int sc[8], mn[8];
                 q4k_scales(hd, sc, mn);
 #pragma unroll
                 for (int p = 0; p < 4; ++p) {
-                    const u32x4 wq = *gp(reinterpret_cast<const u32x4*>(M.p[0] + wsb * 128 + 32 * p + 16 * h));
+                    const u32x4 wq = *gp(reinterpret_cast<const u32x4*>(wt + p * 1024 + lane * 16));
                     const v4i blo = v4i{(int)(wq.x & 0x0F0F0F0Fu), (int)(wq.y & 0x0F0F0F0Fu), (int)(wq.z & 0x0F0F0F0Fu),
                                         (int)(wq.w & 0x0F0F0F0Fu)};
                     const v4i bhi = v4i{(int)((wq.x >> 4) & 0x0F0F0F0Fu), (int)((wq.y >> 4) & 0x0F0F0F0Fu),
                                         (int)((wq.z >> 4) & 0x0F0F0F0Fu), (int)((wq.w >> 4) & 0x0F0F0F0Fu)};
-                    const v4i a0 = *gp(reinterpret_cast<const v4i*>(aq + 64 * p));
-                    const v4i a1 = *gp(reinterpret_cast<const v4i*>(aq + 64 * p + 32));
+                    const v4i a0 = *gp(reinterpret_cast<const v4i*>(aq + (2 * p) * 1024));
+                    const v4i a1 = *gp(reinterpret_cast<const v4i*>(aq + (2 * p + 1) * 1024));
                     const v16i d0 = mfma(a0, blo);
 #pragma unroll
-                    for (int r = 0; r < 16; ++r) S[r] += sc[2 * p] * d0[r];
+                    for (int r = 0; r < 16; ++r) S[r] = __mul24(sc[2 * p], d0[r]) + S[r];
                     const v16i d1 = mfma(a1, bhi);
 #pragma unroll
-                    for (int r = 0; r < 16; ++r) S[r] += sc[2 * p + 1] * d1[r];
+                    for (int r = 0; r < 16; ++r) S[r] = __mul24(sc[2 * p + 1], d1[r]) + S[r];
                 }
                 // sum_j m_j*bsum_j: mins as int8 B operands, k 0-7 (against hi) / k 8-15 (against lo)
                 const int m03 = mn[0] | (mn[1] << 8) | (mn[2] << 16) | (mn[3] << 24);
                 const int m47 = mn[4] | (mn[5] << 8) | (mn[6] << 16) | (mn[7] << 24);
                 const v4i bm1 = h == 0 ? v4i{m03, m47, 0, 0} : v4i{0, 0, 0, 0};
                 const v4i bm2 = h == 0 ? v4i{0, 0, m03, m47} : v4i{0, 0, 0, 0};
-                const v4i ab = h == 0 ? *gp(reinterpret_cast<const v4i*>(act.bsb + ((long long)ta * nb + sb) * 16))
+                const v4i ab = h == 0 ? *gp(reinterpret_cast<const v4i*>(act.bsb + (((long long)(tok0 / 32 + t) * nb + sb) * 32 + col) * 16))
                                       : v4i{0, 0, 0, 0};
                 const v16i x1 = mfma(ab, bm1);
                 const v16i x2 = mfma(ab, bm2);
@@ -262,18 +319,18 @@ __global__ __launch_bounds__(256, 2) void mmq32_t(const GemmParams P, const ActQ
                     for (int i = 0; i < 4; ++i) {
                         const int r = 4 * g + i;
                         const float d = dr * dx[i], dm = dmr * dx[i];
-                        y[r] += d * (float)S[r] - dm * (float)(64 * x1[r] + x2[r]);
+                        y[r] = fmaf(-dm, (float)(64 * x1[r] + x2[r]), fmaf(d, (float)S[r], y[r]));
                     }
                 }
             } else {   // Q6_K: ql[128] qh[64] scales[16] d
-                const u32x4 scw = *gp(reinterpret_cast<const u32x4*>(M.p[2] + wsb * 16));
+                const u32x4 scw = *gp(reinterpret_cast<const u32x4*>(wt + 6144 + col * 16));
                 const unsigned scv[4] = {scw.x, scw.y, scw.z, scw.w};
 #pragma unroll
                 for (int hf = 0; hf < 2; ++hf) {
-                    const u32x4 H = *gp(reinterpret_cast<const u32x4*>(M.p[1] + wsb * 64 + 32 * hf + 16 * h));
+                    const u32x4 H = *gp(reinterpret_cast<const u32x4*>(wt + 4096 + hf * 1024 + lane * 16));
 #pragma unroll
                     for (int c = 0; c < 2; ++c) {
-                        const u32x4 L = *gp(reinterpret_cast<const u32x4*>(M.p[0] + wsb * 128 + 64 * hf + 32 * c + 16 * h));
+                        const u32x4 L = *gp(reinterpret_cast<const u32x4*>(wt + (2 * hf + c) * 1024 + lane * 16));
 #pragma unroll
                         for (int nib = 0; nib < 2; ++nib) {
                             // span (hf, qq): elements 128hf + 32qq + l; this lane's l = 16h + e
@@ -291,29 +348,34 @@ __global__ __launch_bounds__(256, 2) void mmq32_t(const GemmParams P, const ActQ
                             const int is = 2 * s;   // the span's scale groups 2s (k-half 0), 2s+1 (k-half 1)
                             const int g0 = (int)(signed char)((scv[is >> 2] >> (8 * (is & 3))) & 0xFF);
                             const int g1 = (int)(signed char)((scv[is >> 2] >> (8 * (is & 3) + 8)) & 0xFF);
-                            const v4i a = *gp(reinterpret_cast<const v4i*>(aq + 32 * s));
+                            const v4i a = *gp(reinterpret_cast<const v4i*>(aq + s * 1024));
                             const v16i d0 = mfma(a, h == 0 ? bf : z);
 #pragma unroll
-                            for (int r = 0; r < 16; ++r) S[r] += g0 * d0[r];
+                            for (int r = 0; r < 16; ++r) S[r] = __mul24(g0, d0[r]) + S[r];
                             const v16i d1 = mfma(a, h == 1 ? bf : z);
 #pragma unroll
-                            for (int r = 0; r < 16; ++r) S[r] += g1 * d1[r];
+                            for (int r = 0; r < 16; ++r) S[r] = __mul24(g1, d1[r]) + S[r];
                         }
                     }
                 }
-                const float dr = h2f(*gp(reinterpret_cast<const unsigned short*>(M.p[3] + wsb * 2)));
+                const float dr = h2f(*gp(reinterpret_cast<const unsigned short*>(wt + 6656 + col * 2)));
 #pragma unroll
                 for (int g = 0; g < 4; ++g) {
                     const f32x4 dx4 = *gp(reinterpret_cast<const f32x4*>(dT + 8 * g));
                     const float dx[4] = {dx4.x, dx4.y, dx4.z, dx4.w};
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) y[4 * g + i] += (dr * dx[i]) * (float)S[4 * g + i];
+                    for (int i = 0; i < 4; ++i) y[4 * g + i] = fmaf(dr * dx[i], (float)S[4 * g + i], y[4 * g + i]);
                 }
             }
         }
+        if (KSPLIT > 1) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) red[w][t][r][lane] = y[r];
+            for (int r = 0; r < 16; ++r) red[w][t][r][lane] = y[r];
+        } else {
+            mmq_epilogue<AB>(P, act, rope, tok0 + 32 * t, lane, row, y);
+        }
     }
+    if (KSPLIT == 1) return;
     // ---- the superblock splits meet in LDS, in wave order
     __syncthreads();
     const int t = w;   // this wave's epilogue: token tile w
@@ -321,11 +383,19 @@ __global__ __launch_bounds__(256, 2) void mmq32_t(const GemmParams P, const ActQ
     float v[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) v[r] = ((red[0][t][r][lane] + red[1][t][r][lane]) + red[2][t][r][lane]) + red[3][t][r][lane];
+    mmq_epilogue<AB>(P, act, rope, tok0 + 32 * t, lane, row, v);
+}
+
+// The epilogue of one 32-token x 32-row D tile (v: this lane's 16 results).
+template <bool AB>
+__device__ __forceinline__ void mmq_epilogue(const GemmParams& P, const ActQ8& act, const float2* rope, int ttok0,
+                                             int lane, int row, const float v[16]) {
+    const int col = lane & 31, h = lane >> 5;
     const int epi = P.epi;
     const bool roped = epi == EPI_ROPE_Q || epi == EPI_ROPE_K;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-        const int tok = tok0 + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int tok = ttok0 + (r & 3) + 8 * (r >> 2) + 4 * h;
         const float pv = __shfl_xor(v[r], AB ? 16 : 1, 64);   // SwiGLU partner / RoPE partner
         if (tok >= act.ntok) continue;
         if (AB) {
@@ -382,6 +452,21 @@ void launch_rope_table(const int* tokpos, int ntok, int n_rot, float theta_scale
 
 bool mmq32_supported(int type) { return type == T_Q4_K || type == T_Q6_K; }
 
+int mmq32_tile_bytes(int type) { return mmq::mmq32_tile_bytes_d(type); }
+
+size_t mmq32_copy_bytes(const QMat& A, bool pair) {
+    const long long nrt = pair ? (A.rows + 15) / 16 : (A.rows + 31) / 32;
+    return (size_t)nrt * A.nb * mmq32_tile_bytes(A.type);
+}
+
+void launch_mmq32_swizzle(const QMat& A, const QMat* B, uint8_t* dst, hipStream_t s) {
+    if (!mmq32_supported(A.type)) throw Error("mmq32 swizzle: Q4_K / Q6_K only");
+    if (B && (B->type != A.type || B->rows != A.rows || B->K != A.K)) throw Error("mmq32 swizzle: bad pair");
+    const long long nrt = B ? (A.rows + 15) / 16 : (A.rows + 31) / 32;
+    hipLaunchKernelGGL(mmq::swizzle_kernel, dim3((unsigned)(nrt * A.nb)), dim3(256), 0, s, A, B ? *B : A, B ? 1 : 0, dst);
+    MI_HIP(hipGetLastError());
+}
+
 void launch_mmq32(const GemmParams& p, const ActQ8& act, const float2* rope, hipStream_t s) {
     if (!mmq32_supported(p.A.type)) throw Error("mmq32: Q4_K / Q6_K only");
     if (act.K != p.K || p.A.K != p.K) throw Error("mmq32: activation length differs from K");
@@ -392,12 +477,22 @@ void launch_mmq32(const GemmParams& p, const ActQ8& act, const float2* rope, hip
     if ((p.epi == EPI_ROPE_Q || p.epi == EPI_ROPE_K) && (!rope || p.head_dim % 2 || p.n_rot > p.head_dim))
         throw Error("mmq32: RoPE epilogue needs the rope table");
     if (act.ntok < 1 || act.npad % 32 || act.npad > UB_MAX) throw Error("mmq32: bad token count");
+    if (!p.A.sw) throw Error("mmq32: the matrix has no MFMA-order copy");
     const int ntg = (act.npad + 32 * mmq::TT - 1) / (32 * mmq::TT);
     const int nrt = ab ? (p.A.rows + 15) / 16 : (p.A.rows + 31) / 32;
     const int grid = (nrt + 7) / 8 * 8 * ntg;
-    decltype(&mmq::mmq32_t<T_Q4_K, false>) fn;
-    if (p.A.type == T_Q4_K) fn = ab ? mmq::mmq32_t<T_Q4_K, true> : mmq::mmq32_t<T_Q4_K, false>;
-    else fn = ab ? mmq::mmq32_t<T_Q6_K, true> : mmq::mmq32_t<T_Q6_K, false>;
+    // MI_MMQ=<v>: 0 = K split over the waves (2 waves/SIMD), 1 (default) = a token tile per wave over
+    // all superblocks at 2 waves/SIMD, 2 = the same at 3 waves/SIMD.  Measured on the 7B 512-token
+    // prefill: 21.97 / 21.19 / 22.69 ms (profiles/r02_prefill_*).
+    static const int var = getenv("MI_MMQ") ? atoi(getenv("MI_MMQ")) : 1;
+    decltype(&mmq::mmq32_t<T_Q4_K, false, 4, 2>) fn;
+#define MMQ_PICK(KS_, OCC_)                                                                              \
+    fn = p.A.type == T_Q4_K ? (ab ? mmq::mmq32_t<T_Q4_K, true, KS_, OCC_> : mmq::mmq32_t<T_Q4_K, false, KS_, OCC_>) \
+                            : (ab ? mmq::mmq32_t<T_Q6_K, true, KS_, OCC_> : mmq::mmq32_t<T_Q6_K, false, KS_, OCC_>)
+    if (var == 1) MMQ_PICK(1, 2);
+    else if (var == 2) MMQ_PICK(1, 3);
+    else MMQ_PICK(4, 2);
+#undef MMQ_PICK
     hipLaunchKernelGGL(fn, dim3(grid), dim3(256), 0, s, p, act, rope);
     MI_HIP(hipGetLastError());
 }

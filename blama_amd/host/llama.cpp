@@ -1,6 +1,5 @@
 // bl::llama host surface on the MI355X engine (see llama.hpp for the mirrored reference files).
 #include "llama.hpp"
-#include <cstdlib>
 
 #include "mi_engine.h"
 
@@ -501,13 +500,13 @@ std::vector<TokenPrediction> Session::fillCtx(std::span<TokenPrediction> tokens)
     // (Session.cpp:231-244).  When no context shift or Self-Extend step can fall inside the
     // run, the same tokens go through mi_decode(MI_OUT_ALL) in n_batch chunks and row i holds
     // the distribution after token i -- what the i-th single-token decode leaves behind.
-    // BL_SERIAL_VERIFY=1 keeps the reference's per-token loop.
+    // Only with InitParams::batchedVerify (the serial loop below is bit-identical to generation).
     requireGenerating();
     flushPendingState();
     const uint32_t n = (uint32_t)tokens.size();
     const uint32_t batch = mi_n_batch(m_ctx);
-    if (n > 0 && m_params.gaFactor == 1 && m_state.numPast + n < mi_n_ctx(m_ctx) && batch > 0 &&
-        getenv("BL_SERIAL_VERIFY") == nullptr) {
+    if (m_params.batchedVerify && n > 0 && m_params.gaFactor == 1 && m_state.numPast + n < mi_n_ctx(m_ctx) &&
+        batch > 0) {
         for (const TokenPrediction& t : tokens) m_sampler->accept(t.token, false);
         for (uint32_t c0 = 0; c0 < n; c0 += batch) {
             const uint32_t nc = std::min(batch, n - c0);

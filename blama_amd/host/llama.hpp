@@ -170,6 +170,10 @@ public:
         std::string grammar;
         float temperature = 0.80f;
         float topP = 0.95f;
+        // fillCtx as one batched pass (mi_decode MI_OUT_ALL) instead of the reference's one decode
+        // per claimed token.  Off by default: the serial form is bit-identical to generation
+        // (t-integration.cpp:219-248); the batched rows match it within the GEMM's fp32 order.
+        bool batchedVerify = false;
     };
     Session(Instance& instance, mi_ctx* ctx, InitParams params);
     Session(const Session&) = delete;

@@ -1,5 +1,6 @@
 // bl::llama::server::Server: see server.hpp for the reference mapping.
 #include "server.hpp"
+#include <cstdlib>
 
 #include <cstdio>
 
@@ -71,8 +72,11 @@ void Server::completeText(CompleteRequestParams params, std::function<void(Compl
 
 void Server::verify(CompleteRequestParams req, CompleteReponse resp, std::function<void(float)> cb, ErrorCb onError) {
     post([this, req = std::move(req), resp = std::move(resp), cb = std::move(cb)] {
+        // the claimed tokens are pushed in one batched pass (BLAMA_SERIAL_VERIFY=1: one decode per
+        // token, as Session.cpp:231-244, bit-identical to this server's own generation)
+        static const bool batched = getenv("BLAMA_SERIAL_VERIFY") == nullptr;
         auto& session = m_instance->startSession({.seed = req.seed, .temperature = req.temperature,
-                                                  .topP = req.topP});
+                                                  .topP = req.topP, .batchedVerify = batched});
         session.setInitialPrompt(m_model->vocab().tokenize(req.prompt, true, true));
         std::vector<TokenPrediction> claimed;
         claimed.reserve(resp.size());

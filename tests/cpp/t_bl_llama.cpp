@@ -314,6 +314,39 @@ TEST_CASE_G("filling ctx", "gpu") {   // t-integration.cpp:219-248: bit-identica
     CHECK(score == 1.0f);
 }
 
+TEST_CASE_G("filling ctx batched", "gpu") {   // fillCtx as one MI_OUT_ALL pass vs generation
+    Model model(g_model, {});
+    Instance inst(model, {}), inst2(model, {});
+    auto& s = inst.startSession({});
+    auto& s2 = inst2.startSession({.batchedVerify = true});
+    s.setInitialPrompt(kPrompt);
+    s2.setInitialPrompt(kPrompt);
+    auto p = s.complete({.maxTokens = 24});
+    REQUIRE(p.size() > 0);
+    auto p2 = s2.fillCtx(p);
+    REQUIRE(p.size() == p2.size());
+    MetricsAggregator agg;
+    float score = 0;
+    for (size_t i = 0; i < p.size(); i++) {
+        REQUIRE(p2[i].logits.size() == p[i].logits.size());
+        CHECK(p2[i].token == p[i].token);
+        float rms = 0;
+        for (auto& l : p[i].logits) rms += l.logit * l.logit;
+        rms = std::sqrt(rms / p[i].logits.size());
+        for (auto& l : p[i].logits) {   // same ids (gathered), logits within the GEMM's fp32 order
+            auto it = std::find_if(p2[i].logits.begin(), p2[i].logits.end(), [&](const TokenData& d) { return d.token == l.token; });
+            REQUIRE(it != p2[i].logits.end());
+            CHECK(std::fabs(it->logit - l.logit) <= 4e-3f * rms);
+        }
+        auto m = LogitComparer::compare(p[i].logits, p2[i].logits);
+        CHECK(m.top1Match == 1.0f);
+        score = agg.pushAndVerify({&m, 1});
+    }
+    CHECK(score >= 0.999f);
+    // the batch decoded every claimed token: prompt + claimed cells in the cache
+    CHECK(mi_kv_n_cells(inst2.mctx()) == (int32_t)(kPrompt.size() + p.size()));
+}
+
 TEST_CASE_G("states", "gpu") {   // t-integration.cpp:304-421
     Model model(g_model, {});
     Instance inst(model, {});

@@ -77,13 +77,33 @@ def test_out_all_batch_vs_serial(gpu_lib, monkeypatch):
     b = engine.Context(m, n_ctx=64)
     b.decode(prompt)
     b.decode(claimed, all_logits=True)
-    # each path is within LOGIT_TOL of the oracle (test above), so within 2x of each other
-    for i in range(len(claimed)):
-        assert _close(a.logits(row=i), b.logits(row=i), 2 * LOGIT_TOL), i
+    # both paths against the oracle row by row, and against each other through the
+    # reference's gate (identical top-1, LogitComparer score)
+    orc = oracle_from_gguf(buf, n_ctx=64)
+    orc.decode(prompt)
+    agg = R.MetricsAggregator()
+    errs = []
+    for i, t in enumerate(claimed):
+        ref = orc.decode_one(t)
+        rms = float(np.sqrt(np.mean(ref.astype(np.float64) ** 2)))
+        la, lb = a.logits(row=i), b.logits(row=i)
+        errs.append((float(np.max(np.abs(la - ref))) / rms, float(np.max(np.abs(lb - ref))) / rms))
+        # the serial path is the decode graphs (LOGIT_TOL); a batch row may carry one Q8_K
+        # rounding flip from the GEMM's fp32 order (measured: one row of 33 at 4.6e-3)
+        assert _close(lb, ref) and _close(la, ref, 5 * LOGIT_TOL), (i, errs[-1])
+        ia, va = a.topk(10, row=i)
+        ib, vb = b.topk(10, row=i)
+        assert ia[0] == ib[0]
+        score = agg.push_and_verify([R.compare([(int(x), float(v)) for x, v in zip(ia, va)],
+                                               [(int(x), float(v)) for x, v in zip(ib, vb)])])
+    print("max |dlogit|/rms per row (batch, serial):", max(e[0] for e in errs), max(e[1] for e in errs))
+    assert sum(e[0] > LOGIT_TOL for e in errs) <= len(errs) // 16
+    assert score >= 0.99
     for t in [5, 6]:   # caches written by the batch serve later steps
         a.decode([t])
         b.decode([t])
-        assert _close(a.logits(), b.logits(), 2 * LOGIT_TOL)
+        ref = orc.decode_one(t)
+        assert _close(a.logits(), ref) and _close(b.logits(), ref)
 
 
 def test_out_all_row_bounds(gpu_lib):

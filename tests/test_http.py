@@ -6,7 +6,7 @@ CPU: env validation fails with the reference's messages (HttpServerMain.cpp:383-
 GPU work.
 GPU: a synthetic model served on 127.0.0.1.
   - /complete returns the wire format.
-  - Verifying the completion with the server itself scores exactly 1.
+  - Verifying the completion with the server itself scores 1 (to fp32 order on the MFMA batch path).
   - A tampered completion scores lower.
   - The CPU oracle verifies the same HTTP completion like Session::fillCtx (score >= 0.95).
   - Non-POST gives 400, an unknown path 404, a malformed body 500."""
@@ -132,10 +132,13 @@ def test_http_complete_and_verify(served):
     for t in toks:
         lg = [l["logit"] for l in t["logits"]]
         assert len(lg) == 10 and lg == sorted(lg, reverse=True)
-    # self-verification through the wire format scores exactly 1 (Server.cpp:127-161)
+    # self-verification through the wire format (Server.cpp:127-161).  The server pushes the
+    # claimed tokens in one batched pass (mi_decode MI_OUT_ALL on the int8-MFMA GEMM for this
+    # Q4_K_M model), whose rows match its own GEMV generation within fp32 summation order:
+    # the score is 1 up to that (exactly 1 with BLAMA_SERIAL_VERIFY=1, the reference's loop)
     st, body, _ = _post(port, "/verify_completion", {"request": req, "response": out})
     assert st == 200, body
-    assert json.loads(body)["result"] == 1.0
+    assert json.loads(body)["result"] >= 0.999
     # tampered logits score lower
     bad = json.loads(json.dumps(out))
     for t in bad["tokenData"]:
@@ -177,7 +180,8 @@ def test_http_tinyllama_complete_32_verified_by_oracle(served_tinyllama):
     """/complete of 32 tokens on the TinyLlama-shaped Q8_0 model, then the C restatement of the
     CPU path verifies the completion as Session::fillCtx would (Session.cpp:231-282) under the
     reference's gate (t-LogitComparer.cpp:76-78), and the server's own /verify_completion of it
-    scores exactly 1."""
+    scores exactly 1 (Q8_0 has no MFMA batch path: the batched verify runs the same per-token
+    decode graphs as generation)."""
     import ggml_cpu
     port, buf = served_tinyllama
     req = {"prompt": "the quick brown fox", "max_tokens": 32, "seed": 3, "temp": 0.8, "top_p": 0.95}
