@@ -448,6 +448,7 @@ Ctx::Ctx(Model* model, uint32_t nctx, uint32_t nbatch, uint32_t nubatch) : m(mod
                     mmq_ok = mmq_ok && mmq32_supported(q->type);
             out_mmq = mmq_ok && mmq32_supported(m->output.type);
             if (mmq_ok) m->ensure_mmq_copies();
+            attn_mfma = attn_mfma_supported(hp.head_dim) && getenv("MI_ATTN_VALU") == nullptr;
             MI_HIP(hipMalloc(&ub_q, (size_t)UB_MAX * kmax));
             MI_HIP(hipMalloc(&ub_dT, (size_t)UB_MAX * (kmax / 256) * sizeof(float)));
             MI_HIP(hipMalloc(&ub_bsb, (size_t)UB_MAX * (kmax / 256) * 16));
@@ -927,7 +928,8 @@ void Ctx::decode_ubatch(const int32_t* tokens, int n, bool all) {
             }
             AttnParams a{qb, kl, vl, tokpos_b, cell_pos, attn_scores, attn_smax, attnb, hp.n_head, hp.n_head_kv,
                          hp.head_dim, kv_dim, (int)n_ctx, kq_scale};
-            launch_attn_multi(a, nt, attnb, stream);
+            if (attn_mfma) launch_attn_mfma(a, nt, attnb, stream);
+            else launch_attn_multi(a, nt, attnb, stream);
             {   // output projection + residual
                 launch_quant_act(attnb, hp.n_embd, nullptr, hp.eps, a_embd, stream);
                 GemmParams p = b;
@@ -1005,7 +1007,9 @@ int Ctx::decode(const int32_t* tokens, int n, bool all) {
     // prompt ingestion through the batched GEMM when the context stays within the fused
     // attention's reach (dense models; MI_NO_BATCH=1 forces token-by-token decode)
     const bool fits = n >= 2 && batch_ok && n_cells + n <= ATTN_SHORT && prof_layer < 0;
-    if (fits && mmq_ok && (!all || out_mmq)) {
+    // the MFMA batch path attends over any number of cells with the MFMA attention kernel
+    const bool ub = n >= 2 && batch_ok && mmq_ok && prof_layer < 0 && (attn_mfma || n_cells + n <= ATTN_SHORT);
+    if (ub && (!all || out_mmq)) {
         decode_ubatch(tokens, n, all);
         if (all) out_rows = n;
         return 0;

@@ -246,6 +246,11 @@ bool mmq_supported(int type);
 // GemmParams as for launch_gemm (ntok <= MMQ_NT; pro/x/norm ignored: the activations are `act`)
 void launch_gemm_mmq(const GemmParams& p, const Q8Rows& act, hipStream_t s);
 
+// ---- causal attention of ntok query tokens (q [ntok][n_head*hd]) on f16 MFMA (attn_mfma.hip):
+// any number of cells (<= n_ctx); out [ntok][n_head*hd]; head_dim 64 or 128 ----
+bool attn_mfma_supported(int head_dim);
+void launch_attn_mfma(const AttnParams& p, int ntok, float* out, hipStream_t s);
+
 // ---- int8-MFMA GEMM over a physical batch of up to UB_MAX tokens (mmq.hip) ----
 // Prompt ingestion and batched verification: activations quantised to Q8_K once per matrix
 // input (launch_quant_act), then v_mfma_i32_32x32x32_i8 per sub-block (launch_mmq32).

@@ -118,3 +118,28 @@ def test_out_all_row_bounds(gpu_lib):
     ctx.topk(5, row=0)
     with pytest.raises(engine.EngineError):
         ctx.topk(5, row=1)
+
+
+def test_long_prompt_batches_match_cpu_oracle(gpu_lib):
+    """Prompt ingestion past 512 cells in 512-token physical batches (the reference's n_ubatch,
+    Instance.hpp:24): 1100 tokens = 512 + 512 + 76, each batch attending over every earlier cell
+    on the MFMA attention kernel; then a batched verification of 40 more tokens at cells
+    1100-1139.  Checked against the C restatement of the CPU path."""
+    import ggml_cpu
+    cfg = synthetic.CONFIGS["tiny1-q4_k_m"]
+    buf = synthetic.build_gguf(cfg, seed=41)
+    m = engine.Model(buf)
+    rng = np.random.default_rng(12)
+    prompt = [int(t) for t in rng.integers(0, cfg.n_vocab, 1100)]
+    claimed = [int(t) for t in rng.integers(0, cfg.n_vocab, 40)]
+    ctx = engine.Context(m, n_ctx=1200)
+    ctx.decode(prompt)
+    orc = ggml_cpu.Model(buf, n_ctx=1200)
+    ref = orc.decode(prompt)
+    assert _close(ctx.logits(), ref)
+    assert [int(i) for i in ctx.topk(10)[0]] == [j for j, _ in R.topk(ref, 10)]
+    ctx.decode(claimed, all_logits=True)
+    for i, t in enumerate(claimed):
+        ref = orc.decode_one(t)
+        assert _close(ctx.logits(row=i), ref, 5 * LOGIT_TOL), i
+        assert int(ctx.topk(1, row=i)[0][0]) == R.topk(ref, 1)[0][0], i
