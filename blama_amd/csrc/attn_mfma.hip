@@ -10,8 +10,9 @@
 // three passes over the cells (max, sum, weighted V) -- an online softmax would round p
 // before the sum is known.  Only fp32 summation orders differ from the CPU.
 //
-// Geometry.  A workgroup is one query head x 128 tokens (4 waves, a 32-token tile each); the
-// 32-cell chunks of K and V are staged once per workgroup in LDS (V transposed) and shared.
+// Geometry.  A workgroup is one query head x 64 tokens (2 waves, a 32-token tile each); the
+// 32-cell chunks of K and V are staged once per workgroup in LDS (V transposed) and shared,
+// the next chunk's loads in flight while the current one is computed.
 // S^T = K Q^T per chunk (D: lane = token, registers = cells), so a token's softmax statistics
 // are lane-local, and S^T's registers are directly the B operand of O^T = V^T P^T (the
 // accumulator-as-operand idiom: element j of k-step s = register 8s + j = cell
@@ -27,7 +28,7 @@ typedef float f16x16 __attribute__((ext_vector_type(16)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 
-constexpr int WT = 4;          // token tiles (waves) per workgroup
+constexpr int WT = 2;          // token tiles (waves) per workgroup
 constexpr int CH = 32;         // cells per chunk
 
 __device__ __forceinline__ unsigned pack2(float a, float b) {
@@ -37,7 +38,7 @@ __device__ __forceinline__ unsigned pack2(float a, float b) {
 __device__ __forceinline__ half8 as_h8(u32x4 v) { return __builtin_bit_cast(half8, v); }
 
 template <int HD>
-__global__ __launch_bounds__(256) void attn_mfma_kernel(const AttnParams P, int ntok, float* out) {
+__global__ __launch_bounds__(64 * WT) void attn_mfma_kernel(const AttnParams P, int ntok, float* out) {
     constexpr int KS = HD / 16;          // k-steps of KQ
     constexpr int HB = HD / 32;          // 32-wide output blocks
     constexpr int KST = HD + 8;          // K row stride (halfs): 16-B aligned, staggered banks
@@ -88,20 +89,39 @@ __global__ __launch_bounds__(256) void attn_mfma_kernel(const AttnParams P, int 
 #pragma unroll
         for (int r = 0; r < 16; ++r) o[b][r] = 0.0f;
 
+    constexpr int SEG = HD / 8;                     // 16-B pieces per cell row
+    constexpr int NPC = CH * SEG / (64 * WT);       // pieces per thread per chunk
+    static_assert(CH * SEG % (64 * WT) == 0, "chunk pieces split evenly over the threads");
     for (int pass = 0; pass < 3; ++pass) {
-        for (int c0 = 0; c0 < ncell; c0 += CH) {
-            // ---- stage K (and V^T in the last pass) of cells c0 .. c0+31, and their positions
-            __syncthreads();
-            constexpr int SEG = HD / 8;                 // 16-B pieces per cell row
-            for (int pc = tid; pc < CH * SEG; pc += 256) {
+        // the next chunk's K (and V) in registers, issued before the current chunk is computed
+        u32x4 kr[NPC], vr_[NPC];
+        int cpr = 0;
+        auto fetch = [&](int c0) {
+#pragma unroll
+            for (int i = 0; i < NPC; ++i) {
+                const int pc = tid + 64 * WT * i;
                 const int cl = pc / SEG, sg = pc % SEG;
                 const int c = min(c0 + cl, P.n_ctx - 1);
                 const long long ga = (long long)c * P.kv_dim + (long long)g * HD + sg * 8;
-                *reinterpret_cast<u32x4*>(&ks[cl * KST + sg * 8]) = *reinterpret_cast<const u32x4*>(P.kcache + ga);
+                kr[i] = *reinterpret_cast<const u32x4*>(P.kcache + ga);
                 if (pass == 2) {   // cells past the batch's last are zero (p = 0 there; 0 * stale bits)
                     const u32x4 z = {0u, 0u, 0u, 0u};
-                    const u32x4 v = c0 + cl <= last_cell ? *reinterpret_cast<const u32x4*>(P.vcache + ga) : z;
-                    const unsigned vw[4] = {v.x, v.y, v.z, v.w};
+                    vr_[i] = c0 + cl <= last_cell ? *reinterpret_cast<const u32x4*>(P.vcache + ga) : z;
+                }
+            }
+            if (tid < CH) cpr = P.cell_pos[min(c0 + tid, P.n_ctx - 1)];
+        };
+        fetch(0);
+        for (int c0 = 0; c0 < ncell; c0 += CH) {
+            // ---- stage K (and V^T in the last pass) of cells c0 .. c0+31, and their positions
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < NPC; ++i) {
+                const int pc = tid + 64 * WT * i;
+                const int cl = pc / SEG, sg = pc % SEG;
+                *reinterpret_cast<u32x4*>(&ks[cl * KST + sg * 8]) = kr[i];
+                if (pass == 2) {
+                    const unsigned vw[4] = {vr_[i].x, vr_[i].y, vr_[i].z, vr_[i].w};
 #pragma unroll
                     for (int e = 0; e < 4; ++e) {
                         vt[(sg * 8 + 2 * e) * VST + cl] = __ushort_as_half((unsigned short)(vw[e] & 0xFFFFu));
@@ -109,8 +129,9 @@ __global__ __launch_bounds__(256) void attn_mfma_kernel(const AttnParams P, int 
                     }
                 }
             }
-            if (tid < CH) cps[tid] = P.cell_pos[min(c0 + tid, P.n_ctx - 1)];
+            if (tid < CH) cps[tid] = cpr;
             __syncthreads();
+            if (c0 + CH < ncell) fetch(c0 + CH);
             if (c0 > wlast) continue;                   // wave-uniform: nothing of this tile here
             // ---- S^T = K Q^T: lane = token, register r = cell c0 + (r&3) + 8(r>>2) + 4h
             f16x16 st;
@@ -186,8 +207,8 @@ void launch_attn_mfma(const AttnParams& p, int ntok, float* out, hipStream_t s) 
     if (ntok < 1) return;
     if (p.n_head % p.n_head_kv) throw Error("attn_mfma: n_head must be a multiple of n_head_kv");
     const dim3 grid(p.n_head, (ntok + 32 * amf::WT - 1) / (32 * amf::WT));
-    if (p.head_dim == 128) hipLaunchKernelGGL(amf::attn_mfma_kernel<128>, grid, dim3(256), 0, s, p, ntok, out);
-    else if (p.head_dim == 64) hipLaunchKernelGGL(amf::attn_mfma_kernel<64>, grid, dim3(256), 0, s, p, ntok, out);
+    if (p.head_dim == 128) hipLaunchKernelGGL(amf::attn_mfma_kernel<128>, grid, dim3(64 * amf::WT), 0, s, p, ntok, out);
+    else if (p.head_dim == 64) hipLaunchKernelGGL(amf::attn_mfma_kernel<64>, grid, dim3(64 * amf::WT), 0, s, p, ntok, out);
     else throw Error("attn_mfma: head_dim 64 or 128");
     MI_HIP(hipGetLastError());
 }
