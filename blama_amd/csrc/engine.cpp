@@ -288,7 +288,11 @@ void Model::load(const uint8_t* data, size_t size, const mi_model_params& p) {
         throw Error("MoE: this build serves top-2 routing (expert_used_count=2)");
     arena_bytes = off;
     for (const auto& pl : plan) {
-        if (pl.t->name != "token_embd.weight") weight_bytes += (long long)pl.t->nbytes;
+        // bytes one decode step streams: an expert tensor contributes the n_expert_used experts
+        // the router picks (build_moe_ffn reads only those), not all n_expert of them
+        if (pl.t->name != "token_embd.weight")
+            weight_bytes += pl.experts > 1 ? (long long)pl.t->nbytes / pl.experts * hp.n_expert_used
+                                           : (long long)pl.t->nbytes;
         if (pl.t->type >= 0 && pl.t->type < 32) type_bytes[pl.t->type] += (long long)pl.t->nbytes;
     }
     if (i_out < 0) weight_bytes += (long long)plan[i_te].t->nbytes;   // tied output head

@@ -211,7 +211,26 @@ int serve() {
     }
     const std::string modelGguf = modelFromEnv();
     std::cout << "Loading model " << modelGguf << std::endl;
-    Server server(std::make_shared<bl::llama::Model>(modelGguf, bl::llama::Model::Params{}));
+    // BLAMA_DEVICES=0,1,...: one replica (Model + Instance + worker) per listed GPU behind the
+    // server's least-loaded dispatch (extension; default: device 0, the reference's one worker)
+    std::vector<std::shared_ptr<bl::llama::Model>> replicas;
+    {
+        std::string devs = std::getenv("BLAMA_DEVICES") ? std::getenv("BLAMA_DEVICES") : "0";
+        size_t at = 0;
+        while (at <= devs.size()) {
+            const size_t comma = devs.find(',', at);
+            const std::string d = devs.substr(at, comma == std::string::npos ? std::string::npos : comma - at);
+            size_t idx = 0;
+            const int dev = std::stoi(d, &idx, 10);
+            if (idx != d.size() || dev < 0) throw std::invalid_argument("BLAMA_DEVICES: bad device list");
+            bl::llama::Model::Params mp{};
+            mp.device = dev;
+            replicas.push_back(std::make_shared<bl::llama::Model>(modelGguf, mp));
+            if (comma == std::string::npos) break;
+            at = comma + 1;
+        }
+    }
+    Server server(std::move(replicas));
 
     const int lfd = ::socket(AF_INET, SOCK_STREAM, 0);
     const int one = 1;

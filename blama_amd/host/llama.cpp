@@ -66,7 +66,7 @@ size_t utf8_len(unsigned char c) {
 Model::Model(const std::string& gguf, Params params) : m_params(params) {
     if (!params.gpu)
         BL_THROW("Model::Params::gpu=false (the CPU verifier) is not served by the MI355X engine");
-    mi_model_params mp{0, 0, params.vocabOnly ? 1 : 0, 0};
+    mi_model_params mp{params.device, 0, params.vocabOnly ? 1 : 0, 0};
     m_model = mi_model_load(gguf.c_str(), &mp);
     if (!m_model) BL_THROW("Failed to load model " << gguf << ": " << last_error());
     m_vocab.load();
@@ -75,7 +75,7 @@ Model::Model(const std::string& gguf, Params params) : m_params(params) {
 Model::Model(const void* data, size_t size, Params params) : m_params(params) {
     if (!params.gpu)
         BL_THROW("Model::Params::gpu=false (the CPU verifier) is not served by the MI355X engine");
-    mi_model_params mp{0, 0, params.vocabOnly ? 1 : 0, 0};
+    mi_model_params mp{params.device, 0, params.vocabOnly ? 1 : 0, 0};
     m_model = mi_model_load_from_memory(data, size, &mp);
     if (!m_model) BL_THROW("Failed to load model: " << last_error());
     m_vocab.load();

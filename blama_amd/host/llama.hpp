@@ -85,6 +85,7 @@ public:
         bool gpu = true;                   // Model.hpp:29; false = the reference's CPU verifier (not served)
         bool vocabOnly = false;
         bool prefixInputsWithBos = false;
+        int device = 0;                    // HIP device of this replica (extension: one Model per GPU)
         bool operator==(const Params& other) const noexcept = default;
     };
     Model(const std::string& gguf, Params params);

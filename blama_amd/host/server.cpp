@@ -3,13 +3,25 @@
 #include <cstdlib>
 
 #include <cstdio>
+#include <stdexcept>
 
 namespace bl::llama::server {
 
-Server::Server(std::shared_ptr<Model> model)
-    : m_model(std::move(model)), m_instance(std::make_unique<Instance>(*m_model, Instance::InitParams{})) {
-    m_instance->warmup();                                  // Server.cpp:37
-    m_worker = std::thread([this] { run(); });
+Server::Server(std::shared_ptr<Model> model) : Server(std::vector<std::shared_ptr<Model>>{std::move(model)}) {}
+
+Server::Server(std::vector<std::shared_ptr<Model>> replicas) {
+    if (replicas.empty()) throw std::runtime_error("Server: no model");
+    for (auto& m : replicas) {
+        auto r = std::make_unique<Replica>();
+        r->model = std::move(m);
+        r->instance = std::make_unique<Instance>(*r->model, Instance::InitParams{});
+        r->instance->warmup();                             // Server.cpp:37
+        m_reps.push_back(std::move(r));
+    }
+    for (auto& r : m_reps) {
+        Replica* rp = r.get();
+        rp->worker = std::thread([this, rp] { run(*rp); });
+    }
 }
 
 Server::~Server() {
@@ -17,43 +29,59 @@ Server::~Server() {
         std::lock_guard<std::mutex> lk(m_mu);
         m_stop = true;                                     // pending jobs still run (work guard reset)
     }
-    m_cv.notify_all();
-    if (m_worker.joinable()) m_worker.join();
+    for (auto& r : m_reps) r->cv.notify_all();
+    for (auto& r : m_reps)
+        if (r->worker.joinable()) r->worker.join();
 }
 
-void Server::post(std::function<void()> job, ErrorCb onError) {
+std::vector<uint64_t> Server::served() const {
+    std::lock_guard<std::mutex> lk(m_mu);
+    std::vector<uint64_t> v;
+    for (const auto& r : m_reps) v.push_back(r->served);
+    return v;
+}
+
+// least-loaded dispatch: the replica with the fewest queued + running requests
+void Server::post(std::function<void(Replica&)> job, ErrorCb onError) {
+    Replica* best = nullptr;
     {
         std::lock_guard<std::mutex> lk(m_mu);
-        m_jobs.emplace_back(std::move(job), std::move(onError));
+        for (auto& r : m_reps)
+            if (!best || r->load < best->load) best = r.get();
+        best->jobs.emplace_back(std::move(job), std::move(onError));
+        best->load++;
     }
-    m_cv.notify_one();
+    best->cv.notify_one();
 }
 
-void Server::run() {
+void Server::run(Replica& r) {
     for (;;) {
-        std::pair<std::function<void()>, ErrorCb> job;
+        std::pair<std::function<void(Replica&)>, ErrorCb> job;
         {
             std::unique_lock<std::mutex> lk(m_mu);
-            m_cv.wait(lk, [this] { return m_stop || !m_jobs.empty(); });
-            if (m_jobs.empty()) return;
-            job = std::move(m_jobs.front());
-            m_jobs.pop_front();
+            r.cv.wait(lk, [&] { return m_stop || !r.jobs.empty(); });
+            if (r.jobs.empty()) return;
+            job = std::move(r.jobs.front());
+            r.jobs.pop_front();
         }
         try {
-            job.first();
+            job.first(r);
         } catch (...) {
-            m_instance->stopSession();                     // the next request starts clean
+            r.instance->stopSession();                     // the next request starts clean
             if (job.second) job.second(std::current_exception());
             else std::fprintf(stderr, "bl::llama::server: request failed with an exception\n");
         }
+        std::lock_guard<std::mutex> lk(m_mu);
+        r.load--;
+        r.served++;
     }
 }
 
 void Server::completeText(CompleteRequestParams params, std::function<void(CompleteReponse)> cb, ErrorCb onError) {
-    post([this, params = std::move(params), cb = std::move(cb)] {
-        auto& session = m_instance->startSession({.seed = params.seed, .temperature = params.temperature,
+    post([params = std::move(params), cb = std::move(cb)](Replica& rep) {
+        auto& session = rep.instance->startSession({.seed = params.seed, .temperature = params.temperature,
                                                   .topP = params.topP});
-        const Vocab& vocab = m_model->vocab();
+        const Vocab& vocab = rep.model->vocab();
         session.setInitialPrompt(vocab.tokenize(params.prompt, true, true));
         auto iRes = session.complete({.prompt = {}, .maxTokens = (int32_t)params.maxTokens});
         CompleteReponse response;
@@ -66,18 +94,18 @@ void Server::completeText(CompleteRequestParams params, std::function<void(Compl
             for (const auto& l : tp.logits) td.logits.push_back({(uint32_t)l.token, l.logit});
         }
         cb(std::move(response));
-        m_instance->stopSession();
+        rep.instance->stopSession();
     }, std::move(onError));
 }
 
 void Server::verify(CompleteRequestParams req, CompleteReponse resp, std::function<void(float)> cb, ErrorCb onError) {
-    post([this, req = std::move(req), resp = std::move(resp), cb = std::move(cb)] {
+    post([req = std::move(req), resp = std::move(resp), cb = std::move(cb)](Replica& rep) {
         // the claimed tokens are pushed in one batched pass (BLAMA_SERIAL_VERIFY=1: one decode per
         // token, as Session.cpp:231-244, bit-identical to this server's own generation)
         static const bool batched = getenv("BLAMA_SERIAL_VERIFY") == nullptr;
-        auto& session = m_instance->startSession({.seed = req.seed, .temperature = req.temperature,
+        auto& session = rep.instance->startSession({.seed = req.seed, .temperature = req.temperature,
                                                   .topP = req.topP, .batchedVerify = batched});
-        session.setInitialPrompt(m_model->vocab().tokenize(req.prompt, true, true));
+        session.setInitialPrompt(rep.model->vocab().tokenize(req.prompt, true, true));
         std::vector<TokenPrediction> claimed;
         claimed.reserve(resp.size());
         for (const auto& td : resp) {
@@ -94,7 +122,7 @@ void Server::verify(CompleteRequestParams req, CompleteReponse resp, std::functi
             score = agg.pushAndVerify({&m, 1});
         }
         cb(score);
-        m_instance->stopSession();
+        rep.instance->stopSession();
     }, std::move(onError));
 }
 

@@ -17,7 +17,11 @@
 //   them escape the io_context thread.
 // - chatComplete/chatVerify are not served: the chat templating is out of scope.
 //
-// Scaling across GPUs uses one Server per GPU process (replicas).
+// - Replicas (extension): Server(models) runs one Instance and one worker thread per model
+//   (one Model per GPU: Model::Params::device), and each request goes to the replica with the
+//   fewest queued + running requests (lowest index on ties).  A replica is the reference's
+//   single-worker server; requests are independent sessions, so nothing crosses replicas
+//   (replicas only).  Server(model) is one replica, the reference's shape.
 #pragma once
 #include <condition_variable>
 #include <cstdint>
@@ -37,6 +41,8 @@ namespace bl::llama::server {
 class Server {
 public:
     explicit Server(std::shared_ptr<Model> model);
+    // one replica per model (the same model may appear twice: two contexts on one GPU)
+    explicit Server(std::vector<std::shared_ptr<Model>> replicas);
     ~Server();
 
     Server(const Server&) = delete;
@@ -69,17 +75,26 @@ public:
     void verify(CompleteRequestParams req, CompleteReponse resp, std::function<void(float)> cb,
                 ErrorCb onError = {});
 
-private:
-    void post(std::function<void()> job, ErrorCb onError);
-    void run();
+    size_t replicas() const noexcept { return m_reps.size(); }
+    // requests each replica has served so far (tests, load reports)
+    std::vector<uint64_t> served() const;
 
-    std::shared_ptr<Model> m_model;
-    std::unique_ptr<Instance> m_instance;
-    std::mutex m_mu;
-    std::condition_variable m_cv;
-    std::deque<std::pair<std::function<void()>, ErrorCb>> m_jobs;
+private:
+    struct Replica {
+        std::shared_ptr<Model> model;
+        std::unique_ptr<Instance> instance;
+        std::deque<std::pair<std::function<void(Replica&)>, ErrorCb>> jobs;
+        uint32_t load = 0;                 // queued + running requests
+        uint64_t served = 0;
+        std::condition_variable cv;
+        std::thread worker;
+    };
+    void post(std::function<void(Replica&)> job, ErrorCb onError);
+    void run(Replica& r);
+
+    std::vector<std::unique_ptr<Replica>> m_reps;
+    mutable std::mutex m_mu;               // guards every replica's queue, load and stop flag
     bool m_stop = false;
-    std::thread m_worker;
 };
 
 }  // namespace bl::llama::server

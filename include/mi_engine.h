@@ -70,7 +70,8 @@ float mi_model_token_score(const mi_model* model, int32_t token);
 int32_t mi_model_token_type(const mi_model* model, int32_t token);
 int32_t mi_model_tokenizer(const mi_model* model, char* buf, int32_t size);
 int32_t mi_model_meta_str(const mi_model* model, const char* key, char* buf, int32_t size);
-/* Bytes of quantised weights a decode step streams (all tensors but tok_embd). */
+/* Bytes of quantised weights a decode step streams (all tensors but tok_embd; of an MoE expert
+ * tensor only the n_expert_used experts a token is routed to). */
 int64_t mi_model_weight_bytes(const mi_model* model);
 /* The device weight arena (one allocation) -- for the replica broadcast. */
 int32_t mi_model_arena(const mi_model* model, void** dev_ptr, size_t* bytes);
