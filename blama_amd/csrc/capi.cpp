@@ -114,6 +114,19 @@ int32_t mi_model_token_text(const mi_model* m, int32_t token, char* buf, int32_t
     return (int32_t)s.size();
 }
 
+int32_t mi_model_n_merges(const mi_model* m) { return m ? (int32_t)m->impl.merges.size() : -1; }
+
+int32_t mi_model_merge(const mi_model* m, int32_t i, char* buf, int32_t size) {
+    if (!m || i < 0 || i >= (int)m->impl.merges.size()) { set_last_error("merge out of range"); return -1; }
+    const std::string& s = m->impl.merges[i];
+    if (buf && size > 0) {
+        const int n = std::min<int>((int)s.size(), size - 1);
+        std::memcpy(buf, s.data(), n);
+        buf[n] = 0;
+    }
+    return (int32_t)s.size();
+}
+
 int32_t mi_model_meta_str(const mi_model* m, const char* key, char* buf, int32_t size) {
     if (!m || !key) return -1;
     const GgufValue* v = m->impl.gguf.get(key);

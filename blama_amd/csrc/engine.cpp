@@ -217,6 +217,7 @@ void Model::load(const uint8_t* data, size_t size, const mi_model_params& p) {
     if (const GgufValue* ts = gguf.get("tokenizer.ggml.scores"))
         for (double d : ts->arr_num) token_score.push_back((float)d);
     tok_model = gguf.get_str("tokenizer.ggml.model", "llama");
+    if (const GgufValue* mv = gguf.get("tokenizer.ggml.merges")) merges = mv->arr_s;
     hp.n_vocab = (int)tokens.size();
     if (const GgufTensor* te = gguf.tensor("token_embd.weight")) hp.n_vocab = (int)te->ne[1];
     bos = (int)gguf.get_int("tokenizer.ggml.bos_token_id", 1);

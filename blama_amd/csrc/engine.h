@@ -73,6 +73,7 @@ struct Model {
     std::vector<int> token_type;
     std::vector<float> token_score;     // SPM merge scores (tokenizer.ggml.scores)
     std::string tok_model;              // tokenizer.ggml.model ("llama" = SPM, "gpt2" = BPE)
+    std::vector<std::string> merges;    // tokenizer.ggml.merges (BPE: "left right", rank = index)
     int bos = -1, eos = -1, eot = -1;
     bool add_bos = true;
     int device = 0;

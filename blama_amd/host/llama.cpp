@@ -1,5 +1,7 @@
 // bl::llama host surface on the MI355X engine (see llama.hpp for the mirrored reference files).
 #include "llama.hpp"
+#include "unicode_cats.hpp"
+#include <array>
 
 #include "mi_engine.h"
 
@@ -60,6 +62,135 @@ size_t utf8_len(unsigned char c) {
     static const size_t lut[16] = {1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 2, 2, 3, 4};
     return lut[c >> 4];
 }
+
+// ---- byte-level BPE (llm_tokenizer_bpe, unicode.cpp) ----
+// GPT-2's bytes_to_unicode: printable bytes map to themselves, the rest to U+0100.. in byte order
+const std::array<uint32_t, 256>& byte_to_cp() {
+    static const std::array<uint32_t, 256> t = [] {
+        std::array<uint32_t, 256> m{};
+        uint32_t n = 0;
+        for (int b = 0; b < 256; ++b) {
+            const bool keep = (b >= 33 && b <= 126) || (b >= 161 && b <= 172) || (b >= 174);
+            m[b] = keep ? (uint32_t)b : 256 + n++;
+        }
+        return m;
+    }();
+    return t;
+}
+void put_utf8(std::string& o, uint32_t cp) {
+    if (cp < 0x80) o += (char)cp;
+    else if (cp < 0x800) { o += (char)(0xC0 | (cp >> 6)); o += (char)(0x80 | (cp & 0x3F)); }
+    else if (cp < 0x10000) { o += (char)(0xE0 | (cp >> 12)); o += (char)(0x80 | ((cp >> 6) & 0x3F)); o += (char)(0x80 | (cp & 0x3F)); }
+    else { o += (char)(0xF0 | (cp >> 18)); o += (char)(0x80 | ((cp >> 12) & 0x3F)); o += (char)(0x80 | ((cp >> 6) & 0x3F)); o += (char)(0x80 | (cp & 0x3F)); }
+}
+// UTF-8 -> code points with the byte offset of each (an invalid sequence is one U+FFFD per byte)
+void cps_of(std::string_view s, std::vector<uint32_t>& cp, std::vector<size_t>& off) {
+    cp.clear();
+    off.clear();
+    for (size_t i = 0; i < s.size();) {
+        const unsigned char c = (unsigned char)s[i];
+        size_t n = c < 0x80 ? 1 : (c >> 5) == 6 ? 2 : (c >> 4) == 14 ? 3 : (c >> 3) == 30 ? 4 : 0;
+        uint32_t v = 0xFFFD;
+        if (n && i + n <= s.size()) {
+            v = n == 1 ? c : n == 2 ? (c & 0x1F) : n == 3 ? (c & 0x0F) : (c & 0x07);
+            for (size_t k = 1; k < n; ++k) {
+                const unsigned char d = (unsigned char)s[i + k];
+                if ((d & 0xC0) != 0x80) { n = 0; break; }
+                v = (v << 6) | (d & 0x3F);
+            }
+        }
+        if (!n || i + n > s.size()) { n = 1; v = 0xFFFD; }
+        cp.push_back(v);
+        off.push_back(i);
+        i += n;
+    }
+    off.push_back(s.size());
+}
+template <size_t N>
+bool in_ranges(const unicode::CpRange (&r)[N], uint32_t c) {
+    size_t lo = 0, hi = N;
+    while (lo < hi) {
+        const size_t mid = (lo + hi) / 2;
+        if (c < r[mid].lo) hi = mid;
+        else if (c > r[mid].hi) lo = mid + 1;
+        else return true;
+    }
+    return false;
+}
+bool is_L(uint32_t c) { return c < 0x80 ? ((c | 32) >= 'a' && (c | 32) <= 'z') : in_ranges(unicode::kLetter, c); }
+bool is_N(uint32_t c) { return c < 0x80 ? (c >= '0' && c <= '9') : in_ranges(unicode::kNumber, c); }
+bool is_S(uint32_t c) {   // \s: Unicode White_Space
+    return (c >= 9 && c <= 13) || c == 32 || c == 0x85 || c == 0xA0 || c == 0x1680 || (c >= 0x2000 && c <= 0x200A) ||
+           c == 0x2028 || c == 0x2029 || c == 0x202F || c == 0x205F || c == 0x3000;
+}
+bool is_nl(uint32_t c) { return c == '\r' || c == '\n'; }
+uint32_t lower_ascii(uint32_t c) { return (c >= 'A' && c <= 'Z') ? c + 32 : c; }
+
+// Length (code points) of the pre-token starting at i: the first alternative of the regex that
+// matches there, with the regex's greedy / backtracking semantics (unicode.cpp's hand-written
+// splitters do the same).
+//   Llama-3: (?:'[sS]|'[tT]|'[rR][eE]|'[vV][eE]|'[mM]|'[lL][lL]|'[dD])|[^\r\n\p{L}\p{N}]?\p{L}+|
+//            \p{N}{1,3}| ?[^\s\p{L}\p{N}]+[\r\n]*|\s*[\r\n]+|\s+(?!\S)|\s+
+//   GPT-2:   's|'t|'re|'ve|'m|'ll|'d| ?\p{L}+| ?\p{N}+| ?[^\s\p{L}\p{N}]+|\s+(?!\S)|\s+
+size_t pretok_len(const std::vector<uint32_t>& c, size_t i, bool llama3) {
+    const size_t n = c.size();
+    auto other = [&](uint32_t x) { return !is_S(x) && !is_L(x) && !is_N(x); };
+    if (c[i] == '\'' && i + 1 < n) {
+        const uint32_t a = llama3 ? lower_ascii(c[i + 1]) : c[i + 1];
+        if (a == 's' || a == 't' || a == 'm' || a == 'd') return 2;
+        if (i + 2 < n) {
+            const uint32_t b = llama3 ? lower_ascii(c[i + 2]) : c[i + 2];
+            if ((a == 'r' && b == 'e') || (a == 'v' && b == 'e') || (a == 'l' && b == 'l')) return 3;
+        }
+    }
+    size_t j = i;
+    if (llama3) {
+        if (!is_nl(c[j]) && !is_L(c[j]) && !is_N(c[j]) && j + 1 < n && is_L(c[j + 1])) ++j;
+        if (is_L(c[j])) {
+            while (j < n && is_L(c[j])) ++j;
+            return j - i;
+        }
+        if (is_N(c[i])) {
+            j = i;
+            while (j < n && j - i < 3 && is_N(c[j])) ++j;
+            return j - i;
+        }
+    } else {
+        if (c[j] == ' ' && j + 1 < n && is_L(c[j + 1])) ++j;
+        if (is_L(c[j])) {
+            while (j < n && is_L(c[j])) ++j;
+            return j - i;
+        }
+        j = i;
+        if (c[j] == ' ' && j + 1 < n && is_N(c[j + 1])) ++j;
+        if (is_N(c[j])) {
+            while (j < n && is_N(c[j])) ++j;
+            return j - i;
+        }
+    }
+    j = i;
+    if (c[j] == ' ' && j + 1 < n && other(c[j + 1])) ++j;
+    if (other(c[j])) {
+        while (j < n && other(c[j])) ++j;
+        if (llama3)
+            while (j < n && is_nl(c[j])) ++j;
+        return j - i;
+    }
+    if (is_S(c[i])) {
+        size_t e = i;
+        while (e < n && is_S(c[e])) ++e;
+        if (llama3) {   // \s*[\r\n]+ : up to the run's last CR/LF
+            size_t last = n;
+            for (size_t k = i; k < e; ++k)
+                if (is_nl(c[k])) last = k;
+            if (last != n) return last + 1 - i;
+        }
+        if (e == n) return e - i;       // \s+(?!\S) at the end of the text
+        if (e - i >= 2) return e - i - 1;   // \s+(?!\S): leave the last space to the next word
+        return e - i;                   // \s+
+    }
+    return 1;
+}
 }  // namespace
 
 // ------------------------------------------------------------------ Model ---
@@ -118,6 +249,28 @@ void Vocab::load() {
     char tk[32] = {0};
     mi_model_tokenizer(m, tk, sizeof tk);
     m_spm = std::string(tk) == "llama";
+    m_bpe = std::string(tk) == "gpt2";
+    if (m_bpe) {
+        // llama_vocab::impl::load: tokenizer.ggml.pre picks the pre-tokenizer; the Llama-3 family
+        // also takes a whole pre-token from the vocabulary before merging (ignore_merges)
+        char pre[64] = {0};
+        const std::string p = mi_model_meta_str(m, "tokenizer.ggml.pre", pre, sizeof pre) > 0 ? pre : "default";
+        if (p == "llama3" || p == "llama-v3" || p == "llama-bpe" || p == "falcon3") {
+            m_pre = 1;
+            m_ignoreMerges = true;
+        } else if (p == "gpt-2" || p == "default") {
+            m_pre = 0;
+        } else {
+            BL_THROW("tokenizer: BPE pre-tokenizer '" << p << "' is not served (llama-bpe, gpt-2)");
+        }
+        const int nm = mi_model_n_merges(m);
+        for (int i = 0; i < nm; ++i) {
+            const int len = mi_model_merge(m, i, nullptr, 0);
+            buf.assign((size_t)len + 1, '\0');
+            mi_model_merge(m, i, buf.data(), len + 1);
+            m_rank.emplace(std::string(buf.data(), (size_t)len), i);
+        }
+    }
     m_loaded = true;
 }
 
@@ -128,6 +281,23 @@ Token Vocab::decoderStartToken() const noexcept { return m_bos; }
 std::string Vocab::tokenToString(Token token, bool special) const {
     if (token < 0 || token >= nTokens()) return {};
     const std::string& t = m_text[token];
+    if (m_bpe && (m_type[token] == kTypeNormal || m_type[token] == 0)) {   // byte-level: back to bytes
+        static const std::unordered_map<uint32_t, unsigned char> back = [] {
+            std::unordered_map<uint32_t, unsigned char> m;
+            for (int b = 0; b < 256; ++b) m.emplace(byte_to_cp()[b], (unsigned char)b);
+            return m;
+        }();
+        std::vector<uint32_t> cp;
+        std::vector<size_t> off;
+        cps_of(t, cp, off);
+        std::string o;
+        for (size_t i = 0; i < cp.size(); ++i) {
+            auto it = back.find(cp[i]);
+            if (it != back.end()) o += (char)it->second;
+            else o.append(t, off[i], off[i + 1] - off[i]);
+        }
+        return o;
+    }
     switch (m_type[token]) {
     case kTypeNormal: return unescape_whitespace(t);
     case kTypeUnknown: return "\xe2\x96\x85";   // U+2585, what llama_token_to_piece prints
@@ -140,8 +310,65 @@ std::string Vocab::tokenToString(Token token, bool special) const {
     }
 }
 
+// One pre-token of a BPE vocabulary (llm_tokenizer_bpe_session::tokenize): byte-encode it, then
+// merge adjacent symbols lowest merge rank first (leftmost on ties); symbols missing from the
+// vocabulary fall back to their single byte-characters.
+void Vocab::bpeWord(std::string_view word, std::vector<Token>& out) const {
+    std::string enc;
+    for (unsigned char b : word) put_utf8(enc, byte_to_cp()[b]);
+    if (m_ignoreMerges) {
+        auto it = m_index.find(enc);
+        if (it != m_index.end()) { out.push_back(it->second); return; }
+    }
+    struct Sym { int prev, next; size_t off, n; };
+    std::vector<Sym> sym;
+    for (size_t off = 0; off < enc.size();) {
+        const size_t n = std::min(utf8_len((unsigned char)enc[off]), enc.size() - off);
+        sym.push_back({(int)sym.size() - 1, (int)sym.size() + 1, off, n});
+        off += n;
+    }
+    if (sym.empty()) return;
+    sym.back().next = -1;
+    struct Bigram { int left, right, rank; size_t size; };
+    auto worse = [](const Bigram& a, const Bigram& b) { return a.rank > b.rank || (a.rank == b.rank && a.left > b.left); };
+    std::priority_queue<Bigram, std::vector<Bigram>, decltype(worse)> q(worse);
+    auto try_pair = [&](int l, int r) {
+        if (l < 0 || r < 0) return;
+        std::string key = enc.substr(sym[l].off, sym[l].n);
+        key += ' ';
+        key.append(enc, sym[r].off, sym[r].n);
+        auto it = m_rank.find(key);
+        if (it != m_rank.end()) q.push({l, r, it->second, sym[l].n + sym[r].n});
+    };
+    for (size_t i = 1; i < sym.size(); ++i) try_pair((int)i - 1, (int)i);
+    while (!q.empty()) {
+        const Bigram b = q.top();
+        q.pop();
+        Sym& L = sym[b.left];
+        Sym& R = sym[b.right];
+        if (L.n == 0 || R.n == 0 || L.n + R.n != b.size || L.next != b.right) continue;   // stale
+        L.n += R.n;
+        R.n = 0;
+        L.next = R.next;
+        if (R.next >= 0) sym[R.next].prev = b.left;
+        try_pair(L.prev, b.left);
+        try_pair(b.left, L.next);
+    }
+    for (int i = 0; i != -1; i = sym[i].next) {
+        const std::string t = enc.substr(sym[i].off, sym[i].n);
+        auto it = m_index.find(t);
+        if (it != m_index.end()) { out.push_back(it->second); continue; }
+        for (size_t k = 0; k < t.size();) {   // each character alone, where the vocabulary has it
+            const size_t n = std::min(utf8_len((unsigned char)t[k]), t.size() - k);
+            auto bt = m_index.find(t.substr(k, n));
+            if (bt != m_index.end()) out.push_back(bt->second);
+            k += n;
+        }
+    }
+}
+
 std::vector<Token> Vocab::tokenize(std::string_view text, bool addSpecial, bool parseSpecial) const {
-    if (!m_spm) BL_THROW("tokenizer: only SentencePiece (tokenizer.ggml.model = llama) vocabularies are served");
+    if (!m_spm && !m_bpe) BL_THROW("tokenizer: only SentencePiece (llama) and byte-level BPE (gpt2) vocabularies are served");
     std::vector<Token> out;
     if (addSpecial && m_model.shouldAddBosToken() && m_bos >= 0) out.push_back(m_bos);
 
@@ -172,6 +399,20 @@ std::vector<Token> Vocab::tokenize(std::string_view text, bool addSpecial, bool 
         frags.swap(next);
     }
 
+    if (m_bpe) {   // 2'. byte-level BPE: pre-tokenize each raw fragment, then merge each pre-token
+        std::vector<uint32_t> cp;
+        std::vector<size_t> off;
+        for (const Frag& f : frags) {
+            if (f.tok) { out.push_back(f.id); continue; }
+            cps_of(f.s, cp, off);
+            for (size_t i = 0; i < cp.size();) {
+                const size_t n = pretok_len(cp, i, m_pre == 1);
+                bpeWord(f.s.substr(off[i], off[i + n] - off[i]), out);
+                i += n;
+            }
+        }
+        return out;
+    }
     // 2. SentencePiece BPE over each raw fragment (llm_tokenizer_spm semantics)
     bool prev_special = true;   // a raw fragment at the start or after a special token gets a space prefix
     for (const Frag& f : frags) {

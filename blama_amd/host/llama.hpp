@@ -56,8 +56,10 @@ class Model;
 class Vocab {
 public:
     explicit Vocab(const Model& model);
-    // SPM tokenisation (llama.cpp llm_tokenizer_spm) of `text`; addSpecial prepends BOS when the
-    // model asks for it, parseSpecial matches control-token texts (e.g. "<s>") as single tokens.
+    // Tokenisation of `text` (llama_tokenize): SentencePiece (llm_tokenizer_spm) for "llama"
+    // vocabularies, byte-level BPE with the GPT-2 or Llama-3 pre-tokenizer (llm_tokenizer_bpe)
+    // for "gpt2" ones; addSpecial prepends BOS when the model asks for it, parseSpecial matches
+    // control-token texts (e.g. "<s>", "<|begin_of_text|>") as single tokens.
     std::vector<Token> tokenize(std::string_view text, bool addSpecial, bool parseSpecial) const;
     Token decoderStartToken() const noexcept;
     bool isEog(Token token) const noexcept;
@@ -75,6 +77,12 @@ private:
     std::unordered_map<std::string, Token> m_index;
     Token m_bos = -1, m_eos = -1, m_unk = 0;
     bool m_spm = true;
+    // byte-level BPE (tokenizer.ggml.model "gpt2": Llama-3 and GPT-2 vocabularies)
+    bool m_bpe = false;
+    int m_pre = 0;                           // pre-tokenizer: 0 GPT-2, 1 Llama-3 ("llama-bpe")
+    bool m_ignoreMerges = false;             // Llama-3: a pre-token found whole in the vocab is one token
+    std::unordered_map<std::string, int> m_rank;   // "left right" -> merge rank
+    void bpeWord(std::string_view word, std::vector<Token>& out) const;
     bool m_loaded = false;
     friend class Model;
 };

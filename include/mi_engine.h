@@ -70,6 +70,10 @@ float mi_model_token_score(const mi_model* model, int32_t token);
 int32_t mi_model_token_type(const mi_model* model, int32_t token);
 int32_t mi_model_tokenizer(const mi_model* model, char* buf, int32_t size);
 int32_t mi_model_meta_str(const mi_model* model, const char* key, char* buf, int32_t size);
+/* BPE vocabularies (tokenizer.ggml.model "gpt2", e.g. Llama-3): tokenizer.ggml.merges, rank = index;
+ * mi_model_merge returns the length of merge i ("left right") or < 0. */
+int32_t mi_model_n_merges(const mi_model* model);
+int32_t mi_model_merge(const mi_model* model, int32_t i, char* buf, int32_t size);
 /* Bytes of quantised weights a decode step streams (all tensors but tok_embd; of an MoE expert
  * tensor only the n_expert_used experts a token is routed to). */
 int64_t mi_model_weight_bytes(const mi_model* model);

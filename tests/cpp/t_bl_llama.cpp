@@ -17,13 +17,14 @@
 #include <future>
 
 namespace {
-std::string g_model, g_vocab, g_out;
+std::string g_model, g_vocab, g_out, g_in;
 void setup(int argc, char** argv, std::vector<std::string>& groups) {
     for (int i = 1; i < argc; ++i) {
         const std::string a = argv[i];
         if (a.rfind("--model=", 0) == 0) g_model = a.substr(8);
         else if (a.rfind("--vocab=", 0) == 0) g_vocab = a.substr(8);
         else if (a.rfind("--out=", 0) == 0) g_out = a.substr(6);
+        else if (a.rfind("--in=", 0) == 0) g_in = a.substr(5);
         else groups.push_back(a);
     }
 }
@@ -133,6 +134,26 @@ TEST_CASE_G("vocab only", "cpu") {   // t-integration.cpp:25-43
     std::string back;
     for (Token x : by) back += vocab.tokenToString(x);
     CHECK(back == " \xc3\xa9");
+}
+
+// tests/test_tokenizer_bpe.py: tokenise every line of --in (hex-encoded UTF-8) with the vocab-only
+// model --vocab (parseSpecial, no BOS) and write the ids, one line per text, to --out
+TEST_CASE_G("tokenize file", "tok") {
+    REQUIRE(!g_vocab.empty() && !g_in.empty() && !g_out.empty());
+    Model model(g_vocab, {.vocabOnly = true});
+    std::ifstream in(g_in);
+    std::ofstream out(g_out);
+    std::string line;
+    while (std::getline(in, line)) {
+        std::string text;
+        for (size_t i = 0; i + 1 < line.size(); i += 2) text += (char)std::stoi(line.substr(i, 2), nullptr, 16);
+        const auto ids = model.vocab().tokenize(text, false, true);
+        for (size_t i = 0; i < ids.size(); ++i) out << (i ? " " : "") << ids[i];
+        out << "\n";
+        std::string back;   // tokenToString of the ids concatenates to the text again
+        for (Token t : ids) back += model.vocab().tokenToString(t);
+        CHECK(back == text);
+    }
 }
 
 TEST_CASE_G("wire format", "cpu") {   // HttpServerMain.cpp:37-94, 259-288
