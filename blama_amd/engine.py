@@ -56,6 +56,8 @@ _SIGS = {
     "mi_model_token_type": (C.c_int32, [_P, C.c_int32]),
     "mi_model_tokenizer": (C.c_int32, [_P, C.c_char_p, C.c_int32]),
     "mi_model_meta_str": (C.c_int32, [_P, C.c_char_p, C.c_char_p, C.c_int32]),
+    "mi_model_n_merges": (C.c_int32, [_P]),
+    "mi_model_merge": (C.c_int32, [_P, C.c_int32, C.c_char_p, C.c_int32]),
     "mi_model_weight_bytes": (C.c_int64, [_P]),
     "mi_model_arena": (C.c_int32, [_P, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]),
     "mi_model_type_histogram": (C.c_int32, [_P, C.POINTER(C.c_int64), C.c_int32]),
