@@ -200,6 +200,14 @@ int32_t mi_gather(mi_ctx* c, int32_t row, const int32_t* ids, int32_t n, float* 
     MI_TRY(-1)
 }
 
+int32_t mi_gather_rows(mi_ctx* c, int32_t row0, int32_t n_rows, const int32_t* ids, int32_t k, float* out) {
+    try {
+        if (!c || ((int64_t)n_rows * k > 0 && (!ids || !out))) throw Error("null argument");
+        return c->impl->gather_rows(row0, n_rows, ids, k, out);
+    }
+    MI_TRY(-1)
+}
+
 const float* mi_logits(mi_ctx* c, int32_t row) {
     try {
         if (!c) throw Error("null ctx");

@@ -494,9 +494,9 @@ Ctx::~Ctx() {
                     (void*)cell_delta, (void*)move_src, (void*)part_o, (void*)attn_smax, (void*)attn_scores, (void*)stamps,
                     (void*)xb, (void*)qb, (void*)attnb, (void*)hb, (void*)tokpos_b, (void*)q8r_q,
                     (void*)q8r_d, (void*)q8r_bsum, (void*)ub_q, (void*)ub_dT, (void*)ub_bsb, (void*)ub_rope,
-                    (void*)logits_all})
+                    (void*)logits_all, (void*)grows_ids, (void*)grows_out})
         if (p) hipFree(p);
-    for (void* p : {(void*)h_tokpos, (void*)h_topk_ids, (void*)h_topk_vals, (void*)h_logits, (void*)h_gather,
+    for (void* p : {(void*)h_tokpos, (void*)h_topk_ids, (void*)h_topk_vals, (void*)h_logits, (void*)h_gather, (void*)h_grows,
                     (void*)h_tokpos_b})
         if (p) hipHostFree(p);
     if (stream) hipStreamDestroy(stream);
@@ -1115,6 +1115,37 @@ int Ctx::gather(int row, const int32_t* ids, int n, float* out) {
     sync();
     std::memcpy(out, h_gather, n * sizeof(float));
     return n;
+}
+
+// Logits of rows row0..row0+nrows-1 at k ids each (ids [nrows][k]): the batched form of gather
+// for a verification pass -- one copy in, one kernel, one copy out.
+int Ctx::gather_rows(int row0, int nrows, const int32_t* ids, int k, float* out) {
+    if (!logits_valid) throw Error("no logits: decode a token first");
+    if (nrows < 0 || k < 0) throw Error("gather_rows: negative count");
+    const size_t n = (size_t)nrows * k;
+    if (n == 0) return 0;
+    const int avail = out_rows > 0 ? out_rows : 1;
+    if (row0 < 0 || row0 + nrows > avail) throw Error("gather_rows: output rows out of range");
+    for (size_t i = 0; i < n; ++i)
+        if (ids[i] < 0 || ids[i] >= m->hp.n_vocab) throw Error("gather_rows: id out of range");
+    MI_HIP(hipSetDevice(device));
+    if (n > grows_cap) {
+        if (grows_ids) hipFree(grows_ids);
+        if (grows_out) hipFree(grows_out);
+        if (h_grows) hipHostFree(h_grows);
+        grows_ids = nullptr; grows_out = nullptr; h_grows = nullptr; grows_cap = 0;
+        MI_HIP(hipMalloc(&grows_ids, n * sizeof(int)));
+        MI_HIP(hipMalloc(&grows_out, n * sizeof(float)));
+        MI_HIP(hipHostMalloc(&h_grows, n * sizeof(float)));
+        grows_cap = n;
+    }
+    const float* base = out_rows > 0 ? logits_all + (size_t)row0 * m->hp.n_vocab : logits;
+    MI_HIP(hipMemcpyAsync(grows_ids, ids, n * sizeof(int), hipMemcpyHostToDevice, stream));
+    launch_gather_rows(base, m->hp.n_vocab, grows_ids, (int)n, k, grows_out, stream);
+    MI_HIP(hipMemcpyAsync(h_grows, grows_out, n * sizeof(float), hipMemcpyDeviceToHost, stream));
+    sync();
+    std::memcpy(out, h_grows, n * sizeof(float));
+    return (int)n;
 }
 
 const float* Ctx::logits_host(int row) {

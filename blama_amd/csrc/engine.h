@@ -208,6 +208,11 @@ struct Ctx {
     void sync();
     int topk(int row, int k, int32_t* ids, float* vals);
     int gather(int row, const int32_t* ids, int n, float* out);
+    int gather_rows(int row0, int nrows, const int32_t* ids, int k, float* out);
+    int* grows_ids = nullptr;           // gather_rows buffers (grown on demand)
+    float* grows_out = nullptr;
+    float* h_grows = nullptr;
+    size_t grows_cap = 0;
     const float* logits_host(int row);
     void kv_clear();
     int kv_seq_rm(int p0, int p1);

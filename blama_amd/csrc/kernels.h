@@ -163,6 +163,7 @@ struct AttnParams {
     unsigned long long* stamps;    // diagnostics (MI_STAMPS builds): scores / pv launches
     unsigned long long* stamps2;
     int fused;                     // 1: the single-launch kernel (the context has <= ATTN_SHORT cells)
+    int qsplit;                    // fused kernel: 0 = a workgroup per kv head; R = a workgroup per q head
 };
 void launch_attn(const AttnParams& p, hipStream_t s);
 // Combine the partials into out[n_head*hd] (tests / the eager debug path).
@@ -187,6 +188,9 @@ void launch_topk(const TopkParams& p, hipStream_t s);
 
 // ---- gather logits at ids ----
 void launch_gather(const float* logits, const int* ids, int n, float* out, hipStream_t s);
+// n = rows*k ids, k per row: out[i] = base[(i / k) * row_stride + ids[i]]
+void launch_gather_rows(const float* base, long long row_stride, const int* ids, int n, int k, float* out,
+                        hipStream_t s);
 
 // ---- MoE router: softmax gating + top-k + weight normalisation ----
 struct RouterParams {

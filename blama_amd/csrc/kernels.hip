@@ -2984,7 +2984,9 @@ __global__ __launch_bounds__(256) void attn_fused_kernel(const AttnParams P) {
     __shared__ double dred[4][R];
     __shared__ float gm[R], ginv[R];
     __shared__ float red_o[4][R][HD];
-    const int g = blockIdx.x;
+    // kv head, and the first of the R q heads this workgroup serves (qsplit: one q head each)
+    const int g = P.qsplit ? (int)blockIdx.x / P.qsplit : (int)blockIdx.x;
+    const int gq = P.qsplit ? (int)blockIdx.x : (int)blockIdx.x * R;
     const int tok = blockIdx.y;   // query token (launch_attn_multi); 0 for a decode step
 #ifdef MI_STAMPS
     unsigned long long* const stp = P.stamps && tok == 0 ? P.stamps + blockIdx.x * 8 : nullptr;
@@ -3014,7 +3016,7 @@ __global__ __launch_bounds__(256) void attn_fused_kernel(const AttnParams P) {
     float q[R][8];
 #pragma unroll
     for (int t = 0; t < R; ++t) {
-        const float4* qp = reinterpret_cast<const float4*>(qrow + (long long)(g * R + t) * HD + L * 8);
+        const float4* qp = reinterpret_cast<const float4*>(qrow + (long long)(gq + t) * HD + L * 8);
         const float4 a = qp[0], b = qp[1];
         const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
 #pragma unroll
@@ -3142,7 +3144,7 @@ __global__ __launch_bounds__(256) void attn_fused_kernel(const AttnParams P) {
     __syncthreads();
     for (int i = tid; i < R * HD; i += 256) {
         const int t = i / HD, d = i % HD;
-        orow[(long long)(g * R + t) * HD + d] = ((red_o[0][t][d] + red_o[1][t][d]) + red_o[2][t][d]) + red_o[3][t][d];
+        orow[(long long)(gq + t) * HD + d] = ((red_o[0][t][d] + red_o[1][t][d]) + red_o[2][t][d]) + red_o[3][t][d];
     }
 #ifdef MI_STAMPS
     if (stp && threadIdx.x == 0) stp[4] = __builtin_amdgcn_s_memrealtime();
@@ -3174,6 +3176,15 @@ void launch_attn(const AttnParams& p, hipStream_t s) {
     }
     if (!fa) throw Error("attn: unsupported head_dim / GQA ratio (head_dim 32..256, ratio 1/2/4/8)");
     if (p.fused) {   // the caller guarantees <= ATTN_SHORT cells (the kernel clamps anyway)
+        if (r > 1 && p.n_head_kv < 16) {   // few kv heads: one workgroup per q head (R=1 kernel)
+            AttnFn f1 = nullptr, a1 = nullptr, b1 = nullptr;
+            attn_fns_r<1>(p.head_dim, a1, b1, f1);
+            AttnParams q = p;
+            q.qsplit = r;
+            hipLaunchKernelGGL(f1, dim3(p.n_head), dim3(256), 0, s, q);
+            MI_HIP(hipGetLastError());
+            return;
+        }
         hipLaunchKernelGGL(ff, dim3(p.n_head_kv), dim3(256), 0, s, p);
         MI_HIP(hipGetLastError());
         return;
@@ -3320,6 +3331,19 @@ void launch_topk(const TopkParams& p, hipStream_t s) {
 __global__ void gather_kernel(const float* logits, const int* ids, int n, float* out) {
     const int i = threadIdx.x + blockIdx.x * blockDim.x;
     if (i < n) out[i] = logits[ids[i]];
+}
+
+// rows of logits: out[i] = base[(i / k) * row_stride + ids[i]]
+__global__ void gather_rows_kernel(const float* base, long long row_stride, const int* ids, int n, int k, float* out) {
+    const int i = threadIdx.x + blockIdx.x * blockDim.x;
+    if (i < n) out[i] = base[(long long)(i / k) * row_stride + ids[i]];
+}
+
+void launch_gather_rows(const float* base, long long row_stride, const int* ids, int n, int k, float* out,
+                        hipStream_t s) {
+    if (n <= 0 || k <= 0) return;
+    hipLaunchKernelGGL(gather_rows_kernel, dim3((n + 255) / 256), dim3(256), 0, s, base, row_stride, ids, n, k, out);
+    MI_HIP(hipGetLastError());
 }
 
 void launch_gather(const float* logits, const int* ids, int n, float* out, hipStream_t s) {

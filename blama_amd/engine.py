@@ -69,6 +69,7 @@ _SIGS = {
     "mi_topk": (C.c_int32, [_P, C.c_int32, C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_float)]),
     "mi_gather": (C.c_int32, [_P, C.c_int32, C.POINTER(C.c_int32), C.c_int32, C.POINTER(C.c_float)]),
     "mi_logits": (C.POINTER(C.c_float), [_P, C.c_int32]),
+    "mi_gather_rows": (C.c_int32, [_P, C.c_int32, C.c_int32, C.POINTER(C.c_int32), C.c_int32, C.POINTER(C.c_float)]),
     "mi_synchronize": (None, [_P]),
     "mi_kv_clear": (None, [_P]),
     "mi_kv_seq_rm": (C.c_int32, [_P, C.c_int32, C.c_int32]),
@@ -244,6 +245,14 @@ class Context:
         out = np.empty(ids.size, np.float32)
         _check(lib().mi_gather(self.h, row, ids.ctypes.data_as(C.POINTER(C.c_int32)), ids.size,
                                out.ctypes.data_as(C.POINTER(C.c_float))), "gather")
+        return out
+
+    def gather_rows(self, row0: int, ids) -> np.ndarray:
+        """ids [n_rows][k] -> logits of rows row0.. at those ids (mi_gather_rows)."""
+        ids = np.ascontiguousarray(ids, dtype=np.int32)
+        out = np.empty(ids.shape, np.float32)
+        _check(lib().mi_gather_rows(self.h, row0, ids.shape[0], ids.ctypes.data_as(C.POINTER(C.c_int32)),
+                                    ids.shape[1], out.ctypes.data_as(C.POINTER(C.c_float))), "gather_rows")
         return out
 
     def logits(self, row: int = -1) -> np.ndarray:

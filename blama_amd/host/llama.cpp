@@ -755,10 +755,30 @@ std::vector<TokenPrediction> Session::fillCtx(std::span<TokenPrediction> tokens)
             for (uint32_t i = 0; i < nc; ++i) ids[i] = tokens[c0 + i].token;
             if (mi_decode(m_ctx, ids.data(), (int32_t)nc, MI_OUT_ALL) != 0) BL_THROW("Failed to decode tokens");
             m_state.numPast += nc;
+            // every row's claimed ids (each once, in id order, as the reference's vocabulary scan
+            // yields them) in one gather: rows padded to the longest list with their first id
+            std::vector<std::vector<int32_t>> rid(nc);
+            size_t k = 0;
+            for (uint32_t i = 0; i < nc; ++i) {
+                for (const TokenData& t : tokens[c0 + i].logits)
+                    if (t.token >= 0 && t.token < m_instance.model().vocab().nTokens()) rid[i].push_back(t.token);
+                std::sort(rid[i].begin(), rid[i].end());
+                rid[i].erase(std::unique(rid[i].begin(), rid[i].end()), rid[i].end());
+                k = std::max(k, rid[i].size());
+            }
+            std::vector<int32_t> flat(nc * k, 0);
+            for (uint32_t i = 0; i < nc; ++i)
+                for (size_t j = 0; j < k; ++j) flat[i * k + j] = rid[i].empty() ? 0 : rid[i][std::min(j, rid[i].size() - 1)];
+            std::vector<float> lg(flat.size());
+            if (k > 0 && mi_gather_rows(m_ctx, 0, (int32_t)nc, flat.data(), (int32_t)k, lg.data()) < 0)
+                BL_THROW("gather: " << last_error());
             for (uint32_t i = 0; i < nc; ++i) {
                 TokenPrediction r;
                 r.token = tokens[c0 + i].token;
-                r.logits = getLogitsFromCtx(tokens[c0 + i].logits, (int32_t)i);
+                r.logits.resize(rid[i].size());
+                for (size_t j = 0; j < rid[i].size(); ++j) r.logits[j] = {rid[i][j], lg[i * k + j]};
+                std::stable_sort(r.logits.begin(), r.logits.end(),
+                                 [](const TokenData& a, const TokenData& b) { return a.logit > b.logit; });
                 out.push_back(std::move(r));
             }
         }

@@ -106,6 +106,9 @@ int32_t mi_decode(mi_ctx* ctx, const int32_t* tokens, int32_t n, int32_t out_mod
 int32_t mi_topk(mi_ctx* ctx, int32_t row, int32_t k, int32_t* ids, float* logits);
 /* Logits of an output row at the given ids (Session.cpp:263-282).  Synchronises. */
 int32_t mi_gather(mi_ctx* ctx, int32_t row, const int32_t* ids, int32_t n, float* out);
+/* Batched form of mi_gather for a verification pass: rows row0 .. row0+n_rows-1, k ids per row
+ * (ids and out are [n_rows][k]).  Returns n_rows*k or < 0.  Synchronises. */
+int32_t mi_gather_rows(mi_ctx* ctx, int32_t row0, int32_t n_rows, const int32_t* ids, int32_t k, float* out);
 /* Full-vocabulary escape hatch: llama_get_logits_ith(ctx, -1) (Session.cpp:24,
  * Sampler.cpp:111).  Context-owned; valid until the next decode.  Synchronises. */
 const float* mi_logits(mi_ctx* ctx, int32_t row);

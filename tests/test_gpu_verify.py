@@ -55,6 +55,12 @@ def test_out_all_matches_oracle(gpu_lib, cfg_name):
     ctx.decode(prompt)
     ctx.decode(claimed, all_logits=True)
     _check_rows(ctx, buf, prompt, claimed, 96)
+    # the batched gather of every row equals the per-row gathers
+    ids = np.random.default_rng(3).integers(0, cfg.n_vocab, (len(claimed), 7)).astype(np.int32)
+    g = ctx.gather_rows(0, ids)
+    for i in range(len(claimed)):
+        assert np.array_equal(g[i], ctx.gather(ids[i], row=i))
+    assert np.array_equal(ctx.gather_rows(5, ids[5:9]), g[5:9])
     # the last row is also row -1, and the next single-token step sees the whole batch's cache
     assert np.array_equal(ctx.logits(), ctx.logits(row=len(claimed) - 1))
     ids_last, _ = ctx.topk(10)
