@@ -1597,20 +1597,6 @@ __device__ __forceinline__ void gemv_k_body(const float* __restrict__ kx0, const
         if (lane < P.n_rot / 2) ff0 = gptr(P.freq_factors)[lane];
         if (lane + 64 < P.n_rot / 2) ff1 = gptr(P.freq_factors)[lane + 64];
     }
-    // this wave's RMSNorm share (its x arrived with the parameter block)
-    if (rms) {
-        double sacc = 0.0;
-#pragma unroll
-        for (int r = 0; r < KX_PART; ++r) {
-            const f32x4 v = xr[r];
-            sacc += (double)(v.x * v.x);
-            sacc += (double)(v.y * v.y);
-            sacc += (double)(v.z * v.z);
-            sacc += (double)(v.w * v.w);
-        }
-        sacc = wave_sum63_d(sacc);
-        if (lane == 63) red[wave] = sacc;
-    }
 
     // ---- the weight prefetch
     struct Slot { typename K::Ld a, b; };
@@ -1661,6 +1647,22 @@ __device__ __forceinline__ void gemv_k_body(const float* __restrict__ kx0, const
 #pragma unroll
     for (int k = 0; k < D - 1; ++k) issue(ring[k]);
     MI_STAMP(1)
+    // this wave's RMSNorm share: its x loads were issued at entry, before the ring, so waiting
+    // for them here does not wait for the weights (loads retire in order); doing this before the
+    // ring issue held the first weight loads back by one x round trip (r02 stamps: 1.2-2.8 us)
+    if (rms) {
+        double sacc = 0.0;
+#pragma unroll
+        for (int r = 0; r < KX_PART; ++r) {
+            const f32x4 v = xr[r];
+            sacc += (double)(v.x * v.x);
+            sacc += (double)(v.y * v.y);
+            sacc += (double)(v.z * v.z);
+            sacc += (double)(v.w * v.w);
+        }
+        sacc = wave_sum63_d(sacc);
+        if (lane == 63) red[wave] = sacc;
+    }
     // residual values of this workgroup's units: needed only by the epilogue threads
     float ra = 0.0f, rbv = 0.0f;
     const bool has_resid = P.seg[0].resid && (int)threadIdx.x < nwu;

@@ -72,12 +72,14 @@ def main():
         d = buf[i, :, :].astype(np.int64)
         m = d[:, 0] > 0
         det = []
-        for k in (1, 5, 6, 7, 2):
+        for k in (1, 7, 3, 2, 4):
             v = d[m, k]
             v = v[v > 0]
             det.append(f"{(np.median(v) - np.median(d[m, 0])) / 100.0:6.2f}" if len(v) else "   -  ")
-        print(f"{i:3d} from entry: issued {det[0]}  rms-arrive {det[1]}  rms-leave {det[2]}  pro-end {det[3]}"
-              f"  pro-barrier {det[4]}")
+        # gemv_k stamps (wave 0): 1 ring issued, 7 activation slice quantised, 3 first ring
+        # round consumed (first weights landed), 2 stream done + barrier, 4 epilogue done
+        print(f"{i:3d} from params-in-LDS: issued {det[0]}  act-quantised {det[1]}  first-weights {det[2]}"
+              f"  stream-done {det[3]}  epilogue-done {det[4]}")
     print(f"launches {len(rows)}  first entry -> last end {total:.1f} us;  sum of spans {spans.sum():.1f}"
           f"  sum of gaps {gaps.sum():.1f}")
 
