@@ -429,11 +429,12 @@ Ctx::Ctx(Model* model, uint32_t nctx, uint32_t nbatch, uint32_t nubatch) : m(mod
 #endif
     batch_ok = hp.n_expert == 0 && getenv("MI_NO_BATCH") == nullptr;
     if (batch_ok) {
-        // MFMA path when every layer matrix is Q4_K / Q6_K (the Q4_K_M / Q6_K models)
+        // MFMA batch path (decode_ubatch / mmq32) when every layer matrix is Q4_K / Q6_K or every
+        // one Q8_0; otherwise prompt chunks on the v_dot4 GEMM (decode_batch)
         mmq_ok = getenv("MI_NO_MMQ") == nullptr;
         for (const Layer& L : m->layers)
             for (const QMat* q : {&L.wq, &L.wk, &L.wv, &L.wo, &L.gate, &L.up, &L.down})
-                mmq_ok = mmq_ok && mmq_supported(q->type) && q->rows % 16 == 0;
+                mmq_ok = mmq_ok && mmq32_supported(q->type);
         const int NB = kBatchRows;
         MI_HIP(hipMalloc(&xb, (size_t)NB * hp.n_embd * sizeof(float)));
         MI_HIP(hipMalloc(&qb, (size_t)NB * hp.n_embd * sizeof(float)));
@@ -448,14 +449,17 @@ Ctx::Ctx(Model* model, uint32_t nctx, uint32_t nbatch, uint32_t nubatch) : m(mod
         // physical batches on mmq32: every layer matrix Q4_K / Q6_K (the output head too for
         // batched logits of every token)
         if (mmq_ok) {
+            // one activation format per model: every layer matrix a k-quant (Q8_K activations)
+            // or every one Q8_0 (Q8_0 activations)
+            ub_q80 = m->layers[0].wq.type == T_Q8_0;
             for (const Layer& L : m->layers)
                 for (const QMat* q : {&L.wq, &L.wk, &L.wv, &L.wo, &L.gate, &L.up, &L.down})
-                    mmq_ok = mmq_ok && mmq32_supported(q->type);
+                    mmq_ok = mmq_ok && mmq32_supported(q->type) && ((q->type == T_Q8_0) == ub_q80);
             out_mmq = mmq_ok && mmq32_supported(m->output.type);
             if (mmq_ok) m->ensure_mmq_copies();
             attn_mfma = attn_mfma_supported(hp.head_dim) && getenv("MI_ATTN_VALU") == nullptr;
             MI_HIP(hipMalloc(&ub_q, (size_t)UB_MAX * kmax));
-            MI_HIP(hipMalloc(&ub_dT, (size_t)UB_MAX * (kmax / 256) * sizeof(float)));
+            MI_HIP(hipMalloc(&ub_dT, (size_t)UB_MAX * (kmax / 32) * sizeof(float)));   // Q8_0: per 32
             MI_HIP(hipMalloc(&ub_bsb, (size_t)UB_MAX * (kmax / 256) * 16));
             MI_HIP(hipMalloc(&ub_rope, (size_t)UB_MAX * std::max(1, hp.n_rot / 2) * sizeof(float2)));
         }
@@ -872,6 +876,7 @@ ActQ8 Ctx::ub_act(int K, int ntok) const {
     a.K = K;
     a.ntok = ntok;
     a.npad = (ntok + 31) / 32 * 32;
+    a.q80 = ub_q80 ? 1 : 0;
     return a;
 }
 
@@ -969,7 +974,9 @@ void Ctx::decode_ubatch(const int32_t* tokens, int n, bool all) {
             }
         }
         if (all) {   // final norm + output head over every token of the batch
-            launch_quant_act(xb, hp.n_embd, m->output_norm, hp.eps, a_embd, stream);
+            ActQ8 a_out = a_embd;
+            a_out.q80 = m->output.type == T_Q8_0 ? 1 : 0;   // the head's own activation format
+            launch_quant_act(xb, hp.n_embd, m->output_norm, hp.eps, a_out, stream);
             GemmParams p;
             std::memset(&p, 0, sizeof(p));
             p.A = m->output;
@@ -980,7 +987,7 @@ void Ctx::decode_ubatch(const int32_t* tokens, int n, bool all) {
             p.tokpos = tokpos_b;
             p.out = logits_all + (size_t)c0 * hp.n_vocab;
             p.out_stride = hp.n_vocab;
-            launch_mmq32(p, a_embd, ub_rope, stream);
+            launch_mmq32(p, a_out, ub_rope, stream);
             if (c0 + nt == n) {   // the last row also feeds `logits` and the mapped top-k
                 MI_HIP(hipMemcpyAsync(logits, logits_all + (size_t)(n - 1) * hp.n_vocab, (size_t)hp.n_vocab * sizeof(float),
                                       hipMemcpyDeviceToDevice, stream));

@@ -145,6 +145,7 @@ struct Ctx {
     int8_t* ub_bsb = nullptr;           // [UB_MAX][kmax/256][16]
     float2* ub_rope = nullptr;          // [UB_MAX][n_rot/2]
     bool out_mmq = false;               // the output head is mmq32-capable (batched logits of every token)
+    bool ub_q80 = false;                // the layer matrices are Q8_0: Q8_0 batch activations
     bool attn_mfma = false;             // batch attention on f16 MFMA (attn_mfma.hip); MI_ATTN_VALU=1: VALU kernel
     // MI_OUT_ALL: logits of every token of the last decode call, [out_rows][n_vocab]
     float* logits_all = nullptr;

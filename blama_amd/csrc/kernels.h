@@ -265,6 +265,7 @@ struct ActQ8 {
     int8_t* bsb;               // [npad/32][K/256][32][16]: sub-block bsums as 64*hi + lo (bytes 0-7 hi, 8-15 lo)
     int K;
     int ntok, npad;            // tokens; rows allocated (ntok rounded up to 32, <= UB_MAX)
+    int q80;                   // 1: Q8_0 activations (for Q8_0 weights): dT is [K/32][npad] f16-rounded d, no bsb
 };
 void launch_quant_act(const float* x, int x_stride, const float* norm_w, float eps, const ActQ8& a, hipStream_t s);
 // ggml_rope_cache_init per token of the batch: out [ntok][n_rot/2] (cos, sin)

@@ -87,12 +87,13 @@ __global__ __launch_bounds__(256) void quant_act_kernel(const float* x, int x_st
     const int tile = t >> 5, tr = t & 31;
     const int fj = lane >> 3, fh = (lane >> 2) & 1, fw = lane & 3;   // this lane's 4 elements
     int8_t* q = a.q + (long long)tile * nb * 8192 + fj * 1024 + (fh * 32 + tr) * 16 + 4 * fw;
-    int8_t* bsb = a.bsb + ((long long)tile * nb * 32 + tr) * 16;
+    int8_t* bsb = a.q80 ? nullptr : a.bsb + ((long long)tile * nb * 32 + tr) * 16;
     if (t >= a.ntok) {
         for (int blk = wave; blk < nb; blk += 4) {
             *reinterpret_cast<int*>(q + blk * 8192) = 0;
-            if (lane < 4) reinterpret_cast<int*>(bsb + blk * 512)[lane] = 0;
-            if (lane == 0) a.dT[(long long)blk * a.npad + t] = 0.0f;
+            if (!a.q80 && lane < 4) reinterpret_cast<int*>(bsb + blk * 512)[lane] = 0;
+            if (a.q80 && lane < 8) a.dT[(long long)(blk * 8 + lane) * a.npad + t] = 0.0f;
+            if (!a.q80 && lane == 0) a.dT[(long long)blk * a.npad + t] = 0.0f;
         }
         return;
     }
@@ -123,6 +124,21 @@ __global__ __launch_bounds__(256) void quant_act_kernel(const float* x, int x_st
             v[1] = (v[1] * scale) * w.y;
             v[2] = (v[2] * scale) * w.z;
             v[3] = (v[3] * scale) * w.w;
+        }
+        if (a.q80) {   // quantize_row_q8_0 (x86 SIMD form): per 32 elements = 8 lanes
+            float am = fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3])));
+            am = fmaxf(am, __int_as_float(dpp_i<0xB1, 0xf>(__float_as_int(am))));
+            am = fmaxf(am, __int_as_float(dpp_i<0x4E, 0xf>(__float_as_int(am))));
+            am = fmaxf(am, __int_as_float(dpp_i<0x141, 0xf>(__float_as_int(am))));   // row_half_mirror
+            const float d0 = am / 127.0f;
+            const float id = am != 0.0f ? 127.0f / am : 0.0f;
+            int qz[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) qz[k] = (int)rintf(v[k] * id);
+            *reinterpret_cast<int*>(q + blk * 8192) =
+                (qz[0] & 0xFF) | ((qz[1] & 0xFF) << 8) | ((qz[2] & 0xFF) << 16) | ((qz[3] & 0xFF) << 24);
+            if ((lane & 7) == 0) a.dT[(long long)(blk * 8 + (lane >> 3)) * a.npad + t] = __half2float(__float2half_rn(d0));
+            continue;
         }
         const float a0 = fabsf(v[0]), a1 = fabsf(v[1]), a2 = fabsf(v[2]), a3 = fabsf(v[3]);
         const float amax = wave_max_pos(fmaxf(fmaxf(a0, a1), fmaxf(a2, a3)));
@@ -201,7 +217,10 @@ __device__ __forceinline__ void q4k_scales(const u32x4 hd, int sc[8], int mn[8])
 //   Q4_K  [p 4][lane 64][16] qs bytes 32p + 16h.. | [c 32][16] header                       4608 B
 //   Q6_K  [hf 2][cc 2][lane 64][16] ql bytes 64hf + 32cc + 16h.. | [hf 2][lane 64][16] qh bytes
 //         32hf + 16h.. | [c 32][16] scales | [c 32][2] d                                     6720 B
-__host__ __device__ constexpr int mmq32_tile_bytes_d(int type) { return type == T_Q4_K ? 4608 : type == T_Q6_K ? 6720 : 0; }
+//   Q8_0  [j 8][lane 64][16] qs bytes 32j + 16h.. | [c 32][8 f16] d                            8704 B
+__host__ __device__ constexpr int mmq32_tile_bytes_d(int type) {
+    return type == T_Q4_K ? 4608 : type == T_Q6_K ? 6720 : type == T_Q8_0 ? 8704 : 0;
+}
 
 __global__ void swizzle_kernel(const QMat A, const QMat B, int pair, uint8_t* dst) {
     const int nb = A.nb;
@@ -211,7 +230,14 @@ __global__ void swizzle_kernel(const QMat A, const QMat B, int pair, uint8_t* ds
     uint8_t* o = dst + tile * TB;
     for (int off = threadIdx.x; off < TB; off += blockDim.x) {
         int plane, c, byte;
-        if (A.type == T_Q4_K) {
+        if (A.type == T_Q8_0) {
+            if (off < 8192) {
+                const int jj = off >> 10, ln = (off >> 4) & 63, e = off & 15;
+                plane = 0; c = ln & 31; byte = 32 * jj + 16 * (ln >> 5) + e;
+            } else {
+                plane = 1; c = (off - 8192) >> 4; byte = (off - 8192) & 15;
+            }
+        } else if (A.type == T_Q4_K) {
             if (off < 4096) {
                 const int p = off >> 10, ln = (off >> 4) & 63, e = off & 15;
                 plane = 0; c = ln & 31; byte = 32 * p + 16 * (ln >> 5) + e;
@@ -234,7 +260,8 @@ __global__ void swizzle_kernel(const QMat A, const QMat B, int pair, uint8_t* ds
         const QMat& M = (pair && c >= 16) ? B : A;
         long long row = pair ? 16LL * rt + (c & 15) : 32LL * rt + c;
         if (row >= M.rows) row = M.rows - 1;
-        const int pb = A.type == T_Q4_K ? (plane == 0 ? 128 : 16) : (plane == 0 ? 128 : plane == 1 ? 64 : plane == 2 ? 16 : 2);
+        const int pb = A.type == T_Q8_0 ? (plane == 0 ? 256 : 16)
+                     : A.type == T_Q4_K ? (plane == 0 ? 128 : 16) : (plane == 0 ? 128 : plane == 1 ? 64 : plane == 2 ? 16 : 2);
         o[off] = M.p[plane][(row * nb + sb) * pb + byte];
     }
 }
@@ -280,6 +307,26 @@ __global__ __launch_bounds__(256, OCC) void mmq32_t(const GemmParams P, const Ac
 #pragma unroll
             for (int r = 0; r < 16; ++r) S[r] = 0;
             const uint8_t* wt = P.A.sw + ((long long)rt * nb + sb) * mmq32_tile_bytes_d(T);
+            if (T == T_Q8_0) {   // vec_dot_q8_0_q8_0: per 32-block sumi * (d_x * d_y)
+                const u32x4 dwv = *gp(reinterpret_cast<const u32x4*>(wt + 8192 + col * 16));
+                const unsigned dw[4] = {dwv.x, dwv.y, dwv.z, dwv.w};
+                const float* dT8 = act.dT + (long long)sb * 8 * act.npad + tok0 + 32 * t + 4 * h;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const v4i wq = *gp(reinterpret_cast<const v4i*>(wt + j * 1024 + lane * 16));
+                    const v4i a = *gp(reinterpret_cast<const v4i*>(aq + j * 1024));
+                    const v16i dj = mfma(a, wq);
+                    const float dwj = h2f(dw[j >> 1] >> (16 * (j & 1)));
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {
+                        const f32x4 dx4 = *gp(reinterpret_cast<const f32x4*>(dT8 + (long long)j * act.npad + 8 * g));
+                        const float dx[4] = {dx4.x, dx4.y, dx4.z, dx4.w};
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) y[4 * g + i] = fmaf((float)dj[4 * g + i], dwj * dx[i], y[4 * g + i]);
+                    }
+                }
+                continue;
+            }
             if (T == T_Q4_K) {
                 // qs[32p + l]: low nibble = sub-block 2p element l, high nibble = sub-block 2p+1
                 const u32x4 hd = *gp(reinterpret_cast<const u32x4*>(wt + 4096 + col * 16));
@@ -450,7 +497,7 @@ void launch_rope_table(const int* tokpos, int ntok, int n_rot, float theta_scale
     MI_HIP(hipGetLastError());
 }
 
-bool mmq32_supported(int type) { return type == T_Q4_K || type == T_Q6_K; }
+bool mmq32_supported(int type) { return type == T_Q4_K || type == T_Q6_K || type == T_Q8_0; }
 
 int mmq32_tile_bytes(int type) { return mmq::mmq32_tile_bytes_d(type); }
 
@@ -460,7 +507,7 @@ size_t mmq32_copy_bytes(const QMat& A, bool pair) {
 }
 
 void launch_mmq32_swizzle(const QMat& A, const QMat* B, uint8_t* dst, hipStream_t s) {
-    if (!mmq32_supported(A.type)) throw Error("mmq32 swizzle: Q4_K / Q6_K only");
+    if (!mmq32_supported(A.type)) throw Error("mmq32 swizzle: Q4_K / Q6_K / Q8_0 only");
     if (B && (B->type != A.type || B->rows != A.rows || B->K != A.K)) throw Error("mmq32 swizzle: bad pair");
     const long long nrt = B ? (A.rows + 15) / 16 : (A.rows + 31) / 32;
     hipLaunchKernelGGL(mmq::swizzle_kernel, dim3((unsigned)(nrt * A.nb)), dim3(256), 0, s, A, B ? *B : A, B ? 1 : 0, dst);
@@ -468,7 +515,8 @@ void launch_mmq32_swizzle(const QMat& A, const QMat* B, uint8_t* dst, hipStream_
 }
 
 void launch_mmq32(const GemmParams& p, const ActQ8& act, const float2* rope, hipStream_t s) {
-    if (!mmq32_supported(p.A.type)) throw Error("mmq32: Q4_K / Q6_K only");
+    if (!mmq32_supported(p.A.type)) throw Error("mmq32: Q4_K / Q6_K / Q8_0 only");
+    if ((p.A.type == T_Q8_0) != (act.q80 != 0)) throw Error("mmq32: Q8_0 weights take Q8_0 activations, k-quants Q8_K");
     if (act.K != p.K || p.A.K != p.K) throw Error("mmq32: activation length differs from K");
     const bool ab = p.pair == PAIR_AB;
     if (ab && (p.B.type != p.A.type || p.B.rows != p.A.rows || p.epi != EPI_SWIGLU))
@@ -488,7 +536,8 @@ void launch_mmq32(const GemmParams& p, const ActQ8& act, const float2* rope, hip
     decltype(&mmq::mmq32_t<T_Q4_K, false, 4, 2>) fn;
 #define MMQ_PICK(KS_, OCC_)                                                                              \
     fn = p.A.type == T_Q4_K ? (ab ? mmq::mmq32_t<T_Q4_K, true, KS_, OCC_> : mmq::mmq32_t<T_Q4_K, false, KS_, OCC_>) \
-                            : (ab ? mmq::mmq32_t<T_Q6_K, true, KS_, OCC_> : mmq::mmq32_t<T_Q6_K, false, KS_, OCC_>)
+       : p.A.type == T_Q6_K ? (ab ? mmq::mmq32_t<T_Q6_K, true, KS_, OCC_> : mmq::mmq32_t<T_Q6_K, false, KS_, OCC_>) \
+                            : (ab ? mmq::mmq32_t<T_Q8_0, true, KS_, OCC_> : mmq::mmq32_t<T_Q8_0, false, KS_, OCC_>)
     if (var == 1) MMQ_PICK(1, 2);
     else if (var == 2) MMQ_PICK(1, 3);
     else MMQ_PICK(4, 2);

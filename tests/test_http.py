@@ -180,8 +180,8 @@ def test_http_tinyllama_complete_32_verified_by_oracle(served_tinyllama):
     """/complete of 32 tokens on the TinyLlama-shaped Q8_0 model, then the C restatement of the
     CPU path verifies the completion as Session::fillCtx would (Session.cpp:231-282) under the
     reference's gate (t-LogitComparer.cpp:76-78), and the server's own /verify_completion of it
-    scores exactly 1 (Q8_0 has no MFMA batch path: the batched verify runs the same per-token
-    decode graphs as generation)."""
+    scores 1 to the fp32 order of the batched pass (Q8_0 batches run on the int8 MFMA GEMM
+    with Q8_0 activations, as vec_dot_q8_0_q8_0)."""
     import ggml_cpu
     port, buf = served_tinyllama
     req = {"prompt": "the quick brown fox", "max_tokens": 32, "seed": 3, "temp": 0.8, "top_p": 0.95}
@@ -191,7 +191,7 @@ def test_http_tinyllama_complete_32_verified_by_oracle(served_tinyllama):
     toks = out["tokenData"]
     assert len(toks) == 32
     st, vbody, _ = _post(port, "/verify_completion", {"request": req, "response": out})
-    assert st == 200 and json.loads(vbody)["result"] == 1.0
+    assert st == 200 and json.loads(vbody)["result"] >= 0.999
     orc = ggml_cpu.Model(buf, n_ctx=128)
     orc.decode(_prompt_ids(req["prompt"]))
     agg = R.MetricsAggregator()
