@@ -443,9 +443,6 @@ Ctx::Ctx(Model* model, uint32_t nctx, uint32_t nbatch, uint32_t nubatch) : m(mod
         MI_HIP(hipMalloc(&tokpos_b, (size_t)NB * 4 * sizeof(int)));
         MI_HIP(hipHostMalloc(&h_tokpos_b, (size_t)kTokbRing * NB * 4 * sizeof(int)));
         const int kmax = std::max(hp.n_embd, hp.n_ff);
-        MI_HIP(hipMalloc(&q8r_q, (size_t)MMQ_NT * kmax));
-        MI_HIP(hipMalloc(&q8r_d, (size_t)MMQ_NT * (kmax / 256) * sizeof(float)));
-        MI_HIP(hipMalloc(&q8r_bsum, (size_t)MMQ_NT * (kmax / 16) * sizeof(int)));
         // physical batches on mmq32: every layer matrix Q4_K / Q6_K (the output head too for
         // batched logits of every token)
         if (mmq_ok) {
@@ -496,8 +493,7 @@ Ctx::~Ctx() {
                     (void*)q, (void*)attn, (void*)h, (void*)h2, (void*)logits, (void*)cand, (void*)topk_ids,
                     (void*)topk_vals, (void*)sel, (void*)selw, (void*)gather_ids, (void*)gather_out,
                     (void*)cell_delta, (void*)move_src, (void*)part_o, (void*)attn_smax, (void*)attn_scores, (void*)stamps,
-                    (void*)xb, (void*)qb, (void*)attnb, (void*)hb, (void*)tokpos_b, (void*)q8r_q,
-                    (void*)q8r_d, (void*)q8r_bsum, (void*)ub_q, (void*)ub_dT, (void*)ub_bsb, (void*)ub_rope,
+                    (void*)xb, (void*)qb, (void*)attnb, (void*)hb, (void*)tokpos_b, (void*)ub_q, (void*)ub_dT, (void*)ub_bsb, (void*)ub_rope,
                     (void*)logits_all, (void*)grows_ids, (void*)grows_out})
         if (p) hipFree(p);
     for (void* p : {(void*)h_tokpos, (void*)h_topk_ids, (void*)h_topk_vals, (void*)h_logits, (void*)h_gather, (void*)h_grows,
@@ -757,21 +753,14 @@ void Ctx::decode_batch(const int32_t* tokens, int n) {
     const HParams& hp = m->hp;
     const float theta_scale = std::pow(hp.rope_base, -2.0f / (float)hp.n_rot);
     const float kq_scale = 1.0f / std::sqrt((float)hp.head_dim);
-    const int chunk = mmq_ok ? MMQ_NT : GEMM_NT;
-    auto q8 = [&](int K) { return Q8Rows{q8r_q, q8r_d, q8r_bsum, K}; };
-    // one projection: the int8-MFMA kernel on Q8_K rows quantised once per activation, or the
-    // v_dot4 GEMM that quantises its own rows
-    auto proj = [&](GemmParams p, const float* x, int x_stride, const float* norm, bool quantise) {
-        if (mmq_ok) {
-            if (quantise) launch_quant_rows(x, x_stride, norm, m->hp.eps, p.ntok, q8(p.K), stream);
-            launch_gemm_mmq(p, q8(p.K), stream);
-        } else {
-            p.x = x;
-            p.x_stride = x_stride;
-            p.norm_w = norm;
-            p.pro = norm ? PRO_RMSNORM : PRO_PLAIN;
-            launch_gemm(p, stream);
-        }
+    const int chunk = GEMM_NT;
+    // one projection on the v_dot4 GEMM, which quantises its own rows
+    auto proj = [&](GemmParams p, const float* x, int x_stride, const float* norm, bool) {
+        p.x = x;
+        p.x_stride = x_stride;
+        p.norm_w = norm;
+        p.pro = norm ? PRO_RMSNORM : PRO_PLAIN;
+        launch_gemm(p, stream);
     };
     for (int c0 = 0; c0 < n; c0 += chunk) {
         const int nt = std::min(chunk, n - c0);

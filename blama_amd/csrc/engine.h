@@ -153,9 +153,6 @@ struct Ctx {
     int out_rows = 0;                   // rows of logits_all valid (0: the last decode was MI_OUT_LAST)
     int topk_row = -1;                  // output row the mapped top-k buffers hold (-1: the last token)
     bool gemv_mix = getenv("MI_NO_MIX") == nullptr;   // mixed-type Q/K/V in one launch
-    int8_t* q8r_q = nullptr;            // Q8_K rows of one prompt chunk
-    float* q8r_d = nullptr;
-    int* q8r_bsum = nullptr;
     // diagnostics (MI_STAMPS builds only): s_memrealtime stamps of every
     // workgroup of every launch of the last enqueued step [launch][wg][8]
     static constexpr int kStampLaunches = 320, kStampWgs = 512;

@@ -231,24 +231,6 @@ void launch_embed_multi(const EmbedParams& p, int ntok, hipStream_t s);
 // out [ntok][n_head*hd] (the fused single-split arithmetic per token)
 void launch_attn_multi(const AttnParams& p, int ntok, float* out, hipStream_t s);
 
-// ---- int8-MFMA quantised GEMM over up to MMQ_NT tokens (prompt ingestion, Q4_K / Q6_K) ----
-// Activations are quantised once per launch group into global Q8_K rows (quant_rows); each
-// workgroup computes a 16-row x 32-token tile with v_mfma_i32_16x16x32_i8, one MFMA per Q4_K
-// sub-block (two per Q6_K 32-element span, one per 16-element scale group), so every
-// sub-block's integer sum is exact, as in vec_dot_q*_K_q8_K; scales are applied on the VALU.
-constexpr int MMQ_NT = 32;
-struct Q8Rows {               // Q8_K rows of MMQ_NT tokens (padding tokens are zero)
-    int8_t* q;                // [MMQ_NT][K]
-    float* d;                 // [MMQ_NT][K/256]
-    int* bsum;                // [MMQ_NT][K/16]
-    int K;
-};
-// RMSNorm (optional, norm_w != nullptr) + Q8_K quantisation of ntok rows of x (stride x_stride)
-void launch_quant_rows(const float* x, int x_stride, const float* norm_w, float eps, int ntok, const Q8Rows& r,
-                       hipStream_t s);
-bool mmq_supported(int type);
-// GemmParams as for launch_gemm (ntok <= MMQ_NT; pro/x/norm ignored: the activations are `act`)
-void launch_gemm_mmq(const GemmParams& p, const Q8Rows& act, hipStream_t s);
 
 // ---- causal attention of ntok query tokens (q [ntok][n_head*hd]) on f16 MFMA (attn_mfma.hip):
 // any number of cells (<= n_ctx); out [ntok][n_head*hd]; head_dim 64 or 128 ----

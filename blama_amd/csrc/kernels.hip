@@ -2352,307 +2352,6 @@ void launch_gemm(const GemmParams& p_in, hipStream_t s) {
     MI_HIP(hipGetLastError());
 }
 
-// ---------------------------------------------------------------------------
-// int8-MFMA quantised GEMM (prompt ingestion).  Wave tile: 16 weight rows x 16 tokens.
-// v_mfma_i32_16x16x32_i8 lane layout (checked by scripts/exp_mfma_layout.cpp):
-//   A: lane l holds row l%16, k 8*(l/16)..+7     B: token l%16, k 8*(l/16)..+7
-//   D: lane l, register i = row 4*(l/16)+i, token l%16
-// ---------------------------------------------------------------------------
-typedef int v4i_t __attribute__((ext_vector_type(4)));
-
-__global__ __launch_bounds__(256) void quant_rows_kernel(const float* x, int x_stride, const float* norm_w, float eps,
-                                                         int ntok, Q8Rows r) {
-    const int t = blockIdx.x;            // token row 0..MMQ_NT-1
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int nb = r.K >> 8;
-    __shared__ double red[4];
-    int8_t* q = r.q + (long long)t * r.K;
-    float* dd = r.d + (long long)t * nb;
-    int* bs = r.bsum + (long long)t * (r.K / 16);
-    if (t >= ntok) {                     // padding token: zero activations
-        for (int i = threadIdx.x; i < r.K / 4; i += 256) reinterpret_cast<int*>(q)[i] = 0;
-        for (int i = threadIdx.x; i < nb; i += 256) dd[i] = 0.0f;
-        for (int i = threadIdx.x; i < r.K / 16; i += 256) bs[i] = 0;
-        return;
-    }
-    const f32x4* x4 = reinterpret_cast<const f32x4*>(x + (long long)t * x_stride);
-    float scale = 1.0f;
-    if (norm_w) {
-        double sacc = 0.0;
-        for (int blk = wave; blk < nb; blk += 4) {
-            const f32x4 v = x4[blk * 64 + lane];
-            sacc += (double)(v.x * v.x);
-            sacc += (double)(v.y * v.y);
-            sacc += (double)(v.z * v.z);
-            sacc += (double)(v.w * v.w);
-        }
-        sacc = wave_sum63_d(sacc);
-        if (lane == 63) red[wave] = sacc;
-        __syncthreads();
-        const double tot = ((red[0] + red[1]) + red[2]) + red[3];
-        scale = 1.0f / sqrtf((float)(tot / (double)r.K) + eps);
-    }
-    const f32x4* w4 = reinterpret_cast<const f32x4*>(norm_w);
-    for (int blk = wave; blk < nb; blk += 4) {
-        const f32x4 xv = x4[blk * 64 + lane];
-        float v[4] = {xv.x, xv.y, xv.z, xv.w};
-        if (norm_w) {
-            const f32x4 w = w4[blk * 64 + lane];
-            v[0] = (v[0] * scale) * w.x;
-            v[1] = (v[1] * scale) * w.y;
-            v[2] = (v[2] * scale) * w.z;
-            v[3] = (v[3] * scale) * w.w;
-        }
-        quant_q8k_block(v, lane, q + blk * 256, bs + blk * 16, dd + blk);
-    }
-}
-
-void launch_quant_rows(const float* x, int x_stride, const float* norm_w, float eps, int ntok, const Q8Rows& r,
-                       hipStream_t s) {
-    if (r.K % 256) throw Error("quant_rows: K must be a multiple of 256");
-    hipLaunchKernelGGL(quant_rows_kernel, dim3(MMQ_NT), dim3(256), 0, s, x, x_stride, norm_w, eps, ntok, r);
-    MI_HIP(hipGetLastError());
-}
-
-bool mmq_supported(int type) { return type == T_Q4_K || type == T_Q6_K; }
-
-__device__ __forceinline__ long pack8(unsigned lo, unsigned hi) {
-    return (long)(((unsigned long long)hi << 32) | lo);
-}
-
-// One 16-row tile (rows r0..r0+15 of matrix M) x 16 tokens over all superblocks: per lane the
-// float results of rows r0+4*(l/16)+i, token l%16.
-// One 16-row tile (rows r0..r0+15 of M) x MMQ_NT tokens (NH = MMQ_NT/16 MFMA column tiles
-// sharing each A operand), over superblocks sb0, sb0+sbs, ...: per lane the float partial
-// results of rows r0+4*(l/16)+i, tokens 16*h + l%16.
-constexpr int MMQ_NH = MMQ_NT / 16;
-template <int T>
-__device__ __forceinline__ void mmq_tile(const QMat& M, long long r0, const Q8Rows& act, int lane, int sb0, int sbs,
-                                         float y[MMQ_NH][4]) {
-    const int nb = M.K >> 8;
-    const int ra = lane & 15, kq = lane >> 4;
-    const long long arow = r0 + ra;                     // A-operand row of this lane
-#pragma unroll
-    for (int h = 0; h < MMQ_NH; ++h) y[h][0] = y[h][1] = y[h][2] = y[h][3] = 0.0f;
-    const int8_t* aq[MMQ_NH];
-    const int* abs_[MMQ_NH];
-    const float* ad[MMQ_NH];
-#pragma unroll
-    for (int h = 0; h < MMQ_NH; ++h) {
-        const int tok = 16 * h + (lane & 15);
-        aq[h] = act.q + (long long)tok * act.K + 8 * kq;
-        abs_[h] = act.bsum + (long long)tok * (act.K / 16);
-        ad[h] = act.d + (long long)tok * nb;
-    }
-#pragma unroll 2
-    for (int sb = sb0; sb < nb; sb += sbs) {
-        int S[MMQ_NH][4], Mn[MMQ_NH][4];
-#pragma unroll
-        for (int h = 0; h < MMQ_NH; ++h)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) S[h][i] = Mn[h][i] = 0;
-        if (T == T_Q4_K) {
-            const uint8_t* qs = M.p[0] + (arow * nb + sb) * 128 + 8 * kq;
-            u32x4 hd[4];   // headers of this lane's 4 OUTPUT rows
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-                hd[i] = *reinterpret_cast<const u32x4*>(M.p[1] + ((r0 + 4 * kq + i) * nb + sb) * 16);
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                const uint2 wq = *reinterpret_cast<const uint2*>(qs + 32 * c);
-                const long alo = pack8(wq.x & 0x0F0F0F0Fu, wq.y & 0x0F0F0F0Fu);
-                const long ahi = pack8((wq.x >> 4) & 0x0F0F0F0Fu, (wq.y >> 4) & 0x0F0F0F0Fu);
-                unsigned SC[4], MM[4];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {   // get_scale_min_k4 for sub-blocks 2c, 2c+1
-                    const unsigned sh = (c & 1) * 16;
-                    const unsigned Y = hd[i].y >> sh, Zs = hd[i].z >> sh, Wd = hd[i].w >> sh;
-                    SC[i] = c < 2 ? (Y & 0x3F3Fu) : ((Wd & 0x0F0Fu) | ((Y >> 2) & 0x3030u));
-                    MM[i] = c < 2 ? (Zs & 0x3F3Fu) : (((Wd >> 4) & 0x0F0Fu) | ((Zs >> 2) & 0x3030u));
-                }
-#pragma unroll
-                for (int h = 0; h < MMQ_NH; ++h) {
-                    const long blo = *reinterpret_cast<const long*>(aq[h] + sb * 256 + 64 * c);
-                    const long bhi = *reinterpret_cast<const long*>(aq[h] + sb * 256 + 64 * c + 32);
-                    v4i_t z = {0, 0, 0, 0};
-                    const v4i_t ilo = __builtin_amdgcn_mfma_i32_16x16x32_i8(alo, blo, z, 0, 0, 0);
-                    const v4i_t ihi = __builtin_amdgcn_mfma_i32_16x16x32_i8(ahi, bhi, z, 0, 0, 0);
-                    // bsums of sub-blocks 2c, 2c+1 (Q8_K bsums are per 16 elements)
-                    const int bslo = abs_[h][sb * 16 + 4 * c] + abs_[h][sb * 16 + 4 * c + 1];
-                    const int bshi = abs_[h][sb * 16 + 4 * c + 2] + abs_[h][sb * 16 + 4 * c + 3];
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        S[h][i] += (int)(SC[i] & 0xFF) * ilo[i] + (int)((SC[i] >> 8) & 0xFF) * ihi[i];
-                        Mn[h][i] += (int)(MM[i] & 0xFF) * bslo + (int)((MM[i] >> 8) & 0xFF) * bshi;
-                    }
-                }
-            }
-#pragma unroll
-            for (int h = 0; h < MMQ_NH; ++h) {
-                const float dx = ad[h][sb];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const float d = h2f(hd[i].x) * dx;
-                    const float dm = h2f(hd[i].x >> 16) * dx;
-                    y[h][i] += d * (float)S[h][i] - dm * (float)Mn[h][i];
-                }
-            }
-        } else {   // Q6_K: ql[128] qh[64] scales[16] d; a lane's 8 elements share one 16-group
-            const uint8_t* ql = M.p[0] + (arow * nb + sb) * 128;
-            const uint8_t* qh = M.p[1] + (arow * nb + sb) * 64;
-            u32x4 scw[4];
-            float dr[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                scw[i] = *reinterpret_cast<const u32x4*>(M.p[2] + ((r0 + 4 * kq + i) * nb + sb) * 16);
-                dr[i] = h2f(*reinterpret_cast<const unsigned short*>(M.p[3] + ((r0 + 4 * kq + i) * nb + sb) * 2));
-            }
-            // element e of the superblock (dequantize_row_q6_K): half hf = e/128, l = e%32, quarter
-            // qq = (e%128)/32: ql byte l + 32*(qq&1) (+64hf), nibble qq>>1; qh byte l (+32hf), bits 2qq
-#pragma unroll
-            for (int span = 0; span < 8; ++span) {
-                const int hf = span >> 2, qq = span & 3;
-                const int l0 = 8 * kq;
-                const uint2 lb = *reinterpret_cast<const uint2*>(ql + 64 * hf + 32 * (qq & 1) + l0);
-                const uint2 hb = *reinterpret_cast<const uint2*>(qh + 32 * hf + l0);
-                const unsigned nsh = (qq >> 1) * 4, hsh = 2 * qq;
-                auto q6 = [&](unsigned lw, unsigned hw) {
-                    const unsigned v = ((lw >> nsh) & 0x0F0F0F0Fu) | (((hw >> hsh) & 0x03030303u) << 4);
-                    // minus 32 per byte (0..63 -> -32..31) without borrows between bytes
-                    return ((v | 0x80808080u) - 0x20202020u) ^ 0x80808080u;
-                };
-                const unsigned a0 = q6(lb.x, hb.x), a1 = q6(lb.y, hb.y);
-                // the span's two 16-element scale groups: lanes kq 0,1 -> group 0, kq 2,3 -> group 1
-                const long ag0 = kq < 2 ? pack8(a0, a1) : 0;
-                const long ag1 = kq < 2 ? 0 : pack8(a0, a1);
-                const int is = 8 * hf + 2 * qq;   // scale index of group 0
-                int sc0[4], sc1[4];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const unsigned wv[4] = {scw[i].x, scw[i].y, scw[i].z, scw[i].w};
-                    sc0[i] = (int)(signed char)((wv[is >> 2] >> (8 * (is & 3))) & 0xFF);
-                    sc1[i] = (int)(signed char)((wv[(is + 1) >> 2] >> (8 * ((is + 1) & 3))) & 0xFF);
-                }
-#pragma unroll
-                for (int h = 0; h < MMQ_NH; ++h) {
-                    const long b = *reinterpret_cast<const long*>(aq[h] + sb * 256 + 32 * span);
-                    v4i_t z = {0, 0, 0, 0};
-                    const v4i_t i0 = __builtin_amdgcn_mfma_i32_16x16x32_i8(ag0, b, z, 0, 0, 0);
-                    const v4i_t i1 = __builtin_amdgcn_mfma_i32_16x16x32_i8(ag1, b, z, 0, 0, 0);
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) S[h][i] += sc0[i] * i0[i] + sc1[i] * i1[i];
-                }
-            }
-#pragma unroll
-            for (int h = 0; h < MMQ_NH; ++h) {
-                const float dx = ad[h][sb];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) y[h][i] += (dr[i] * dx) * (float)S[h][i];
-            }
-        }
-    }
-}
-
-template <int T>
-__global__ __launch_bounds__(256) void gemm_mmq_t(const GemmParams P, const Q8Rows act) {
-    // one workgroup per 16-row tile; its 4 waves split the superblocks (sb = wave mod 4) and
-    // their partial results are added in wave order through LDS (deterministic)
-    __shared__ float red[2][4][MMQ_NH][4][64];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const bool adj = P.pair == PAIR_ADJ;
-    const long long r0 = (long long)blockIdx.x * 16;
-    if (r0 >= P.A.rows) return;
-    float y[MMQ_NH][4], yb[MMQ_NH][4];
-    mmq_tile<T>(P.A, r0, act, lane, w, 4, y);
-    if (!adj) mmq_tile<T>(P.B, r0, act, lane, w, 4, yb);
-#pragma unroll
-    for (int h = 0; h < MMQ_NH; ++h)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            red[0][w][h][i][lane] = y[h][i];
-            if (!adj) red[1][w][h][i][lane] = yb[h][i];
-        }
-    __syncthreads();
-    if (w != 0) return;
-    const int kq = lane >> 4;
-#pragma unroll
-    for (int h = 0; h < MMQ_NH; ++h) {
-        const int t = 16 * h + (lane & 15);
-        float ya4[4], yb4[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            ya4[i] = ((red[0][0][h][i][lane] + red[0][1][h][i][lane]) + red[0][2][h][i][lane]) + red[0][3][h][i][lane];
-            yb4[i] = adj ? 0.0f
-                         : ((red[1][0][h][i][lane] + red[1][1][h][i][lane]) + red[1][2][h][i][lane]) +
-                               red[1][3][h][i][lane];
-        }
-        if (t >= P.ntok) continue;
-        const int pos = P.tokpos ? P.tokpos[t * 4 + 1] : 0, cell = P.tokpos ? P.tokpos[t * 4 + 2] : 0;
-        float* out = P.out + (long long)t * P.out_stride;
-        const float* res = P.resid ? P.resid + (long long)t * P.out_stride : nullptr;
-#pragma unroll
-        for (int pr = 0; pr < 2; ++pr) {   // output row pairs (4kq+2pr, 4kq+2pr+1)
-            const long long ra = r0 + 4 * kq + 2 * pr, rb = ra + 1;
-            const float ya = ya4[2 * pr], yb2 = ya4[2 * pr + 1];
-            switch (P.epi) {
-            case EPI_STORE: out[ra] = ya; out[rb] = yb2; break;
-            case EPI_ADD: {
-                const float r0v = res[ra], r1v = res[rb];
-                out[ra] = ya + r0v;
-                out[rb] = yb2 + r1v;
-                break;
-            }
-            case EPI_ROPE_Q:
-            case EPI_ROPE_K: {
-                const int i0 = (int)(ra % P.head_dim);
-                float o0 = ya, o1 = yb2;
-                if (i0 < P.n_rot) {   // ggml_rope_cache_init for this token's position, pair i0/2
-                    float theta = (float)pos;
-                    for (int k2 = 0; k2 < i0 / 2; ++k2) theta = theta * P.theta_scale;
-                    const float ff = P.freq_factors ? P.freq_factors[i0 / 2] : 1.0f;
-                    const float th = P.freq_scale * (theta / ff);
-                    const float cs = cosf(th), sn = sinf(th);
-                    o0 = ya * cs - yb2 * sn;
-                    o1 = ya * sn + yb2 * cs;
-                }
-                if (P.epi == EPI_ROPE_Q) {
-                    out[ra] = o0;
-                    out[rb] = o1;
-                } else {
-                    __half* kr = P.kcache + (long long)cell * P.kv_dim;
-                    kr[ra] = __float2half_rn(o0);
-                    kr[rb] = __float2half_rn(o1);
-                    if (ra == 0) P.cell_pos[cell] = pos;
-                }
-                break;
-            }
-            case EPI_V: {
-                __half* vr = P.vcache + (long long)cell * P.kv_dim;
-                vr[ra] = __float2half_rn(ya);
-                vr[rb] = __float2half_rn(yb2);
-                break;
-            }
-            case EPI_SWIGLU:   // PAIR_AB: gate rows in ya4, up rows in yb4 (same row indices)
-                out[ra] = silu_f(ya4[2 * pr]) * yb4[2 * pr];
-                out[rb] = silu_f(ya4[2 * pr + 1]) * yb4[2 * pr + 1];
-                break;
-            default: break;
-            }
-        }
-    }
-}
-
-void launch_gemm_mmq(const GemmParams& p, const Q8Rows& act, hipStream_t s) {
-    if (!mmq_supported(p.A.type)) throw Error("gemm_mmq: Q4_K / Q6_K only");
-    if (p.ntok < 1 || p.ntok > MMQ_NT) throw Error("gemm_mmq: 1..MMQ_NT tokens");
-    if (p.A.rows % 16) throw Error("gemm_mmq: rows must be a multiple of 16");
-    if (act.K != p.A.K) throw Error("gemm_mmq: activation length differs from K");
-    if (p.pair == PAIR_AB && (p.B.type != p.A.type || p.B.rows != p.A.rows)) throw Error("gemm_mmq: bad pair");
-    const int grid = p.A.rows / 16;   // one workgroup per 16-row tile
-    auto fn = p.A.type == T_Q4_K ? gemm_mmq_t<T_Q4_K> : gemm_mmq_t<T_Q6_K>;
-    hipLaunchKernelGGL(fn, dim3(grid), dim3(256), 0, s, p, act);
-    MI_HIP(hipGetLastError());
-}
 
 // ---------------------------------------------------------------------------
 // Exact ggml dequantisation of one element (dequantize_row_*, ggml-quants.c)
