@@ -91,11 +91,13 @@ def served(tmp_path):
     yield from _serve(tmp_path, synthetic.CONFIGS["tiny-q4_k_m"])
 
 
-def _serve(tmp_path, cfg):
+def _serve(tmp_path, cfg, devices=None):
     buf = synthetic.build_gguf(cfg, seed=5)
     path = str(tmp_path / "model.gguf")
     buf.tofile(path)
     env = dict(os.environ, BLAMA_MODEL=path, BLAMA_HOST="127.0.0.1", BLAMA_PORT="0")
+    if devices:
+        env["BLAMA_DEVICES"] = devices
     proc = subprocess.Popen([_binary()], env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
                             text=True)
     port = None
@@ -206,3 +208,54 @@ def test_http_tinyllama_complete_32_verified_by_oracle(served_tinyllama):
         sims.append(R.logit_similarity(claimed, mine))
     orc.close()
     assert score >= 0.95 and float(np.mean(sims)) >= 0.98 and min(top1) == 1.0, (score, np.mean(sims))
+
+
+@pytest.fixture
+def served_replicas(tmp_path):
+    # configs[3]'s shape at small scale: 4 replicas (one Model + Instance + worker each) behind
+    # the least-loaded dispatcher; on the 8-GPU node BLAMA_DEVICES=0,...,7 puts one per GPU
+    yield from _serve(tmp_path, synthetic.CONFIGS["tiny-q4_k_m"], devices="0,0,0,0")
+
+
+@pytest.mark.gpu
+def test_http_concurrent_verify_on_replicas(served_replicas):
+    """8 concurrent /verify_completion requests (BASELINE configs[3] is 8 concurrent sessions on
+    8 GPUs) against a server with 4 replicas: every request is answered, each completion
+    verifies itself (score >= 0.999 through the batched pass), and a tampered one scores low."""
+    import threading
+    port, _ = served_replicas
+    reqs = [{"prompt": f"request number {i}", "max_tokens": 12, "seed": i, "temp": 0.8, "top_p": 0.95}
+            for i in range(8)]
+    outs = [None] * 8
+
+    def complete(i):
+        st, body, _ = _post(port, "/complete", reqs[i])
+        assert st == 200, body
+        outs[i] = json.loads(body)
+
+    th = [threading.Thread(target=complete, args=(i,)) for i in range(8)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    assert all(o is not None and len(o["tokenData"]) == 12 for o in outs)
+    results = [None] * 8
+
+    def verify(i):
+        body = {"request": reqs[i], "response": outs[i]}
+        if i == 7:   # one tampered completion
+            body = json.loads(json.dumps(body))
+            for t in body["response"]["tokenData"]:
+                for l in t["logits"]:
+                    l["logit"] *= 1.5
+        st, rb, _ = _post(port, "/verify_completion", body)
+        assert st == 200, rb
+        results[i] = json.loads(rb)["result"]
+
+    th = [threading.Thread(target=verify, args=(i,)) for i in range(8)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    assert all(r is not None and r >= 0.999 for r in results[:7]), results
+    assert results[7] < 0.95
