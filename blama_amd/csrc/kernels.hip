@@ -14,6 +14,7 @@
 #include <hip/hip_ext.h>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 
 namespace mi {
 
@@ -1964,7 +1965,9 @@ int gemv_default_grid(const GemvParams& p, int role) {
     int per = gemv_waves(p.seg[0].A.type, role, p.K);
     if (gemv_k_on(p.K)) per /= gemv_k_groups(p.K);
     const int g = (p.total_units + per - 1) / per;
-    return g < 1 ? 1 : (g > 256 ? 256 : g);
+    // at most one workgroup per CU by default; MI_GEMV_GRID raises the cap (A/B)
+    static const int cap = getenv("MI_GEMV_GRID") ? std::max(1, atoi(getenv("MI_GEMV_GRID"))) : 256;
+    return g < 1 ? 1 : (g > cap ? cap : g);
 }
 
 // Validates a launch and fixes its grid-dependent fields; returns the kernel configuration
