@@ -2494,7 +2494,9 @@ __global__ __launch_bounds__(256) void attn_scores_kernel(const AttnParams P) {
     constexpr int CPW = 64 / LPC;
     constexpr int HD = LPC * 8;
     __shared__ float red[4][R];
-    const int g = blockIdx.x, s = blockIdx.y;
+    // kv head, and the first of the R q heads this workgroup serves (qsplit: one q head each)
+    const int g = P.qsplit ? (int)blockIdx.x / P.qsplit : (int)blockIdx.x, s = blockIdx.y;
+    const int gq = P.qsplit ? (int)blockIdx.x : (int)blockIdx.x * R;
 #ifdef MI_STAMPS
     unsigned long long* const stp = P.stamps ? P.stamps + (blockIdx.y * gridDim.x + blockIdx.x) * 8 : nullptr;
     if (stp && threadIdx.x == 0) stp[0] = __builtin_amdgcn_s_memrealtime();
@@ -2509,7 +2511,7 @@ __global__ __launch_bounds__(256) void attn_scores_kernel(const AttnParams P) {
     float q[R][8];
 #pragma unroll
     for (int t = 0; t < R; ++t) {
-        const float4* qp = reinterpret_cast<const float4*>(P.q + (long long)(g * R + t) * HD + L * 8);
+        const float4* qp = reinterpret_cast<const float4*>(P.q + (long long)(gq + t) * HD + L * 8);
         const float4 a = qp[0], b = qp[1];
         const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
 #pragma unroll
@@ -2550,7 +2552,7 @@ __global__ __launch_bounds__(256) void attn_scores_kernel(const AttnParams P) {
                 for (int off = LPC / 2; off > 0; off >>= 1) d += __shfl_xor(d, off, 64);
                 const float w = valid ? d * P.scale : -INFINITY;
                 mx[t] = fmaxf(mx[t], w);
-                if (L == 0 && c < c1) P.scores[(long long)(g * R + t) * P.n_ctx + c] = w;
+                if (L == 0 && c < c1) P.scores[(long long)(gq + t) * P.n_ctx + c] = w;
             }
         }
     }
@@ -2563,7 +2565,7 @@ __global__ __launch_bounds__(256) void attn_scores_kernel(const AttnParams P) {
     if (threadIdx.x < R) {
         const int t = threadIdx.x;
         const float m = fmaxf(fmaxf(red[0][t], red[1][t]), fmaxf(red[2][t], red[3][t]));
-        P.smax[s * P.n_head + g * R + t] = m;
+        P.smax[s * P.n_head + gq + t] = m;
     }
 #ifdef MI_STAMPS
     if (stp && threadIdx.x == 0) stp[4] = __builtin_amdgcn_s_memrealtime();
@@ -2577,7 +2579,9 @@ __global__ __launch_bounds__(256) void attn_pv_kernel(const AttnParams P) {
     __shared__ double dred[4][R];
     __shared__ float gm[R], ginv[R];
     __shared__ float red_o[4][R][HD];
-    const int g = blockIdx.x, s = blockIdx.y;
+    // kv head, and the first of the R q heads this workgroup serves (qsplit: one q head each)
+    const int g = P.qsplit ? (int)blockIdx.x / P.qsplit : (int)blockIdx.x, s = blockIdx.y;
+    const int gq = P.qsplit ? (int)blockIdx.x : (int)blockIdx.x * R;
 #ifdef MI_STAMPS
     unsigned long long* const stp = P.stamps2 ? P.stamps2 + (blockIdx.y * gridDim.x + blockIdx.x) * 8 : nullptr;
     if (stp && threadIdx.x == 0) stp[0] = __builtin_amdgcn_s_memrealtime();
@@ -2595,13 +2599,13 @@ __global__ __launch_bounds__(256) void attn_pv_kernel(const AttnParams P) {
 #pragma unroll
     for (int t = 0; t < R; ++t) {
         float m = -INFINITY;
-        for (int k = 0; k < nsplit; ++k) m = fmaxf(m, P.smax[k * P.n_head + g * R + t]);
+        for (int k = 0; k < nsplit; ++k) m = fmaxf(m, P.smax[k * P.n_head + gq + t]);
         M[t] = m;
     }
     // sum over all cells of expf(w - max), in double, fixed order
 #pragma unroll
     for (int t = 0; t < R; ++t) {
-        const float* w = P.scores + (long long)(g * R + t) * P.n_ctx;
+        const float* w = P.scores + (long long)(gq + t) * P.n_ctx;
         double acc = 0.0;
         for (int c = tid; c < ncell; c += 256) acc += (double)expf(w[c] - M[t]);
         acc = wave_sum_d(acc);
@@ -2631,7 +2635,7 @@ __global__ __launch_bounds__(256) void attn_pv_kernel(const AttnParams P) {
             vv[u] = *reinterpret_cast<const u32x4*>(P.vcache + (long long)c * P.kv_dim + row_off);
 #pragma unroll
             for (int t = 0; t < R; ++t) {
-                const float w = P.scores[(long long)(g * R + t) * P.n_ctx + c];
+                const float w = P.scores[(long long)(gq + t) * P.n_ctx + c];
                 // ggml_vec_soft_max_f32 then the f16 vec_dot_type conversion of KQV's src1
                 const float p = expf(w - gm[t]) * ginv[t];
                 pw[u][t] = in ? __half2float(__float2half_rn(p)) : 0.0f;
@@ -2669,7 +2673,7 @@ __global__ __launch_bounds__(256) void attn_pv_kernel(const AttnParams P) {
     for (int i = tid; i < R * HD; i += 256) {
         const int t = i / HD, d = i % HD;
         const float acc = ((red_o[0][t][d] + red_o[1][t][d]) + red_o[2][t][d]) + red_o[3][t][d];
-        P.part_o[((long long)s * P.n_head + g * R + t) * HD + d] = acc;
+        P.part_o[((long long)s * P.n_head + gq + t) * HD + d] = acc;
     }
 #ifdef MI_STAMPS
     if (stp && threadIdx.x == 0) stp[4] = __builtin_amdgcn_s_memrealtime();
@@ -2890,6 +2894,17 @@ void launch_attn(const AttnParams& p, hipStream_t s) {
             return;
         }
         hipLaunchKernelGGL(ff, dim3(p.n_head_kv), dim3(256), 0, s, p);
+        MI_HIP(hipGetLastError());
+        return;
+    }
+    if (r > 1 && p.n_head_kv < 16) {   // few kv heads: one workgroup per q head and split
+        AttnFn f1 = nullptr, a1 = nullptr, b1 = nullptr;
+        attn_fns_r<1>(p.head_dim, a1, b1, f1);
+        AttnParams q = p;
+        q.qsplit = r;
+        hipLaunchKernelGGL(a1, dim3(p.n_head, ATTN_SMAX), dim3(256), 0, s, q);
+        MI_HIP(hipGetLastError());
+        hipLaunchKernelGGL(b1, dim3(p.n_head, ATTN_SMAX), dim3(256), 0, s, q);
         MI_HIP(hipGetLastError());
         return;
     }
