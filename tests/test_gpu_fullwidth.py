@@ -142,3 +142,48 @@ def test_fullwidth_7b_crosses_512_cells(gpu_lib):
     finally:
         ctx.close()
         orc.close()
+
+
+@pytest.mark.parametrize("name", ["llama2-7b-q4_k_m", "llama3-8b-q6_k", "tinyllama-1.1b-q8_0"])
+def test_fullwidth_batched_verification_matches_oracle(gpu_lib, name):
+    """MI_OUT_ALL at real widths: 24 claimed tokens after a 20-token prompt in one batched pass
+    (mmq32 for every projection and the output head, MFMA attention); every row against the C
+    oracle decoding the same tokens one at a time, with this file's tolerances and the
+    reference gate, and the claimed ids gathered per row (mi_gather_rows) as fillCtx does."""
+    cfg, buf, m = full_model(name)
+    ctx = engine.Context(m, n_ctx=64)
+    orc = ggml_cpu.Model(buf, n_ctx=64)
+    rng = np.random.default_rng(13)
+    prompt = [int(t) for t in rng.integers(0, cfg.n_vocab, 20)]
+    claimed = [int(t) for t in rng.integers(0, cfg.n_vocab, 24)]
+    try:
+        ctx.decode(prompt)
+        orc.decode(prompt)
+        assert ctx.decode(claimed, all_logits=True) == 0
+        agg = R.MetricsAggregator()
+        sims, top1 = [], []
+        score = None
+        ids_rows = np.zeros((len(claimed), 10), np.int32)
+        refs = []
+        for i, t in enumerate(claimed):
+            ref = orc.decode_one(t).astype(np.float64)
+            refs.append(ref)
+            got = ctx.logits(row=i)
+            dmax, rmax, rl2 = _err(got, ref)
+            assert rmax <= TOL_MAX and rl2 <= TOL_L2, (name, i, rmax, rl2)
+            ids, vals = ctx.topk(10, row=i)
+            ids_rows[i] = ids
+            ref_sorted = np.sort(ref)[::-1][:10]
+            assert np.all(np.abs(ref[ids.astype(np.int64)] - ref_sorted) <= 2 * dmax + 1e-6), (name, i)
+            a = [(int(x), float(v)) for x, v in zip(ids, vals)]
+            cm = R.compare(a, R.gather(ref.astype(np.float32), [x for x, _ in a]))
+            top1.append(cm.top1Match)
+            score = agg.push_and_verify([cm])
+            sims.append(R.logit_similarity(a, R.gather(ref.astype(np.float32), [x for x, _ in a])))
+        g = ctx.gather_rows(0, ids_rows)
+        for i in range(len(claimed)):
+            assert np.array_equal(g[i], ctx.logits(row=i)[ids_rows[i]])
+        assert score >= 0.95 and float(np.mean(sims)) >= 0.98 and min(top1) == 1.0, (score, np.mean(sims))
+    finally:
+        ctx.close()
+        orc.close()
