@@ -485,8 +485,10 @@ std::vector<Token> Vocab::tokenize(std::string_view text, bool addSpecial, bool 
 }
 
 // ---------------------------------------------------------------- Sampler ---
-Sampler::Sampler(Model& model, const Params& params) : m_model(model), m_params(params), m_rng(params.rngSeed) {
+Sampler::Sampler(Model& model, const Params& params)
+    : m_model(model), m_params(params), m_mu(2.0f * params.mirostat.tau), m_xtcRng(params.rngSeed), m_rng(params.rngSeed) {
     if (!params.grammar.empty()) BL_THROW("grammar-constrained sampling is not served by this build");
+    if (params.mirostat.ver > 2) BL_THROW("Unsupported mirostat version");   // Sampler.cpp:67-69
 }
 
 void Sampler::accept(Token id, bool) {
@@ -498,6 +500,8 @@ void Sampler::accept(Token id, bool) {
 void Sampler::reset() {
     m_prev.clear();
     m_rng.seed(m_params.rngSeed);   // llama_sampler_dist reset re-seeds
+    m_xtcRng.seed(m_params.rngSeed);
+    m_mu = 2.0f * m_params.mirostat.tau;
 }
 
 namespace {
@@ -533,6 +537,7 @@ Token Sampler::applyChain(std::vector<Candidate>& cur) {
         }
         std::stable_sort(cur.begin(), cur.end(), [](auto& a, auto& b) { return a.logit > b.logit; });
     }
+    if (P.mirostat.ver == 1 || P.mirostat.ver == 2) return applyMirostat(cur);
     for (SamplingType st : P.samplerSequence) {
         switch (st) {
         case SamplingType::Top_K: {
@@ -541,9 +546,30 @@ Token Sampler::applyChain(std::vector<Candidate>& cur) {
             cur.resize(k);
             break;
         }
-        case SamplingType::Typical_P:
-            if (P.typicalP < 1.0f) BL_THROW("typical_p < 1 is not served by this build");
+        case SamplingType::Typical_P: {   // llama_sampler_typical_apply (locally typical sampling)
+            if (P.typicalP >= 1.0f) break;
+            softmax(cur);
+            float entropy = 0.0f;
+            for (auto& c : cur) entropy += -c.p * std::log(c.p);
+            std::vector<float> shifted(cur.size());
+            for (size_t i = 0; i < cur.size(); ++i) shifted[i] = std::fabs(-std::log(cur[i].p) - entropy);
+            std::vector<size_t> idx(cur.size());
+            for (size_t i = 0; i < idx.size(); ++i) idx[i] = i;
+            std::sort(idx.begin(), idx.end(), [&](size_t a, size_t b) { return shifted[a] < shifted[b]; });
+            float cum = 0.0f;
+            size_t last = idx.size();
+            for (size_t i = 0; i < idx.size(); ++i) {
+                cum += cur[idx[i]].p;
+                // min_keep is size_t there: min_keep 0 makes (min_keep - 1) the maximum value, so
+                // the set is never cut (reproduced as is)
+                if (cum > P.typicalP && i >= min_keep - 1) { last = i + 1; break; }
+            }
+            std::vector<Candidate> nw;
+            for (size_t i = 0; i < last; ++i) nw.push_back(cur[idx[i]]);
+            std::stable_sort(nw.begin(), nw.end(), [](auto& a, auto& b) { return a.logit > b.logit; });
+            cur.swap(nw);
             break;
+        }
         case SamplingType::Top_P: {
             if (P.topP >= 1.0f) break;
             softmax(cur);
@@ -565,8 +591,32 @@ Token Sampler::applyChain(std::vector<Candidate>& cur) {
             cur.resize(i);
             break;
         }
+        case SamplingType::XTC: {   // llama_sampler_xtc_apply: drop the top choices above threshold
+            if (P.xtc.probability <= 0.0f || P.xtc.threshold > 0.5f || cur.size() < 2) break;
+            std::uniform_real_distribution<float> u(0.0f, 1.0f);
+            if (u(m_xtcRng) > P.xtc.probability) break;
+            softmax(cur);
+            size_t pos_last = 0;
+            for (size_t i = 0; i < cur.size(); ++i) {
+                if (cur[i].p >= P.xtc.threshold) pos_last = i;
+                else break;
+            }
+            if (cur.size() - pos_last >= min_keep && pos_last > 0) cur.erase(cur.begin(), cur.begin() + (std::ptrdiff_t)pos_last);
+            break;
+        }
         case SamplingType::Temperature:
-            if (P.tempRange > 0.0f) BL_THROW("dynamic temperature is not served by this build");
+            if (P.tempRange > 0.0f) {   // llama_sampler_temp_ext_apply: entropy-scaled temperature
+                if (cur.size() <= 1) break;
+                const float min_t = std::max(0.0f, P.temp - P.tempRange), max_t = P.temp + P.tempRange;
+                softmax(cur);
+                const float max_entropy = -std::log(1.0f / (float)cur.size());
+                float entropy = 0.0f;
+                for (auto& c : cur)
+                    if (c.p > 0.0f) entropy -= c.p * std::log(c.p);
+                const float dyn_t = min_t + (max_t - min_t) * std::pow(entropy / max_entropy, P.tempExp);
+                for (auto& c : cur) c.logit /= dyn_t;
+                break;
+            }
             if (P.temp <= 0.0f) {
                 cur.resize(1);   // greedy: keep the max (list is sorted)
             } else {
@@ -583,13 +633,51 @@ Token Sampler::applyChain(std::vector<Candidate>& cur) {
     return cur[(size_t)dist(m_rng)].id;
 }
 
+// Sampler.cpp:47-70: temp, then mirostat (v1: llama_sampler_mirostat_apply with m = 100; v2:
+// llama_sampler_mirostat_v2_apply) sampling from its own target surprise mu.
+Token Sampler::applyMirostat(std::vector<Candidate>& cur) {
+    const Params& P = m_params;
+    if (P.temp <= 0.0f) cur.resize(1);
+    else for (auto& c : cur) c.logit /= P.temp;
+    softmax(cur);
+    if (P.mirostat.ver == 1) {
+        const int m = 100;
+        float sum_ti_bi = 0.0f, sum_ti_sq = 0.0f;
+        for (size_t i = 0; i < (size_t)(m - 1) && i + 1 < cur.size(); ++i) {
+            const float t_i = std::log((float)(i + 2) / (float)(i + 1));
+            const float b_i = std::log(cur[i].p / cur[i + 1].p);
+            sum_ti_bi += t_i * b_i;
+            sum_ti_sq += t_i * t_i;
+        }
+        const float s_hat = sum_ti_bi / sum_ti_sq;
+        const float eps_hat = s_hat - 1;
+        const float n_vocab = (float)mi_model_n_vocab(m_model.mmodel());
+        const float k = std::pow((eps_hat * std::pow(2.0f, m_mu)) / (1 - std::pow(n_vocab, -eps_hat)), 1 / s_hat);
+        // int(k) as llama.cpp converts it on x86: out of range or NaN gives INT_MIN, so top-1
+        const int ki = (k >= -2147483648.0f && k < 2147483648.0f) ? (int)k : INT32_MIN;
+        cur.resize(std::min(cur.size(), (size_t)std::max(ki, 1)));
+    } else {
+        size_t keep = 0;
+        while (keep < cur.size() && !(-std::log2(cur[keep].p) > m_mu)) ++keep;
+        cur.resize(std::max<size_t>(keep, 1));
+    }
+    softmax(cur);
+    std::vector<float> p(cur.size());
+    for (size_t i = 0; i < cur.size(); ++i) p[i] = cur[i].p;
+    std::discrete_distribution<int> dist(p.begin(), p.end());
+    const size_t idx = (size_t)dist(m_rng);
+    const float observed = -std::log2(cur[idx].p);
+    m_mu = m_mu - P.mirostat.eta * (observed - P.mirostat.tau);
+    return cur[idx].id;
+}
+
 Token Sampler::sample(mi_ctx* ctx) {
     std::vector<Candidate> cur;
     // The GPU top-k may stand in for the vocabulary only when nothing before top_k in the chain
     // (logit_bias, penalties: Sampler.cpp:30-41) can move a token across the top-k boundary.
     const auto& rp = m_params.repetitionPenalty;
     const bool penalties = rp.numTokens != 0 && !(rp.repeat == 1.0f && rp.freq == 0.0f && rp.present == 0.0f);
-    if (m_params.topK > 0 && m_params.topK <= 64 && m_params.samplerSequence.size() &&
+    if (m_params.mirostat.ver == 0 && m_params.topK > 0 && m_params.topK <= 64 && m_params.samplerSequence.size() &&
         m_params.samplerSequence[0] == SamplingType::Top_K && m_params.logitBias.empty() && !penalties) {
         const int k = m_params.topK;
         std::vector<int32_t> ids(k);

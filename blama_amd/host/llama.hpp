@@ -18,7 +18,7 @@
 //   LogitComparer / MetricsAggregator                     LogitComparer.hpp:12-34
 //
 // Not served (engine scope): Model::Params::gpu=false (the reference's CPU
-// verifier), LoRA, control vectors, grammar constraints, encoder models, mirostat/XTC/infill.
+// verifier), LoRA, control vectors, grammar constraints, encoder models, the infill sampler.
 #pragma once
 #include <cstdint>
 #include <memory>
@@ -142,6 +142,15 @@ public:
         std::vector<SamplingType> samplerSequence = {SamplingType::Top_K, SamplingType::Typical_P,
                                                      SamplingType::Top_P, SamplingType::Min_P,
                                                      SamplingType::Temperature};
+        struct Mirostat {                  // Sampler.hpp:55-59
+            int32_t ver = 0;               // 0 = disabled, 1 = mirostat, 2 = mirostat 2.0
+            float tau = 5.00f;
+            float eta = 0.10f;
+        } mirostat;
+        struct Xtc {                       // Sampler.hpp:60-64
+            float probability = 0.00f;     // 0 = disabled
+            float threshold = 0.10f;       // > 0.5 disables
+        } xtc;
         std::string grammar;
         std::vector<std::pair<Token, float>> logitBias;
     };
@@ -159,10 +168,13 @@ public:
     // The chain applied to a candidate list sorted by logit descending (exposed for tests).
     struct Candidate { Token id; float logit; float p; };
     Token applyChain(std::vector<Candidate>& cur);
+    Token applyMirostat(std::vector<Candidate>& cur);
 
 private:
     Model& m_model;
     Params m_params;
+    float m_mu = 0.0f;                     // mirostat state (2 tau at start and on reset)
+    std::mt19937 m_xtcRng;                 // llama_sampler_init_xtc's own generator
     std::mt19937 m_rng;
     std::vector<Token> m_prev;          // penalty window
 };

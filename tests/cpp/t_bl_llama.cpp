@@ -10,11 +10,13 @@
 #include "server.hpp"
 #include "wire.hpp"
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <fstream>
 #include <future>
+#include <unordered_set>
 
 namespace {
 std::string g_model, g_vocab, g_out, g_in;
@@ -104,6 +106,87 @@ TEST_CASE_G("sampler chain", "cpu") {
     int maxid = 0;
     for (int i = 0; i < 400; ++i) { make(c); maxid = std::max(maxid, s3.applyChain(c) - 100); }
     CHECK(maxid <= 12);
+}
+
+// The stages after the reference's default chain (Sampler.cpp:47-95): mirostat v1/v2, typical_p,
+// dynamic temperature, XTC.  Parity unpinned (llama.cpp is not vendored in the reference); these
+// check each stage's defining property on a geometric candidate list.
+TEST_CASE_G("sampler stages", "cpu") {
+    REQUIRE(!g_vocab.empty());
+    Model model(g_vocab, {.vocabOnly = true});
+    auto make = [](std::vector<Sampler::Candidate>& c, float step) {
+        c.clear();
+        for (int i = 0; i < 40; ++i) c.push_back({100 + i, 8.0f - step * i, 0.0f});
+    };
+    std::vector<Sampler::Candidate> c;
+    auto draws = [&](const Sampler::Params& p, float step, int n) {
+        Sampler s(model, p);
+        std::vector<Token> out;
+        for (int i = 0; i < n; ++i) { make(c, step); out.push_back(s.applyChain(c) - 100); }
+        return out;
+    };
+    auto distinct = [](const std::vector<Token>& v) {
+        return (int)std::unordered_set<Token>(v.begin(), v.end()).size();
+    };
+    Sampler::Params base;
+    base.rngSeed = 7;
+    base.temp = 1.0f;
+    base.topK = 0;
+    base.topP = 1.0f;
+    base.minP = 0.0f;
+    // XTC always on, threshold 0.1: at step 0.25 the top four have p >= 0.1 (0.221 .. 0.104),
+    // so the first three are removed and nothing below id 3 is ever drawn
+    {
+        Sampler::Params p = base;
+        p.samplerSequence = {Sampler::SamplingType::XTC, Sampler::SamplingType::Temperature};
+        p.xtc = {1.0f, 0.1f};
+        auto v = draws(p, 0.25f, 300);
+        CHECK(*std::min_element(v.begin(), v.end()) == 3);
+        p.xtc = {1.0f, 0.6f};   // threshold > 0.5 disables
+        v = draws(p, 0.25f, 300);
+        CHECK(*std::min_element(v.begin(), v.end()) == 0);
+    }
+    // mirostat: a low target surprise keeps the draws near the top, a high one spreads them;
+    // the same seed repeats the same draws (mu restarts at 2 tau)
+    for (int ver : {1, 2}) {
+        Sampler::Params p = base;
+        p.mirostat = {ver, 1.0f, 0.1f};
+        auto lo = draws(p, 0.25f, 300);
+        CHECK(lo == draws(p, 0.25f, 300));
+        // v1's k = (eps 2^mu / (1 - n_vocab^-eps))^(1/s) leaves int range for a large mu, and
+        // the x86 conversion then gives top-1 (as llama.cpp's int(k) does): tau 5 keeps k finite
+        p.mirostat.tau = ver == 1 ? 5.0f : 10.0f;
+        auto hi = draws(p, 0.1f, 300);   // flatter list: the full 40 are in reach
+        CHECK(*std::max_element(lo.begin(), lo.end()) <= 8);
+        CHECK(distinct(hi) >= 15);
+    }
+    {
+        Sampler::Params p = base;
+        p.mirostat.ver = 3;
+        CHECK_THROWS(Sampler(model, p));
+    }
+    // typical_p with min_keep 0 never cuts (llama.cpp's size_t min_keep - 1); with min_keep 1 it
+    // keeps the candidates whose surprise is nearest the entropy, which excludes the top one here
+    {
+        Sampler::Params p = base;
+        auto ref = draws(p, 0.25f, 200);
+        p.typicalP = 0.3f;
+        CHECK(draws(p, 0.25f, 200) == ref);
+        p.minKeep = 1;
+        auto v = draws(p, 0.25f, 200);
+        CHECK(v != ref);
+        CHECK(std::count(v.begin(), v.end(), 0) == 0);
+    }
+    // dynamic temperature: temp 0.5 +- 0.5 on a peaked list (low entropy) is near greedy; on a
+    // flat list (normalised entropy 1) it is temp 1 over all 40
+    {
+        Sampler::Params p = base;
+        p.temp = 0.5f;
+        p.tempRange = 0.5f;
+        auto peaked = draws(p, 3.0f, 200);
+        CHECK(std::count(peaked.begin(), peaked.end(), 0) == 200);
+        CHECK(distinct(draws(p, 0.0f, 400)) >= 30);
+    }
 }
 
 TEST_CASE_G("vocab only", "cpu") {   // t-integration.cpp:25-43
