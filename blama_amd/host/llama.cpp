@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <limits>
 #include <cstring>
 #include <functional>
 #include <queue>
@@ -246,6 +247,14 @@ void Vocab::load() {
     m_eos = mi_model_token_eos(m);
     for (int i = 0; i < n; ++i)
         if (m_type[i] == kTypeUnknown) { m_unk = i; break; }
+    // the engine's end-of-generation set is {eos, tokenizer.ggml.eot_token_id}
+    for (int i = 0; i < n && m_eot < 0; ++i)
+        if (i != m_eos && mi_model_token_is_eog(m, i) == 1) m_eot = i;
+    for (const char* t : {"<|eot_id|>", "<|im_end|>", "<|end|>", "<end_of_turn>", "<|endoftext|>", "<EOT>"}) {
+        if (m_eot >= 0) break;
+        auto it = m_index.find(t);
+        if (it != m_index.end()) m_eot = it->second;
+    }
     char tk[32] = {0};
     mi_model_tokenizer(m, tk, sizeof tk);
     m_spm = std::string(tk) == "llama";
@@ -623,6 +632,58 @@ Token Sampler::applyChain(std::vector<Candidate>& cur) {
                 for (auto& c : cur) c.logit /= P.temp;
             }
             break;
+        case SamplingType::Infill: {   // llama_sampler_infill_apply (fill-in-the-middle)
+            const Vocab& voc = m_model.vocab();
+            softmax(cur);
+            float p_txt = 0.0f, p_eog = 0.0f;
+            for (auto& c : cur) (voc.isEog(c.id) ? p_eog : p_txt) += c.p;
+            if (3 * p_eog * (float)cur.size() > p_txt) {   // end of generation is likely: EOG only
+                std::vector<Candidate> nw;
+                for (auto& c : cur)
+                    if (voc.isEog(c.id)) nw.push_back(c);
+                cur.swap(nw);
+                break;
+            }
+            // merge each token into another whose piece it prefixes (the likelier one keeps both)
+            std::vector<std::string> piece(cur.size());
+            for (size_t i = 0; i < cur.size(); ++i) piece[i] = voc.tokenToString(cur[i].id, false);
+            const float NEG = -std::numeric_limits<float>::infinity();
+            for (size_t i0 = 0; i0 < cur.size(); ++i0) {
+                for (size_t i1 = 0; i1 < cur.size(); ++i1) {
+                    if (cur[i0].logit == NEG) break;
+                    if (i0 == i1 || cur[i1].logit == NEG) continue;
+                    const std::string &a = piece[i0], &b = piece[i1];
+                    if (!a.empty() && a.size() <= b.size() && b.compare(0, a.size(), a) == 0) {
+                        size_t dst = i0, src = i1;
+                        if (cur[i1].p > cur[i0].p) std::swap(dst, src);
+                        cur[dst].p += cur[src].p;
+                        cur[src].logit = NEG;
+                        cur[src].p = 0.0f;
+                    }
+                }
+            }
+            // keep EOG and text tokens with p >= 0.2, then text tokens >= 1 / (n_text + 1)
+            size_t n_txt = 0;
+            float psum = 0.0f;
+            std::vector<Candidate> nw;
+            for (auto& c : cur) {
+                const bool eog = voc.isEog(c.id);
+                if (c.p < 0.2f && !eog) continue;
+                n_txt += !eog;
+                psum += c.p;
+                nw.push_back(c);
+            }
+            if (n_txt == 0) {   // nothing but EOG left: the end-of-turn token
+                cur.assign(1, Candidate{voc.eot(), 1.0f, 1.0f});
+                break;
+            }
+            for (auto& c : nw) c.p /= psum;
+            const float th = 1.0f / (float)(n_txt + 1);
+            cur.clear();
+            for (auto& c : nw)
+                if (c.p >= th || voc.isEog(c.id)) cur.push_back(c);
+            break;
+        }
         default: BL_THROW("Unsupported sampler type");
         }
     }

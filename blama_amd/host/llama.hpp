@@ -18,7 +18,7 @@
 //   LogitComparer / MetricsAggregator                     LogitComparer.hpp:12-34
 //
 // Not served (engine scope): Model::Params::gpu=false (the reference's CPU
-// verifier), LoRA, control vectors, grammar constraints, encoder models, the infill sampler.
+// verifier), LoRA, control vectors, grammar constraints, encoder models.
 #pragma once
 #include <cstdint>
 #include <memory>
@@ -67,6 +67,9 @@ public:
     std::string tokenToString(Token token, bool special = true) const;
     Token bos() const noexcept { return m_bos; }
     Token eos() const noexcept { return m_eos; }
+    // end-of-turn token (llama_vocab::token_eot): the GGUF's eot id, else a known end-of-turn
+    // text found in the vocabulary, else -1 (LLAMA_TOKEN_NULL)
+    Token eot() const noexcept { return m_eot; }
 
 private:
     void load();
@@ -75,7 +78,7 @@ private:
     std::vector<float> m_score;
     std::vector<int> m_type;
     std::unordered_map<std::string, Token> m_index;
-    Token m_bos = -1, m_eos = -1, m_unk = 0;
+    Token m_bos = -1, m_eos = -1, m_eot = -1, m_unk = 0;
     bool m_spm = true;
     // byte-level BPE (tokenizer.ggml.model "gpt2": Llama-3 and GPT-2 vocabularies)
     bool m_bpe = false;

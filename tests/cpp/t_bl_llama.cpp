@@ -187,6 +187,54 @@ TEST_CASE_G("sampler stages", "cpu") {
         CHECK(std::count(peaked.begin(), peaked.end(), 0) == 200);
         CHECK(distinct(draws(p, 0.0f, 400)) >= 30);
     }
+    // infill: a token absorbs the tokens its piece prefixes, text below 0.2 is dropped, and a
+    // likely end of generation leaves only the EOG tokens
+    {
+        const Vocab& voc = model.vocab();
+        Token a = -1, b = -1;
+        std::vector<Token> text;
+        for (Token i = 0; i < voc.nTokens(); ++i) {
+            const std::string s = voc.tokenToString(i, false);
+            if (s.empty() || voc.isEog(i)) continue;
+            text.push_back(i);
+        }
+        for (Token i : text)
+            for (Token j : text) {
+                const std::string si = voc.tokenToString(i, false), sj = voc.tokenToString(j, false);
+                if (a < 0 && i != j && si.size() >= 2 && si.size() < sj.size() && sj.compare(0, si.size(), si) == 0) {
+                    a = i;
+                    b = j;
+                }
+            }
+        REQUIRE(a >= 0 && voc.eos() >= 0);
+        std::vector<Token> filler;
+        for (Token t : text)
+            if (t != a && t != b && filler.size() < 10) filler.push_back(t);
+        Sampler::Params p = base;
+        p.samplerSequence = {Sampler::SamplingType::Infill, Sampler::SamplingType::Temperature};
+        Sampler s(model, p), plain(model, base);
+        auto build = [&](float la, float lb, float leos, float lf) {
+            c.clear();
+            c.push_back({a, la, 0});
+            c.push_back({b, lb, 0});
+            for (Token t : filler) c.push_back({t, lf, 0});
+            c.push_back({voc.eos(), leos, 0});
+            std::stable_sort(c.begin(), c.end(), [](auto& x, auto& y) { return x.logit > y.logit; });
+        };
+        int got_a = 0, plain_b = 0;
+        for (int i = 0; i < 200; ++i) {
+            build(5.0f, 4.9f, -10.0f, 0.0f);
+            got_a += s.applyChain(c) == a;       // b merged into a; fillers < 0.2
+            build(5.0f, 4.9f, -10.0f, 0.0f);
+            plain_b += plain.applyChain(c) == b;
+        }
+        CHECK(got_a == 200);
+        CHECK(plain_b > 40);
+        build(0.0f, 0.0f, 3.0f, 0.0f);           // 3 p_eog n > p_text: EOG only
+        CHECK(s.applyChain(c) == voc.eos());
+        build(0.0f, -5.0f, -10.0f, 0.0f);        // flat text, none >= 0.2 after merging: EOT
+        if (filler.size() == 10) CHECK(s.applyChain(c) == voc.eot());
+    }
 }
 
 TEST_CASE_G("vocab only", "cpu") {   // t-integration.cpp:25-43
