@@ -436,6 +436,55 @@ TEST_CASE_G("sampler bias beyond top-k", "gpu") {   // Sampler.cpp:30-41: bias b
     CHECK(second != top);
 }
 
+TEST_CASE_G("sampler stages on the logits", "gpu") {   // Sampler.cpp:47-96 over a real context
+    Model model(g_model, {});
+    Instance inst(model, {});
+    REQUIRE(mi_decode(inst.mctx(), kPrompt.data(), (int32_t)kPrompt.size(), MI_OUT_LAST) == 0);
+    const int32_t n = mi_model_n_vocab(model.mmodel());
+    Sampler::Params g;
+    g.temp = 0.0f;
+    const Token top = Sampler(model, g).sample(inst.mctx());
+    auto run = [&](const Sampler::Params& p) {
+        Sampler s(model, p);
+        std::vector<Token> out;
+        for (int i = 0; i < 32; ++i) out.push_back(s.sample(inst.mctx()));
+        return out;
+    };
+    std::vector<Sampler::Params> ps;
+    for (int ver : {1, 2}) {            // mirostat: the full vocabulary, not the engine's top-k
+        Sampler::Params p;
+        p.rngSeed = 11;
+        p.mirostat = {ver, 5.0f, 0.1f};
+        ps.push_back(p);
+    }
+    {
+        Sampler::Params p;               // XTC, typical and dynamic temperature after top-k
+        p.rngSeed = 12;
+        p.typicalP = 0.5f;
+        p.minKeep = 1;
+        p.tempRange = 0.3f;
+        p.xtc = {0.5f, 0.1f};
+        p.samplerSequence = {Sampler::SamplingType::Top_K, Sampler::SamplingType::Typical_P,
+                             Sampler::SamplingType::XTC, Sampler::SamplingType::Temperature};
+        ps.push_back(p);
+    }
+    {
+        Sampler::Params p;               // infill after top-k
+        p.rngSeed = 13;
+        p.samplerSequence = {Sampler::SamplingType::Top_K, Sampler::SamplingType::Infill,
+                             Sampler::SamplingType::Temperature};
+        ps.push_back(p);
+    }
+    for (auto& p : ps) {
+        auto a = run(p);
+        CHECK(a == run(p));              // same seed, same draws
+        for (Token t : a) CHECK((t >= 0 && t < n) || t == model.vocab().eot());
+    }
+    Sampler::Params p;                    // a near-zero target surprise: mirostat v2 is greedy
+    p.mirostat = {2, 0.0f, 0.1f};
+    CHECK(Sampler(model, p).sample(inst.mctx()) == top);
+}
+
 TEST_CASE_G("filling ctx", "gpu") {   // t-integration.cpp:219-248: bit-identical verification
     Model model(g_model, {});
     Instance inst(model, {}), inst2(model, {});
