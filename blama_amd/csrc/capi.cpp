@@ -2,7 +2,9 @@
 // catches exceptions and reports them through mi_last_error().
 #include "engine.h"
 
+#include <dlfcn.h>
 #include <fcntl.h>
+#include <rccl/rccl.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -19,6 +21,41 @@ struct mi_ctx { std::unique_ptr<Ctx> impl; };
 
 #define MI_TRY(fail) catch (const std::exception& e) { set_last_error(e.what()); return fail; } \
                      catch (...) { set_last_error("unknown error"); return fail; }
+
+// ---- replicas: fill the arenas of header-only models (no_upload) from a loaded one ----
+// Weights cross devices by one RCCL broadcast over xGMI (single process: ncclCommInitAll over the
+// distinct devices, root = the loaded model's device); replicas on a device that already holds
+// a filled arena take a device-to-device copy.  librccl is opened on first use (dlopen), so the
+// engine carries no link-time RCCL dependency.
+namespace {
+struct Rccl {
+    decltype(&ncclCommInitAll) init = nullptr;
+    decltype(&ncclBroadcast) bcast = nullptr;
+    decltype(&ncclGroupStart) gstart = nullptr;
+    decltype(&ncclGroupEnd) gend = nullptr;
+    decltype(&ncclCommDestroy) destroy = nullptr;
+    decltype(&ncclGetErrorString) err = nullptr;
+};
+const Rccl& rccl() {
+    static const Rccl r = [] {
+        Rccl x;
+        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_LOCAL);
+        if (!h) return x;
+        x.init = reinterpret_cast<decltype(x.init)>(dlsym(h, "ncclCommInitAll"));
+        x.bcast = reinterpret_cast<decltype(x.bcast)>(dlsym(h, "ncclBroadcast"));
+        x.gstart = reinterpret_cast<decltype(x.gstart)>(dlsym(h, "ncclGroupStart"));
+        x.gend = reinterpret_cast<decltype(x.gend)>(dlsym(h, "ncclGroupEnd"));
+        x.destroy = reinterpret_cast<decltype(x.destroy)>(dlsym(h, "ncclCommDestroy"));
+        x.err = reinterpret_cast<decltype(x.err)>(dlsym(h, "ncclGetErrorString"));
+        return x;
+    }();
+    return r;
+}
+void nccl_ck(ncclResult_t r, const char* what) {
+    if (r != ncclSuccess) throw Error(std::string("RCCL ") + what + ": " + (rccl().err ? rccl().err(r) : "error"));
+}
+}  // namespace
 
 extern "C" {
 
@@ -147,6 +184,87 @@ int32_t mi_model_arena(const mi_model* m, void** dev_ptr, size_t* bytes) {
     if (dev_ptr) *dev_ptr = m->impl.arena;
     if (bytes) *bytes = m->impl.arena_bytes;
     return 0;
+}
+
+
+int32_t mi_model_replicate(mi_model* const* models, int32_t n) {
+    try {
+        if (!models || n < 1 || !models[0]) throw Error("replicate: no source model");
+        const Model& src = models[0]->impl;
+        if (!src.arena) throw Error("replicate: the source model has no weights");
+        for (int i = 1; i < n; ++i) {
+            const Model& d = models[i]->impl;
+            if (!d.arena || d.arena_bytes != src.arena_bytes || d.gguf.tensors.size() != src.gguf.tensors.size())
+                throw Error("replicate: replica " + std::to_string(i) + " was not loaded from the same GGUF header");
+            // the MFMA-order copies are built from the arena when the first context needs them
+            if (d.mmq_arena) throw Error("replicate: replica " + std::to_string(i) + " already has a context");
+        }
+        std::vector<int> filled(n, 0);
+        filled[0] = 1;
+        // one receiver per distinct device other than the source's (RCCL ranks 1..); MI_REPLICATE_RCCL=1
+        // also sends the first same-device replica through a one-rank broadcast (exercises the path on
+        // a single GPU)
+        std::vector<int> devs = {src.device}, recv = {0};
+        static const bool force = getenv("MI_REPLICATE_RCCL") != nullptr;
+        for (int i = 1; i < n; ++i) {
+            const int dv = models[i]->impl.device;
+            if (std::find(devs.begin(), devs.end(), dv) == devs.end()) {
+                devs.push_back(dv);
+                recv.push_back(i);
+            }
+        }
+        int self_recv = -1;
+        if (force && devs.size() == 1)
+            for (int i = 1; i < n && self_recv < 0; ++i)
+                if (models[i]->impl.device == src.device) self_recv = i;
+        if (devs.size() > 1 || self_recv > 0) {
+            const Rccl& R = rccl();
+            if (!R.init || !R.bcast || !R.gstart || !R.gend || !R.destroy) throw Error("replicate: librccl not found");
+            const int nd = (int)devs.size();
+            std::vector<ncclComm_t> comms(nd);
+            nccl_ck(R.init(comms.data(), nd, devs.data()), "ncclCommInitAll");
+            std::vector<hipStream_t> st(nd);
+            for (int r = 0; r < nd; ++r) {
+                MI_HIP(hipSetDevice(devs[r]));
+                MI_HIP(hipStreamCreateWithFlags(&st[r], hipStreamNonBlocking));
+            }
+            nccl_ck(R.gstart(), "ncclGroupStart");
+            for (int r = 0; r < nd; ++r) {
+                MI_HIP(hipSetDevice(devs[r]));
+                uint8_t* dst = r == 0 ? (self_recv > 0 ? models[self_recv]->impl.arena : src.arena)
+                                      : models[recv[r]]->impl.arena;
+                nccl_ck(R.bcast(src.arena, dst, src.arena_bytes, ncclUint8, 0, comms[r], st[r]), "ncclBroadcast");
+            }
+            nccl_ck(R.gend(), "ncclGroupEnd");
+            for (int r = 0; r < nd; ++r) {
+                MI_HIP(hipSetDevice(devs[r]));
+                MI_HIP(hipStreamSynchronize(st[r]));
+                MI_HIP(hipStreamDestroy(st[r]));
+                R.destroy(comms[r]);
+            }
+            for (int r = 1; r < nd; ++r) filled[recv[r]] = 1;
+            if (self_recv > 0) filled[self_recv] = 1;
+        }
+        // the rest: a copy from a filled arena on the same device (or a peer copy from the source)
+        for (int i = 1; i < n; ++i) {
+            if (filled[i]) continue;
+            Model& d = models[i]->impl;
+            const uint8_t* from = src.arena;
+            int from_dev = src.device;
+            for (int j = 0; j < n; ++j)
+                if (filled[j] && models[j]->impl.device == d.device) { from = models[j]->impl.arena; from_dev = d.device; break; }
+            MI_HIP(hipSetDevice(d.device));
+            if (from_dev == d.device) MI_HIP(hipMemcpy(d.arena, from, src.arena_bytes, hipMemcpyDeviceToDevice));
+            else MI_HIP(hipMemcpyPeer(d.arena, d.device, from, from_dev, src.arena_bytes));
+            filled[i] = 1;
+        }
+        for (int i = 0; i < n; ++i) {
+            MI_HIP(hipSetDevice(models[i]->impl.device));
+            MI_HIP(hipDeviceSynchronize());
+        }
+        return 0;
+    }
+    MI_TRY(-1)
 }
 
 int32_t mi_model_type_histogram(const mi_model* m, int64_t* out, int32_t n) {

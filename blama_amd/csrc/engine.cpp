@@ -145,9 +145,9 @@ Model::~Model() {
     if (mmq_arena) hipFree(mmq_arena);
 }
 
-void Model::ensure_mmq_copies() {
+bool Model::ensure_mmq_copies() {
     std::lock_guard<std::mutex> lk(mmq_mu);
-    if (mmq_arena) return;
+    if (mmq_arena) return true;
     MI_HIP(hipSetDevice(device));
     // every Q4_K / Q6_K projection (gate and up as one pair copy) and the output head
     std::vector<std::pair<QMat*, QMat*>> todo;
@@ -163,14 +163,19 @@ void Model::ensure_mmq_copies() {
         offs.push_back(total);
         total = (total + mmq32_copy_bytes(*t.first, t.second != nullptr) + 255) & ~size_t(255);
     }
-    if (!total) return;
-    MI_HIP(hipMalloc(&mmq_arena, total));
+    if (!total) return true;
+    if (hipMalloc(&mmq_arena, total) != hipSuccess) {
+        (void)hipGetLastError();   // clear the sticky error; the caller falls back
+        mmq_arena = nullptr;
+        return false;
+    }
     mmq_bytes = total;
     for (size_t i = 0; i < todo.size(); ++i) {
         launch_mmq32_swizzle(*todo[i].first, todo[i].second, mmq_arena + offs[i], nullptr);
         todo[i].first->sw = mmq_arena + offs[i];
     }
     MI_HIP(hipDeviceSynchronize());
+    return true;
 }
 
 const QMat* Model::find_qmat(const std::string&) const { return nullptr; }
@@ -435,6 +440,9 @@ Ctx::Ctx(Model* model, uint32_t nctx, uint32_t nbatch, uint32_t nubatch) : m(mod
         for (const Layer& L : m->layers)
             for (const QMat* q : {&L.wq, &L.wk, &L.wv, &L.wo, &L.gate, &L.up, &L.down})
                 mmq_ok = mmq_ok && mmq32_supported(q->type);
+        // the gate/up pair shares one MFMA-order copy (16 gate + 16 up rows per tile)
+        for (const Layer& L : m->layers)
+            mmq_ok = mmq_ok && L.gate.type == L.up.type && L.gate.rows == L.up.rows;
         const int NB = kBatchRows;
         MI_HIP(hipMalloc(&xb, (size_t)NB * hp.n_embd * sizeof(float)));
         MI_HIP(hipMalloc(&qb, (size_t)NB * hp.n_embd * sizeof(float)));
@@ -452,8 +460,9 @@ Ctx::Ctx(Model* model, uint32_t nctx, uint32_t nbatch, uint32_t nubatch) : m(mod
             for (const Layer& L : m->layers)
                 for (const QMat* q : {&L.wq, &L.wk, &L.wv, &L.wo, &L.gate, &L.up, &L.down})
                     mmq_ok = mmq_ok && mmq32_supported(q->type) && ((q->type == T_Q8_0) == ub_q80);
+            // no room for the copy: prompt batches fall back to the v_dot4 GEMM
+            if (mmq_ok) mmq_ok = m->ensure_mmq_copies();
             out_mmq = mmq_ok && mmq32_supported(m->output.type);
-            if (mmq_ok) m->ensure_mmq_copies();
             attn_mfma = attn_mfma_supported(hp.head_dim) && getenv("MI_ATTN_VALU") == nullptr;
             MI_HIP(hipMalloc(&ub_q, (size_t)UB_MAX * kmax));
             MI_HIP(hipMalloc(&ub_dT, (size_t)UB_MAX * (kmax / 32) * sizeof(float)));   // Q8_0: per 32
@@ -1156,6 +1165,8 @@ const float* Ctx::logits_host(int row) {
 void Ctx::kv_clear() {
     n_cells = 0;
     pos_max = -1;
+    out_rows = 0;      // rows of the last MI_OUT_ALL pass belong to the cleared cache
+    topk_row = -1;
 }
 
 // Remove cells with pos in [p0, p1); the survivors keep their order and are
@@ -1285,6 +1296,8 @@ size_t Ctx::state_set(const uint8_t* src, size_t size) {
     const uint8_t* s = src + sizeof(hd);
     n_cells = hd.n_cells;
     pos_max = hd.pos_max;
+    out_rows = 0;      // only the restored last-token row (-1 / 0) is valid after a restore
+    topk_row = -1;
     std::memcpy(h_cell_pos.data(), s, n_cells * sizeof(int));
     s += n_cells * sizeof(int);
     MI_HIP(hipSetDevice(device));

@@ -87,7 +87,10 @@ struct Model {
     uint8_t* mmq_arena = nullptr;
     size_t mmq_bytes = 0;
     std::mutex mmq_mu;
-    void ensure_mmq_copies();
+    // false when the copy does not fit (the batch path then uses the v_dot4 GEMM).  The copies are
+    // taken from the arena once: writes to the arena (mi_model_arena, mi_model_replicate) must
+    // come before the first context (mi_model_replicate checks this).
+    bool ensure_mmq_copies();
     long long weight_bytes = 0;         // GGUF bytes streamed per token (all but tok_embd)
     long long type_bytes[32] = {0};
 

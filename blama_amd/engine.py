@@ -61,6 +61,7 @@ _SIGS = {
     "mi_model_weight_bytes": (C.c_int64, [_P]),
     "mi_model_arena": (C.c_int32, [_P, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]),
     "mi_model_type_histogram": (C.c_int32, [_P, C.POINTER(C.c_int64), C.c_int32]),
+    "mi_model_replicate": (C.c_int32, [C.POINTER(_P), C.c_int32]),
     "mi_ctx_create": (_P, [_P, C.c_uint32, C.c_uint32, C.c_uint32]),
     "mi_ctx_free": (None, [_P]),
     "mi_n_ctx": (C.c_uint32, [_P]),

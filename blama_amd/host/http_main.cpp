@@ -19,6 +19,7 @@
 // - /chat/completions and /chat/verify_completion return 501: chat templating is out of scope.
 // - A malformed request head or Content-Length gets a 400, a body over 64 MB a 413.
 #include <arpa/inet.h>
+#include <net/if.h>
 #include <netinet/in.h>
 #include <signal.h>
 #include <sys/socket.h>
@@ -196,10 +197,41 @@ int main() {
 
 int serve() {
     ::signal(SIGPIPE, SIG_IGN);
-    in_addr host{};
-    host.s_addr = htonl(INADDR_ANY);
+    // BLAMA_HOST: an IPv4 or IPv6 address, as boost::asio::ip::make_address accepts it
+    // (HttpServerMain.cpp:386); default 0.0.0.0
+    sockaddr_storage ss{};
+    socklen_t slen = sizeof(sockaddr_in);
+    {
+        auto* a4 = reinterpret_cast<sockaddr_in*>(&ss);
+        a4->sin_family = AF_INET;
+        a4->sin_addr.s_addr = htonl(INADDR_ANY);
+    }
     if (const char* h = std::getenv("BLAMA_HOST")) {
-        if (::inet_pton(AF_INET, h, &host) != 1) throw std::invalid_argument("Invalid BLAMA_HOST");
+        auto* a4 = reinterpret_cast<sockaddr_in*>(&ss);
+        auto* a6 = reinterpret_cast<sockaddr_in6*>(&ss);
+        if (::inet_pton(AF_INET, h, &a4->sin_addr) == 1) {
+            a4->sin_family = AF_INET;
+        } else {
+            // an IPv6 literal, optionally with a %scope (link-local)
+            std::string s6 = h, scope;
+            if (const size_t pc = s6.find('%'); pc != std::string::npos) {
+                scope = s6.substr(pc + 1);
+                s6.resize(pc);
+            }
+            ss = sockaddr_storage{};
+            if (::inet_pton(AF_INET6, s6.c_str(), &a6->sin6_addr) != 1) throw std::invalid_argument("Invalid BLAMA_HOST");
+            a6->sin6_family = AF_INET6;
+            if (!scope.empty()) {
+                a6->sin6_scope_id = ::if_nametoindex(scope.c_str());
+                if (a6->sin6_scope_id == 0) {
+                    char* end = nullptr;
+                    const unsigned long v = std::strtoul(scope.c_str(), &end, 10);
+                    if (!end || *end) throw std::invalid_argument("Invalid BLAMA_HOST");
+                    a6->sin6_scope_id = (uint32_t)v;
+                }
+            }
+            slen = sizeof(sockaddr_in6);
+        }
     }
     uint16_t port = 7331;
     if (const char* p = std::getenv("BLAMA_PORT")) {
@@ -213,7 +245,9 @@ int serve() {
     std::cout << "Loading model " << modelGguf << std::endl;
     // BLAMA_DEVICES=0,1,...: one replica (Model + Instance + worker) per listed GPU behind the
     // server's least-loaded dispatch (extension; default: device 0, the reference's one worker)
-    std::vector<std::shared_ptr<bl::llama::Model>> replicas;
+    // the first replica parses the GGUF; the others receive its weight arena (RCCL broadcast
+    // across GPUs, a device copy on the same GPU) instead of re-reading the file
+    std::vector<int> devices;
     {
         std::string devs = std::getenv("BLAMA_DEVICES") ? std::getenv("BLAMA_DEVICES") : "0";
         size_t at = 0;
@@ -223,29 +257,27 @@ int serve() {
             size_t idx = 0;
             const int dev = std::stoi(d, &idx, 10);
             if (idx != d.size() || dev < 0) throw std::invalid_argument("BLAMA_DEVICES: bad device list");
-            bl::llama::Model::Params mp{};
-            mp.device = dev;
-            replicas.push_back(std::make_shared<bl::llama::Model>(modelGguf, mp));
+            devices.push_back(dev);
             if (comma == std::string::npos) break;
             at = comma + 1;
         }
     }
-    Server server(std::move(replicas));
+    Server server(bl::llama::Model::loadReplicas(modelGguf, devices));
 
-    const int lfd = ::socket(AF_INET, SOCK_STREAM, 0);
+    const int lfd = ::socket(ss.ss_family, SOCK_STREAM, 0);
     const int one = 1;
     ::setsockopt(lfd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
-    sockaddr_in addr{};
-    addr.sin_family = AF_INET;
-    addr.sin_addr = host;
-    addr.sin_port = htons(port);
-    if (::bind(lfd, (sockaddr*)&addr, sizeof addr) != 0 || ::listen(lfd, 64) != 0) {
+    if (ss.ss_family == AF_INET) reinterpret_cast<sockaddr_in*>(&ss)->sin_port = htons(port);
+    else reinterpret_cast<sockaddr_in6*>(&ss)->sin6_port = htons(port);
+    if (::bind(lfd, (sockaddr*)&ss, slen) != 0 || ::listen(lfd, 64) != 0) {
         std::perror("bind/listen");
         return 1;
     }
-    socklen_t alen = sizeof addr;
-    ::getsockname(lfd, (sockaddr*)&addr, &alen);
-    std::cout << "Listening on port " << ntohs(addr.sin_port) << std::endl;
+    socklen_t alen = sizeof ss;
+    ::getsockname(lfd, (sockaddr*)&ss, &alen);
+    const uint16_t bound = ss.ss_family == AF_INET ? reinterpret_cast<sockaddr_in*>(&ss)->sin_port
+                                                   : reinterpret_cast<sockaddr_in6*>(&ss)->sin6_port;
+    std::cout << "Listening on port " << ntohs(bound) << std::endl;
     for (;;) {
         const int fd = ::accept(lfd, nullptr, nullptr);
         if (fd < 0) continue;

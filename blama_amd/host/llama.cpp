@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <cmath>
 #include <limits>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <queue>
@@ -198,7 +199,7 @@ size_t pretok_len(const std::vector<uint32_t>& c, size_t i, bool llama3) {
 Model::Model(const std::string& gguf, Params params) : m_params(params) {
     if (!params.gpu)
         BL_THROW("Model::Params::gpu=false (the CPU verifier) is not served by the MI355X engine");
-    mi_model_params mp{params.device, 0, params.vocabOnly ? 1 : 0, 0};
+    mi_model_params mp{params.device, 0, params.vocabOnly ? 1 : 0, params.noUpload ? 1 : 0};
     m_model = mi_model_load(gguf.c_str(), &mp);
     if (!m_model) BL_THROW("Failed to load model " << gguf << ": " << last_error());
     m_vocab.load();
@@ -207,7 +208,7 @@ Model::Model(const std::string& gguf, Params params) : m_params(params) {
 Model::Model(const void* data, size_t size, Params params) : m_params(params) {
     if (!params.gpu)
         BL_THROW("Model::Params::gpu=false (the CPU verifier) is not served by the MI355X engine");
-    mi_model_params mp{params.device, 0, params.vocabOnly ? 1 : 0, 0};
+    mi_model_params mp{params.device, 0, params.vocabOnly ? 1 : 0, params.noUpload ? 1 : 0};
     m_model = mi_model_load_from_memory(data, size, &mp);
     if (!m_model) BL_THROW("Failed to load model: " << last_error());
     m_vocab.load();
@@ -215,6 +216,28 @@ Model::Model(const void* data, size_t size, Params params) : m_params(params) {
 
 Model::~Model() {
     if (m_model) mi_model_free(m_model);
+}
+
+std::vector<std::shared_ptr<Model>> Model::loadReplicas(const std::string& gguf, const std::vector<int>& devices,
+                                                        Params params) {
+    if (devices.empty()) BL_THROW("loadReplicas: no device");
+    std::vector<std::shared_ptr<Model>> out;
+    Params p = params;
+    p.device = devices[0];
+    p.noUpload = false;
+    out.push_back(std::make_shared<Model>(gguf, p));   // parses and repacks the weights once
+    for (size_t i = 1; i < devices.size(); ++i) {
+        Params r = params;
+        r.device = devices[i];
+        r.noUpload = true;                             // header only: the arena is filled below
+        out.push_back(std::make_shared<Model>(gguf, r));
+    }
+    if (out.size() > 1) {
+        std::vector<mi_model*> ms;
+        for (auto& m : out) ms.push_back(m->mmodel());
+        if (mi_model_replicate(ms.data(), (int32_t)ms.size()) != 0) BL_THROW("loadReplicas: " << last_error());
+    }
+    return out;
 }
 
 uint32_t Model::trainCtxLength() const noexcept {
@@ -255,6 +278,36 @@ void Vocab::load() {
         auto it = m_index.find(t);
         if (it != m_index.end()) m_eot = it->second;
     }
+    // FIM ids (llama_vocab::impl::load: the GGUF keys, then the b5187 text auto-detection)
+    auto meta_id = [&](std::initializer_list<const char*> keys) -> Token {
+        for (const char* k : keys) {
+            char v[32] = {0};
+            if (mi_model_meta_str(m, k, v, sizeof v) > 0) {
+                const long id = std::strtol(v, nullptr, 10);
+                if (id >= 0 && id < n) return (Token)id;
+            }
+        }
+        return -1;
+    };
+    auto text_id = [&](std::initializer_list<const char*> texts) -> Token {
+        for (const char* t : texts) {
+            auto it = m_index.find(t);
+            if (it != m_index.end()) return it->second;
+        }
+        return -1;
+    };
+    m_fimPre = meta_id({"tokenizer.ggml.fim_pre_token_id", "tokenizer.ggml.prefix_token_id"});
+    m_fimSuf = meta_id({"tokenizer.ggml.fim_suf_token_id", "tokenizer.ggml.suffix_token_id"});
+    m_fimMid = meta_id({"tokenizer.ggml.fim_mid_token_id", "tokenizer.ggml.middle_token_id"});
+    if (m_fimPre < 0)
+        m_fimPre = text_id({"<|fim_prefix|>", "<fim-prefix>", "<fim_prefix>", "<｜fim▁begin｜>",
+                            "<PRE>", "▁<PRE>"});
+    if (m_fimSuf < 0)
+        m_fimSuf = text_id({"<|fim_suffix|>", "<fim-suffix>", "<fim_suffix>", "<｜fim▁hole｜>",
+                            "<SUF>", "▁<SUF>"});
+    if (m_fimMid < 0)
+        m_fimMid = text_id({"<|fim_middle|>", "<fim-middle>", "<fim_middle>", "<｜fim▁end｜>",
+                            "<MID>", "▁<MID>"});
     char tk[32] = {0};
     mi_model_tokenizer(m, tk, sizeof tk);
     m_spm = std::string(tk) == "llama";
@@ -830,11 +883,18 @@ void Session::pushPrompt(std::span<const Token> prompt, std::span<const Token> p
     if (prompt.empty() && postfix.empty()) BL_THROW("Prompt and postfix are empty");
     m_sampler->reset();
     std::vector<Token> toks;
-    if (m_instance.model().prefixInputsWithBos()) toks.push_back(m_instance.model().vocab().bos());
-    // FIM prefix/suffix/middle tokens: this engine's vocab exposes none (the reference only
-    // warns and skips when a model lacks them, Session.cpp:134-140)
+    const Vocab& voc = m_instance.model().vocab();
+    if (m_instance.model().prefixInputsWithBos()) toks.push_back(voc.bos());
+    // a postfix is framed by the FIM tokens (Session.cpp:142-159); a model without one of them
+    // skips it (the reference logs a warning there)
+    auto add = [&](Token t) { if (t >= 0) toks.push_back(t); };
+    if (!postfix.empty()) add(voc.fimPre());
     toks.insert(toks.end(), prompt.begin(), prompt.end());
-    toks.insert(toks.end(), postfix.begin(), postfix.end());
+    if (!postfix.empty()) {
+        add(voc.fimSuf());
+        toks.insert(toks.end(), postfix.begin(), postfix.end());
+        add(voc.fimMid());
+    }
     if (toks.size() > m_state.maxTokens)
         BL_THROW("Prompt too long. Got " << toks.size() << " tokens, max: " << mi_n_ctx(m_ctx) - 4);
     doDecode(toks, Source::InteractivePrompt);
@@ -895,9 +955,15 @@ std::vector<TokenPrediction> Session::fillCtx(std::span<TokenPrediction> tokens)
     flushPendingState();
     const uint32_t n = (uint32_t)tokens.size();
     const uint32_t batch = mi_n_batch(m_ctx);
+    // Not with prefixInputsWithBos: the serial loop's pushPrompt decodes a BOS before every
+    // claimed token, which changes every position after the first.
     if (m_params.batchedVerify && n > 0 && m_params.gaFactor == 1 && m_state.numPast + n < mi_n_ctx(m_ctx) &&
-        batch > 0) {
-        for (const TokenPrediction& t : tokens) m_sampler->accept(t.token, false);
+        batch > 0 && !m_instance.model().prefixInputsWithBos()) {
+        // the sampler ends as the serial loop leaves it: pushPrompt resets it (RNG re-seeded,
+        // penalty window and mirostat state cleared) before each token, so only the last
+        // claimed token is in its history (Session.cpp:123)
+        m_sampler->reset();
+        m_sampler->accept(tokens[n - 1].token, false);
         for (uint32_t c0 = 0; c0 < n; c0 += batch) {
             const uint32_t nc = std::min(batch, n - c0);
             std::vector<Token> ids(nc);

@@ -2,9 +2,10 @@
 //
 // This is the C++ layer Blama's L4/L5 call (reference inference/code/llama/*.hpp). The names,
 // parameter structs, call order and error messages are kept, so Server code and tests written
-// against the reference compile against this header unchanged. Below it, every decode, logit
-// extraction and KV operation goes through the engine's C ABI (include/mi_engine.h). There is
-// no llama.cpp here.
+// against the reference port with small edits (INTEGRATION.md lists them: e.g. Model takes
+// Params by value, there is no ChatFormat or lvocab()); they do not compile unchanged. Below
+// it, every decode, logit extraction and KV operation goes through the engine's C ABI
+// (include/mi_engine.h). There is no llama.cpp here.
 //
 // What is mirrored (reference file:line):
 //   Token / TokenData / TokenDataVector       Token.hpp:9-17
@@ -70,6 +71,12 @@ public:
     // end-of-turn token (llama_vocab::token_eot): the GGUF's eot id, else a known end-of-turn
     // text found in the vocabulary, else -1 (LLAMA_TOKEN_NULL)
     Token eot() const noexcept { return m_eot; }
+    // fill-in-the-middle tokens (llama_vocab_fim_pre/suf/mid, used by Session::pushPrompt for a
+    // postfix, Session.cpp:142-159): tokenizer.ggml.fim_{pre,suf,mid}_token_id (or the older
+    // prefix/suffix/middle keys), else a known FIM text in the vocabulary, else -1
+    Token fimPre() const noexcept { return m_fimPre; }
+    Token fimSuf() const noexcept { return m_fimSuf; }
+    Token fimMid() const noexcept { return m_fimMid; }
 
 private:
     void load();
@@ -79,6 +86,7 @@ private:
     std::vector<int> m_type;
     std::unordered_map<std::string, Token> m_index;
     Token m_bos = -1, m_eos = -1, m_eot = -1, m_unk = 0;
+    Token m_fimPre = -1, m_fimSuf = -1, m_fimMid = -1;
     bool m_spm = true;
     // byte-level BPE (tokenizer.ggml.model "gpt2": Llama-3 and GPT-2 vocabularies)
     bool m_bpe = false;
@@ -97,8 +105,17 @@ public:
         bool vocabOnly = false;
         bool prefixInputsWithBos = false;
         int device = 0;                    // HIP device of this replica (extension: one Model per GPU)
+        bool noUpload = false;             // header only, weights filled by loadReplicas (extension)
         bool operator==(const Params& other) const noexcept = default;
     };
+    // One Model per entry of `devices` (extension for the replica server): the first
+    // parses and uploads the GGUF, the others read only its header and receive the weights from
+    // it (mi_model_replicate: an RCCL broadcast across devices, device copies on one device).
+    static std::vector<std::shared_ptr<Model>> loadReplicas(const std::string& gguf, const std::vector<int>& devices,
+                                                            Params params);
+    static std::vector<std::shared_ptr<Model>> loadReplicas(const std::string& gguf, const std::vector<int>& devices) {
+        return loadReplicas(gguf, devices, Params{});
+    }
     Model(const std::string& gguf, Params params);
     // Load from a GGUF image in memory (tests, replicas).
     Model(const void* data, size_t size, Params params);

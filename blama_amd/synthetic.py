@@ -377,9 +377,57 @@ def _init_std(P, name):
     return P["base"]
 
 
-def build_gguf(cfg: LlamaConfig, seed: int = 0, header_only: bool = False) -> np.ndarray:
+BPE_CORPUS = [
+    "The quick brown fox jumps over the lazy dog. It's a test, isn't it? We'll see.",
+    "Verification sessions run concurrently on every replica of the model.",
+    "request number 0 1 2 3 4 5 6 7 8 9 10 11 12 13 14 15 and 3.14159 pies",
+    "Hello world! Numbers 1 22 333 4444, naive cafe, resume -- quotes and text.",
+]
+
+
+def bpe_vocab(n_vocab: int, n_merges_vocab: int = 800) -> dict:
+    """A Llama-3-shaped byte-level BPE vocabulary of exactly n_vocab entries ("gpt2" tokenizer,
+    pre-tokenizer "llama-bpe"): a BPE model trained here with HuggingFace `tokenizers` (the
+    byte alphabet and up to n_merges_vocab pieces with their merges), then
+    <|begin_of_text|> / <|end_of_text|> / <|eot_id|> and <|reserved_special_token_i|> control
+    tokens up to n_vocab, as Llama-3's 128256-entry vocabulary ends in 256 reserved specials.
+    Returns tokens, token types, merges, bos/eos ids and the trained `tokenizers.Tokenizer`
+    (which encodes prompts exactly as the host mirror does, tests/test_tokenizer_bpe.py)."""
+    import json
+    from tokenizers import Regex, Tokenizer, decoders, models, pre_tokenizers, trainers
+    llama3 = (r"(?:'[sS]|'[tT]|'[rR][eE]|'[vV][eE]|'[mM]|'[lL][lL]|'[dD])|[^\r\n\p{L}\p{N}]?\p{L}+|"
+              r"\p{N}{1,3}| ?[^\s\p{L}\p{N}]+[\r\n]*|\s*[\r\n]+|\s+(?!\S)|\s+")
+    tok = Tokenizer(models.BPE(ignore_merges=True))
+    tok.pre_tokenizer = pre_tokenizers.Sequence([
+        pre_tokenizers.Split(Regex(llama3), behavior="isolated", invert=False),
+        pre_tokenizers.ByteLevel(add_prefix_space=False, trim_offsets=False, use_regex=False)])
+    tok.decoder = decoders.ByteLevel()
+    trainer = trainers.BpeTrainer(vocab_size=n_merges_vocab, min_frequency=1,
+                                  initial_alphabet=pre_tokenizers.ByteLevel.alphabet(), show_progress=False)
+    tok.train_from_iterator(BPE_CORPUS * 20, trainer=trainer)
+    model = json.loads(tok.to_str())["model"]
+    toks = [None] * len(model["vocab"])
+    for t, i in model["vocab"].items():
+        toks[i] = t
+    merges = [m if isinstance(m, str) else " ".join(m) for m in model["merges"]]
+    types = [1] * len(toks)
+    specials = ["<|begin_of_text|>", "<|end_of_text|>", "<|eot_id|>"]
+    k = 0
+    while len(toks) + len(specials) < n_vocab:
+        specials.append("<|reserved_special_token_%d|>" % k)
+        k += 1
+    base = len(toks)
+    toks += specials
+    types += [3] * len(specials)
+    assert len(toks) == n_vocab
+    return dict(tokens=toks, types=types, merges=merges, pre="llama-bpe", bos=base, eos=base + 1,
+                eot=base + 2, tokenizer=tok)
+
+
+def build_gguf(cfg: LlamaConfig, seed: int = 0, header_only: bool = False, vocab: dict | None = None) -> np.ndarray:
     """The whole synthetic GGUF file as one uint8 array (header_only: just the
-    metadata + tensor table, enough for a vocab-only or no_upload replica load)."""
+    metadata + tensor table, enough for a vocab-only or no_upload replica load).
+    vocab: a byte-level BPE vocabulary from bpe_vocab() instead of the SPM one."""
     w = gguf.GGUFWriter()
     arch = "llama"
     w.add_str("general.architecture", arch)
@@ -399,15 +447,26 @@ def build_gguf(cfg: LlamaConfig, seed: int = 0, header_only: bool = False) -> np
     if cfg.n_expert:
         w.add_u32(f"{arch}.expert_count", cfg.n_expert)
         w.add_u32(f"{arch}.expert_used_count", cfg.n_expert_used)
-    w.add_str("tokenizer.ggml.model", "llama")
-    toks = vocab_tokens(cfg.n_vocab)
-    w.add_array("tokenizer.ggml.tokens", gguf.T_STRING, toks)
-    w.add_array("tokenizer.ggml.scores", gguf.T_FLOAT32, [-float(i) for i in range(len(toks))])
-    ttype = [2, 3, 3] + [6] * 256 + [1] * (len(toks) - 259)
-    w.add_array("tokenizer.ggml.token_type", gguf.T_INT32, ttype[:len(toks)])
-    w.add_u32("tokenizer.ggml.bos_token_id", 1)
-    w.add_u32("tokenizer.ggml.eos_token_id", 2)
-    w.add_u32("tokenizer.ggml.unknown_token_id", 0)
+    if vocab is None:
+        w.add_str("tokenizer.ggml.model", "llama")
+        toks = vocab_tokens(cfg.n_vocab)
+        w.add_array("tokenizer.ggml.tokens", gguf.T_STRING, toks)
+        w.add_array("tokenizer.ggml.scores", gguf.T_FLOAT32, [-float(i) for i in range(len(toks))])
+        ttype = [2, 3, 3] + [6] * 256 + [1] * (len(toks) - 259)
+        w.add_array("tokenizer.ggml.token_type", gguf.T_INT32, ttype[:len(toks)])
+        w.add_u32("tokenizer.ggml.bos_token_id", 1)
+        w.add_u32("tokenizer.ggml.eos_token_id", 2)
+        w.add_u32("tokenizer.ggml.unknown_token_id", 0)
+    else:
+        assert len(vocab["tokens"]) == cfg.n_vocab
+        w.add_str("tokenizer.ggml.model", "gpt2")
+        w.add_str("tokenizer.ggml.pre", vocab["pre"])
+        w.add_array("tokenizer.ggml.tokens", gguf.T_STRING, vocab["tokens"])
+        w.add_array("tokenizer.ggml.token_type", gguf.T_INT32, vocab["types"])
+        w.add_array("tokenizer.ggml.merges", gguf.T_STRING, vocab["merges"])
+        w.add_u32("tokenizer.ggml.bos_token_id", vocab["bos"])
+        w.add_u32("tokenizer.ggml.eos_token_id", vocab["eos"])
+        w.add_u32("tokenizer.ggml.eot_token_id", vocab["eot"])
     w.add_bool("tokenizer.ggml.add_bos_token", True)
     types = tensor_types(cfg)
     shapes = tensor_shapes(cfg)

@@ -79,6 +79,13 @@ int32_t mi_model_merge(const mi_model* model, int32_t i, char* buf, int32_t size
 int64_t mi_model_weight_bytes(const mi_model* model);
 /* The device weight arena (one allocation) -- for the replica broadcast. */
 int32_t mi_model_arena(const mi_model* model, void** dev_ptr, size_t* bytes);
+/* Replicas for concurrent sessions (one worker per replica, Server.cpp:36): fills
+ * the weight arenas of models[1..n-1] -- each loaded from the same GGUF with no_upload, i.e. the
+ * header only -- from models[0].  Devices other than models[0]'s receive the arena by one RCCL
+ * broadcast over xGMI (ncclCommInitAll over the distinct devices, root models[0]); further
+ * replicas on a device take a device-to-device copy.  Call before any mi_ctx_create on the
+ * replicas (their prompt-batch weight copies are built from the arena then).  0 ok, < 0 error. */
+int32_t mi_model_replicate(mi_model* const* models, int32_t n);
 /* Per ggml type id (0..31): bytes of weights of that type (the GGUF's byte histogram). */
 int32_t mi_model_type_histogram(const mi_model* model, int64_t* bytes_by_type, int32_t n);
 

@@ -94,6 +94,10 @@ class Model:
             raise RuntimeError("orc_decode: no KV space")
         return out
 
+    def reset(self):
+        """llama_kv_self_clear: an empty cache (a new session)."""
+        lib().orc_kv_clear(self.h)
+
     def decode(self, tokens):
         out = None
         for t in tokens:

@@ -259,3 +259,115 @@ def test_http_concurrent_verify_on_replicas(served_replicas):
         t.join(timeout=120)
     assert all(r is not None and r >= 0.999 for r in results[:7]), results
     assert results[7] < 0.95
+
+
+@pytest.fixture(scope="module")
+def llama3_bpe_model(tmp_path_factory):
+    """BASELINE configs[3]'s model at full width: Llama-3-8B Q6_K shape (n_embd 4096, heads
+    32/8, n_ff 14336, V = 128256; 2 layers instead of 32 to bound the file) with a byte-level
+    BPE ("gpt2") vocabulary of 128256 entries, so prompts go through the BPE tokenizer."""
+    cfg = synthetic.small_config("llama3-8b-q6_k", n_layer=2)
+    vocab = synthetic.bpe_vocab(cfg.n_vocab)
+    buf = synthetic.build_gguf(cfg, seed=7, vocab=vocab)
+    path = str(tmp_path_factory.mktemp("l3") / "llama3.gguf")
+    buf.tofile(path)
+    return cfg, vocab, buf, path
+
+
+def _serve_path(path, env_extra):
+    env = dict(os.environ, BLAMA_MODEL=path, BLAMA_HOST="127.0.0.1", BLAMA_PORT="0", **env_extra)
+    proc = subprocess.Popen([_binary()], env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    port = None
+    t0 = time.time()
+    while time.time() - t0 < 180:
+        line = proc.stdout.readline()
+        if not line:
+            break
+        if line.startswith("Listening on port "):
+            port = int(line.split()[-1])
+            break
+    if not port:
+        proc.kill()
+        proc.wait(timeout=30)
+        raise AssertionError("server did not start: " + proc.stderr.read()[-2000:])
+    return proc, port
+
+
+@pytest.mark.gpu
+def test_http_llama3_width_concurrent_verify_on_replicas(llama3_bpe_model):
+    """configs[3] at its shape on one GPU: Llama-3-8B width, BPE vocabulary, 4 replicas
+    (BLAMA_DEVICES=0,0,0,0; replica 1 receives the weight arena through a one-rank RCCL
+    broadcast, MI_REPLICATE_RCCL=1, replicas 2-3 by device copies -- none re-reads the GGUF's
+    tensor data), 8 concurrent /complete then 8 concurrent /verify_completion:
+      * every completion self-verifies (score >= 0.999 through the batched pass);
+      * one tampered completion scores < 0.95;
+      * the C restatement of the CPU path verifies every completion as Session::fillCtx would
+        (Session.cpp:231-282), each under the reference gate (t-LogitComparer.cpp:76-78)."""
+    import threading
+    import ggml_cpu
+    cfg, vocab, buf, path = llama3_bpe_model
+    proc, port = _serve_path(path, {"BLAMA_DEVICES": "0,0,0,0", "MI_REPLICATE_RCCL": "1"})
+    try:
+        reqs = [{"prompt": f"request number {i}: the quick brown fox", "max_tokens": 10, "seed": 100 + i,
+                 "temp": 0.8, "top_p": 0.95} for i in range(8)]
+        outs = [None] * 8
+
+        def complete(i):
+            st, body, _ = _post(port, "/complete", reqs[i])
+            assert st == 200, body
+            outs[i] = json.loads(body)
+
+        th = [threading.Thread(target=complete, args=(i,)) for i in range(8)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=300)
+        assert all(o is not None and len(o["tokenData"]) == 10 for o in outs), outs
+        # the wire's token strings are the BPE vocabulary's pieces, decoded from byte-level form
+        tk = vocab["tokenizer"]
+        for o in outs:
+            for t in o["tokenData"]:
+                if vocab["types"][t["id"]] == 1:
+                    assert t["str"] == tk.decode([t["id"]]), t
+        results = [None] * 8
+
+        def verify(i):
+            body = {"request": reqs[i], "response": outs[i]}
+            if i == 7:
+                body = json.loads(json.dumps(body))
+                for t in body["response"]["tokenData"]:
+                    for l in t["logits"]:
+                        l["logit"] *= 1.5
+            st, rb, _ = _post(port, "/verify_completion", body)
+            assert st == 200, rb
+            results[i] = json.loads(rb)["result"]
+
+        th = [threading.Thread(target=verify, args=(i,)) for i in range(8)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=300)
+        assert all(r is not None and r >= 0.999 for r in results[:7]), results
+        assert results[7] < 0.95, results
+    finally:
+        proc.kill()
+        proc.wait(timeout=30)
+    # the CPU oracle verifies each completion on its own session (prompt: BOS + BPE ids)
+    orc = ggml_cpu.Model(buf, n_ctx=64)
+    try:
+        for i in range(8):
+            orc.reset()
+            orc.decode([vocab["bos"]] + tk.encode(reqs[i]["prompt"], add_special_tokens=False).ids)
+            agg = R.MetricsAggregator()
+            sims, top1, score = [], [], None
+            for t in outs[i]["tokenData"]:
+                claimed = [(l["id"], l["logit"]) for l in t["logits"]]
+                lg = orc.decode_one(t["id"])
+                mine = sorted(R.gather(lg, sorted({x for x, _ in claimed})), key=lambda x: -x[1])
+                cm = R.compare(claimed, mine)
+                top1.append(cm.top1Match)
+                score = agg.push_and_verify([cm])
+                sims.append(R.logit_similarity(claimed, mine))
+            assert score >= 0.95 and float(np.mean(sims)) >= 0.98 and min(top1) == 1.0, (i, score, np.mean(sims))
+    finally:
+        orc.close()
