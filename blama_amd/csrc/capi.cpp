@@ -440,14 +440,11 @@ GemvParams single_gemv(const QMat& m, const float* x, float* y) {
     p.K = m.K;
     p.nseg = 1;
     p.seg[0].A = m;
+    p.seg[0].B = m;
     p.seg[0].pair = PAIR_ADJ;
     p.seg[0].epi = EPI_STORE;
-    p.seg[0].units = (m.rows + 1) / 2;
     p.seg[0].expA = p.seg[0].expB = -1;
     p.seg[0].out = y;
-    p.total_units = p.seg[0].units;
-    p.need_q8k = m.type != T_Q8_0;
-    p.need_q80 = m.type == T_Q8_0;
     return p;
 }
 
@@ -470,7 +467,7 @@ int32_t mi_op_gemv(int32_t device, int32_t type, const void* raw, int32_t rows, 
         const QMat m = upload_qmat(type, raw, rows, K, keep);
         DevBuf dx(K * sizeof(float)), dy(rows * sizeof(float));
         MI_HIP(hipMemcpy(dx.p, x, K * sizeof(float), hipMemcpyHostToDevice));
-        launch_gemv(single_gemv(m, dx.as<float>(), dy.as<float>()), ROLE_GENERIC, 0, nullptr);
+        launch_gemv(single_gemv(m, dx.as<float>(), dy.as<float>()), nullptr);
         MI_HIP(hipDeviceSynchronize());
         MI_HIP(hipMemcpy(y, dy.p, rows * sizeof(float), hipMemcpyDeviceToHost));
         return 0;
@@ -507,11 +504,11 @@ int32_t mi_op_gemv_bench(int32_t device, int32_t type, const void* raw, int32_t 
         MI_HIP(hipEventCreate(&b));
         std::vector<float> t;
         for (int i = 0; i < copies + 2; ++i)
-            launch_gemv(single_gemv(mats[i % copies], dx.as<float>(), dy.as<float>()), ROLE_GENERIC, 0, nullptr);
+            launch_gemv(single_gemv(mats[i % copies], dx.as<float>(), dy.as<float>()), nullptr);
         for (int i = 0; i < iters; ++i) {
             const GemvParams p = single_gemv(mats[i % copies], dx.as<float>(), dy.as<float>());
             MI_HIP(hipEventRecord(a, nullptr));
-            launch_gemv(p, ROLE_GENERIC, 0, nullptr);
+            launch_gemv(p, nullptr);
             MI_HIP(hipEventRecord(b, nullptr));
             MI_HIP(hipEventSynchronize(b));
             float ms = 0;

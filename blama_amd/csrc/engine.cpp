@@ -262,7 +262,38 @@ void Model::load(const uint8_t* data, size_t size, const mi_model_params& p) {
         plan.push_back(pl);
         return (int)plan.size() - 1;
     };
-    struct LayerIdx { int an, fn, q, k, v, o, g, u, d, r; };
+    // Q/K/V of one layer as groups of adjacent same-type tensors whose planes are stored back to
+    // back (plane k of the group = plane k of each tensor in order): one decode-GEMV matrix each
+    auto add_group = [&](const std::vector<std::string>& names, std::vector<int>& idx) {
+        std::vector<const GgufTensor*> ts;
+        for (const auto& n : names) {
+            const GgufTensor* t = gguf.tensor(n);
+            if (!t) throw Error("GGUF: missing tensor " + n);
+            ts.push_back(t);
+        }
+        const int type = ts[0]->type;
+        const int K = (int)ts[0]->ne[0];
+        if (!is_quant(type) || K % 256) throw Error("tensor " + names[0] + ": not a quantised matrix with K % 256 == 0");
+        const size_t first = plan.size();
+        for (const GgufTensor* t : ts) {
+            if (t->type != type || (int)t->ne[0] != K) throw Error("add_group: mixed tensors");
+            Planned pl{};
+            pl.t = t;
+            pl.K = K;
+            pl.experts = 1;
+            pl.rows = t->ne[1];
+            plan.push_back(pl);
+            idx.push_back((int)plan.size() - 1);
+        }
+        for (int k = 0; k < plane_count(type); ++k) {
+            for (size_t i = first; i < plan.size(); ++i) {
+                plan[i].off[k] = off;
+                off += (size_t)plan[i].rows * (K / 256) * plane_sb_bytes(type, k);
+            }
+            off = align256(off + (size_t)kPlanePadSb * plane_sb_bytes(type, k));
+        }
+    };
+    struct LayerIdx { int an, fn, q, k, v, o, g, u, d, r; std::vector<std::vector<int>> qkv_groups; };
     const int i_te = add("token_embd.weight", true, 1);
     const int i_on = add("output_norm.weight", true, 1);
     int i_out = add("output.weight", false, 1);
@@ -274,9 +305,26 @@ void Model::load(const uint8_t* data, size_t size, const mi_model_params& p) {
         LayerIdx& x = li[l];
         x.an = add(b + "attn_norm.weight", true, 1);
         x.fn = add(b + "ffn_norm.weight", true, 1);
-        x.q = add(b + "attn_q.weight", true, 1);
-        x.k = add(b + "attn_k.weight", true, 1);
-        x.v = add(b + "attn_v.weight", true, 1);
+        {
+            const std::string nq = b + "attn_q.weight", nk = b + "attn_k.weight", nv = b + "attn_v.weight";
+            const GgufTensor *tq = gguf.tensor(nq), *tk = gguf.tensor(nk), *tv = gguf.tensor(nv);
+            if (!tq || !tk || !tv) throw Error("GGUF: missing attention tensors in " + b);
+            std::vector<std::vector<std::string>> groups;
+            if (tq->type == tk->type && tk->type == tv->type) groups = {{nq, nk, nv}};
+            else if (tq->type == tk->type) groups = {{nq, nk}, {nv}};
+            else if (tk->type == tv->type) groups = {{nq}, {nk, nv}};
+            else groups = {{nq}, {nk}, {nv}};
+            std::vector<int> all;
+            for (const auto& g : groups) {
+                std::vector<int> idx;
+                add_group(g, idx);
+                x.qkv_groups.push_back(idx);
+                all.insert(all.end(), idx.begin(), idx.end());
+            }
+            x.q = all[0];
+            x.k = all[1];
+            x.v = all[2];
+        }
         x.o = add(b + "attn_output.weight", true, 1);
         if (hp.n_expert > 0) {
             x.r = add(b + "ffn_gate_inp.weight", true, 1);
@@ -370,6 +418,23 @@ void Model::load(const uint8_t* data, size_t size, const mi_model_params& p) {
         L.router = f32p(x.r);
         for (const QMat* m : {&L.wq, &L.wk, &L.wv, &L.wo, &L.gate, &L.up, &L.down})
             if (!is_quant(m->type)) throw Error("layer weights must be quantised (Q4_K/Q5_K/Q6_K/Q8_0)");
+        L.n_qkv = (int)x.qkv_groups.size();
+        int seen = 0;   // Q rows, then K rows, then V rows across the groups
+        for (int g = 0; g < L.n_qkv; ++g) {
+            QMat m = qm(x.qkv_groups[g][0]);
+            int nq = 0, nk = 0, rows = 0;
+            for (int i : x.qkv_groups[g]) {
+                const int r = (int)plan[i].rows;
+                if (seen == 0) nq += r;
+                else if (seen == 1) nk += r;
+                rows += r;
+                ++seen;
+            }
+            m.rows = rows;
+            L.qkv[g] = m;
+            L.qkv_nq[g] = nq;
+            L.qkv_nk[g] = nk;
+        }
     }
 }
 
@@ -377,22 +442,16 @@ void Model::load(const uint8_t* data, size_t size, const mi_model_params& p) {
 namespace {
 std::vector<int> g_attr_done(64, 0);
 
-void seg_init(GemvSeg& s) {
-    std::memset(&s, 0, sizeof(s));
-    s.expA = s.expB = -1;
-}
-void params_finish(GemvParams& p) {
-    int u = 0;
-    p.need_q8k = p.need_q80 = 0;
-    for (int i = 0; i < p.nseg; ++i) {
-        p.seg[i].unit0 = u;
-        u += p.seg[i].units;
-        for (const QMat* m : {&p.seg[i].A, &p.seg[i].B}) {
-            if (!m->p[0]) continue;
-            if (m->type == T_Q8_0) p.need_q80 = 1; else p.need_q8k = 1;
-        }
-    }
-    p.total_units = u;
+GemvSeg seg_of(const QMat& A, int pair, int epi, float* out) {
+    GemvSeg g;
+    std::memset(&g, 0, sizeof(g));
+    g.A = A;
+    g.B = A;
+    g.pair = pair;
+    g.epi = epi;
+    g.expA = g.expB = -1;
+    g.out = out;
+    return g;
 }
 }  // namespace
 
@@ -557,7 +616,7 @@ void Ctx::enqueue_step(bool with_logits) {
         base.kv_dim = kv_dim;
         base.eps = hp.eps;
         base.nslots = 1;
-        // ---- Q/K/V projections + RoPE + KV append ----
+        // ---- Q/K/V projections + RoPE + KV append: one launch per pair of row groups ----
         {
             GemvParams p = base;
             p.pro = PRO_RMSNORM;
@@ -570,41 +629,18 @@ void Ctx::enqueue_step(bool with_logits) {
             p.freq_factors = m->rope_freqs;
             p.kcache = kl;
             p.vcache = vl;
-            // one launch per distinct quant type (Q4_K_M mixes Q6_K attn_v into some layers)
-            const QMat* mats[3] = {&L.wq, &L.wk, &L.wv};
-            const int epis[3] = {EPI_ROPE_Q, EPI_ROPE_K, EPI_V};
-            bool done[3] = {false, false, false};
-            GemvParams pend;             // the first type's launch, held back to pair it
-            bool have_pend = false;
-            for (int a = 0; a < 3; ++a) {
-                if (done[a]) continue;
-                GemvParams pl = p;
-                pl.nseg = 0;
-                for (int i = a; i < 3; ++i) {
-                    if (done[i] || mats[i]->type != mats[a]->type) continue;
-                    GemvSeg& sg = pl.seg[pl.nseg++];
-                    seg_init(sg);
-                    sg.A = *mats[i];
-                    sg.pair = PAIR_ADJ;
-                    sg.epi = epis[i];
-                    sg.units = (mats[i]->rows + 1) / 2;
-                    sg.out = q;
-                    done[i] = true;
+            for (int g = 0; g < L.n_qkv;) {
+                p.nseg = 0;
+                for (; g < L.n_qkv && p.nseg < GEMV_MAX_SEG; ++g) {
+                    if (p.nseg == 1 && !gemv_pair_supported(p.seg[0].A.type, L.qkv[g].type)) break;
+                    GemvSeg& sg = p.seg[p.nseg++];
+                    sg = seg_of(L.qkv[g], PAIR_ADJ, EPI_QKV, q);
+                    sg.nq = L.qkv_nq[g];
+                    sg.nk = L.qkv_nk[g];
                 }
-                params_finish(pl);
-                pl.stamps = stamp();
-                if (have_pend) {   // second quant type: one mixed launch when the pair has a kernel
-                    have_pend = false;
-                    if (gemv_mix && gemv_mix_supported(pend.seg[0].A.type, pl.seg[0].A.type, ROLE_QKV)) {
-                        if (on()) launch_gemv_mix(pend, pl, ROLE_QKV, stream);
-                        continue;
-                    }
-                    if (on()) launch_gemv(pend, ROLE_QKV, 0, stream);
-                }
-                pend = pl;
-                have_pend = true;
+                p.stamps = stamp();
+                if (on()) launch_gemv(p, stream);
             }
-            if (have_pend && on()) launch_gemv(pend, ROLE_QKV, 0, stream);
         }
         // ---- attention ----
         {
@@ -615,24 +651,18 @@ void Ctx::enqueue_step(bool with_logits) {
             a.stamps2 = stamp();
             if (on()) launch_attn(a, stream);
         }
-        // ---- output projection + residual ----
+        // ---- output projection + residual (prologue: the attention splits combined) ----
         {
             GemvParams p = base;
-            p.pro = PRO_ATTN;   // slot 0 = the attention partials combined
+            p.pro = PRO_ATTN;
             p.attn = AttnPartials{part_o, hp.n_head, hp.head_dim};
-            p.x[0] = attn;
+            p.attn_nsplit = attn_fused ? 1 : 0;   // the split graph reads the count from the cell count
             p.K = hp.n_embd;
             p.nseg = 1;
-            seg_init(p.seg[0]);
-            p.seg[0].A = L.wo;
-            p.seg[0].pair = PAIR_ADJ;
-            p.seg[0].epi = EPI_ADD;
-            p.seg[0].units = (L.wo.rows + 1) / 2;
-            p.seg[0].out = x;
+            p.seg[0] = seg_of(L.wo, PAIR_ADJ, EPI_ADD, x);
             p.seg[0].resid = x;
-            params_finish(p);
             p.stamps = stamp();
-            if (on()) launch_gemv(p, ROLE_WO, 0, stream);
+            if (on()) launch_gemv(p, stream);
         }
         if (hp.n_expert > 0) {
             RouterParams rp{x, L.ffn_norm, hp.eps, L.router, hp.n_embd, hp.n_expert, hp.n_expert_used, sel, selw};
@@ -652,21 +682,15 @@ void Ctx::enqueue_step(bool with_logits) {
             }
             p.nseg = nsl;
             for (int k = 0; k < nsl; ++k) {
-                seg_init(p.seg[k]);
-                p.seg[k].A = L.gate;
+                p.seg[k] = seg_of(L.gate, PAIR_AB, EPI_SWIGLU, k == 0 ? h : h2);
                 p.seg[k].B = L.up;
-                p.seg[k].pair = PAIR_AB;
-                p.seg[k].epi = EPI_SWIGLU;
-                p.seg[k].units = L.gate.rows;
-                p.seg[k].out = k == 0 ? h : h2;
                 if (hp.n_expert > 0) p.seg[k].expA = p.seg[k].expB = k;
             }
-            params_finish(p);
             p.stamps = stamp();
             if (l == prof_layer) seg = 1;
             // the profiled launch (segment 1, always eager) carries the event pair
             const bool timed = l == prof_layer && seg_filter == 1;
-            if (on()) launch_gemv(p, ROLE_FFN_UP, 0, stream, timed ? prof_ev[0] : nullptr, timed ? prof_ev[1] : nullptr);
+            if (on()) launch_gemv(p, stream, timed ? prof_ev[0] : nullptr, timed ? prof_ev[1] : nullptr);
             if (l == prof_layer) seg = 2;
         }
         // ---- FFN down + residual ----
@@ -676,32 +700,21 @@ void Ctx::enqueue_step(bool with_logits) {
             p.x[0] = h;
             p.K = hp.n_ff;
             p.nseg = 1;
-            seg_init(p.seg[0]);
             if (hp.n_expert > 0) {
                 p.sel = sel;
                 p.selw = selw;
                 p.nslots = 2;
                 p.x[1] = h2;
-                p.seg[0].A = L.down;
-                p.seg[0].B = L.down;
-                p.seg[0].pair = PAIR_AB;
-                p.seg[0].epi = EPI_MOE_DOWN;
-                p.seg[0].units = L.down.rows;
-                p.seg[0].actA = 0;
-                p.seg[0].actB = 1;
+                p.seg[0] = seg_of(L.down, PAIR_AB, EPI_MOE_DOWN, x);
                 p.seg[0].expA = 0;
                 p.seg[0].expB = 1;
+                p.seg[0].actB = 1;
             } else {
-                p.seg[0].A = L.down;
-                p.seg[0].pair = PAIR_ADJ;
-                p.seg[0].epi = EPI_ADD;
-                p.seg[0].units = (L.down.rows + 1) / 2;
+                p.seg[0] = seg_of(L.down, PAIR_ADJ, EPI_ADD, x);
             }
-            p.seg[0].out = x;
             p.seg[0].resid = x;
-            params_finish(p);
             p.stamps = stamp();
-            if (on()) launch_gemv(p, ROLE_FFN_DOWN, 0, stream);
+            if (on()) launch_gemv(p, stream);
         }
     }
     if (with_logits && on()) enqueue_output(x, stamp());
@@ -710,29 +723,21 @@ void Ctx::enqueue_step(bool with_logits) {
 // final RMSNorm + output head GEMV of one residual row, then the top-k
 void Ctx::enqueue_output(const float* xrow, unsigned long long* stamps_slab) {
     const HParams& hp = m->hp;
-    {
-        GemvParams p;
-        std::memset(&p, 0, sizeof(p));
-        p.pro = PRO_RMSNORM;
-        p.nslots = 1;
-        p.x[0] = xrow;
-        p.norm_w = m->output_norm;
-        p.eps = hp.eps;
-        p.K = hp.n_embd;
-        p.tokpos = tokpos;
-        p.nseg = 1;
-        seg_init(p.seg[0]);
-        p.seg[0].A = m->output;
-        p.seg[0].pair = PAIR_ADJ;
-        p.seg[0].epi = EPI_STORE;
-        p.seg[0].units = (m->output.rows + 1) / 2;
-        p.seg[0].out = logits;
-        params_finish(p);
-        p.stamps = stamps_slab;
-        launch_gemv(p, ROLE_OUTPUT, 0, stream);
-        TopkParams tp{logits, hp.n_vocab, cand, topk_ids, topk_vals, d_h_topk_ids, d_h_topk_vals};
-        launch_topk(tp, stream);
-    }
+    GemvParams p;
+    std::memset(&p, 0, sizeof(p));
+    p.pro = PRO_RMSNORM;
+    p.nslots = 1;
+    p.x[0] = xrow;
+    p.norm_w = m->output_norm;
+    p.eps = hp.eps;
+    p.K = hp.n_embd;
+    p.tokpos = tokpos;
+    p.nseg = 1;
+    p.seg[0] = seg_of(m->output, PAIR_ADJ, EPI_STORE, logits);
+    p.stamps = stamps_slab;
+    launch_gemv(p, stream);
+    TopkParams tp{logits, hp.n_vocab, cand, topk_ids, topk_vals, d_h_topk_ids, d_h_topk_vals};
+    launch_topk(tp, stream);
 }
 
 hipGraphExec_t Ctx::build_graph(bool with_logits, int seg) {

@@ -64,6 +64,12 @@ struct Layer {
     QMat wq{}, wk{}, wv{}, wo{};
     QMat gate{}, up{}, down{};          // dense FFN, or the *_exps tensors for MoE
     float* router = nullptr;            // ffn_gate_inp (F32) for MoE
+    // Q, K, V as 1-3 groups of adjacent same-type rows (the arena stores the planes of a group's
+    // tensors back to back, so a group is one matrix to the decode GEMV): group g holds nq[g] Q
+    // rows, then nk[g] K rows, then V rows
+    int n_qkv = 0;
+    QMat qkv[3]{};
+    int qkv_nq[3] = {0, 0, 0}, qkv_nk[3] = {0, 0, 0};
 };
 
 struct Model {
@@ -155,7 +161,6 @@ struct Ctx {
     int logits_all_cap = 0;
     int out_rows = 0;                   // rows of logits_all valid (0: the last decode was MI_OUT_LAST)
     int topk_row = -1;                  // output row the mapped top-k buffers hold (-1: the last token)
-    bool gemv_mix = getenv("MI_NO_MIX") == nullptr;   // mixed-type Q/K/V in one launch
     // diagnostics (MI_STAMPS builds only): s_memrealtime stamps of every
     // workgroup of every launch of the last enqueued step [launch][wg][8]
     static constexpr int kStampLaunches = 320, kStampWgs = 512;

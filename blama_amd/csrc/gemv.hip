@@ -1,0 +1,651 @@
+// Batch-1 decode GEMV for gfx950 (CDNA4, wave64): ggml_mul_mat of one token against a
+// Q4_K / Q5_K / Q6_K / Q8_0 matrix, fused with its neighbours in
+// llm_build_llama: the RMSNorm or attention-combine prologue, the Q8_K / Q8_0 activation
+// quantisation of the CPU path, and the RoPE / KV-append / residual / SwiGLU / MoE epilogues.
+//
+// Numerics: every per-block integer dot is ggml b5187's vec_dot_q*_K_q8_K / vec_dot_q8_0_q8_0
+// bit for bit (qdot.h); only the fp32 sum order across superblocks differs from the CPU's.
+//
+// Structure (measured, scripts/exp_gemv2.cpp):
+//  * A workgroup of GV_NW waves serves one segment.  A wave walks "items" -- one 8-superblock
+//    chunk of the RW rows of one unit -- through a D-deep register ring: one aligned 16-byte load
+//    per lane of the main quant plane (+ side planes), the next items in flight while one is
+//    reduced against the activation in LDS.
+//  * Activation requests go out first: every wave issues its x slices, then a workgroup barrier
+//    that waits for no counter, and only then any weight request.  Without it the CU's x requests
+//    queue behind its weight stream (a decode launch has ~100 KB in flight per CU: x landed
+//    3-6 us after entry, in-kernel stamps); with it x lands while the first weights stream.
+//  * The whole parameter block is ~0.5 KB of kernarg read by independent scalar loads; a
+//    workgroup's segment is a compile-time index (no dependent kernarg reads).
+#include "qdot.h"
+#include <hip/hip_ext.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+
+namespace mi {
+
+namespace {
+
+constexpr int GV_NW = 16;       // waves per workgroup (one workgroup per CU)
+constexpr int GV_ASTR = 272;    // LDS bytes per activation block: 256 int8 + 16 (b128 reads spread over banks)
+constexpr int GV_KMAX = 14336;  // largest activation (Llama-3 / Mixtral n_ff)
+
+struct GvSeg {
+    const uint8_t* a[4];        // planes of A (expert 0, row 0)
+    const uint8_t* b[4];        // PAIR_AB: planes of B
+    float* out;
+    const float* resid;
+    int units, blk0, nblk, rows;
+    int epi, nq, nk, expA, expB, actB;
+};
+
+struct GvArgs {
+    GvSeg seg[2];
+    const float* x[2];
+    const float* norm_w;
+    const float* attn_o;        // PRO_ATTN: split partials [split][attn_stride]
+    const int* tokpos;
+    int* cell_pos;
+    __half* kcache;
+    __half* vcache;
+    const float* freq_factors;
+    const int* sel;
+    const float* selw;
+    float eps, theta_scale, freq_scale;
+    int K, pro, nslots, attn_nsplit, attn_stride, n_rot, head_dim, kv_dim;
+    unsigned long long* stamps;   // MI_STAMPS builds: [grid][8] s_memrealtime per workgroup
+};
+
+// LDS layout of one activation slot: Q8_K blocks [nb][GV_ASTR] | bsums [nb][16] int | d [nb]
+// (padded to 16 B) | Q8_0 blocks [nb][GV_ASTR] | Q8_0 d [nb][8].  Then the RoPE table and the
+// RMSNorm shares.
+struct GvLds {
+    int q8k, bsum, dk, q80, d0, slot;
+};
+__host__ __device__ inline GvLds gv_lds(int nb) {
+    GvLds L;
+    int o = 0;
+    L.q8k = o; o += nb * GV_ASTR;
+    L.bsum = o; o += nb * 64;
+    L.dk = o; o += (nb * 4 + 15) & ~15;
+    L.q80 = o; o += nb * GV_ASTR;
+    L.d0 = o; o += nb * 32;
+    L.slot = o;
+    return L;
+}
+__host__ __device__ inline int gv_rope_off(int nb, int nslots) { return gv_lds(nb).slot * nslots; }
+__host__ __device__ inline int gv_red_off(int nb, int nslots, int n_rot) {
+    return gv_rope_off(nb, nslots) + (((n_rot / 2) * 8 + 15) & ~15);
+}
+__host__ inline size_t gv_lds_bytes(int nb, int nslots, int n_rot) {
+    return (size_t)gv_red_off(nb, nslots, n_rot) + GV_NW * 8;
+}
+
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_s_waitcnt((0xF) | (0x3 << 14) | (0x7 << 4));   // lgkmcnt(0): LDS writes done; vmcnt untouched
+    __builtin_amdgcn_s_barrier();
+}
+
+// The activation registers Kq<T>::dot needs for lane j of superblock sb, from the LDS slot.
+template <int T> struct GvAct;
+template <> struct GvAct<T_Q4_K> {
+    __device__ static Kq<T_Q4_K>::AR get(const char* s, const GvLds& L, int sb, int j) {
+        const int g = j >> 1, half = j & 1;
+        const char* ab = s + L.q8k + sb * GV_ASTR + 64 * g + 16 * half;
+        Kq<T_Q4_K>::AR r;
+        r.alo = *reinterpret_cast<const i32x4*>(ab);
+        r.ahi = *reinterpret_cast<const i32x4*>(ab + 32);
+        const int* bs = reinterpret_cast<const int*>(s + L.bsum) + sb * 16 + 4 * g + half;
+        r.bs_lo = bs[0];
+        r.bs_hi = bs[2];
+        r.dx = reinterpret_cast<const float*>(s + L.dk)[sb];
+        return r;
+    }
+};
+template <> struct GvAct<T_Q5_K> {
+    __device__ static Kq<T_Q5_K>::AR get(const char* s, const GvLds& L, int sb, int j) {
+        return GvAct<T_Q4_K>::get(s, L, sb, j);
+    }
+};
+template <> struct GvAct<T_Q6_K> {
+    __device__ static Kq<T_Q6_K>::AR get(const char* s, const GvLds& L, int sb, int j) {
+        const int h = j >> 2, hq = (j >> 1) & 1, half = j & 1;
+        const char* ab = s + L.q8k + sb * GV_ASTR + 128 * h + 32 * hq + 16 * half;
+        Kq<T_Q6_K>::AR r;
+        r.alo = *reinterpret_cast<const i32x4*>(ab);
+        r.ahi = *reinterpret_cast<const i32x4*>(ab + 64);
+        const int* bs = reinterpret_cast<const int*>(s + L.bsum) + sb * 16 + 8 * h + 2 * hq + half;
+        r.bs_lo = bs[0];
+        r.bs_hi = bs[4];
+        r.dx = reinterpret_cast<const float*>(s + L.dk)[sb];
+        return r;
+    }
+};
+template <> struct GvAct<T_Q8_0> {
+    __device__ static Kq<T_Q8_0>::AR get(const char* s, const GvLds& L, int sb, int j) {
+        const char* ab = s + L.q80 + sb * GV_ASTR + 32 * j;
+        Kq<T_Q8_0>::AR r;
+        r.a0 = *reinterpret_cast<const i32x4*>(ab);
+        r.a1 = *reinterpret_cast<const i32x4*>(ab + 16);
+        r.d0 = reinterpret_cast<const float*>(s + L.d0)[sb * 8 + j];
+        return r;
+    }
+};
+
+// Which activation formats a workgroup of segment types (T0, T1) must build.
+template <int T> __host__ __device__ constexpr bool gv_q80() { return T == T_Q8_0; }
+
+// ---------------------------------------------------------------------------------------------
+// One workgroup's work for segment SI of type T.
+//   RW  rows per unit: 2 (PAIR_AB pairs, RoPE pairs of EPI_QKV) or 1
+//   KB  activation blocks of 256 per wave held in registers by the prologue: ceil(nb / GV_NW)
+//   D   register ring depth (items in flight per wave)
+// ---------------------------------------------------------------------------------------------
+template <int T, int SI, int RW, int KB, int D>
+__device__ __forceinline__ void gv_body(const GvArgs& a, char* lds) {
+    using K = Kq<T>;
+    constexpr bool Q80 = gv_q80<T>();
+    const GvSeg& S = a.seg[SI];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int sbl = lane >> 3, j = lane & 7;
+    const int nb = a.K >> 8;
+    const int C = (nb + 7) >> 3;                       // 8-superblock chunks per row
+    const int pro = a.pro;
+    const int epi = S.epi;
+    const bool dual = a.nslots > 1;
+    const GvLds L = gv_lds(nb);
+    const int slot_bytes = L.slot;
+#ifdef MI_STAMPS   // diagnostic build only (scripts/timeline.py): 0 entry, 1 prefill issued,
+                   // 2 activation in LDS, 3 first item consumed, 4 end
+#define GV_STAMP(k) \
+    if (a.stamps && threadIdx.x == 0) a.stamps[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime();
+#else
+#define GV_STAMP(k)
+#endif
+    GV_STAMP(0)
+
+    // ---- 1. entry loads: token position, MoE routing, the activation slices -------------------
+    const bool qkv = epi == EPI_QKV;
+    const bool need_tp = qkv || (pro == PRO_ATTN && a.attn_nsplit == 0);
+    i32x4 tp = {0, 0, 0, 0};
+    if (need_tp) tp = *gptr(reinterpret_cast<const i32x4*>(a.tokpos));
+    f32x4 xv[KB], wv[KB], yv[KB];
+#pragma unroll
+    for (int i = 0; i < KB; ++i) {
+        const int blk = wave + GV_NW * i;
+        if (blk < nb) {
+            const float* x0 = pro == PRO_ATTN ? a.attn_o : a.x[0];
+            xv[i] = gptr(reinterpret_cast<const f32x4*>(x0))[blk * 64 + lane];
+            if (pro == PRO_RMSNORM) wv[i] = gptr(reinterpret_cast<const f32x4*>(a.norm_w))[blk * 64 + lane];
+            if (dual) yv[i] = gptr(reinterpret_cast<const f32x4*>(a.x[1]))[blk * 64 + lane];
+        }
+    }
+    int e0 = 0, e1 = 0;
+    float w0 = 0.0f, w1 = 0.0f;
+    const bool moe = S.expA >= 0 || S.expB >= 0;
+    if (moe) {   // the router's choice decides the weight addresses
+        e0 = __builtin_amdgcn_readfirstlane(gptr(a.sel)[0]);
+        e1 = __builtin_amdgcn_readfirstlane(gptr(a.sel)[1]);
+        w0 = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(gptr(a.selw)[0])));
+        w1 = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(gptr(a.selw)[1])));
+    }
+    float ff0 = 1.0f, ff1 = 1.0f;
+    const bool rope_wave = qkv && a.n_rot > 0 && wave == GV_NW - 1;
+    if (rope_wave && a.freq_factors) {
+        if (lane < a.n_rot / 2) ff0 = gptr(a.freq_factors)[lane];
+        if (lane + 64 < a.n_rot / 2) ff1 = gptr(a.freq_factors)[lane + 64];
+    }
+    // every wave's activation requests ahead of any weight request of this CU
+    __builtin_amdgcn_s_barrier();
+
+    // ---- 2. the weight ring: item = (unit, chunk) of this wave's units -------------------------
+    const int wg = (int)blockIdx.x - S.blk0;
+    const int stride = S.nblk * GV_NW;                 // units between a wave's consecutive units
+    const int u_first = wg * GV_NW + wave;
+    const int n_units = u_first < S.units ? (S.units - u_first + stride - 1) / stride : 0;
+    const int n_items = n_units * C;
+    const bool ab = RW == 2 && (epi == EPI_SWIGLU || epi == EPI_MOE_DOWN);
+    // row r of unit u: PAIR_AB: row u of A (r = 0) / of B (r = 1); else row RW*u + r of A
+    const long long eA = S.expA == 0 ? e0 : S.expA == 1 ? e1 : 0;
+    const long long eB = S.expB == 0 ? e0 : S.expB == 1 ? e1 : 0;
+    const uint8_t* rp[RW][4];
+    long long step[4];                                  // bytes between a row and the next unit's row
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        const long long rowb = (long long)nb * PlaneBytes<T>::b[p];
+        const long long ex = (long long)S.rows * rowb;   // one expert's plane bytes
+        const long long r0 = ab ? u_first : (long long)u_first * RW;
+        const long long rc = r0 < S.rows ? r0 : 0;       // a wave without units re-reads row 0 (parked)
+#pragma unroll
+        for (int r = 0; r < RW; ++r) {
+            const bool isB = ab && r == 1;
+            const uint8_t* base = isB ? S.b[p] + eB * ex : S.a[p] + eA * ex;
+            long long row = ab ? rc : rc + r;
+            if (row >= S.rows) row = S.rows - 1;         // an odd last pair re-reads its row (result unused)
+            rp[r][p] = rfl_ptr(base + row * rowb);
+        }
+        step[p] = (ab ? (long long)stride : (long long)stride * RW) * rowb;
+    }
+    struct Slot {
+        typename K::Ld w[RW];
+        float2 res;
+    };
+    Slot ring[D];
+    int iu = 0, ic = 0;                                 // issue cursor: unit index (0..n_units), chunk
+    const bool has_res = S.resid != nullptr;
+    auto issue = [&](Slot& s) {
+        const int sb0 = ic * 8 + sbl;
+        const int sb = sb0 < nb ? sb0 : nb - 1;
+#pragma unroll
+        for (int r = 0; r < RW; ++r) s.w[r] = K::load(rp[r], sb, j);
+        if (has_res) {   // the unit's residual values (every chunk of the unit reads them: cache hits)
+            const long long u = u_first + (long long)(iu < n_units ? iu : (n_units > 0 ? n_units - 1 : 0)) * stride;
+            const long long r0 = ab ? u : u * RW;
+            const long long rr = r0 < S.rows ? r0 : S.rows - 1;
+            if (RW == 2 && !ab) {
+                const long long r1 = rr + 1 < S.rows ? rr + 1 : rr;
+                s.res.x = gptr(S.resid)[rr];
+                s.res.y = gptr(S.resid)[r1];
+            } else {
+                s.res.x = gptr(S.resid)[rr];
+                s.res.y = 0.0f;
+            }
+        }
+        if (iu < n_units) {
+            if (++ic == C) {
+                ic = 0;
+                if (++iu < n_units) {
+#pragma unroll
+                    for (int r = 0; r < RW; ++r)
+#pragma unroll
+                        for (int p = 0; p < 4; ++p) rp[r][p] += step[p];
+                } else {
+                    ic = C - 1;   // parked: every later issue re-reads the last chunk (cache hits)
+                }
+            }
+        }
+    };
+#pragma unroll
+    for (int k = 0; k < D - 1; ++k) issue(ring[k]);
+    GV_STAMP(1)
+
+    // ---- 3. prologue: the activation into LDS while the weights stream ---------------------------
+    double* red = reinterpret_cast<double*>(lds + gv_red_off(nb, a.nslots, a.n_rot));
+    float* rope = reinterpret_cast<float*>(lds + gv_rope_off(nb, a.nslots));
+    float scale = 1.0f;
+    if (pro == PRO_RMSNORM) {
+        // ggml_compute_forward_rms_norm_f32: sum of float squares in double
+        double s = 0.0;
+#pragma unroll
+        for (int i = 0; i < KB; ++i)
+            if (wave + GV_NW * i < nb) {
+                s += (double)(xv[i].x * xv[i].x);
+                s += (double)(xv[i].y * xv[i].y);
+                s += (double)(xv[i].z * xv[i].z);
+                s += (double)(xv[i].w * xv[i].w);
+            }
+        s = wave_sum63_d(s);
+        if (lane == 63) red[wave] = s;
+        lds_barrier();
+        double tot = 0.0;
+#pragma unroll
+        for (int w = 0; w < GV_NW; ++w) tot += red[w];
+        scale = 1.0f / sqrtf((float)(tot / (double)a.K) + a.eps);
+    }
+    if (pro == PRO_ATTN) {
+        // the other splits of the attention partials (contexts past ATTN_SHORT cells), in split order
+        int nsplit = a.attn_nsplit;
+        if (nsplit == 0) {
+            int chunk;
+            attn_split(__builtin_amdgcn_readfirstlane(tp.z) + 1, chunk, nsplit);
+        }
+        for (int sp = 1; sp < nsplit; ++sp) {
+#pragma unroll
+            for (int i = 0; i < KB; ++i) {
+                const int blk = wave + GV_NW * i;
+                if (blk < nb)
+                    xv[i] += gptr(reinterpret_cast<const f32x4*>(a.attn_o + (long long)sp * a.attn_stride))[blk * 64 + lane];
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < KB; ++i) {
+        const int blk = wave + GV_NW * i;
+        if (blk >= nb) continue;
+        float v[4] = {xv[i].x, xv[i].y, xv[i].z, xv[i].w};
+        if (pro == PRO_RMSNORM) {
+            v[0] = (v[0] * scale) * wv[i].x;   // ggml_vec_scale_f32 then ggml_mul
+            v[1] = (v[1] * scale) * wv[i].y;
+            v[2] = (v[2] * scale) * wv[i].z;
+            v[3] = (v[3] * scale) * wv[i].w;
+        }
+        if (Q80)
+            quant_q80_block(v, lane, reinterpret_cast<int8_t*>(lds + L.q80 + blk * GV_ASTR),
+                            reinterpret_cast<float*>(lds + L.d0) + blk * 8);
+        else
+            quant_q8k_block(v, lane, reinterpret_cast<int8_t*>(lds + L.q8k + blk * GV_ASTR),
+                            reinterpret_cast<int*>(lds + L.bsum) + blk * 16, reinterpret_cast<float*>(lds + L.dk) + blk);
+        if (dual) {
+            float y[4] = {yv[i].x, yv[i].y, yv[i].z, yv[i].w};
+            char* s1 = lds + slot_bytes;
+            if (Q80)
+                quant_q80_block(y, lane, reinterpret_cast<int8_t*>(s1 + L.q80 + blk * GV_ASTR),
+                                reinterpret_cast<float*>(s1 + L.d0) + blk * 8);
+            else
+                quant_q8k_block(y, lane, reinterpret_cast<int8_t*>(s1 + L.q8k + blk * GV_ASTR),
+                                reinterpret_cast<int*>(s1 + L.bsum) + blk * 16, reinterpret_cast<float*>(s1 + L.dk) + blk);
+        }
+    }
+    const int pos = __builtin_amdgcn_readfirstlane(tp.y);
+    const int cell = __builtin_amdgcn_readfirstlane(tp.z);
+    if (rope_wave) {   // ggml_rope_cache_init for this token's position (ext_factor 0, mscale 1)
+        for (int i = lane; i < a.n_rot / 2; i += 64) {
+            float theta = (float)pos;
+            for (int k = 0; k < i; ++k) theta = theta * a.theta_scale;
+            const float ff = i < 64 ? ff0 : ff1;
+            const float th = a.freq_scale * (theta / ff);
+            rope[2 * i] = cosf(th);
+            rope[2 * i + 1] = sinf(th);
+        }
+    }
+    lds_barrier();
+    GV_STAMP(2)
+
+    // ---- 4. the stream: consume item i while items i+1 .. i+D-1 are in flight -----------------
+    const char* act0 = lds;
+    const char* actB = (dual && S.actB == 1) ? lds + slot_bytes : lds;
+    float acc[RW];
+#pragma unroll
+    for (int r = 0; r < RW; ++r) acc[r] = 0.0f;
+    int cu = 0, cc = 0;                                 // consume cursor
+    auto consume = [&](const Slot& s) {
+        const int sb0 = cc * 8 + sbl;
+        const bool lv = sb0 < nb;
+        const int sb = lv ? sb0 : nb - 1;
+        const typename K::AR ar = GvAct<T>::get(act0, L, sb, j);
+#pragma unroll
+        for (int r = 0; r < RW; ++r) {
+            float p;
+            if (RW == 2 && r == 1 && dual) {
+                const typename K::AR arB = GvAct<T>::get(actB, L, sb, j);
+                p = K::dot(s.w[r], arB, j);
+            } else {
+                p = K::dot(s.w[r], ar, j);
+            }
+            acc[r] += lv ? p : 0.0f;
+        }
+        if (++cc == C) {
+            float y[RW];
+#pragma unroll
+            for (int r = 0; r < RW; ++r) {
+                y[r] = wave_sum63(acc[r]);
+                acc[r] = 0.0f;
+            }
+            if (lane == 63) {
+                const long long u = u_first + (long long)cu * stride;
+                const auto out = gptr_w(S.out);
+                if (ab) {
+                    if (epi == EPI_SWIGLU) out[u] = silu_f(y[0]) * y[RW - 1];
+                    else out[u] = (y[0] * w0 + y[RW - 1] * w1) + s.res.x;   // EPI_MOE_DOWN
+                } else {
+                    const long long r0 = u * RW;
+                    if (epi == EPI_QKV) {
+                        // RoPE pairs (RW == 2): rows r0, r0+1 of Q or K; or two V rows
+                        float o0 = y[0], o1 = y[RW - 1];
+                        const bool isq = r0 < S.nq, isk = !isq && r0 < S.nq + S.nk;
+                        if (isq || isk) {
+                            const int i0 = (int)((isq ? r0 : r0 - S.nq) % a.head_dim);
+                            if (i0 < a.n_rot) {
+                                const float cs = rope[i0], sn = rope[i0 + 1];
+                                o0 = y[0] * cs - y[RW - 1] * sn;
+                                o1 = y[0] * sn + y[RW - 1] * cs;
+                            }
+                        }
+                        if (isq) {
+                            out[r0] = o0;
+                            out[r0 + 1] = o1;
+                        } else if (isk) {
+                            const long long rk = r0 - S.nq;
+                            const auto kr = gptr_w(reinterpret_cast<unsigned short*>(a.kcache + (long long)cell * a.kv_dim));
+                            kr[rk] = __half_as_ushort(__float2half_rn(o0));
+                            kr[rk + 1] = __half_as_ushort(__float2half_rn(o1));
+                            if (rk == 0) gptr_w(a.cell_pos)[cell] = pos;
+                        } else {
+                            const long long rv = r0 - S.nq - S.nk;
+                            const auto vr = gptr_w(reinterpret_cast<unsigned short*>(a.vcache + (long long)cell * a.kv_dim));
+                            vr[rv] = __half_as_ushort(__float2half_rn(o0));
+                            if (RW == 2 && r0 + 1 < S.rows) vr[rv + 1] = __half_as_ushort(__float2half_rn(o1));
+                        }
+                    } else {
+#pragma unroll
+                        for (int r = 0; r < RW; ++r) {
+                            if (r0 + r >= S.rows) break;
+                            const float v = r == 0 ? y[0] : y[RW - 1];
+                            const float rv = r == 0 ? s.res.x : s.res.y;
+                            out[r0 + r] = epi == EPI_ADD ? v + rv : v;
+                        }
+                    }
+                }
+            }
+            cc = 0;
+            ++cu;
+        }
+    };
+    for (int base = 0; base < n_items; base += D) {
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+            issue(ring[(k + D - 1) % D]);
+            if (base + k < n_items) consume(ring[k]);
+            if (base + k == 0) { GV_STAMP(3) }
+        }
+    }
+    GV_STAMP(4)
+#undef GV_STAMP
+}
+
+// T1: -1 one segment; -2 two segments of type T0; else the type of segment 1.
+// TAG: 1 for the FFN gate/up launches, so that the roofline kernel has a symbol of its own in
+// kernel traces (the same code as the QKV launches of an all-Q4_K layer).
+template <int T0, int T1, int RW, int KB, int D, int TAG>
+__global__ __launch_bounds__(GV_NW * 64) void gemv_kernel(const GvArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    if (T1 == -1 || (int)blockIdx.x < a.seg[1].blk0) gv_body<T0, 0, RW, KB, D>(a, lds);
+    else gv_body<(T1 < 0 ? T0 : T1), 1, RW, KB, D>(a, lds);
+}
+
+typedef void (*GvFn)(const GvArgs);
+
+// ring depth: items of one wave in flight (an item is RW rows x one 8-superblock chunk);
+// KB activation blocks per wave (K <= 4096: 1, <= 8192: 2, <= 16384: 4 at 16 waves)
+// (the 128-VGPR budget of a 16-wave workgroup: 4 one-row items, 3 two-row items; 2 for the
+// wider Q5_K / Q6_K / Q8_0 two-row items)
+template <int T, int RW> struct GvD { static constexpr int D = RW == 1 ? 4 : (T == T_Q4_K ? 3 : 2); };
+
+template <int T0, int T1, int RW, int TAG>
+GvFn gv_fn_kb(int kb) {
+    constexpr int D = GvD<T0, RW>::D < GvD<(T1 < 0 ? T0 : T1), RW>::D ? GvD<T0, RW>::D : GvD<(T1 < 0 ? T0 : T1), RW>::D;
+    switch (kb) {
+    case 1: return gemv_kernel<T0, T1, RW, 1, D, TAG>;
+    case 2: return gemv_kernel<T0, T1, RW, 2, D, TAG>;
+    case 4: return gemv_kernel<T0, T1, RW, 4, D, TAG>;
+    default: return nullptr;
+    }
+}
+// t1: -1 one segment, -2 two of type T0, else the second segment's type (Q6_K / Q8_0)
+template <int T0, int RW>
+GvFn gv_fn_pair(int t1, int kb, int tag) {
+    switch (t1) {
+    case -1: return tag && RW == 2 ? gv_fn_kb<T0, -1, RW, 1>(kb) : gv_fn_kb<T0, -1, RW, 0>(kb);
+    case -2: return gv_fn_kb<T0, -2, RW, 0>(kb);
+    case T_Q6_K: return gv_fn_kb<T0, T_Q6_K, RW, 0>(kb);
+    case T_Q8_0: return gv_fn_kb<T0, T_Q8_0, RW, 0>(kb);
+    default: return nullptr;
+    }
+}
+template <int RW>
+GvFn gv_fn_rw(int t0, int t1, int kb, int tag) {
+    switch (t0) {
+    case T_Q4_K: return gv_fn_pair<T_Q4_K, RW>(t1, kb, tag);
+    case T_Q5_K: return gv_fn_pair<T_Q5_K, RW>(t1, kb, tag);
+    case T_Q6_K: return t1 == T_Q6_K ? nullptr : gv_fn_pair<T_Q6_K, RW>(t1, kb, tag);
+    case T_Q8_0: return t1 >= 0 ? nullptr : gv_fn_pair<T_Q8_0, RW>(t1, kb, tag);
+    default: return nullptr;
+    }
+}
+// nseg segments of types t0 (, t1); tag: the FFN gate/up launch
+GvFn gv_fn(int nseg, int t0, int t1, int rw, int kb, int tag) {
+    const int k = nseg == 1 ? -1 : (t1 == t0 ? -2 : t1);
+    return rw == 2 ? gv_fn_rw<2>(t0, k, kb, tag) : gv_fn_rw<1>(t0, k, kb, tag);
+}
+
+int gv_kb(int K) {
+    const int nb = K / 256;
+    const int kb = (nb + GV_NW - 1) / GV_NW;
+    return kb <= 1 ? 1 : kb <= 2 ? 2 : kb <= 4 ? 4 : -1;
+}
+
+bool gv_rw2(const GemvSeg& s) { return s.pair == PAIR_AB || s.epi == EPI_QKV; }
+
+long long seg_bytes(const GemvSeg& s) {
+    auto mb = [](const QMat& q) {
+        return (long long)q.rows * q.nb * ((long long)block_bytes(q.type) * 256 / block_elems(q.type));
+    };
+    return s.pair == PAIR_AB ? mb(s.A) + mb(s.B) : mb(s.A);
+}
+
+// cap on workgroups: the weight ring keeps D items x RW rows in flight per wave
+int gv_grid_cap() {
+    static const int cap = getenv("MI_GEMV_GRID") ? std::max(1, atoi(getenv("MI_GEMV_GRID"))) : 256;
+    return cap;
+}
+
+}  // namespace
+
+bool gemv_pair_supported(int t1, int t2) {
+    if (t1 == t2) return is_quant(t1);
+    return (t2 == T_Q6_K && (t1 == T_Q4_K || t1 == T_Q5_K)) ||
+           (t2 == T_Q8_0 && (t1 == T_Q4_K || t1 == T_Q5_K || t1 == T_Q6_K));
+}
+
+int gemv_grid(const GemvParams& p) {
+    int units = 0;
+    for (int i = 0; i < p.nseg; ++i) {
+        const GemvSeg& s = p.seg[i];
+        const int rw = gv_rw2(s) ? 2 : 1;
+        units += s.pair == PAIR_AB ? s.A.rows : (s.A.rows + rw - 1) / rw;
+    }
+    return std::max(p.nseg, std::min(gv_grid_cap(), (units + GV_NW - 1) / GV_NW));
+}
+
+void init_kernel_attributes() {
+    init_gemm_attributes();
+    const int types[4] = {T_Q4_K, T_Q5_K, T_Q6_K, T_Q8_0};
+    for (int rw = 1; rw <= 2; ++rw)
+        for (int kb : {1, 2, 4})
+            for (int t0 : types)
+                for (int t1 : {-1, t0, (int)T_Q6_K, (int)T_Q8_0}) {
+                    for (int tag = 0; tag <= 1; ++tag) {
+                        GvFn f = t1 < 0 ? gv_fn(1, t0, t0, rw, kb, tag) : gv_fn(2, t0, t1, rw, kb, tag);
+                        if (f)
+                            MI_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(f),
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024));
+                    }
+                }
+}
+
+void launch_gemv(const GemvParams& p, hipStream_t s, hipEvent_t ev_start, hipEvent_t ev_stop) {
+    if (p.nseg < 1 || p.nseg > GEMV_MAX_SEG) throw Error("gemv: 1 or 2 segments per launch");
+    if (p.K % 256 != 0 || p.K > GV_KMAX) throw Error("gemv: K must be a multiple of 256 and <= 14336");
+    const bool rw2 = gv_rw2(p.seg[0]);
+    for (int i = 0; i < p.nseg; ++i) {
+        const GemvSeg& g = p.seg[i];
+        if (gv_rw2(g) != rw2) throw Error("gemv: segments of one launch must share their unit shape");
+        if (g.A.K != p.K || (g.pair == PAIR_AB && (g.B.K != p.K || g.B.type != g.A.type || g.B.rows != g.A.rows)))
+            throw Error("gemv: matrix shapes do not match the activation");
+        if (!is_quant(g.A.type)) throw Error("gemv: unsupported quant type");
+        if (g.epi == EPI_QKV && (g.A.rows & 1)) throw Error("gemv: fused QKV rows must be even");
+        if ((g.epi == EPI_SWIGLU || g.epi == EPI_MOE_DOWN) != (g.pair == PAIR_AB))
+            throw Error("gemv: SwiGLU / MoE-down epilogues take a PAIR_AB segment");
+        if ((g.epi == EPI_ADD || g.epi == EPI_MOE_DOWN) && !g.resid) throw Error("gemv: residual epilogue without resid");
+    }
+    if (p.nseg == 2 && !gemv_pair_supported(p.seg[0].A.type, p.seg[1].A.type))
+        throw Error("gemv: unsupported pair of segment types");
+    if (p.pro == PRO_ATTN && (p.attn.n_head * p.attn.head_dim != p.K)) throw Error("gemv: attention combine needs K == n_head*head_dim");
+    if (p.nslots == 2 && p.pro == PRO_RMSNORM) throw Error("gemv: a second activation slot is plain");
+    const int kb = gv_kb(p.K);
+    GvFn fn = gv_fn(p.nseg, p.seg[0].A.type, p.seg[p.nseg - 1].A.type, rw2 ? 2 : 1, kb,
+                    p.nseg == 1 && p.seg[0].epi == EPI_SWIGLU ? 1 : 0);
+    if (!fn) throw Error("gemv: no kernel for this type / shape");
+
+    GvArgs a;
+    std::memset(&a, 0, sizeof(a));
+    // workgroups per segment in proportion to its bytes (at least one each)
+    const int grid = gemv_grid(p);
+    long long tot = 0;
+    for (int i = 0; i < p.nseg; ++i) tot += seg_bytes(p.seg[i]);
+    int blk = 0;
+    for (int i = 0; i < p.nseg; ++i) {
+        const GemvSeg& g = p.seg[i];
+        GvSeg& o = a.seg[i];
+        for (int k = 0; k < 4; ++k) {
+            o.a[k] = g.A.p[k];
+            o.b[k] = g.pair == PAIR_AB ? g.B.p[k] : g.A.p[k];
+        }
+        o.out = g.out;
+        o.resid = g.resid;
+        o.rows = g.A.rows;
+        const int rw = rw2 ? 2 : 1;
+        o.units = g.pair == PAIR_AB ? g.A.rows : (g.A.rows + rw - 1) / rw;
+        o.epi = g.epi;
+        o.nq = g.nq;
+        o.nk = g.nk;
+        o.expA = g.expA;
+        o.expB = g.expB;
+        o.actB = g.actB;
+        int nblk = i + 1 == p.nseg ? grid - blk
+                                   : (int)std::max(1LL, std::min<long long>(grid - blk - 1, grid * seg_bytes(g) / std::max(1LL, tot)));
+        nblk = std::max(1, std::min(nblk, (o.units + GV_NW - 1) / GV_NW));
+        o.blk0 = blk;
+        o.nblk = nblk;
+        blk += nblk;
+    }
+    if (p.nseg == 1) a.seg[1].blk0 = blk;   // every workgroup is segment 0's
+    a.x[0] = p.x[0];
+    a.x[1] = p.nslots > 1 ? p.x[1] : p.x[0];
+    a.norm_w = p.norm_w;
+    a.attn_o = p.attn.o;
+    a.tokpos = p.tokpos;
+    a.cell_pos = p.cell_pos;
+    a.kcache = p.kcache;
+    a.vcache = p.vcache;
+    a.freq_factors = p.freq_factors;
+    a.sel = p.sel;
+    a.selw = p.selw;
+    a.eps = p.eps;
+    a.theta_scale = p.theta_scale;
+    a.freq_scale = p.freq_scale;
+    a.K = p.K;
+    a.pro = p.pro;
+    a.nslots = p.nslots < 1 ? 1 : p.nslots;
+    a.attn_nsplit = p.attn_nsplit;
+    a.attn_stride = p.attn.n_head * p.attn.head_dim;
+    a.n_rot = p.n_rot;
+    a.head_dim = p.head_dim > 0 ? p.head_dim : 1;
+    a.kv_dim = p.kv_dim;
+    a.stamps = p.stamps;
+    for (int i = 0; i < p.nseg; ++i)
+        if (p.seg[i].epi == EPI_QKV && (!p.tokpos || (p.n_rot > 0 && p.head_dim <= 0)))
+            throw Error("gemv: QKV epilogue needs tokpos and the head geometry");
+    const size_t smem = gv_lds_bytes(p.K / 256, a.nslots, p.n_rot);
+    if (smem > 96 * 1024) throw Error("gemv: activation too large for LDS");
+    if (ev_start || ev_stop)
+        hipExtLaunchKernelGGL(fn, dim3(blk), dim3(GV_NW * 64), smem, s, ev_start, ev_stop, 0, a);
+    else
+        hipLaunchKernelGGL(fn, dim3(blk), dim3(GV_NW * 64), smem, s, a);
+    MI_HIP(hipGetLastError());
+}
+
+}  // namespace mi

@@ -4,38 +4,37 @@
 
 namespace mi {
 
-// ---- fused quantised GEMV ------------------------------------------------
-// One launch computes several "segments".  A segment is a list of units; a
-// unit is a PAIR of output rows computed by one wave (so RoPE pairs and the
-// SwiGLU gate/up pair are available together in the epilogue):
-//   PAIR_ADJ: rows (2u, 2u+1) of A          PAIR_AB: row u of A and row u of B
+// ---- decode GEMV (gemv.hip) -------------------------------------------------
+// One launch computes one or two "segments" (a matrix, or a gate/up pair) against one
+// activation: ggml_mul_mat of batch 1 with the CPU path's integer arithmetic (activations
+// quantised to Q8_K / Q8_0, per-block integer dots), fused with the producer's epilogue.
 enum Pair { PAIR_ADJ = 0, PAIR_AB = 1 };
 enum Epi {
     EPI_STORE = 0,    // out[r] = y
     EPI_ADD = 1,      // out[r] = y + resid[r]            (residual add, llm_build_llama)
-    EPI_ROPE_Q = 2,   // rope(pair) -> out (f32)
-    EPI_ROPE_K = 3,   // rope(pair) -> f16 K cache row of this token's cell
-    EPI_V = 4,        // -> f16 V cache row of this token's cell
+    EPI_QKV = 2,      // fused Q|K|V rows: rows < nq -> RoPE -> out (f32 q); rows < nq+nk ->
+                      // RoPE -> f16 K cache row of this token's cell; the rest -> f16 V cache
+    EPI_ROPE_Q = 3,   // batch GEMM epilogues (gemm_t / mmq32): RoPE -> out
+    EPI_ROPE_K = 4,   //   RoPE -> f16 K cache
+    EPI_V = 7,        //   -> f16 V cache
     EPI_SWIGLU = 5,   // out[u] = silu(yA) * yB            (LLM_FFN_SILU + LLM_FFN_PAR)
     EPI_MOE_DOWN = 6, // out[u] = (yA*wA + yB*wB) + resid[u] (build_moe_ffn aggregation)
 };
 enum Pro {
-    PRO_PLAIN = 0,    // slot 0 = x[0]
-    PRO_RMSNORM = 1,  // slot 0 = rms_norm(x[0]) * norm_w
-    PRO_ATTN = 2,     // slot 0 = the split-K attention partials combined (attn_split_kernel)
+    PRO_PLAIN = 0,    // activation = x[0] (and x[1] for a second slot)
+    PRO_RMSNORM = 1,  // activation = rms_norm(x[0]) * norm_w
+    PRO_ATTN = 2,     // activation = the attention partials of the splits, added in split order
 };
 
 struct GemvSeg {
-    QMat A, B;
+    QMat A, B;            // B: the PAIR_AB partner (gate/up: up; MoE down: the same tensor)
     int pair, epi;
-    int units, unit0;     // unit count, first global unit index
-    int actA, actB;       // activation slot feeding A / B rows
-    int expA, expB;       // MoE: slot in sel[] choosing the expert (-1: dense)
+    int nq, nk;           // EPI_QKV: rows of Q and K in A (the rest are V)
+    int expA, expB;       // MoE: slot in sel[] choosing the expert of A / B (-1: dense)
+    int actB;             // activation slot of the B rows (MoE down: 1)
     float* out;
-    const float* resid;
+    const float* resid;   // EPI_ADD / EPI_MOE_DOWN (may alias out)
 };
-
-constexpr int GEMV_MAX_SEG = 4;
 
 // Attention split over cells: split s of q head h holds the partial sum
 // O_s = sum_{c in s} f16(p_c) v_c with the head's exact softmax weights p (the
@@ -63,20 +62,19 @@ struct AttnPartials {
     int n_head, head_dim;
 };
 
+constexpr int GEMV_MAX_SEG = 2;
 struct GemvParams {
     GemvSeg seg[GEMV_MAX_SEG];
-    int nseg, total_units;
-    // prologue: activation slots are built in LDS by every workgroup
-    int pro;                  // PRO_RMSNORM applies to slot 0 only
-    int nslots;               // 1 or 2
+    int nseg;
+    int pro;                  // Pro
+    int nslots;               // 1, or 2 (MoE down: x[1] feeds the B rows)
     const float* x[2];
     const float* norm_w;
     float eps;
-    int K;                    // activation length (multiple of 256)
-    int need_q8k, need_q80;   // which activation formats the segments consume
-    // RoPE / KV cache (decode)
-    const int* tokpos;        // {token, pos, cell}
-    int* cell_pos;            // cell -> position (written by the K epilogue)
+    int K;                    // activation length (multiple of 256, <= 14336)
+    // RoPE / KV cache (EPI_QKV)
+    const int* tokpos;        // {token, pos, cell, -}
+    int* cell_pos;            // cell -> position (written with the K rows)
     float theta_scale, freq_scale;
     int n_rot, head_dim;
     const float* freq_factors;
@@ -87,23 +85,19 @@ struct GemvParams {
     const int* sel;
     const float* selw;
     AttnPartials attn;        // PRO_ATTN input
-    int wg_units;             // max units one workgroup owns (set by launch_gemv; LDS residual staging)
-    int grid;                 // == gridDim.x (set by launch_gemv)
-    unsigned long long* stamps;   // diagnostics: per-workgroup s_memrealtime stamps [grid][8] (nullptr: off)
+    int attn_nsplit;          // PRO_ATTN: splits to add (0: from the cell count in tokpos)
+    unsigned long long* stamps;   // diagnostics (MI_STAMPS builds): per-workgroup stamps [grid][8]
 };
 
-enum GemvRole { ROLE_QKV = 0, ROLE_WO = 1, ROLE_FFN_UP = 2, ROLE_FFN_DOWN = 3, ROLE_OUTPUT = 4, ROLE_GENERIC = 5 };
-size_t gemv_smem_bytes(const GemvParams& p);
-// ev_start/ev_stop (optional): recorded at the kernel's own start and end
-// (hipExtLaunchKernel) -- the bench's in-kernel timing of one launch.
-void launch_gemv(const GemvParams& p, int role, int grid, hipStream_t s,
-                 hipEvent_t ev_start = nullptr, hipEvent_t ev_stop = nullptr);
-// Two launches of different quant types over the same activation as one launch (QKV of
-// Q4_K_M / Q5_K_M layers with a Q6_K attn_v); gemv_mix_supported says whether the pair has one.
-bool gemv_mix_supported(int t1, int t2, int role);
-void launch_gemv_mix(const GemvParams& p1, const GemvParams& p2, int role, hipStream_t s);
 void init_kernel_attributes();   // once per device, before any graph capture
-int gemv_default_grid(const GemvParams& p, int role = ROLE_GENERIC);
+// ev_start/ev_stop (optional): recorded at the kernel's own start and end (hipExtLaunchKernel)
+// -- the bench's in-kernel timing of one launch.
+void launch_gemv(const GemvParams& p, hipStream_t s, hipEvent_t ev_start = nullptr, hipEvent_t ev_stop = nullptr);
+// whether one launch can carry segments of these two quant types
+bool gemv_pair_supported(int t1, int t2);
+// workgroups of a launch
+int gemv_grid(const GemvParams& p);
+void init_gemm_attributes();     // the batch GEMMs' LDS limits (kernels.hip)
 
 // ---- batched quantised GEMM over up to GEMM_NT tokens (prompt ingestion) ----
 // The GEMV's integer arithmetic per token (Q8_K / Q8_0 activations, per-block integer

@@ -10,6 +10,7 @@
 // file is compiled with -ffp-contract=off so that no a*b+c is silently fused
 // where ggml rounds twice.
 #include "kernels.h"
+#include "qdot.h"
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
 #include <cstdlib>
@@ -17,2088 +18,6 @@
 #include <algorithm>
 
 namespace mi {
-
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-typedef int i32x4 __attribute__((ext_vector_type(4)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-// Pointers the GEMV reads from its LDS copy of the parameter block are generic
-// to the compiler, which would emit flat_* accesses: those retire out of order
-// (every wait becomes vmcnt(0) & lgkmcnt(0)) and would serialise the weight
-// ring.  Every global access of the GEMV goes through gptr() -> global_*.
-template <typename T>
-__device__ __forceinline__ const __attribute__((address_space(1))) T* gptr(const T* p) {
-    return (const __attribute__((address_space(1))) T*)(p);
-}
-template <typename T>
-__device__ __forceinline__ __attribute__((address_space(1))) T* gptr_w(T* p) {
-    return (__attribute__((address_space(1))) T*)(p);
-}
-// A wave-uniform pointer (e.g. read from LDS) moved to SGPRs.
-template <typename T>
-__device__ __forceinline__ T* rfl_ptr(T* p) {
-    const unsigned long long v = reinterpret_cast<unsigned long long>(p);
-    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
-    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
-    return reinterpret_cast<T*>(((unsigned long long)hi << 32) | lo);
-}
-__device__ __forceinline__ u32x4 ldg16(const uint8_t* p) {
-    return __builtin_nontemporal_load(gptr(reinterpret_cast<const u32x4*>(p)));
-}
-__device__ __forceinline__ float h2f(uint32_t bits) {
-    return __half2float(__ushort_as_half(static_cast<unsigned short>(bits & 0xFFFFu)));
-}
-__device__ __forceinline__ int dot4(int a, int b, int c) { return __builtin_amdgcn_sdot4(a, b, c, false); }
-
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
-// Full-wave sum through DPP (row_shr 1/2/4/8, row_bcast 15/31): the total
-// lands in lane 63.  Fixed combination order -> deterministic.
-#define MI_DPP(v, ctrl, rmask) \
-    __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), ctrl, rmask, 0xf, false))
-__device__ __forceinline__ float wave_sum63(float v) {
-    v += MI_DPP(v, 0x111, 0xf);   // row_shr:1
-    v += MI_DPP(v, 0x112, 0xf);   // row_shr:2
-    v += MI_DPP(v, 0x114, 0xf);   // row_shr:4
-    v += MI_DPP(v, 0x118, 0xf);   // row_shr:8  -> lane 15 of each row holds the row sum
-    v += MI_DPP(v, 0x142, 0xa);   // row_bcast:15 -> rows 1,3 add lane 15 of rows 0,2
-    v += MI_DPP(v, 0x143, 0xc);   // row_bcast:31 -> rows 2,3 add lane 31
-    return v;                     // lane 63 = total
-}
-#undef MI_DPP
-__device__ __forceinline__ double wave_sum_d(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
-// DPP forms of the prologue reductions (__shfl_xor lowers to ds_bpermute: an
-// LDS round trip per step, ~16 dependent ones per Q8_K block).
-template <int CTRL, int RMASK>
-__device__ __forceinline__ int dpp_i(int v) {
-    return __builtin_amdgcn_update_dpp(0, v, CTRL, RMASK, 0xf, false);
-}
-template <int CTRL, int RMASK>
-__device__ __forceinline__ double dpp_d(double v) {
-    const long long b = __double_as_longlong(v);
-    const int lo = dpp_i<CTRL, RMASK>((int)b), hi = dpp_i<CTRL, RMASK>((int)(b >> 32));
-    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-}
-// Full-wave double sum, total in lane 63 (same scan as wave_sum63).
-__device__ __forceinline__ double wave_sum63_d(double v) {
-    v += dpp_d<0x111, 0xf>(v);
-    v += dpp_d<0x112, 0xf>(v);
-    v += dpp_d<0x114, 0xf>(v);
-    v += dpp_d<0x118, 0xf>(v);
-    v += dpp_d<0x142, 0xa>(v);
-    v += dpp_d<0x143, 0xc>(v);
-    return v;
-}
-// Full-wave max of non-negative floats (0 is the identity), broadcast to all lanes.
-__device__ __forceinline__ float wave_max_pos(float v) {
-#define MX(ctrl, rm) v = fmaxf(v, __int_as_float(dpp_i<ctrl, rm>(__float_as_int(v))))
-    MX(0x111, 0xf); MX(0x112, 0xf); MX(0x114, 0xf); MX(0x118, 0xf); MX(0x142, 0xa); MX(0x143, 0xc);
-#undef MX
-    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
-}
-__device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-    return v;
-}
-
-// ---------------------------------------------------------------------------
-// Activation quantisation (per 256-block, one wave, 4 values per lane)
-// ---------------------------------------------------------------------------
-
-// quantize_row_q8_K_ref: max = signed value of the largest |x| (first index on
-// ties), iscale = -127/max, q = min(127, nearest_int(iscale*x)), d = 1/iscale.
-__device__ __forceinline__ void quant_q8k_block(const float v[4], int lane, int8_t* q8, int* bsum,
-                                                float* dk) {
-    const float a0 = fabsf(v[0]), a1 = fabsf(v[1]), a2 = fabsf(v[2]), a3 = fabsf(v[3]);
-    const float amax = wave_max_pos(fmaxf(fmaxf(a0, a1), fmaxf(a2, a3)));
-    int q[4];
-    float d;
-    if (amax == 0.0f) {
-        q[0] = q[1] = q[2] = q[3] = 0;
-        d = 0.0f;
-    } else {
-        // the signed value at the FIRST index whose |x| is the maximum
-        const int e = a0 == amax ? 0 : a1 == amax ? 1 : a2 == amax ? 2 : a3 == amax ? 3 : 4;
-        const float mine = e == 0 ? v[0] : e == 1 ? v[1] : e == 2 ? v[2] : v[3];
-        const unsigned long long m = __ballot(e < 4);
-        const int src = __builtin_ctzll(m);
-        const float mx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mine), src));
-        const float iscale = -127.0f / mx;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) q[k] = min(127, (int)rintf(iscale * v[k]));
-        d = 1.0f / iscale;
-    }
-    const int packed = (q[0] & 0xFF) | ((q[1] & 0xFF) << 8) | ((q[2] & 0xFF) << 16) | ((q[3] & 0xFF) << 24);
-    reinterpret_cast<int*>(q8)[lane] = packed;
-    int sm = q[0] + q[1] + q[2] + q[3];
-    sm += dpp_i<0xB1, 0xf>(sm);   // quad_perm [1,0,3,2]
-    sm += dpp_i<0x4E, 0xf>(sm);   // quad_perm [2,3,0,1] -> every lane of the quad has its 16-sum
-    if ((lane & 3) == 0) bsum[lane >> 2] = sm;
-    if (lane == 0) *dk = d;
-}
-
-// x86 SIMD form of quantize_row_q8_0: d = fp16(amax/127), id = 127/amax,
-// q = round-to-nearest-even(x*id).  8 lanes per 32-block.
-__device__ __forceinline__ void quant_q80_block(const float v[4], int lane, int8_t* q8, float* d0) {
-    float am = fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3])));
-    am = fmaxf(am, __int_as_float(dpp_i<0xB1, 0xf>(__float_as_int(am))));
-    am = fmaxf(am, __int_as_float(dpp_i<0x4E, 0xf>(__float_as_int(am))));
-    am = fmaxf(am, __int_as_float(dpp_i<0x141, 0xf>(__float_as_int(am))));   // row_half_mirror
-    const float d = am / 127.0f;
-    const float id = am != 0.0f ? 127.0f / am : 0.0f;
-    int q[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) q[e] = (int)rintf(v[e] * id);
-    const int packed = (q[0] & 0xFF) | ((q[1] & 0xFF) << 8) | ((q[2] & 0xFF) << 16) | ((q[3] & 0xFF) << 24);
-    reinterpret_cast<int*>(q8)[lane] = packed;
-    if ((lane & 7) == 0) d0[lane >> 3] = __half2float(__float2half_rn(d));
-}
-
-// ---------------------------------------------------------------------------
-// LDS layout of the GEMV prologue
-// ---------------------------------------------------------------------------
-struct ActLayout {
-    int nb, q8k, q80, bsum, dk, d0, slot_bytes;
-};
-__host__ __device__ inline ActLayout act_layout(int K, int need_q8k, int need_q80) {
-    ActLayout L;
-    L.nb = K / 256;
-    int off = 0;
-    L.q8k = off; off += need_q8k ? L.nb * 256 : 0;
-    L.q80 = off; off += need_q80 ? L.nb * 256 : 0;
-    L.bsum = off; off += need_q8k ? L.nb * 64 : 0;
-    L.dk = off; off += need_q8k ? ((L.nb * 4 + 15) & ~15) : 0;
-    L.d0 = off; off += need_q80 ? L.nb * 32 : 0;
-    L.slot_bytes = (off + 15) & ~15;
-    return L;
-}
-
-struct Act {
-    const int8_t* q8k;
-    const int* bsum;
-    const float* dk;
-    const int8_t* q80;
-    const float* d0;
-};
-
-__device__ __forceinline__ Act act_view(const char* smem, const ActLayout& L, int slot) {
-    const char* b = smem + slot * L.slot_bytes;
-    Act a;
-    a.q8k = reinterpret_cast<const int8_t*>(b + L.q8k);
-    a.bsum = reinterpret_cast<const int*>(b + L.bsum);
-    a.dk = reinterpret_cast<const float*>(b + L.dk);
-    a.q80 = reinterpret_cast<const int8_t*>(b + L.q80);
-    a.d0 = reinterpret_cast<const float*>(b + L.d0);
-    return a;
-}
-
-// ---------------------------------------------------------------------------
-// Per-type superblock dot products.  A wave step covers SPS superblocks with
-// LPS lanes each; each lane issues one aligned 16-byte load of the main
-// quant plane (plus its side planes) and returns its fp32 partial.
-// ---------------------------------------------------------------------------
-template <int T> struct Kq;
-template <int T> struct PlaneBytes;   // bytes per superblock of each plane (common.h plane_sb_bytes)
-template <> struct PlaneBytes<T_Q4_K> { static constexpr int b[4] = {128, 16, 0, 0}; };
-template <> struct PlaneBytes<T_Q5_K> { static constexpr int b[4] = {128, 32, 16, 0}; };
-template <> struct PlaneBytes<T_Q6_K> { static constexpr int b[4] = {128, 64, 16, 2}; };
-template <> struct PlaneBytes<T_Q8_0> { static constexpr int b[4] = {256, 16, 0, 0}; };
-
-template <> struct Kq<T_Q4_K> {
-    static constexpr int LPS = 8;
-    struct Ld { u32x4 qs, hdr; };
-    // rp: plane pointers at the start of the row (wave-uniform); sb = s*8 + sbl
-    __device__ static Ld load(const uint8_t* const* rp, int sb, int j) {
-        Ld l;
-        l.qs = ldg16(rp[0] + sb * 128 + j * 16);
-#ifdef MI_EXP_NOHDR   // bandwidth experiment only (wrong numerics): no header loads
-        l.hdr = u32x4{0x3c003c00u, 0x01010101u, 0x01010101u, 0x01010101u};
-#else
-        l.hdr = ldg16(rp[1] + sb * 16);
-#endif
-        return l;
-    }
-    // the activation slice lane (sb, j) needs -- identical for every row
-    struct AR { i32x4 alo, ahi; int bs_lo, bs_hi; float dx; };
-    __device__ static AR act(const Act& a, int sb, int j) {
-        const int g = j >> 1, half = j & 1;
-        const int8_t* ab = a.q8k + sb * 256 + 64 * g + 16 * half;
-        AR r;
-        r.alo = *reinterpret_cast<const i32x4*>(ab);
-        r.ahi = *reinterpret_cast<const i32x4*>(ab + 32);
-        r.bs_lo = a.bsum[sb * 16 + 4 * g + half];
-        r.bs_hi = a.bsum[sb * 16 + 4 * g + 2 + half];
-        r.dx = a.dk[sb];
-        return r;
-    }
-    __device__ static float dot(const Ld& l, const AR& r, int j) {
-        const int g = j >> 1;
-        const i32x4 alo = r.alo, ahi = r.ahi;
-        int dlo = 0, dhi = 0;
-        dlo = dot4(l.qs.x & 0x0F0F0F0F, alo.x, dlo);
-        dlo = dot4(l.qs.y & 0x0F0F0F0F, alo.y, dlo);
-        dlo = dot4(l.qs.z & 0x0F0F0F0F, alo.z, dlo);
-        dlo = dot4(l.qs.w & 0x0F0F0F0F, alo.w, dlo);
-        dhi = dot4((l.qs.x >> 4) & 0x0F0F0F0F, ahi.x, dhi);
-        dhi = dot4((l.qs.y >> 4) & 0x0F0F0F0F, ahi.y, dhi);
-        dhi = dot4((l.qs.z >> 4) & 0x0F0F0F0F, ahi.z, dhi);
-        dhi = dot4((l.qs.w >> 4) & 0x0F0F0F0F, ahi.w, dhi);
-        // get_scale_min_k4 for sub-blocks 2g, 2g+1 (bytes 2(g&1), 2(g&1)+1 of each header dword)
-        const unsigned sh = (g & 1) * 16;
-        const unsigned Y = l.hdr.y >> sh, Z = l.hdr.z >> sh, W = l.hdr.w >> sh;
-        const unsigned SC = g < 2 ? (Y & 0x3F3Fu) : ((W & 0x0F0Fu) | ((Y >> 2) & 0x3030u));
-        const unsigned MM = g < 2 ? (Z & 0x3F3Fu) : (((W >> 4) & 0x0F0Fu) | ((Z >> 2) & 0x3030u));
-        const int S = (int)(SC & 0xFF) * dlo + (int)((SC >> 8) & 0xFF) * dhi;
-        const int M = (int)(MM & 0xFF) * r.bs_lo + (int)((MM >> 8) & 0xFF) * r.bs_hi;
-        const float d = h2f(l.hdr.x) * r.dx;
-        const float dm = h2f(l.hdr.x >> 16) * r.dx;
-        return d * (float)S - dm * (float)M;
-    }
-};
-
-template <> struct Kq<T_Q5_K> {
-    static constexpr int LPS = 8;
-    struct Ld { u32x4 qs, qh, hdr; };
-    __device__ static Ld load(const uint8_t* const* rp, int sb, int j) {
-        Ld l;
-        l.qs = ldg16(rp[0] + sb * 128 + j * 16);
-        l.qh = ldg16(rp[1] + sb * 32 + (j & 1) * 16);
-        l.hdr = ldg16(rp[2] + sb * 16);
-        return l;
-    }
-    using AR = Kq<T_Q4_K>::AR;
-    __device__ static AR act(const Act& a, int sb, int j) { return Kq<T_Q4_K>::act(a, sb, j); }
-    __device__ static float dot(const Ld& l, const AR& r, int j) {
-        const int g = j >> 1;
-        const i32x4 alo = r.alo, ahi = r.ahi;
-        const unsigned s0 = 2 * g, s1 = 2 * g + 1;
-        int dlo = 0, dhi = 0;
-#define Q5L(c) ((l.qs.c & 0x0F0F0F0Fu) | (((l.qh.c >> s0) & 0x01010101u) << 4))
-#define Q5H(c) (((l.qs.c >> 4) & 0x0F0F0F0Fu) | (((l.qh.c >> s1) & 0x01010101u) << 4))
-        dlo = dot4((int)Q5L(x), alo.x, dlo);
-        dlo = dot4((int)Q5L(y), alo.y, dlo);
-        dlo = dot4((int)Q5L(z), alo.z, dlo);
-        dlo = dot4((int)Q5L(w), alo.w, dlo);
-        dhi = dot4((int)Q5H(x), ahi.x, dhi);
-        dhi = dot4((int)Q5H(y), ahi.y, dhi);
-        dhi = dot4((int)Q5H(z), ahi.z, dhi);
-        dhi = dot4((int)Q5H(w), ahi.w, dhi);
-#undef Q5L
-#undef Q5H
-        const unsigned sh = (g & 1) * 16;
-        const unsigned Y = l.hdr.y >> sh, Z = l.hdr.z >> sh, W = l.hdr.w >> sh;
-        const unsigned SC = g < 2 ? (Y & 0x3F3Fu) : ((W & 0x0F0Fu) | ((Y >> 2) & 0x3030u));
-        const unsigned MM = g < 2 ? (Z & 0x3F3Fu) : (((W >> 4) & 0x0F0Fu) | ((Z >> 2) & 0x3030u));
-        const int S = (int)(SC & 0xFF) * dlo + (int)((SC >> 8) & 0xFF) * dhi;
-        const int M = (int)(MM & 0xFF) * r.bs_lo + (int)((MM >> 8) & 0xFF) * r.bs_hi;
-        const float d = h2f(l.hdr.x) * r.dx;
-        const float dm = h2f(l.hdr.x >> 16) * r.dx;
-        return d * (float)S - dm * (float)M;
-    }
-};
-
-template <> struct Kq<T_Q6_K> {
-    static constexpr int LPS = 8;
-    struct Ld { u32x4 ql, qh; unsigned sc0, sc1, d; };
-    __device__ static Ld load(const uint8_t* const* rp, int sb, int j) {
-        Ld l;
-        const int h = j >> 2, half = j & 1;
-        l.ql = ldg16(rp[0] + sb * 128 + j * 16);
-        l.qh = ldg16(rp[1] + sb * 64 + 32 * h + 16 * half);
-        // scales 8h..8h+7: is_lo = 8h+2hq+half lives in word 0, is_hi = is_lo+4 in word 1
-        typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-        const u32x2 sc = __builtin_nontemporal_load(gptr(reinterpret_cast<const u32x2*>(rp[2] + sb * 16) + h));
-        l.sc0 = sc.x;
-        l.sc1 = sc.y;
-        l.d = __builtin_nontemporal_load(gptr(reinterpret_cast<const unsigned short*>(rp[3] + sb * 2)));
-        return l;
-    }
-    struct AR { i32x4 alo, ahi; int bs_lo, bs_hi; float dx; };
-    __device__ static AR act(const Act& a, int sb, int j) {
-        const int h = j >> 2, hq = (j >> 1) & 1, half = j & 1;
-        const int e_lo = 128 * h + 32 * hq + 16 * half;
-        const int8_t* ab = a.q8k + sb * 256 + e_lo;
-        const int is_lo = 8 * h + 2 * hq + half;
-        AR r;
-        r.alo = *reinterpret_cast<const i32x4*>(ab);
-        r.ahi = *reinterpret_cast<const i32x4*>(ab + 64);
-        r.bs_lo = a.bsum[sb * 16 + is_lo];
-        r.bs_hi = a.bsum[sb * 16 + is_lo + 4];
-        r.dx = a.dk[sb];
-        return r;
-    }
-    __device__ static float dot(const Ld& l, const AR& r, int j) {
-        const int hq = (j >> 1) & 1, half = j & 1;
-        const unsigned sh = hq * 2;
-        const i32x4 alo = r.alo, ahi = r.ahi;
-        int dlo = 0, dhi = 0;
-#define Q6L(c) ((l.ql.c & 0x0F0F0F0Fu) | (((l.qh.c >> sh) & 0x03030303u) << 4))
-#define Q6H(c) (((l.ql.c >> 4) & 0x0F0F0F0Fu) | (((l.qh.c >> (sh + 4)) & 0x03030303u) << 4))
-        dlo = dot4((int)Q6L(x), alo.x, dlo);
-        dlo = dot4((int)Q6L(y), alo.y, dlo);
-        dlo = dot4((int)Q6L(z), alo.z, dlo);
-        dlo = dot4((int)Q6L(w), alo.w, dlo);
-        dhi = dot4((int)Q6H(x), ahi.x, dhi);
-        dhi = dot4((int)Q6H(y), ahi.y, dhi);
-        dhi = dot4((int)Q6H(z), ahi.z, dhi);
-        dhi = dot4((int)Q6H(w), ahi.w, dhi);
-#undef Q6L
-#undef Q6H
-        // unsigned 6-bit q times q8, minus 32*sum(q8) == sum((q-32)*q8) exactly
-        const int bsh = 8 * (2 * hq + half);
-        const int sc_lo = (int)(signed char)((l.sc0 >> bsh) & 0xFF);
-        const int sc_hi = (int)(signed char)((l.sc1 >> bsh) & 0xFF);
-        const int S = sc_lo * (dlo - 32 * r.bs_lo) + sc_hi * (dhi - 32 * r.bs_hi);
-        const float d = h2f(l.d) * r.dx;
-        return d * (float)S;
-    }
-};
-
-template <> struct Kq<T_Q8_0> {
-    static constexpr int LPS = 8;          // lane j owns block j (32 weights) of the superblock
-    struct Ld { u32x4 q0, q1; unsigned d; };
-    __device__ static Ld load(const uint8_t* const* rp, int sb, int j) {
-        Ld l;
-        l.q0 = ldg16(rp[0] + sb * 256 + j * 32);
-        l.q1 = ldg16(rp[0] + sb * 256 + j * 32 + 16);
-        l.d = __builtin_nontemporal_load(gptr(reinterpret_cast<const unsigned short*>(rp[1] + sb * 16 + j * 2)));
-        return l;
-    }
-    struct AR { i32x4 a0, a1; float d0; };
-    __device__ static AR act(const Act& a, int sb, int j) {
-        const int8_t* ab = a.q80 + sb * 256 + j * 32;
-        AR r;
-        r.a0 = *reinterpret_cast<const i32x4*>(ab);
-        r.a1 = *reinterpret_cast<const i32x4*>(ab + 16);
-        r.d0 = a.d0[sb * 8 + j];
-        return r;
-    }
-    __device__ static float dot(const Ld& l, const AR& r, int j) {
-        const i32x4 a0 = r.a0, a1 = r.a1;
-        int s = 0;
-        s = dot4((int)l.q0.x, a0.x, s);
-        s = dot4((int)l.q0.y, a0.y, s);
-        s = dot4((int)l.q0.z, a0.z, s);
-        s = dot4((int)l.q0.w, a0.w, s);
-        s = dot4((int)l.q1.x, a1.x, s);
-        s = dot4((int)l.q1.y, a1.y, s);
-        s = dot4((int)l.q1.z, a1.z, s);
-        s = dot4((int)l.q1.w, a1.w, s);
-        const float d = h2f(l.d) * r.d0;   // fp16(x.d) * fp16(y.d), then * sumi
-        return d * (float)s;
-    }
-};
-
-// ---------------------------------------------------------------------------
-// The fused GEMV kernel, specialised per quant type T.
-//
-// Work decomposition: a unit is a PAIR of output rows (see kernels.h).  Every
-// wave owns a contiguous range of units (so a workgroup owns a contiguous
-// range, whose residual rows it stages in LDS).  A unit's two rows are
-// streamed in "chunks": one aligned 16-byte load per lane of the main quant
-// plane plus its side planes, 8 superblocks per row and chunk (8 lanes per
-// superblock).  The wave walks its (unit, chunk) items through a D-deep
-// register ring: while item i is reduced against the LDS activations, items
-// i+1 .. i+D-1 are in flight -- across unit boundaries, so a wave's weight
-// stream never stops until its range is done.  The first D-1 items are issued
-// before the prologue, so the stream starts while the activations are
-// normalised and quantised.  Loads past the end of the range repeat the last
-// item's addresses (cache hits) so that every ring step issues the same loads
-// and the compiler's vmcnt bookkeeping stays exact (no wait-for-all).
-// ---------------------------------------------------------------------------
-struct SmemPlan {
-    ActLayout L;
-    int act_bytes, rope_off, resid_off, attn_off, red_off, total;
-};
-__host__ __device__ inline SmemPlan smem_plan(const GemvParams& p) {
-    SmemPlan S;
-    S.L = act_layout(p.K, p.need_q8k, p.need_q80);
-    S.act_bytes = S.L.slot_bytes * p.nslots;
-    S.rope_off = S.act_bytes;
-    S.resid_off = S.rope_off + ((p.n_rot / 2) * 8 + 15) / 16 * 16;
-    S.attn_off = S.resid_off + ((p.wg_units * 2 * 4 + 15) / 16) * 16;
-    S.red_off = S.attn_off;
-    S.total = S.red_off + 32 * 8;
-    return S;
-}
-
-__device__ __forceinline__ float silu_f(float x) { return x / (1.0f + expf(-x)); }
-
-__device__ __forceinline__ void unit_range(int total, int W, int gw, int& u0, int& u1) {
-    // total * (gw + 1) < 2^32 (total <= 65536 units, W <= 4096 waves)
-    u0 = (int)(((unsigned)total * (unsigned)gw) / (unsigned)W);
-    u1 = (int)(((unsigned)total * (unsigned)(gw + 1)) / (unsigned)W);
-}
-
-struct UnitRef {
-    int si;           // segment
-    int lu;           // unit within segment
-    long long ra, rb; // rows
-    bool hasB;
-};
-
-__device__ __forceinline__ UnitRef unit_ref(const GemvParams& P, int u) {
-    UnitRef c;
-    int si = 0;
-    while (si + 1 < P.nseg && u >= P.seg[si + 1].unit0) ++si;
-    c.si = si;
-    c.lu = u - P.seg[si].unit0;
-    if (P.seg[si].pair == PAIR_ADJ) {
-        c.ra = 2LL * c.lu;
-        c.rb = c.ra + 1;
-        c.hasB = c.rb < P.seg[si].A.rows;
-    } else {
-        c.ra = c.rb = c.lu;
-        c.hasB = true;
-    }
-    return c;
-}
-
-// Scalar (constant-cache) load of a wave-uniform int written by an earlier
-// kernel or copy: it retires on lgkmcnt, so waiting for it never waits for the
-// weight stream (vector loads retire in order on vmcnt).
-__device__ __forceinline__ int sload_i32(const int* p) {
-    return *(const __attribute__((address_space(4))) int*)(p);
-}
-
-// Prologue, split in two so that its global loads are issued BEFORE the first
-// weight load: vmcnt retires in issue order, so the prologue's waits then never
-// wait for the weight stream.
-//  pro_load:   this wave's activation blocks (blocks wave, wave+NW, ...; and the
-//              RMSNorm weights) into registers, the residual values of this
-//              workgroup's units.
-//  pro_finish: (after the weight prefill) RMSNorm / attention combine, Q8_K or
-//              Q8_0 quantisation into LDS, residuals and the RoPE table to LDS.
-constexpr int PRO_MAXB = 8;   // activation blocks one wave keeps in registers
-struct ProRegs {
-    f32x4 x[PRO_MAXB], w[PRO_MAXB];
-    i32x4 tp;                  // {token, pos, cell, -} (a vector load: a scalar one would
-                              // hold every LDS wait behind it, lgkmcnt counts both)
-    float ra, rb;
-    float ff[2];              // RoPE freq factors of pairs lane, lane+64 (wave 0)
-    int nsplit;               // PRO_ATTN: attention splits to add
-    bool regs;                // blocks held in registers (else re-read in pro_finish)
-    bool attn_regs;           // PRO_ATTN: the splits' partials held in x[] (block i, split s: x[i*nsplit+s])
-};
-
-// Entry loads: the activation, RMSNorm weight and token position.  Their pointers
-// arrive preloaded in SGPRs (kernarg preload, the kernel's leading arguments), so
-// these loads are in flight at once, racing the load of the parameter block.
-__device__ __forceinline__ void pro_load_entry(ProRegs& R, const float* x0, const float* nw_, const int* tp, int nb,
-                                               bool regs, bool rms, int nw, int wave, int lane) {
-    R.tp = tp ? *gptr(reinterpret_cast<const i32x4*>(tp)) : i32x4{0, 0, 0, 0};
-    R.regs = regs;
-    if (regs) {
-        const auto x4 = gptr(reinterpret_cast<const f32x4*>(x0));
-        const auto w4 = gptr(reinterpret_cast<const f32x4*>(nw_));
-#pragma unroll
-        for (int i = 0; i < PRO_MAXB; ++i) {
-            const int blk = wave + i * nw;
-            if (blk < nb) {
-                R.x[i] = x4[blk * 64 + lane];
-                if (rms) R.w[i] = w4[blk * 64 + lane];
-            }
-        }
-    }
-}
-
-// Loads that need the parameter block: RoPE freq factors, the attention partials
-// (their count depends on the cell count in R.tp) and the residuals of this
-// workgroup's units.  Returns whether any were issued.
-__device__ __forceinline__ bool pro_load_rest(const GemvParams& P, ProRegs& R, int nb, int nw, int wave, int lane,
-                                              int wg_u0, int wg_u1) {
-    const int tid = threadIdx.x;
-    bool any = false;
-    R.ff[0] = R.ff[1] = 1.0f;
-    if (P.freq_factors) {
-        any = true;
-        if (wave == 0) {
-            if (lane < P.n_rot / 2) R.ff[0] = gptr(P.freq_factors)[lane];
-            if (lane + 64 < P.n_rot / 2) R.ff[1] = gptr(P.freq_factors)[lane + 64];
-        }
-    }
-    R.nsplit = 0;
-    R.attn_regs = false;
-    if (P.pro == PRO_ATTN) {
-        any = true;
-        int chunk;
-        attn_split(__builtin_amdgcn_readfirstlane(R.tp.z) + 1, chunk, R.nsplit);
-        const int bpw = (nb + nw - 1) / nw;   // blocks per wave
-        R.attn_regs = P.nslots == 1 && R.nsplit * bpw <= PRO_MAXB;
-        if (R.attn_regs) {
-            const AttnPartials& A = P.attn;
-#pragma unroll
-            for (int k = 0; k < PRO_MAXB; ++k) {   // register k = (block i, split s)
-                const int i = k / R.nsplit, s = k % R.nsplit;
-                const int blk = wave + i * nw;
-                if (i < bpw && blk < nb)
-                    R.x[k] = *gptr(reinterpret_cast<const f32x4*>(
-                        A.o + (long long)s * A.n_head * A.head_dim + blk * 256 + lane * 4));
-            }
-        }
-    }
-    // residual values of this workgroup's units (the in-place residual add reads
-    // them before any wave of the workgroup overwrites its rows).  Residual
-    // launches have one segment (launch_gemv checks), so the lookup is scalar.
-    R.ra = R.rb = 0.0f;
-    const GemvSeg& S0 = P.seg[0];
-    if (S0.resid) {
-        any = true;
-        if (tid < wg_u1 - wg_u0) {
-            const long long lu = wg_u0 + tid;
-            if (S0.pair == PAIR_ADJ) {
-                const long long ra = 2 * lu;
-                R.ra = gptr(S0.resid)[ra];
-                R.rb = gptr(S0.resid)[ra + 1 < S0.A.rows ? ra + 1 : ra];
-            } else {
-                R.ra = gptr(S0.resid)[lu];
-                R.rb = gptr(S0.resid)[lu];   // a second load, not a copy (a copy waits for the load)
-            }
-        }
-    }
-    return any;
-}
-
-// RAW_BARRIER: LDS-DMA is in flight (gemv_ring_body), so the reduction's barrier must not
-// wait vmcnt(0) (see lds_barrier).
-template <bool RAW_BARRIER>
-__device__ __forceinline__ void pro_finish(const GemvParams& P, const ProRegs& R, char* smem, const SmemPlan& SP,
-                                           int pos, int ncell, int wg_u0, int wg_u1, int bid) {
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int nwaves = blockDim.x >> 6;
-    const ActLayout& L = SP.L;
-    double* red = reinterpret_cast<double*>(smem + SP.red_off);
-    {
-        float* rs = reinterpret_cast<float*>(smem + SP.resid_off);
-        if (tid < wg_u1 - wg_u0) {
-            rs[2 * tid] = R.ra;
-            rs[2 * tid + 1] = R.rb;
-        }
-    }
-    float scale = 1.0f;
-    if (P.pro == PRO_RMSNORM) {
-        // ggml_compute_forward_rms_norm_f32: sum of float squares in double
-        double s = 0.0;
-        if (R.regs) {
-#pragma unroll
-            for (int i = 0; i < PRO_MAXB; ++i) {
-                if (wave + i * nwaves < L.nb) {
-                    const f32x4 v = R.x[i];
-                    s += (double)(v.x * v.x);
-                    s += (double)(v.y * v.y);
-                    s += (double)(v.z * v.z);
-                    s += (double)(v.w * v.w);
-                }
-            }
-        } else {
-            const auto x4 = gptr(reinterpret_cast<const f32x4*>(P.x[0]));
-            for (int i = tid; i < P.K / 4; i += blockDim.x) {
-                const f32x4 v = x4[i];
-                s += (double)(v.x * v.x);
-                s += (double)(v.y * v.y);
-                s += (double)(v.z * v.z);
-                s += (double)(v.w * v.w);
-            }
-        }
-        s = wave_sum63_d(s);
-        if (lane == 63) red[wave] = s;
-#ifdef MI_STAMPS
-        if (P.stamps && threadIdx.x == 0) P.stamps[bid * 8 + 5] = __builtin_amdgcn_s_memrealtime();
-#endif
-        if (RAW_BARRIER) {
-            __builtin_amdgcn_s_waitcnt((0xF) | (0x3 << 14) | (0x7 << 4));   // lgkmcnt(0) only
-            __builtin_amdgcn_s_barrier();
-        } else {
-            __syncthreads();
-        }
-#ifdef MI_STAMPS
-        if (P.stamps && threadIdx.x == 0) P.stamps[bid * 8 + 6] = __builtin_amdgcn_s_memrealtime();
-#endif
-        double tot = 0.0;
-        for (int w = 0; w < nwaves; ++w) tot += red[w];
-        const float mean = (float)(tot / (double)P.K);
-        scale = 1.0f / sqrtf(mean + P.eps);
-    }
-    int nsplit = 0;
-    if (P.pro == PRO_ATTN) {
-        int chunk;
-        attn_split(ncell, chunk, nsplit);
-    }
-    auto quant = [&](char* base, int blk, float v[4]) {
-        if (P.need_q8k)
-            quant_q8k_block(v, lane, reinterpret_cast<int8_t*>(base + L.q8k) + blk * 256,
-                            reinterpret_cast<int*>(base + L.bsum) + blk * 16,
-                            reinterpret_cast<float*>(base + L.dk) + blk);
-        if (P.need_q80)
-            quant_q80_block(v, lane, reinterpret_cast<int8_t*>(base + L.q80) + blk * 256,
-                            reinterpret_cast<float*>(base + L.d0) + blk * 8);
-    };
-    if (R.attn_regs) {
-        // the attention splits' partial sums (prefetched), added in split order
-#pragma unroll
-        for (int i = 0; i < PRO_MAXB; ++i) {
-            const int blk = wave + i * nwaves;
-            if (i * R.nsplit < PRO_MAXB && blk < L.nb) {
-                f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-                for (int k = 0; k < PRO_MAXB; ++k)
-                    if (k / R.nsplit == i) acc += R.x[k];
-                float v[4] = {acc.x, acc.y, acc.z, acc.w};
-                quant(smem, blk, v);
-            }
-        }
-    } else if (R.regs) {
-#pragma unroll
-        for (int i = 0; i < PRO_MAXB; ++i) {
-            const int blk = wave + i * nwaves;
-            if (blk < L.nb) {
-                float v[4] = {R.x[i].x, R.x[i].y, R.x[i].z, R.x[i].w};
-                if (P.pro == PRO_RMSNORM) {
-                    v[0] = (v[0] * scale) * R.w[i].x;   // ggml_vec_scale_f32 then ggml_mul
-                    v[1] = (v[1] * scale) * R.w[i].y;
-                    v[2] = (v[2] * scale) * R.w[i].z;
-                    v[3] = (v[3] * scale) * R.w[i].w;
-                }
-                quant(smem, blk, v);
-            }
-        }
-    } else {
-        for (int slot = 0; slot < P.nslots; ++slot) {
-            char* base = smem + slot * L.slot_bytes;
-            const auto x4 = gptr(reinterpret_cast<const f32x4*>(P.x[slot]));
-            for (int blk = wave; blk < L.nb; blk += nwaves) {
-                float v[4];
-                if (slot == 0 && P.pro == PRO_ATTN) {
-                    // the attention splits' partial sums, added in split order
-                    const AttnPartials& A = P.attn;
-                    const int e0 = blk * 256 + lane * 4;
-                    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-                    for (int s = 0; s < nsplit; ++s) {
-                        const f32x4 o =
-                            *gptr(reinterpret_cast<const f32x4*>(A.o + (long long)s * A.n_head * A.head_dim + e0));
-                        acc.x += o.x;
-                        acc.y += o.y;
-                        acc.z += o.z;
-                        acc.w += o.w;
-                    }
-                    v[0] = acc.x; v[1] = acc.y; v[2] = acc.z; v[3] = acc.w;
-                } else {
-                    const f32x4 xv = x4[blk * 64 + lane];
-                    v[0] = xv.x; v[1] = xv.y; v[2] = xv.z; v[3] = xv.w;
-                    if (slot == 0 && P.pro == PRO_RMSNORM) {
-                        const f32x4 w = gptr(reinterpret_cast<const f32x4*>(P.norm_w))[blk * 64 + lane];
-                        v[0] = (v[0] * scale) * w.x;
-                        v[1] = (v[1] * scale) * w.y;
-                        v[2] = (v[2] * scale) * w.z;
-                        v[3] = (v[3] * scale) * w.w;
-                    }
-                }
-                quant(base, blk, v);
-            }
-        }
-    }
-    // RoPE cache for this token's position (ggml_rope_cache_init, ext_factor 0, mscale 1)
-    if (P.n_rot > 0 && wave == 0) {
-        float* rope = reinterpret_cast<float*>(smem + SP.rope_off);
-        for (int i = lane; i < P.n_rot / 2; i += 64) {
-            float theta = (float)pos;
-            for (int k = 0; k < i; ++k) theta = theta * P.theta_scale;
-            const float ff = i < 64 ? R.ff[0] : R.ff[1];
-            const float th = P.freq_scale * (theta / ff);
-            rope[2 * i] = cosf(th);
-            rope[2 * i + 1] = sinf(th);
-        }
-    }
-}
-
-// Epilogue inputs, uniform and kept in SGPRs: per launch (EpiConst) and per
-// segment (EpiSeg, re-read from the LDS parameters only when the consumer enters a
-// new segment).
-struct EpiConst {
-    __half* kcache;
-    __half* vcache;
-    int* cell_pos;
-    int head_dim, n_rot, kv_dim;
-};
-struct EpiSeg {
-    float* out;
-    int epi, pair, unit0, end, rows;
-};
-__device__ __forceinline__ EpiConst epi_const(const GemvParams& P) {
-    EpiConst E;
-    E.kcache = rfl_ptr(P.kcache);
-    E.vcache = rfl_ptr(P.vcache);
-    E.cell_pos = rfl_ptr(P.cell_pos);
-    E.head_dim = __builtin_amdgcn_readfirstlane(P.head_dim);
-    E.n_rot = __builtin_amdgcn_readfirstlane(P.n_rot);
-    E.kv_dim = __builtin_amdgcn_readfirstlane(P.kv_dim);
-    return E;
-}
-__device__ __forceinline__ EpiSeg epi_seg(const GemvParams& P, int u) {
-    int si = 0;
-    while (si + 1 < P.nseg && u >= P.seg[si + 1].unit0) ++si;
-    const GemvSeg& S = P.seg[si];
-    EpiSeg e;
-    e.out = rfl_ptr(S.out);
-    e.epi = __builtin_amdgcn_readfirstlane(S.epi);
-    e.pair = __builtin_amdgcn_readfirstlane(S.pair);
-    e.unit0 = __builtin_amdgcn_readfirstlane(S.unit0);
-    e.end = __builtin_amdgcn_readfirstlane(S.unit0 + S.units);
-    e.rows = __builtin_amdgcn_readfirstlane(S.A.rows);
-    return e;
-}
-
-// rva / rvb: residual values of rows A / B
-__device__ __forceinline__ void gemv_epilogue(const EpiConst& E, const EpiSeg& S, int u, const float* rope,
-                                              float rva, float rvb, float wa, float wb,
-                                              int pos, int cell, float yA, float yB) {
-    const auto out = gptr_w(S.out);
-    const int lu = u - S.unit0;
-    const bool adj = S.pair == PAIR_ADJ;
-    const long long ra = adj ? 2LL * lu : lu, rb = adj ? ra + 1 : lu;
-    const bool hasB = !adj || rb < S.rows;
-    switch (S.epi) {
-    case EPI_STORE:
-        out[ra] = yA;
-        if (hasB) out[rb] = yB;
-        break;
-    case EPI_ADD:
-        out[ra] = yA + rva;
-        if (hasB) out[rb] = yB + rvb;
-        break;
-    case EPI_ROPE_Q:
-    case EPI_ROPE_K: {
-        const int i0 = (int)(ra % E.head_dim);   // even
-        float o0 = yA, o1 = yB;
-        if (i0 < E.n_rot) {
-            const float cs = rope[i0], sn = rope[i0 + 1];
-            o0 = yA * cs - yB * sn;
-            o1 = yA * sn + yB * cs;
-        }
-        if (S.epi == EPI_ROPE_Q) {
-            out[ra] = o0;
-            out[rb] = o1;
-        } else {
-            const auto kr = gptr_w(reinterpret_cast<unsigned short*>(E.kcache + (long long)cell * E.kv_dim));
-            kr[ra] = __half_as_ushort(__float2half_rn(o0));
-            kr[rb] = __half_as_ushort(__float2half_rn(o1));
-            if (lu == 0) gptr_w(E.cell_pos)[cell] = pos;
-        }
-        break;
-    }
-    case EPI_V: {
-        const auto vr = gptr_w(reinterpret_cast<unsigned short*>(E.vcache + (long long)cell * E.kv_dim));
-        vr[ra] = __half_as_ushort(__float2half_rn(yA));
-        if (hasB) vr[rb] = __half_as_ushort(__float2half_rn(yB));
-        break;
-    }
-    case EPI_SWIGLU:
-        out[lu] = silu_f(yA) * yB;
-        break;
-    case EPI_MOE_DOWN:
-        out[lu] = (yA * wa + yB * wb) + rva;
-        break;
-    default: break;
-    }
-}
-
-constexpr int kGemvParamVecs = (int)((sizeof(GemvParams) + 15) / 16);
-
-// The GEMV of one workgroup: workgroup `bid` of P.grid.  NW waves per workgroup, D-deep ring.
-// ROLE (template only, so the roofline kernel has its own symbol): 0 generic, 1 FFN gate/up.
-// DUAL: two activation slots (MoE down).
-template <int T, int D, int NW, int DUAL>
-__device__ __forceinline__ void gemv_body(const float* __restrict__ kx0, const float* __restrict__ knw,
-                                          const int* __restrict__ ktp, int kflags, const GemvParams& Pk,
-                                          u32x4* sparams, const int bid) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    using K = Kq<T>;
-    static_assert(K::LPS == 8, "8 lanes per superblock");
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    // The launch's parameter block (~1 KB of kernarg) is copied to LDS by one
-    // 16-byte vector load per lane: a single memory round trip.  Reading the
-    // fields straight from kernarg compiles to a chain of ~15 dependent scalar
-    // loads (segment lookup, plane bases, ...), each a full memory latency, which
-    // cost 5-10 us per launch before the first weight load was issued.
-    ProRegs pr;
-    pro_load_entry(pr, kx0, knw, ktp, (kflags & 0xFFFFF) >> 8, (kflags >> 20) & 1, (kflags >> 21) & 1, NW, wave,
-                   lane);
-    {
-        const u32x4* src = reinterpret_cast<const u32x4*>(&Pk);
-        for (int i = threadIdx.x; i < kGemvParamVecs; i += NW * 64) sparams[i] = src[i];
-        __syncthreads();
-    }
-    const GemvParams& P = *reinterpret_cast<const GemvParams*>(sparams);
-    const int sbl = lane >> 3, j = lane & 7;
-    const SmemPlan SP = smem_plan(P);
-    const int nb = P.K >> 8;
-    const int cpr = (nb + 7) >> 3;   // chunks per row
-    int e0 = 0, e1 = 0;
-    float w0 = 0.0f, w1 = 0.0f;
-    if (P.sel) {
-        e0 = __builtin_amdgcn_readfirstlane(gptr(P.sel)[0]);
-        e1 = __builtin_amdgcn_readfirstlane(gptr(P.sel)[1]);
-        w0 = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(gptr(P.selw)[0])));
-        w1 = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(gptr(P.selw)[1])));
-    }
-#ifdef MI_STAMPS   // diagnostic build only (scripts/exp_gemv_stamps)
-#define MI_STAMP(k) \
-    if (P.stamps && threadIdx.x == 0) P.stamps[bid * 8 + (k)] = __builtin_amdgcn_s_memrealtime();
-#else
-#define MI_STAMP(k)
-#endif
-    MI_STAMP(0)
-    // P.grid == gridDim.x (set by launch_gemv; reading gridDim costs a hidden-kernarg round trip)
-    const int W = P.grid * NW;
-    int u0, u1, wg_u0, wg_u1, dummy;
-    unit_range(P.total_units, W, bid * NW + wave, u0, u1);
-    unit_range(P.total_units, P.grid, bid, wg_u0, dummy);
-    unit_range(P.total_units, W, bid * NW + NW - 1, dummy, wg_u1);
-    const int n_items = (u1 - u0) * cpr;
-
-    struct Slot { typename K::Ld a, b; };
-    Slot ring[D];
-    // Issue cursor: unit iu, chunk ic and the plane bases of the unit's two rows, kept in
-    // SGPRs.  Moving to the next unit of the same segment is a pointer increment; only a
-    // segment change (or a PAIR_ADJ odd-row tail) re-derives the bases from the LDS copy of
-    // the parameters (a chain of dependent LDS reads, ~0.4 us: far too slow per unit).
-    int iu = u0, ic = 0;
-    const uint8_t* pa[4] = {nullptr, nullptr, nullptr, nullptr};
-    const uint8_t* pb[4] = {nullptr, nullptr, nullptr, nullptr};
-    int fast_end = 0;          // units < fast_end advance by a pointer increment
-    int step_rows = 0;         // rows per unit: 2 (PAIR_ADJ) or 1 (PAIR_AB)
-    auto bases = [&](int u) {
-        const UnitRef c = unit_ref(P, u);
-        const GemvSeg& S = P.seg[c.si];
-        const QMat& MB = S.pair == PAIR_ADJ ? S.A : S.B;
-        const long long ea = S.expA == 0 ? e0 : S.expA == 1 ? e1 : 0;
-        const long long eb = S.expB == 0 ? e0 : S.expB == 1 ? e1 : 0;
-        const long long rb = c.hasB ? c.rb : c.ra;   // odd tail: re-read row A, result unused
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            pa[i] = rfl_ptr(S.A.p[i] + ea * S.A.expert_stride[i] + c.ra * nb * PlaneBytes<T>::b[i]);
-            pb[i] = rfl_ptr(MB.p[i] + eb * MB.expert_stride[i] + rb * nb * PlaneBytes<T>::b[i]);
-        }
-        const int pair = __builtin_amdgcn_readfirstlane(S.pair);
-        const int end = __builtin_amdgcn_readfirstlane(S.unit0 + S.units);
-        const int rows = __builtin_amdgcn_readfirstlane(S.A.rows);
-        step_rows = pair == PAIR_ADJ ? 2 : 1;
-        fast_end = (pair == PAIR_ADJ && (rows & 1)) ? end - 1 : end;   // the odd tail takes the slow path
-    };
-    auto next_unit = [&](int u) {
-        if (u < fast_end) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const long long d = (long long)step_rows * nb * PlaneBytes<T>::b[i];
-                pa[i] += d;
-                pb[i] += d;
-            }
-        } else {
-            bases(u);
-        }
-    };
-    bases(u0 < P.total_units ? u0 : P.total_units - 1);   // idle waves re-read a valid row
-    // Issue the next item (past the end: the last item again, a cache hit).
-    // Past the end of its range a wave keeps issuing (so every ring step issues the same
-    // loads and the compiler's vmcnt bookkeeping stays exact), but "parked": every lane
-    // reads the same 16 bytes of the last row, one request per load instead of 16 lines.
-    int park_sb = -1;          // -1: streaming; else 0 (every lane at offset 0)
-    auto issue = [&](Slot& S) {
-        const int sb = park_sb < 0 ? ic * 8 + sbl : 0;
-        const int jj = park_sb < 0 ? j : 0;
-        S.a = K::load(pa, sb, jj);
-        S.b = K::load(pb, sb, jj);
-        if (iu < u1) {
-            if (++ic == cpr) {
-                ic = 0;
-                if (++iu < u1) next_unit(iu);
-                else { iu = u1; park_sb = 0; }   // park
-            }
-        }
-    };
-
-    // Wait for the prologue loads that needed the parameter block BEFORE issuing the
-    // weight prefill.  Issued together, those requests of late CUs queue behind
-    // every CU's prefill at the memory channels (measured: ~3 us to land); alone
-    // they land in ~1 us and the prologue then computes while the prefill streams.
-    if (pro_load_rest(P, pr, nb, NW, wave, lane, wg_u0, wg_u1)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-    for (int k = 0; k < D - 1; ++k) issue(ring[k]);
-    MI_STAMP(1)
-    const int pos = __builtin_amdgcn_readfirstlane(pr.tp.y);
-    const int cell = __builtin_amdgcn_readfirstlane(pr.tp.z);
-    pro_finish<false>(P, pr, smem, SP, pos, cell + 1, wg_u0, wg_u1, bid);
-    MI_STAMP(7)
-    __syncthreads();
-    MI_STAMP(2)
-    const float* rope = reinterpret_cast<const float*>(smem + SP.rope_off);
-    const float* rs = reinterpret_cast<const float*>(smem + SP.resid_off);
-    const Act a0 = act_view(smem, SP.L, 0);
-    const Act a1 = act_view(smem, SP.L, DUAL ? 1 : 0);
-
-    int cu = u0, cc = 0;
-    float accA = 0.0f, accB = 0.0f;
-    const EpiConst EC = epi_const(P);
-    EpiSeg cseg = epi_seg(P, u0 < P.total_units ? u0 : P.total_units - 1);
-    auto consume = [&](const Slot& S) {
-        const int sb = cc * 8 + sbl;
-        const bool lv = sb < nb;
-        const int sbc = lv ? sb : nb - 1;
-        const typename K::AR arA = K::act(a0, sbc, j);
-        const float pa_ = K::dot(S.a, arA, j);
-        float pb_;
-        if (DUAL) {
-            const typename K::AR arB = K::act(a1, sbc, j);
-            pb_ = K::dot(S.b, arB, j);
-        } else {
-            pb_ = K::dot(S.b, arA, j);
-        }
-        accA += lv ? pa_ : 0.0f;
-        accB += lv ? pb_ : 0.0f;
-        if (++cc == cpr) {
-            const float yA = wave_sum63(accA);
-            const float yB = wave_sum63(accB);
-            if (cu >= cseg.end) cseg = epi_seg(P, cu);   // segment change (rare)
-            if (lane == 63) {
-                const int i = cu - wg_u0;
-                gemv_epilogue(EC, cseg, cu, rope, rs[2 * i], rs[2 * i + 1], w0, w1, pos, cell, yA, yB);
-            }
-            accA = accB = 0.0f;
-            cc = 0;
-            ++cu;
-        }
-    };
-    for (int base = 0; base < n_items; base += D) {
-#pragma unroll
-        for (int k = 0; k < D; ++k) {
-            issue(ring[(k + D - 1) % D]);
-            if (base + k < n_items) consume(ring[k]);
-        }
-        if (base == 0) { MI_STAMP(3) }
-    }
-    MI_STAMP(4)
-#undef MI_STAMP
-}
-
-template <int T, int D, int NW, int DUAL, int ROLE>
-__global__ __launch_bounds__(NW * 64) void gemv_t(const float* __restrict__ kx0, const float* __restrict__ knw,
-                                                   const int* __restrict__ ktp, int kflags, const GemvParams Pk) {
-    __shared__ __attribute__((aligned(16))) u32x4 sparams[kGemvParamVecs];
-    gemv_body<T, D, NW, DUAL>(kx0, knw, ktp, kflags, Pk, sparams, blockIdx.x);
-}
-
-// Two quant types in one launch (the Q/K/V projections of a Q4_K_M / Q5_K_M layer whose
-// attn_v is Q6_K): workgroups [0, P1.grid) run the T1 matrices, the rest the T2 ones, each
-// half with its own unit split.  Saves one launch (its fixed entry/prologue cost) per such
-// layer.  Both halves consume the same activation (Q8_K of the RMS-normed residual).
-template <int T1, int T2, int D, int NW>
-__global__ __launch_bounds__(NW * 64) void gemv_mix_t(const float* __restrict__ kx0, const float* __restrict__ knw,
-                                                       const int* __restrict__ ktp, int kflags, const GemvParams P1,
-                                                       const GemvParams P2) {
-    __shared__ __attribute__((aligned(16))) u32x4 sparams[kGemvParamVecs];
-    const int g1 = P1.grid;
-    if ((int)blockIdx.x < g1) gemv_body<T1, D, NW, 0>(kx0, knw, ktp, kflags, P1, sparams, blockIdx.x);
-    else gemv_body<T2, D, NW, 0>(kx0, knw, ktp, kflags, P2, sparams, blockIdx.x - g1);
-}
-
-// ---------------------------------------------------------------------------
-// The GEMV with its weight stream staged through LDS by LDS-DMA (global_load_lds).
-//
-// gemv_body keeps its in-flight weights in registers: D-1 items per wave, which at the
-// register budget of its prologue is ~50 KB per CU, ~2 us of the CU's share of HBM
-// bandwidth -- less than the prologue (activation arrival, RMSNorm, Q8_K quantisation) takes,
-// so HBM idles until the prologue is done.  Here every wave owns a private ring of D item
-// slots in LDS, filled by global_load_lds: ~110 KB in flight per CU from the moment the
-// prologue starts, no VGPRs held, and no cross-wave synchronisation in the stream (a wave
-// only ever reads the slots it filled itself, so its own vmcnt orders it).
-// An item is one 8-superblock chunk of the unit's two rows, every plane (Rq<T>::ROW bytes a
-// row); the LDS image is lane-linear per plane, so the consumer's reads are the register
-// ring's loads with an LDS base.
-// ---------------------------------------------------------------------------
-// One LDS-DMA of 16 bytes a lane (global_load_lds_dwordx4, non-temporal: decode weights are
-// read once).  Inline asm, not __builtin_amdgcn_global_load_lds: with the builtin, hipcc
-// (ROCm 7.2) tail-merges an exec-masked DMA (the 8-lane header planes) with the full-wave one
-// after it into ONE instruction whose M0 comes from v_readfirstlane of a per-lane select --
-// the wrong LDS base for every lane outside the first (found by the GEMV op tests).  M0 is
-// written and restored inside the statement (it is compiler-reserved); hipcc does not count
-// these loads, the ring's wait_vm() does.
-__device__ __forceinline__ void gl16(const uint8_t* g, char* l) {
-    const unsigned la = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)l;
-    unsigned keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(g), "s"(la) : "memory");
-}
-// s_waitcnt vmcnt(N) and nothing else (expcnt 7, lgkmcnt 15 = no wait)
-template <int N>
-__device__ __forceinline__ void wait_vm() {
-    static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
-    __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
-}
-// workgroup barrier that leaves LDS-DMA in flight: this wave's LDS accesses complete (the
-// data other waves read after the barrier), then s_barrier; __syncthreads() would also wait
-// vmcnt(0), draining every wave's ring.
-__device__ __forceinline__ void lds_barrier() {
-    __builtin_amdgcn_s_waitcnt((0xF) | (0x3 << 14) | (0x7 << 4) | (0x0 << 8));   // lgkmcnt(0)
-    __builtin_amdgcn_s_barrier();
-}
-
-template <int T> struct Rq;
-template <> struct Rq<T_Q4_K> {   // qs 8x128 | hdr 8x16
-    static constexpr int ROW = 1152, G = 2;
-    __device__ static int glds(const uint8_t* const* rp, int sb0, char* d, int lane) {
-        gl16(rp[0] + sb0 * 128 + lane * 16, d);
-        if (lane < 8) gl16(rp[1] + (sb0 + lane) * 16, d + 1024);
-        return 0;
-    }
-    __device__ static Kq<T_Q4_K>::Ld lds(const char* s, int sbl, int j, int) {
-        Kq<T_Q4_K>::Ld l;
-        l.qs = *reinterpret_cast<const u32x4*>(s + sbl * 128 + j * 16);
-        l.hdr = *reinterpret_cast<const u32x4*>(s + 1024 + sbl * 16);
-        return l;
-    }
-};
-template <> struct Rq<T_Q5_K> {   // qs 8x128 | qh 8x32 | hdr 8x16
-    static constexpr int ROW = 1408, G = 3;
-    __device__ static int glds(const uint8_t* const* rp, int sb0, char* d, int lane) {
-        gl16(rp[0] + sb0 * 128 + lane * 16, d);
-        if (lane < 16) gl16(rp[1] + sb0 * 32 + lane * 16, d + 1024);
-        if (lane < 8) gl16(rp[2] + (sb0 + lane) * 16, d + 1280);
-        return 0;
-    }
-    __device__ static Kq<T_Q5_K>::Ld lds(const char* s, int sbl, int j, int) {
-        Kq<T_Q5_K>::Ld l;
-        l.qs = *reinterpret_cast<const u32x4*>(s + sbl * 128 + j * 16);
-        l.qh = *reinterpret_cast<const u32x4*>(s + 1024 + sbl * 32 + (j & 1) * 16);
-        l.hdr = *reinterpret_cast<const u32x4*>(s + 1280 + sbl * 16);
-        return l;
-    }
-};
-template <> struct Rq<T_Q6_K> {   // ql 8x128 | qh 8x64 | scales 8x16 | d: 32 B holding 8x2
-    static constexpr int ROW = 1696, G = 4;
-    // The d plane has 2 bytes a superblock, so a chunk's 16 bytes need not be 16-B aligned: two
-    // lanes fetch the 32 aligned bytes around them; returns the chunk's offset within those.
-    __device__ static int glds(const uint8_t* const* rp, int sb0, char* d, int lane) {
-        gl16(rp[0] + sb0 * 128 + lane * 16, d);
-        if (lane < 32) gl16(rp[1] + sb0 * 64 + lane * 16, d + 1024);
-        if (lane < 8) gl16(rp[2] + (sb0 + lane) * 16, d + 1536);
-        const uint8_t* dp = rp[3] + sb0 * 2;
-        const uint8_t* da = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(dp) & ~(uintptr_t)15);
-        if (lane < 2) gl16(da + lane * 16, d + 1664);
-        return (int)(dp - da);
-    }
-    __device__ static Kq<T_Q6_K>::Ld lds(const char* s, int sbl, int j, int doff) {
-        typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-        Kq<T_Q6_K>::Ld l;
-        const int h = j >> 2, half = j & 1;
-        l.ql = *reinterpret_cast<const u32x4*>(s + sbl * 128 + j * 16);
-        l.qh = *reinterpret_cast<const u32x4*>(s + 1024 + sbl * 64 + 32 * h + 16 * half);
-        const u32x2 sc = *reinterpret_cast<const u32x2*>(s + 1536 + sbl * 16 + h * 8);
-        l.sc0 = sc.x;
-        l.sc1 = sc.y;
-        l.d = *reinterpret_cast<const unsigned short*>(s + 1664 + doff + sbl * 2);
-        return l;
-    }
-};
-template <> struct Rq<T_Q8_0> {   // qs 8x256 | d 8x16
-    static constexpr int ROW = 2176, G = 3;
-    __device__ static int glds(const uint8_t* const* rp, int sb0, char* d, int lane) {
-        gl16(rp[0] + sb0 * 256 + lane * 16, d);
-        gl16(rp[0] + sb0 * 256 + 1024 + lane * 16, d + 1024);
-        if (lane < 8) gl16(rp[1] + (sb0 + lane) * 16, d + 2048);
-        return 0;
-    }
-    __device__ static Kq<T_Q8_0>::Ld lds(const char* s, int sbl, int j, int) {
-        Kq<T_Q8_0>::Ld l;
-        l.q0 = *reinterpret_cast<const u32x4*>(s + sbl * 256 + j * 32);
-        l.q1 = *reinterpret_cast<const u32x4*>(s + sbl * 256 + j * 32 + 16);
-        l.d = *reinterpret_cast<const unsigned short*>(s + 2048 + sbl * 16 + j * 2);
-        return l;
-    }
-};
-
-// LDS ring depth per type at 8 waves (ring = 8 x D x 2 x ROW bytes, ~105-113 KB)
-template <int T> struct RingD;
-template <> struct RingD<T_Q4_K> { static constexpr int D = 6; };
-template <> struct RingD<T_Q5_K> { static constexpr int D = 5; };
-template <> struct RingD<T_Q6_K> { static constexpr int D = 4; };
-template <> struct RingD<T_Q8_0> { static constexpr int D = 3; };
-constexpr int RING_NW = 8;
-__host__ __device__ inline int ring_bytes(int t) {
-    switch (t) {
-    case T_Q4_K: return RING_NW * 6 * 2 * 1152;
-    case T_Q5_K: return RING_NW * 5 * 2 * 1408;
-    case T_Q6_K: return RING_NW * 4 * 2 * 1696;
-    case T_Q8_0: return RING_NW * 3 * 2 * 2176;
-    default: return 0;
-    }
-}
-
-template <int T, int DUAL>
-__device__ __forceinline__ void gemv_ring_body(const float* __restrict__ kx0, const float* __restrict__ knw,
-                                               const int* __restrict__ ktp, int kflags, const GemvParams& Pk,
-                                               u32x4* sparams, const int bid) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    using K = Kq<T>;
-    using RQ = Rq<T>;
-    constexpr int NW = RING_NW, D = RingD<T>::D, ITEM = 2 * RQ::ROW, GI = 2 * RQ::G;
-    static_assert((D - 1) * GI < 64, "in-flight LDS-DMA count must fit vmcnt");
-    static_assert(D <= 8, "8 bits of slot offsets per slot in 64");
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    ProRegs pr;
-    pro_load_entry(pr, kx0, knw, ktp, (kflags & 0xFFFFF) >> 8, (kflags >> 20) & 1, (kflags >> 21) & 1, NW, wave,
-                   lane);
-    {
-        const u32x4* src = reinterpret_cast<const u32x4*>(&Pk);
-        for (int i = threadIdx.x; i < kGemvParamVecs; i += NW * 64) sparams[i] = src[i];
-        __syncthreads();   // no LDS-DMA in flight yet: waits for the parameters (and x) only
-    }
-    const GemvParams& P = *reinterpret_cast<const GemvParams*>(sparams);
-#ifdef MI_STAMPS   // diagnostic build only (scripts/timeline.py)
-#define MI_STAMP(k) \
-    if (P.stamps && threadIdx.x == 0) P.stamps[bid * 8 + (k)] = __builtin_amdgcn_s_memrealtime();
-#else
-#define MI_STAMP(k)
-#endif
-    MI_STAMP(0)
-    const int sbl = lane >> 3, j = lane & 7;
-    const SmemPlan SP = smem_plan(P);
-    char* const ring = smem + ((SP.total + 15) & ~15) + wave * (D * ITEM);
-    const int nb = P.K >> 8;
-    const int cpr = (nb + 7) >> 3;   // chunks per row
-    int e0 = 0, e1 = 0;
-    float w0 = 0.0f, w1 = 0.0f;
-    if (P.sel) {
-        e0 = __builtin_amdgcn_readfirstlane(gptr(P.sel)[0]);
-        e1 = __builtin_amdgcn_readfirstlane(gptr(P.sel)[1]);
-        w0 = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(gptr(P.selw)[0])));
-        w1 = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(gptr(P.selw)[1])));
-    }
-    const int W = P.grid * NW;
-    int u0, u1, wg_u0, wg_u1, dummy;
-    unit_range(P.total_units, W, bid * NW + wave, u0, u1);
-    unit_range(P.total_units, P.grid, bid, wg_u0, dummy);
-    unit_range(P.total_units, W, bid * NW + NW - 1, dummy, wg_u1);
-    const int n_items = (u1 - u0) * cpr;
-
-    int iu = u0, ic = 0, islot = 0;
-    unsigned long long doffs = 0;   // per ring slot: the A and B rows' Rq::glds offsets (4 bits each)
-    const uint8_t* pa[4] = {nullptr, nullptr, nullptr, nullptr};
-    const uint8_t* pb[4] = {nullptr, nullptr, nullptr, nullptr};
-    int fast_end = 0, step_rows = 0;
-    auto bases = [&](int u) {
-        const UnitRef c = unit_ref(P, u);
-        const GemvSeg& S = P.seg[c.si];
-        const QMat& MB = S.pair == PAIR_ADJ ? S.A : S.B;
-        const long long ea = S.expA == 0 ? e0 : S.expA == 1 ? e1 : 0;
-        const long long eb = S.expB == 0 ? e0 : S.expB == 1 ? e1 : 0;
-        const long long rb = c.hasB ? c.rb : c.ra;   // odd tail: re-read row A, result unused
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            pa[i] = rfl_ptr(S.A.p[i] + ea * S.A.expert_stride[i] + c.ra * nb * PlaneBytes<T>::b[i]);
-            pb[i] = rfl_ptr(MB.p[i] + eb * MB.expert_stride[i] + rb * nb * PlaneBytes<T>::b[i]);
-        }
-        const int pair = __builtin_amdgcn_readfirstlane(S.pair);
-        const int end = __builtin_amdgcn_readfirstlane(S.unit0 + S.units);
-        const int rows = __builtin_amdgcn_readfirstlane(S.A.rows);
-        step_rows = pair == PAIR_ADJ ? 2 : 1;
-        fast_end = (pair == PAIR_ADJ && (rows & 1)) ? end - 1 : end;
-    };
-    auto next_unit = [&](int u) {
-        if (u < fast_end) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const long long d = (long long)step_rows * nb * PlaneBytes<T>::b[i];
-                pa[i] += d;
-                pb[i] += d;
-            }
-        } else {
-            bases(u);
-        }
-    };
-    bases(u0 < P.total_units ? u0 : P.total_units - 1);
-    // Issue the next item into the next ring slot.  Past the end of its range a wave keeps
-    // issuing the last item again (cache hits into a free slot), so every step issues exactly
-    // GI LDS-DMA instructions and the counted vmcnt waits stay exact.
-    auto issue = [&]() {
-        char* slot = ring + islot * ITEM;
-        const unsigned oa = (unsigned)RQ::glds(pa, ic * 8, slot, lane);
-        const unsigned ob = (unsigned)RQ::glds(pb, ic * 8, slot + RQ::ROW, lane);
-        doffs = (doffs & ~(0xFFull << (8 * islot))) | ((unsigned long long)(oa | (ob << 4)) << (8 * islot));
-        islot = islot + 1 == D ? 0 : islot + 1;
-        if (iu < u1) {
-            if (++ic == cpr) {
-                if (iu + 1 < u1) {
-                    ic = 0;
-                    ++iu;
-                    next_unit(iu);
-                } else {
-                    ic = cpr - 1;   // park on the last item
-                    iu = u1;
-                }
-            }
-        }
-    };
-    pro_load_rest(P, pr, nb, NW, wave, lane, wg_u0, wg_u1);
-    // Every ordinary load the prologue consumes has landed before the first LDS-DMA: hipcc does
-    // not count the asm DMAs, so a wait it placed later for one of those loads would count
-    // them as younger loads and drain the ring's prefill.  The builtin (not asm) tells hipcc.
-    wait_vm<0>();
-#pragma unroll
-    for (int k = 0; k < D - 1; ++k) issue();
-    MI_STAMP(1)
-    const int pos = __builtin_amdgcn_readfirstlane(pr.tp.y);
-    const int cell = __builtin_amdgcn_readfirstlane(pr.tp.z);
-    pro_finish<true>(P, pr, smem, SP, pos, cell + 1, wg_u0, wg_u1, bid);
-    MI_STAMP(7)
-    lds_barrier();
-    MI_STAMP(2)
-    const float* rope = reinterpret_cast<const float*>(smem + SP.rope_off);
-    const float* rs = reinterpret_cast<const float*>(smem + SP.resid_off);
-    const Act a0 = act_view(smem, SP.L, 0);
-    const Act a1 = act_view(smem, SP.L, DUAL ? 1 : 0);
-
-    int cu = u0, cc = 0, cslot = 0;
-    float accA = 0.0f, accB = 0.0f;
-    const EpiConst EC = epi_const(P);
-    EpiSeg cseg = epi_seg(P, u0 < P.total_units ? u0 : P.total_units - 1);
-    for (int it = 0; it < n_items; ++it) {
-        issue();
-        wait_vm<(D - 1) * GI>();   // this item's GI transfers have landed (D-1 items stay in flight)
-        const char* slot = ring + cslot * ITEM;
-        const unsigned off = (unsigned)(doffs >> (8 * cslot)) & 0xFFu;
-        cslot = cslot + 1 == D ? 0 : cslot + 1;
-        const typename K::Ld la = RQ::lds(slot, sbl, j, (int)(off & 0xF));
-        const typename K::Ld lb = RQ::lds(slot + RQ::ROW, sbl, j, (int)(off >> 4));
-        const int sb = cc * 8 + sbl;
-        const bool lv = sb < nb;
-        const int sbc = lv ? sb : nb - 1;
-        const typename K::AR arA = K::act(a0, sbc, j);
-        const float pa_ = K::dot(la, arA, j);
-        float pb_;
-        if (DUAL) {
-            const typename K::AR arB = K::act(a1, sbc, j);
-            pb_ = K::dot(lb, arB, j);
-        } else {
-            pb_ = K::dot(lb, arA, j);
-        }
-        accA += lv ? pa_ : 0.0f;
-        accB += lv ? pb_ : 0.0f;
-        if (++cc == cpr) {
-            const float yA = wave_sum63(accA);
-            const float yB = wave_sum63(accB);
-            if (cu >= cseg.end) cseg = epi_seg(P, cu);   // segment change (rare)
-            if (lane == 63) {
-                const int i = cu - wg_u0;
-                gemv_epilogue(EC, cseg, cu, rope, rs[2 * i], rs[2 * i + 1], w0, w1, pos, cell, yA, yB);
-            }
-            accA = accB = 0.0f;
-            cc = 0;
-            ++cu;
-        }
-        if (it == 0) { MI_STAMP(3) }
-    }
-    MI_STAMP(4)
-    wait_vm<0>();   // the parked transfers land before the wave (and its LDS) retires
-#undef MI_STAMP
-}
-
-template <int T, int DUAL, int ROLE>
-__global__ __launch_bounds__(RING_NW * 64) void gemv_r(const float* __restrict__ kx0, const float* __restrict__ knw,
-                                                        const int* __restrict__ ktp, int kflags, const GemvParams Pk) {
-    __shared__ __attribute__((aligned(16))) u32x4 sparams[kGemvParamVecs];
-    gemv_ring_body<T, DUAL>(kx0, knw, ktp, kflags, Pk, sparams, blockIdx.x);
-}
-
-template <int T1, int T2>
-__global__ __launch_bounds__(RING_NW * 64) void gemv_r_mix(const float* __restrict__ kx0, const float* __restrict__ knw,
-                                                            const int* __restrict__ ktp, int kflags, const GemvParams P1,
-                                                            const GemvParams P2) {
-    __shared__ __attribute__((aligned(16))) u32x4 sparams[kGemvParamVecs];
-    if ((int)blockIdx.x < P1.grid) gemv_ring_body<T1, 0>(kx0, knw, ktp, kflags, P1, sparams, blockIdx.x);
-    else gemv_ring_body<T2, 0>(kx0, knw, ktp, kflags, P2, sparams, blockIdx.x - P1.grid);
-}
-
-// ---------------------------------------------------------------------------
-// The K-split GEMV (gemv_k): the decode GEMV without a workgroup-wide prologue.
-//
-// gemv_body / gemv_ring_body quantise the whole activation into LDS before any wave can
-// consume a weight: x arrives, RMSNorm (a workgroup reduction), Q8_K of every block, a
-// barrier -- 4-6 us per launch during which the weight stream is throttled (the stamp
-// timelines of profiles/r02_timeline_*.txt).  Here the waves of a workgroup split K instead:
-// G = ceil(K/2048) groups of m waves; group g streams superblocks [8g, 8g+8) of every unit the
-// workgroup owns, so each lane needs the activation of ONE 32-element slice only, for the
-// whole launch.  Every wave builds that slice itself, in registers:
-//   RMSNorm   each wave sums the squares of the full x (the same double sum in every wave, so
-//             every wave gets the bit-identical scale) -- no barrier;
-//   Q8_K      the 8 lanes of a superblock reduce its amax (and the sign of its first
-//             maximal element, ggml's tie rule) by DPP; each lane quantises its own 32 values
-//             and forms its own two 16-element bsums, exactly as quantize_row_q8_K_ref;
-//   Q8_0      a lane owns a whole 32-block (quantize_row_q8_0's x86 form), no reduction.
-// The weight ring is issued right after the parameter block arrives and the slice math runs
-// while it is in flight.  A unit's G chunk partials meet in LDS and are added in chunk order
-// (deterministic) by the epilogue threads after one barrier at the end.
-// ---------------------------------------------------------------------------
-template <int T> struct KAct;
-// Q8_K element positions of lane j within its superblock (Kq<T>::act's slices): two runs of 16
-__device__ __forceinline__ int kpos_lo_q45(int j) { return 64 * (j >> 1) + 16 * (j & 1); }
-__device__ __forceinline__ int kpos_lo_q6(int j) { return 128 * (j >> 2) + 32 * ((j >> 1) & 1) + 16 * (j & 1); }
-
-// max over the 8 lanes of a lane group (lanes 8k..8k+7), every lane gets it
-__device__ __forceinline__ float max8(float v) {
-    v = fmaxf(v, __int_as_float(dpp_i<0xB1, 0xf>(__float_as_int(v))));   // quad_perm [1,0,3,2]
-    v = fmaxf(v, __int_as_float(dpp_i<0x4E, 0xf>(__float_as_int(v))));   // quad_perm [2,3,0,1]
-    v = fmaxf(v, __int_as_float(dpp_i<0x141, 0xf>(__float_as_int(v))));  // row_half_mirror
-    return v;
-}
-__device__ __forceinline__ int min8(int v) {
-    v = min(v, dpp_i<0xB1, 0xf>(v));
-    v = min(v, dpp_i<0x4E, 0xf>(v));
-    v = min(v, dpp_i<0x141, 0xf>(v));
-    return v;
-}
-
-// quantize_row_q8_K_ref on one 256-block held as 32 values per lane by 8 lanes: lo[16] are
-// elements plo..plo+15 and hi[16] elements phi..phi+15 (plo < phi).  Returns this lane's
-// packed int8 values and bsums, and the block's d.
-__device__ __forceinline__ void q8k_slice(const float lo[16], const float hi[16], int plo, int phi, i32x4& alo,
-                                          i32x4& ahi, int& bs_lo, int& bs_hi, float& dx) {
-    float am = 0.0f;
-#pragma unroll
-    for (int e = 0; e < 16; ++e) am = fmaxf(am, fmaxf(fabsf(lo[e]), fabsf(hi[e])));
-    const float amax = max8(am);
-    int q[32];
-    if (amax == 0.0f) {
-#pragma unroll
-        for (int e = 0; e < 32; ++e) q[e] = 0;
-        dx = 0.0f;
-    } else {
-        // the signed value at the FIRST index whose |x| is the maximum: key = 2*index + sign
-        int key = 1 << 20;
-#pragma unroll
-        for (int e = 15; e >= 0; --e)
-            if (fabsf(hi[e]) == amax) key = 2 * (phi + e) + (hi[e] < 0.0f ? 1 : 0);
-#pragma unroll
-        for (int e = 15; e >= 0; --e)
-            if (fabsf(lo[e]) == amax) key = 2 * (plo + e) + (lo[e] < 0.0f ? 1 : 0);
-        key = min8(key);
-        const float mx = (key & 1) ? -amax : amax;
-        const float iscale = -127.0f / mx;
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-            q[e] = min(127, (int)rintf(iscale * lo[e]));
-            q[16 + e] = min(127, (int)rintf(iscale * hi[e]));
-        }
-        dx = 1.0f / iscale;
-    }
-    int sl = 0, sh = 0;
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-        sl += q[e];
-        sh += q[16 + e];
-    }
-    bs_lo = sl;
-    bs_hi = sh;
-    int pk[8];
-#pragma unroll
-    for (int w = 0; w < 8; ++w)
-        pk[w] = (q[4 * w] & 0xFF) | ((q[4 * w + 1] & 0xFF) << 8) | ((q[4 * w + 2] & 0xFF) << 16) | ((q[4 * w + 3] & 0xFF) << 24);
-    alo = i32x4{pk[0], pk[1], pk[2], pk[3]};
-    ahi = i32x4{pk[4], pk[5], pk[6], pk[7]};
-}
-
-template <> struct KAct<T_Q4_K> {
-    __device__ static void pos(int j, int& lo, int& hi) { lo = kpos_lo_q45(j); hi = lo + 32; }
-    __device__ static Kq<T_Q4_K>::AR quant(const float lo[16], const float hi[16], int j) {
-        int plo, phi;
-        pos(j, plo, phi);
-        Kq<T_Q4_K>::AR r;
-        q8k_slice(lo, hi, plo, phi, r.alo, r.ahi, r.bs_lo, r.bs_hi, r.dx);
-        return r;
-    }
-};
-template <> struct KAct<T_Q5_K> {
-    __device__ static void pos(int j, int& lo, int& hi) { KAct<T_Q4_K>::pos(j, lo, hi); }
-    __device__ static Kq<T_Q5_K>::AR quant(const float lo[16], const float hi[16], int j) {
-        return KAct<T_Q4_K>::quant(lo, hi, j);
-    }
-};
-template <> struct KAct<T_Q6_K> {
-    __device__ static void pos(int j, int& lo, int& hi) { lo = kpos_lo_q6(j); hi = lo + 64; }
-    __device__ static Kq<T_Q6_K>::AR quant(const float lo[16], const float hi[16], int j) {
-        int plo, phi;
-        pos(j, plo, phi);
-        Kq<T_Q6_K>::AR r;
-        q8k_slice(lo, hi, plo, phi, r.alo, r.ahi, r.bs_lo, r.bs_hi, r.dx);
-        return r;
-    }
-};
-template <> struct KAct<T_Q8_0> {   // lane j: elements 32j..32j+31 = one Q8_0 block
-    __device__ static void pos(int j, int& lo, int& hi) { lo = 32 * j; hi = lo + 16; }
-    __device__ static Kq<T_Q8_0>::AR quant(const float lo[16], const float hi[16], int) {
-        float am = 0.0f;
-#pragma unroll
-        for (int e = 0; e < 16; ++e) am = fmaxf(am, fmaxf(fabsf(lo[e]), fabsf(hi[e])));
-        const float d = am / 127.0f;
-        const float id = am != 0.0f ? 127.0f / am : 0.0f;
-        int pk[8];
-#pragma unroll
-        for (int w = 0; w < 8; ++w) {
-            const float* src = w < 4 ? lo + 4 * w : hi + 4 * (w - 4);
-            int q0 = (int)rintf(src[0] * id), q1 = (int)rintf(src[1] * id), q2 = (int)rintf(src[2] * id),
-                q3 = (int)rintf(src[3] * id);
-            pk[w] = (q0 & 0xFF) | ((q1 & 0xFF) << 8) | ((q2 & 0xFF) << 16) | ((q3 & 0xFF) << 24);
-        }
-        Kq<T_Q8_0>::AR r;
-        r.a0 = i32x4{pk[0], pk[1], pk[2], pk[3]};
-        r.a1 = i32x4{pk[4], pk[5], pk[6], pk[7]};
-        r.d0 = __half2float(__float2half_rn(d));
-        return r;
-    }
-};
-
-// K-split geometry: G chunk groups of m waves, NW = G*m <= 8 (two waves a SIMD: the
-// prologue's x slices and the ring need the 256-VGPR budget)
-__host__ __device__ inline int gemv_k_groups(int K) { return (K / 256 + 7) / 8; }
-__host__ __device__ inline int gemv_k_waves(int K) {
-    const int G = gemv_k_groups(K);
-    return G * (8 / G);
-}
-template <int T> struct KRingD { static constexpr int D = 4; };   // register ring depth
-
-// LDS: [params copy (static)] [rope table | resid | partials[wg_units][G] float2]
-struct KPlan { int rope_off, resid_off, part_off, total; };
-__host__ __device__ inline KPlan kplan(const GemvParams& p) {
-    KPlan k;
-    k.rope_off = 0;
-    k.resid_off = ((p.n_rot / 2) * 8 + 15) / 16 * 16;
-    k.part_off = k.resid_off + ((p.wg_units * 2 * 4 + 15) / 16) * 16;
-    k.total = k.part_off + p.wg_units * gemv_k_groups(p.K) * 8;
-    k.total = (k.total + 15) & ~15;   // then [16] doubles of RMSNorm shares (the kernel's red[])
-    return k;
-}
-
-__device__ __forceinline__ void k_load_slice(const float* __restrict__ p, int e0, int e1, float lo[16], float hi[16]) {
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-        const f32x4 a = *gptr(reinterpret_cast<const f32x4*>(p + e0) + v);
-        const f32x4 b = *gptr(reinterpret_cast<const f32x4*>(p + e1) + v);
-        lo[4 * v] = a.x; lo[4 * v + 1] = a.y; lo[4 * v + 2] = a.z; lo[4 * v + 3] = a.w;
-        hi[4 * v] = b.x; hi[4 * v + 1] = b.y; hi[4 * v + 2] = b.z; hi[4 * v + 3] = b.w;
-    }
-}
-
-// This wave's share of ggml_compute_forward_rms_norm_f32's sum of squares: float4 i of x for
-// i = lane + 64*(wave + NW*r); KX_PART float4 a lane are loaded at kernel entry (K <= 8192 at 8
-// waves), the rest (larger K) after.  The shares meet in LDS in wave order.
-constexpr int KX_PART = 4;
-
-// kflags: K (bits 0-19) | RMSNorm prologue (21) | attention-combine prologue (22); for the
-// attention prologue kx0 is split 0 of the attention partials.
-template <int T, int D, int DUAL>
-__device__ __forceinline__ void gemv_k_body(const float* __restrict__ kx0, const float* __restrict__ knw,
-                                            const int* __restrict__ ktp, int kflags, const GemvParams& Pk,
-                                            u32x4* sparams, const int bid) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    using K = Kq<T>;
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int NW = blockDim.x >> 6;
-    const int Kdim = kflags & 0xFFFFF;
-    const int nb = Kdim >> 8;
-    const int G = (nb + 7) >> 3;
-    const int m = NW / G;
-    const int g = wave / m, wk = wave - g * m;
-    const int sbl = lane >> 3, j = lane & 7;
-    const int sb = 8 * g + sbl;
-    const bool lv = sb < nb;
-    const bool rms = (kflags >> 21) & 1;
-    const bool attn_pro = (kflags >> 22) & 1;
-    int plo, phi;
-    KAct<T>::pos(j, plo, phi);
-    const int xe0 = (lv ? sb : 0) * 256 + plo, xe1 = (lv ? sb : 0) * 256 + phi;
-    // ---- entry: loads that need only the direct arguments (this lane's activation slice of
-    // slot 0, its norm weights, this wave's share of the RMSNorm sum, the token position) and
-    // the parameter block: one round trip for all of them
-    float xlo[16], xhi[16], wlo[16], whi[16];
-    k_load_slice(kx0, xe0, xe1, xlo, xhi);
-    if (rms) k_load_slice(knw, xe0, xe1, wlo, whi);
-    f32x4 xr[KX_PART];
-    const int n4 = Kdim / 4;
-    if (rms) {
-        const auto x4 = gptr(reinterpret_cast<const f32x4*>(kx0));
-#pragma unroll
-        for (int r = 0; r < KX_PART; ++r) {
-            const int i = lane + 64 * (wave + NW * r);
-            xr[r] = i < n4 ? x4[i] : f32x4{0.f, 0.f, 0.f, 0.f};
-        }
-    }
-    const i32x4 tp = ktp ? *gptr(reinterpret_cast<const i32x4*>(ktp)) : i32x4{0, 0, 0, 0};
-    {
-        const u32x4* src = reinterpret_cast<const u32x4*>(&Pk);
-        for (int i = threadIdx.x; i < kGemvParamVecs; i += blockDim.x) sparams[i] = src[i];
-        __syncthreads();
-    }
-    const GemvParams& P = *reinterpret_cast<const GemvParams*>(sparams);
-#ifdef MI_STAMPS   // diagnostic build only (scripts/timeline.py)
-#define MI_STAMP(k) \
-    if (P.stamps && threadIdx.x == 0) P.stamps[bid * 8 + (k)] = __builtin_amdgcn_s_memrealtime();
-#else
-#define MI_STAMP(k)
-#endif
-    MI_STAMP(0)
-    const KPlan KP = kplan(P);
-    double* red = reinterpret_cast<double*>(smem + KP.total);   // [NW] RMSNorm shares
-    int e0 = 0, e1 = 0;
-    float w0 = 0.0f, w1 = 0.0f;
-    if (P.sel) {   // MoE: the experts decide the weight addresses
-        e0 = __builtin_amdgcn_readfirstlane(gptr(P.sel)[0]);
-        e1 = __builtin_amdgcn_readfirstlane(gptr(P.sel)[1]);
-        w0 = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(gptr(P.selw)[0])));
-        w1 = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(gptr(P.selw)[1])));
-    }
-    int wg_u0, wg_u1;
-    unit_range(P.total_units, P.grid, bid, wg_u0, wg_u1);
-    const int nwu = wg_u1 - wg_u0;
-    const int u0 = wg_u0 + (int)(((unsigned)nwu * (unsigned)wk) / (unsigned)m);
-    const int u1 = wg_u0 + (int)(((unsigned)nwu * (unsigned)(wk + 1)) / (unsigned)m);
-    const int n_items = u1 - u0;
-    // attention splits past the first (contexts over ATTN_SHORT cells): added in split order
-    // before the prefetch -- a load issued behind it would wait for all of it
-    if (attn_pro) {
-        int chunk_, nsplit;
-        attn_split(__builtin_amdgcn_readfirstlane(tp.z) + 1, chunk_, nsplit);
-        const AttnPartials& A = P.attn;
-        for (int s = 1; s < nsplit; ++s) {
-            float lo[16], hi[16];
-            k_load_slice(A.o + (long long)s * A.n_head * A.head_dim, xe0, xe1, lo, hi);
-#pragma unroll
-            for (int e = 0; e < 16; ++e) {
-                xlo[e] += lo[e];
-                xhi[e] += hi[e];
-            }
-        }
-    }
-    // the other inputs of the prologue, issued before the prefetch, consumed after it
-    float ylo[16], yhi[16];
-    if (DUAL) k_load_slice(P.x[1], xe0, xe1, ylo, yhi);
-    const bool rope_wave = P.n_rot > 0 && wave == NW - 1;
-    float ff0 = 1.0f, ff1 = 1.0f;
-    if (rope_wave && P.freq_factors) {
-        if (lane < P.n_rot / 2) ff0 = gptr(P.freq_factors)[lane];
-        if (lane + 64 < P.n_rot / 2) ff1 = gptr(P.freq_factors)[lane + 64];
-    }
-
-    // ---- the weight prefetch
-    struct Slot { typename K::Ld a, b; };
-    Slot ring[D];
-    int iu = u0;
-    const uint8_t* pa[4] = {nullptr, nullptr, nullptr, nullptr};
-    const uint8_t* pb[4] = {nullptr, nullptr, nullptr, nullptr};
-    int fast_end = 0, step_rows = 0;
-    auto bases = [&](int u) {
-        const UnitRef c = unit_ref(P, u);
-        const GemvSeg& S = P.seg[c.si];
-        const QMat& MB = S.pair == PAIR_ADJ ? S.A : S.B;
-        const long long ea = S.expA == 0 ? e0 : S.expA == 1 ? e1 : 0;
-        const long long eb = S.expB == 0 ? e0 : S.expB == 1 ? e1 : 0;
-        const long long rb = c.hasB ? c.rb : c.ra;   // odd tail: re-read row A, result unused
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            pa[i] = rfl_ptr(S.A.p[i] + ea * S.A.expert_stride[i] + c.ra * nb * PlaneBytes<T>::b[i]);
-            pb[i] = rfl_ptr(MB.p[i] + eb * MB.expert_stride[i] + rb * nb * PlaneBytes<T>::b[i]);
-        }
-        const int pair = __builtin_amdgcn_readfirstlane(S.pair);
-        const int end = __builtin_amdgcn_readfirstlane(S.unit0 + S.units);
-        const int rows = __builtin_amdgcn_readfirstlane(S.A.rows);
-        step_rows = pair == PAIR_ADJ ? 2 : 1;
-        fast_end = (pair == PAIR_ADJ && (rows & 1)) ? end - 1 : end;
-    };
-    auto next_unit = [&](int u) {
-        if (u < fast_end) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const long long d = (long long)step_rows * nb * PlaneBytes<T>::b[i];
-                pa[i] += d;
-                pb[i] += d;
-            }
-        } else {
-            bases(u);
-        }
-    };
-    bases(u0 < P.total_units ? u0 : P.total_units - 1);
-    // past the end of its range a wave re-issues its last item (cache hits) so every ring step
-    // issues the same loads and hipcc's vmcnt bookkeeping stays exact
-    const int sbi = lv ? sb : nb - 1;
-    auto issue = [&](Slot& S) {
-        S.a = K::load(pa, sbi, j);
-        S.b = K::load(pb, sbi, j);
-        if (iu + 1 < u1) next_unit(++iu);
-    };
-#pragma unroll
-    for (int k = 0; k < D - 1; ++k) issue(ring[k]);
-    MI_STAMP(1)
-    // this wave's RMSNorm share: its x loads were issued at entry, before the ring, so waiting
-    // for them here does not wait for the weights (loads retire in order); doing this before the
-    // ring issue held the first weight loads back by one x round trip (r02 stamps: 1.2-2.8 us)
-    if (rms) {
-        double sacc = 0.0;
-#pragma unroll
-        for (int r = 0; r < KX_PART; ++r) {
-            const f32x4 v = xr[r];
-            sacc += (double)(v.x * v.x);
-            sacc += (double)(v.y * v.y);
-            sacc += (double)(v.z * v.z);
-            sacc += (double)(v.w * v.w);
-        }
-        sacc = wave_sum63_d(sacc);
-        if (lane == 63) red[wave] = sacc;
-    }
-    // residual values of this workgroup's units: needed only by the epilogue threads
-    float ra = 0.0f, rbv = 0.0f;
-    const bool has_resid = P.seg[0].resid && (int)threadIdx.x < nwu;
-    if (has_resid) {
-        const GemvSeg& S0 = P.seg[0];
-        const long long lu = wg_u0 + threadIdx.x;
-        if (S0.pair == PAIR_ADJ) {
-            ra = gptr(S0.resid)[2 * lu];
-            rbv = gptr(S0.resid)[2 * lu + 1 < S0.A.rows ? 2 * lu + 1 : 2 * lu];
-        } else {
-            ra = gptr(S0.resid)[lu];
-            rbv = gptr(S0.resid)[lu];
-        }
-    }
-    // ---- the activation slice, while the prefetch is in flight
-    typename K::AR arA, arB;
-    {
-        if (rms) {
-            __syncthreads();   // every wave's RMSNorm share is in LDS (loads stay in flight)
-            double tot = 0.0;
-            for (int w = 0; w < NW; ++w) tot += red[w];
-            if (n4 > 64 * NW * KX_PART) {   // K > 8192 at 8 waves: the rest of the sum (rare)
-                const auto x4 = gptr(reinterpret_cast<const f32x4*>(kx0));
-                double sacc = 0.0;
-                for (int i = lane + 64 * NW * KX_PART; i < n4; i += 64) {
-                    const f32x4 v = x4[i];
-                    sacc += (double)(v.x * v.x);
-                    sacc += (double)(v.y * v.y);
-                    sacc += (double)(v.z * v.z);
-                    sacc += (double)(v.w * v.w);
-                }
-                sacc = wave_sum63_d(sacc);
-                const long long b = __double_as_longlong(sacc);
-                const int lo = __builtin_amdgcn_readlane((int)b, 63), hi = __builtin_amdgcn_readlane((int)(b >> 32), 63);
-                tot += __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-            }
-            const float mean = (float)(tot / (double)Kdim);
-            const float scale = 1.0f / sqrtf(mean + P.eps);
-#pragma unroll
-            for (int e = 0; e < 16; ++e) {
-                xlo[e] = (xlo[e] * scale) * wlo[e];   // ggml_vec_scale_f32 then ggml_mul
-                xhi[e] = (xhi[e] * scale) * whi[e];
-            }
-        }
-        if (!lv) {
-#pragma unroll
-            for (int e = 0; e < 16; ++e) xlo[e] = xhi[e] = 0.0f;
-        }
-        arA = KAct<T>::quant(xlo, xhi, j);
-        if (DUAL) {
-            if (!lv) {
-#pragma unroll
-                for (int e = 0; e < 16; ++e) ylo[e] = yhi[e] = 0.0f;
-            }
-            arB = KAct<T>::quant(ylo, yhi, j);
-        } else {
-            arB = arA;
-        }
-    }
-    const int pos = __builtin_amdgcn_readfirstlane(tp.y);
-    const int cell = __builtin_amdgcn_readfirstlane(tp.z);
-    float* rope = reinterpret_cast<float*>(smem + KP.rope_off);
-    float* rs = reinterpret_cast<float*>(smem + KP.resid_off);
-    float2* part = reinterpret_cast<float2*>(smem + KP.part_off);
-    if (rope_wave) {   // ggml_rope_cache_init for this token's position (the epilogue reads it)
-        for (int i = lane; i < P.n_rot / 2; i += 64) {
-            float theta = (float)pos;
-            for (int k = 0; k < i; ++k) theta = theta * P.theta_scale;
-            const float ff = i < 64 ? ff0 : ff1;
-            const float th = P.freq_scale * (theta / ff);
-            rope[2 * i] = cosf(th);
-            rope[2 * i + 1] = sinf(th);
-        }
-    }
-    MI_STAMP(7)
-    // ---- the stream: one item (this chunk of one unit's two rows) per unit
-    int cu = u0;
-    auto consume = [&](const Slot& S) {
-        const float pa_ = K::dot(S.a, arA, j);
-        const float pb_ = K::dot(S.b, arB, j);
-        const float yA = wave_sum63(lv ? pa_ : 0.0f);
-        const float yB = wave_sum63(lv ? pb_ : 0.0f);
-        if (lane == 63) part[(cu - wg_u0) * G + g] = make_float2(yA, yB);
-        ++cu;
-    };
-    for (int base = 0; base < n_items; base += D) {
-#pragma unroll
-        for (int k = 0; k < D; ++k) {
-            issue(ring[(k + D - 1) % D]);
-            if (base + k < n_items) consume(ring[k]);
-        }
-        if (base == 0) { MI_STAMP(3) }
-    }
-    if (has_resid) {
-        rs[2 * threadIdx.x] = ra;
-        rs[2 * threadIdx.x + 1] = rbv;
-    }
-    __syncthreads();
-    MI_STAMP(2)
-    // ---- epilogue: one thread per unit adds its G chunk partials in chunk order
-    const EpiConst EC = epi_const(P);
-    for (int i = threadIdx.x; i < nwu; i += blockDim.x) {
-        const int u = wg_u0 + i;
-        float yA = 0.0f, yB = 0.0f;
-        for (int q = 0; q < G; ++q) {
-            const float2 v = part[i * G + q];
-            yA += v.x;
-            yB += v.y;
-        }
-        int si = 0;
-        while (si + 1 < P.nseg && u >= P.seg[si + 1].unit0) ++si;
-        const GemvSeg& S = P.seg[si];
-        EpiSeg es;
-        es.out = S.out;
-        es.epi = S.epi;
-        es.pair = S.pair;
-        es.unit0 = S.unit0;
-        es.end = S.unit0 + S.units;
-        es.rows = S.A.rows;
-        gemv_epilogue(EC, es, u, rope, rs[2 * i], rs[2 * i + 1], w0, w1, pos, cell, yA, yB);
-    }
-    MI_STAMP(4)
-#undef MI_STAMP
-}
-
-template <int T, int DUAL, int ROLE>
-__global__ __launch_bounds__(512) void gemv_k(const float* __restrict__ kx0, const float* __restrict__ knw,
-                                               const int* __restrict__ ktp, int kflags, const GemvParams Pk) {
-    __shared__ __attribute__((aligned(16))) u32x4 sparams[kGemvParamVecs];
-    gemv_k_body<T, KRingD<T>::D, DUAL>(kx0, knw, ktp, kflags, Pk, sparams, blockIdx.x);
-}
-
-template <int T1, int T2>
-__global__ __launch_bounds__(512) void gemv_k_mix(const float* __restrict__ kx0, const float* __restrict__ knw,
-                                                   const int* __restrict__ ktp, int kflags, const GemvParams P1,
-                                                   const GemvParams P2) {
-    __shared__ __attribute__((aligned(16))) u32x4 sparams[kGemvParamVecs];
-    if ((int)blockIdx.x < P1.grid) gemv_k_body<T1, KRingD<T1>::D, 0>(kx0, knw, ktp, kflags, P1, sparams, blockIdx.x);
-    else gemv_k_body<T2, KRingD<T2>::D, 0>(kx0, knw, ktp, kflags, P2, sparams, blockIdx.x - P1.grid);
-}
-
-typedef void (*GemvFn)(const float*, const float*, const int*, int, const GemvParams);
-typedef void (*GemvMixFn)(const float*, const float*, const int*, int, const GemvParams, const GemvParams);
-
-// Kernel configurations: waves per workgroup NW and ring depth D (one
-// workgroup per CU).  MI_GEMV_CFG=n selects config n for every type
-// (micro-benchmarks); otherwise gemv_cfg_for(type).
-struct GemvCfg { int nw, d; };
-constexpr GemvCfg kGemvCfgs[] = {{16, 2}, {8, 4}, {8, 3}, {16, 3}, {8, 6}, {8, 8}, {4, 8}};
-constexpr int kNumGemvCfgs = sizeof(kGemvCfgs) / sizeof(kGemvCfgs[0]);
-// Per launch role (measured on the 7B Q4_K_M decode, profiles/r01_*): the FFN gate/up
-// launch (the largest, 50 MB) runs best with 16 waves x 2-deep rings, the others with 8 x 4.
-// MI_GEMV_CFG / MI_GEMV_CFG_<ROLE> override (sweeps).
-static int gemv_cfg_for(int type, int role) {
-    static const int forced = getenv("MI_GEMV_CFG") ? atoi(getenv("MI_GEMV_CFG")) : -1;
-    if (forced >= 0 && forced < kNumGemvCfgs) return forced;
-    static const char* names[6] = {"MI_GEMV_CFG_QKV", "MI_GEMV_CFG_WO", "MI_GEMV_CFG_UP", "MI_GEMV_CFG_DOWN",
-                                   "MI_GEMV_CFG_OUT", "MI_GEMV_CFG_GEN"};
-    static int per_role[6] = {-2, -2, -2, -2, -2, -2};
-    if (role >= 0 && role < 6) {
-        if (per_role[role] == -2) per_role[role] = getenv(names[role]) ? atoi(getenv(names[role])) : -1;
-        if (per_role[role] >= 0 && per_role[role] < kNumGemvCfgs) return per_role[role];
-    }
-    (void)type;
-    return role == ROLE_FFN_UP ? 0 : 1;
-}
-
-template <int T, int DUAL, int ROLE>
-static GemvFn gemv_fn_cfg(int cfg) {
-    switch (cfg) {
-    case 0: return gemv_t<T, 2, 16, DUAL, ROLE>;
-    case 1: return gemv_t<T, 4, 8, DUAL, ROLE>;
-    case 2: return gemv_t<T, 3, 8, DUAL, ROLE>;
-    case 3: return gemv_t<T, 3, 16, DUAL, ROLE>;
-    case 4: return gemv_t<T, 6, 8, DUAL, ROLE>;
-    case 5: return gemv_t<T, 8, 8, DUAL, ROLE>;
-    case 6: return gemv_t<T, 8, 4, DUAL, ROLE>;
-    default: return nullptr;
-    }
-}
-
-template <int DUAL, int ROLE>
-static GemvFn gemv_fn_t(int type, int cfg) {
-    switch (type) {
-    case T_Q4_K: return gemv_fn_cfg<T_Q4_K, DUAL, ROLE>(cfg);
-    case T_Q5_K: return gemv_fn_cfg<T_Q5_K, DUAL, ROLE>(cfg);
-    case T_Q6_K: return gemv_fn_cfg<T_Q6_K, DUAL, ROLE>(cfg);
-    case T_Q8_0: return gemv_fn_cfg<T_Q8_0, DUAL, ROLE>(cfg);
-    default: return nullptr;
-    }
-}
-
-static GemvFn gemv_fn(int role, int type, int nslots, int cfg) {
-    if (nslots > 1) return gemv_fn_t<1, 2>(type, cfg);
-    return role == ROLE_FFN_UP ? gemv_fn_t<0, 1>(type, cfg) : gemv_fn_t<0, 0>(type, cfg);
-}
-
-
-// Dynamic LDS a GEMV may use: 160 KB minus its static copy of the parameters.
-constexpr int kGemvDynLds = 160 * 1024 - (int)((sizeof(GemvParams) + 15) / 16 * 16);
-
-template <int T, int D> __global__ void gemm_t(const GemmParams P);
-static void gemm_attrs();
-static GemvMixFn gemv_mix_fn(int t1, int t2);
-
-// Decode GEMV implementation: MI_GEMV=k (default: the K-split gemv_k), ring (the LDS-DMA ring
-// gemv_r), reg (the register ring gemv_t with a workgroup prologue) -- A/B switches.
-enum GemvImpl { GEMV_REG = 0, GEMV_RING = 1, GEMV_KSPLIT = 2 };
-static int gemv_impl() {
-    static const int impl = [] {
-        const char* e = getenv("MI_GEMV");
-        if (getenv("MI_GEMV_REG")) return (int)GEMV_REG;
-        if (!e || !*e || !strcmp(e, "k")) return (int)GEMV_KSPLIT;
-        if (!strcmp(e, "ring")) return (int)GEMV_RING;
-        return (int)GEMV_REG;
-    }();
-    return impl;
-}
-static bool gemv_ring_on() { return gemv_impl() == GEMV_RING; }
-static bool gemv_k_on(int K) { return gemv_impl() == GEMV_KSPLIT && gemv_k_groups(K) <= 8; }
-
-template <int DUAL, int ROLE>
-static GemvFn gemv_k_fn_t(int type) {
-    switch (type) {
-    case T_Q4_K: return gemv_k<T_Q4_K, DUAL, ROLE>;
-    case T_Q5_K: return gemv_k<T_Q5_K, DUAL, ROLE>;
-    case T_Q6_K: return gemv_k<T_Q6_K, DUAL, ROLE>;
-    case T_Q8_0: return gemv_k<T_Q8_0, DUAL, ROLE>;
-    default: return nullptr;
-    }
-}
-static GemvFn gemv_k_fn(int role, int type, int nslots) {
-    if (nslots > 1) return gemv_k_fn_t<1, 2>(type);
-    return role == ROLE_FFN_UP ? gemv_k_fn_t<0, 1>(type) : gemv_k_fn_t<0, 0>(type);
-}
-static GemvMixFn gemv_k_mix_fn(int t1, int t2) {
-    if (t1 == T_Q4_K && t2 == T_Q6_K) return gemv_k_mix<T_Q4_K, T_Q6_K>;
-    if (t1 == T_Q5_K && t2 == T_Q6_K) return gemv_k_mix<T_Q5_K, T_Q6_K>;
-    return nullptr;
-}
-
-template <int DUAL, int ROLE>
-static GemvFn gemv_r_fn_t(int type) {
-    switch (type) {
-    case T_Q4_K: return gemv_r<T_Q4_K, DUAL, ROLE>;
-    case T_Q5_K: return gemv_r<T_Q5_K, DUAL, ROLE>;
-    case T_Q6_K: return gemv_r<T_Q6_K, DUAL, ROLE>;
-    case T_Q8_0: return gemv_r<T_Q8_0, DUAL, ROLE>;
-    default: return nullptr;
-    }
-}
-static GemvFn gemv_r_fn(int role, int type, int nslots) {
-    if (nslots > 1) return gemv_r_fn_t<1, 2>(type);
-    return role == ROLE_FFN_UP ? gemv_r_fn_t<0, 1>(type) : gemv_r_fn_t<0, 0>(type);
-}
-static GemvMixFn gemv_r_mix_fn(int t1, int t2) {
-    if (t1 == T_Q4_K && t2 == T_Q6_K) return gemv_r_mix<T_Q4_K, T_Q6_K>;
-    if (t1 == T_Q5_K && t2 == T_Q6_K) return gemv_r_mix<T_Q5_K, T_Q6_K>;
-    return nullptr;
-}
-
-void init_kernel_attributes() {
-    gemm_attrs();
-    const int types[4] = {T_Q4_K, T_Q5_K, T_Q6_K, T_Q8_0};
-    for (int r : {ROLE_GENERIC, ROLE_FFN_UP})
-        for (int t : types)
-            for (int nsl = 1; nsl <= 2; ++nsl) {
-                for (int c = 0; c < kNumGemvCfgs; ++c)
-                    MI_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(gemv_fn(r, t, nsl, c)),
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, kGemvDynLds));
-                MI_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(gemv_r_fn(r, t, nsl)),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, kGemvDynLds));
-            }
-    for (int t1 : {T_Q4_K, T_Q5_K}) {
-        MI_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(gemv_mix_fn(t1, T_Q6_K)),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, kGemvDynLds));
-        MI_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(gemv_r_mix_fn(t1, T_Q6_K)),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, kGemvDynLds));
-    }
-}
-
-// Units one workgroup owns at most (its residual staging in LDS).
-static int wg_units_max(int total_units, int grid) { return (total_units + grid - 1) / grid + 1; }
-
-size_t gemv_smem_bytes(const GemvParams& p) { return (size_t)smem_plan(p).total; }
-// the LDS-DMA ring kernel: prologue plan, then the rings
-static size_t gemv_r_smem_bytes(const GemvParams& p) {
-    return (((size_t)smem_plan(p).total + 15) & ~(size_t)15) + (size_t)ring_bytes(p.seg[0].A.type);
-}
-
-static int gemv_waves(int type, int role, int K) {
-    if (gemv_k_on(K)) return gemv_k_waves(K);
-    return gemv_ring_on() ? RING_NW : kGemvCfgs[gemv_cfg_for(type, role)].nw;
-}
-
-int gemv_default_grid(const GemvParams& p, int role) {
-    // One workgroup per CU (256 CUs).  Small launches use fewer workgroups so that every
-    // wave (of a K group, for gemv_k) still gets a unit.
-    int per = gemv_waves(p.seg[0].A.type, role, p.K);
-    if (gemv_k_on(p.K)) per /= gemv_k_groups(p.K);
-    const int g = (p.total_units + per - 1) / per;
-    // at most one workgroup per CU by default; MI_GEMV_GRID raises the cap (A/B)
-    static const int cap = getenv("MI_GEMV_GRID") ? std::max(1, atoi(getenv("MI_GEMV_GRID"))) : 256;
-    return g < 1 ? 1 : (g > cap ? cap : g);
-}
-
-// Validates a launch and fixes its grid-dependent fields; returns the kernel configuration
-// (register ring), -1 (LDS-DMA ring) or -2 (K-split).
-static int gemv_prepare(GemvParams& p, int role, int grid) {
-    if (p.K % 256 != 0) throw Error("gemv: K must be a multiple of 256");
-    const int type = p.seg[0].A.type;
-    for (int i = 0; i < p.nseg; ++i)
-        if (p.seg[i].A.type != type || (p.seg[i].pair == PAIR_AB && p.seg[i].B.type != type))
-            throw Error("gemv: all matrices of one launch must share a quant type");
-    if (p.pro == PRO_ATTN && (p.attn.n_head * p.attn.head_dim != p.K || p.attn.head_dim % 4 != 0))
-        throw Error("gemv: attention combine needs K == n_head*head_dim");
-    const bool kk = gemv_k_on(p.K);
-    const int cfg = kk ? -2 : gemv_ring_on() ? -1 : gemv_cfg_for(type, role);
-    const int nw = gemv_waves(type, role, p.K);
-    if (grid <= 0) grid = gemv_default_grid(p, role);
-    if ((long long)p.total_units * grid * nw >= (1LL << 32))
-        throw Error("gemv: too many units for the 32-bit unit split");
-    p.wg_units = wg_units_max(p.total_units, grid);
-    p.grid = grid;
-    for (int i = 0; i < p.nseg; ++i)
-        if (p.seg[i].resid && (p.nseg != 1 || p.wg_units > nw * 64))
-            throw Error("gemv: residual launches must have one segment and <= 64*NW units per workgroup");
-    const size_t lds = kk ? (size_t)kplan(p).total : cfg < 0 ? gemv_r_smem_bytes(p) : gemv_smem_bytes(p);
-    if (lds > (size_t)kGemvDynLds) throw Error("gemv: activation too large for LDS");
-    return cfg;
-}
-
-// leading arguments: K | flags (activation kept in registers, RMSNorm prologue)
-static int gemv_kflags(const GemvParams& p, int nw) {
-    const int nb = p.K / 256;
-    const bool regs = p.pro != PRO_ATTN && p.nslots == 1 && nb <= PRO_MAXB * nw;
-    const bool rms = p.pro == PRO_RMSNORM;
-    return p.K | (regs ? 1 << 20 : 0) | (rms ? 1 << 21 : 0);
-}
-
-// gemv_k's leading arguments: K | RMSNorm (bit 21) | attention combine (bit 22); kx0 is the
-// activation, or split 0 of the attention partials
-static int gemv_k_kflags(const GemvParams& p) {
-    return p.K | (p.pro == PRO_RMSNORM ? 1 << 21 : 0) | (p.pro == PRO_ATTN ? 1 << 22 : 0);
-}
-static const float* gemv_k_x0(const GemvParams& p) { return p.pro == PRO_ATTN ? p.attn.o : p.x[0]; }
-
-void launch_gemv(const GemvParams& p_in, int role, int grid, hipStream_t s, hipEvent_t ev_start,
-                 hipEvent_t ev_stop) {
-    GemvParams p = p_in;
-    const int cfg = gemv_prepare(p, role, grid);
-    const int type = p.seg[0].A.type;
-    GemvFn fn;
-    size_t smem;
-    int nw, kflags;
-    const float* kx0 = p.x[0];
-    if (cfg == -2) {
-        fn = gemv_k_fn(role, type, p.nslots);
-        smem = (size_t)kplan(p).total + 16 * sizeof(double);
-        nw = gemv_k_waves(p.K);
-        kflags = gemv_k_kflags(p);
-        kx0 = gemv_k_x0(p);
-    } else {
-        const bool ring = cfg < 0;
-        smem = ring ? gemv_r_smem_bytes(p) : gemv_smem_bytes(p);
-        fn = ring ? gemv_r_fn(role, type, p.nslots) : gemv_fn(role, type, p.nslots, cfg);
-        nw = ring ? RING_NW : kGemvCfgs[cfg].nw;
-        kflags = gemv_kflags(p, nw);
-    }
-    if (!fn) throw Error("gemv: unsupported quant type");
-    const dim3 block(nw * 64);
-    const float* knw = p.pro == PRO_RMSNORM ? p.norm_w : nullptr;
-    const int* ktp = p.tokpos;
-    if (ev_start || ev_stop)
-        hipExtLaunchKernelGGL(fn, dim3(p.grid), block, smem, s, ev_start, ev_stop, 0, kx0, knw, ktp, kflags, p);
-    else
-        hipLaunchKernelGGL(fn, dim3(p.grid), block, smem, s, kx0, knw, ktp, kflags, p);
-    MI_HIP(hipGetLastError());
-}
-
-// Config 1 (8 waves, 4-deep ring) is the QKV role's; the pairs are the Q*_K_M layer mixes.
-static GemvMixFn gemv_mix_fn(int t1, int t2) {
-    if (t1 == T_Q4_K && t2 == T_Q6_K) return gemv_mix_t<T_Q4_K, T_Q6_K, 4, 8>;
-    if (t1 == T_Q5_K && t2 == T_Q6_K) return gemv_mix_t<T_Q5_K, T_Q6_K, 4, 8>;
-    return nullptr;
-}
-
-bool gemv_mix_supported(int t1, int t2, int role) {
-    if (gemv_impl() == GEMV_KSPLIT) return gemv_k_mix_fn(t1, t2) != nullptr;
-    if (gemv_ring_on()) return gemv_r_mix_fn(t1, t2) != nullptr;
-    return gemv_mix_fn(t1, t2) != nullptr && gemv_cfg_for(t1, role) == 1 && gemv_cfg_for(t2, role) == 1;
-}
-
-void launch_gemv_mix(const GemvParams& p1_in, const GemvParams& p2_in, int role, hipStream_t s) {
-    GemvParams p1 = p1_in, p2 = p2_in;
-    const int t1 = p1.seg[0].A.type, t2 = p2.seg[0].A.type;
-    const bool ring = gemv_ring_on();
-    const bool kk = gemv_k_on(p1.K);
-    GemvMixFn fn = kk ? gemv_k_mix_fn(t1, t2) : ring ? gemv_r_mix_fn(t1, t2) : gemv_mix_fn(t1, t2);
-    if (!fn || !gemv_mix_supported(t1, t2, role)) throw Error("gemv: unsupported type pair for a mixed launch");
-    if (p1.K != p2.K || p1.pro != p2.pro || p1.x[0] != p2.x[0] || p1.norm_w != p2.norm_w || p1.tokpos != p2.tokpos ||
-        p1.nslots != 1 || p2.nslots != 1)
-        throw Error("gemv: the halves of a mixed launch must share their activation");
-    // split the 256 workgroups in proportion to the bytes each half streams
-    auto bytes = [](const GemvParams& p) {
-        double b = 0;
-        for (int i = 0; i < p.nseg; ++i) b += (double)p.seg[i].A.rows * (p.K / block_elems(p.seg[i].A.type)) * block_bytes(p.seg[i].A.type);
-        return b;
-    };
-    const int total = gemv_default_grid(p1, role) + gemv_default_grid(p2, role) >= 256 ? 256 : 128;
-    const double b1 = bytes(p1), b2 = bytes(p2);
-    int g1 = (int)(total * b1 / (b1 + b2) + 0.5);
-    g1 = std::max(1, std::min(total - 1, std::min(g1, gemv_default_grid(p1, role))));
-    const int g2 = std::min(total - g1, gemv_default_grid(p2, role));
-    const int cfg = gemv_prepare(p1, role, g1);
-    gemv_prepare(p2, role, g2);
-    size_t smem;
-    int nw, kflags;
-    const float* kx0 = p1.x[0];
-    if (kk) {
-        smem = (size_t)std::max(kplan(p1).total, kplan(p2).total) + 16 * sizeof(double);
-        nw = gemv_k_waves(p1.K);
-        kflags = gemv_k_kflags(p1);
-        kx0 = gemv_k_x0(p1);
-    } else {
-        smem = ring ? std::max(gemv_r_smem_bytes(p1), gemv_r_smem_bytes(p2))
-                    : std::max(gemv_smem_bytes(p1), gemv_smem_bytes(p2));
-        nw = ring ? RING_NW : kGemvCfgs[cfg].nw;
-        kflags = gemv_kflags(p1, nw);
-    }
-    const dim3 block(nw * 64);
-    const float* knw = p1.pro == PRO_RMSNORM ? p1.norm_w : nullptr;
-    hipLaunchKernelGGL(fn, dim3(p1.grid + p2.grid), block, smem, s, kx0, knw, p1.tokpos, kflags, p1, p2);
-    MI_HIP(hipGetLastError());
-}
 
 // ---------------------------------------------------------------------------
 // Batched GEMM (prompt ingestion): gemv_t's weight ring and integer dots, with every
@@ -2316,7 +235,7 @@ __global__ __launch_bounds__(512) void gemm_t(const GemmParams P) {
 
 typedef void (*GemmFn)(const GemmParams);
 static GemmFn gemm_fn(int type);
-static void gemm_attrs() {
+void init_gemm_attributes() {
     for (int t : {T_Q4_K, T_Q5_K, T_Q6_K, T_Q8_0})
         MI_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_fn(t)),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024));
