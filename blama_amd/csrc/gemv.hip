@@ -55,6 +55,9 @@ struct GvArgs {
     const float* selw;
     float eps, theta_scale, freq_scale;
     int K, pro, nslots, attn_nsplit, attn_stride, n_rot, head_dim, kv_dim;
+    int order;                    // 0: weights right after the activation requests; 1: after a
+                                  // workgroup barrier; 2: after this wave's activation landed
+    int pre;                      // ring items issued before the prologue (the rest after it)
     unsigned long long* stamps;   // MI_STAMPS builds: [grid][8] s_memrealtime per workgroup
 };
 
@@ -166,6 +169,9 @@ __device__ __forceinline__ void gv_body(const GvArgs& a, char* lds) {
 #define GV_STAMP(k)
 #endif
     GV_STAMP(0)
+#ifdef MI_STAMPS   // 6: the workgroup's last wave to start
+    if (a.stamps && lane == 0) atomicMax(a.stamps + blockIdx.x * 8 + 6, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+#endif
 
     // ---- 1. entry loads: token position, MoE routing, the activation slices -------------------
     const bool qkv = epi == EPI_QKV;
@@ -198,13 +204,20 @@ __device__ __forceinline__ void gv_body(const GvArgs& a, char* lds) {
         if (lane < a.n_rot / 2) ff0 = gptr(a.freq_factors)[lane];
         if (lane + 64 < a.n_rot / 2) ff1 = gptr(a.freq_factors)[lane + 64];
     }
-    // every wave's activation requests ahead of any weight request of this CU
-    __builtin_amdgcn_s_barrier();
+    // the activation requests ahead of the weight requests (a.order, measured: DESIGN.md §4)
+    if (a.order == 1) __builtin_amdgcn_s_barrier();
+    if (a.order == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#ifdef MI_STAMPS   // 7 (order 2): the workgroup's last wave whose activation landed
+    if (a.stamps && lane == 0 && a.order == 2)
+        atomicMax(a.stamps + blockIdx.x * 8 + 7, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+#endif
 
     // ---- 2. the weight ring: item = (unit, chunk) of this wave's units -------------------------
+    // units are dealt wave-major over the segment's workgroups (unit u -> workgroup u % nblk), so
+    // every workgroup -- every CU's share of the stream -- gets the same number of units +-1
     const int wg = (int)blockIdx.x - S.blk0;
     const int stride = S.nblk * GV_NW;                 // units between a wave's consecutive units
-    const int u_first = wg * GV_NW + wave;
+    const int u_first = wave * S.nblk + wg;
     const int n_units = u_first < S.units ? (S.units - u_first + stride - 1) / stride : 0;
     const int n_items = n_units * C;
     const bool ab = RW == 2 && (epi == EPI_SWIGLU || epi == EPI_MOE_DOWN);
@@ -239,37 +252,33 @@ __device__ __forceinline__ void gv_body(const GvArgs& a, char* lds) {
     auto issue = [&](Slot& s) {
         const int sb0 = ic * 8 + sbl;
         const int sb = sb0 < nb ? sb0 : nb - 1;
+        const bool park = iu >= n_units;               // no item left: out-of-range loads (zeros)
 #pragma unroll
-        for (int r = 0; r < RW; ++r) s.w[r] = K::load(rp[r], sb, j);
-        if (has_res) {   // the unit's residual values (every chunk of the unit reads them: cache hits)
-            const long long u = u_first + (long long)(iu < n_units ? iu : (n_units > 0 ? n_units - 1 : 0)) * stride;
+        for (int r = 0; r < RW; ++r) s.w[r] = K::bload(rp[r], sb, j, park);
+        if (has_res) {   // the unit's residual values, with the unit's last chunk
+            const long long u = u_first + (long long)iu * stride;
             const long long r0 = ab ? u : u * RW;
-            const long long rr = r0 < S.rows ? r0 : S.rows - 1;
-            if (RW == 2 && !ab) {
-                const long long r1 = rr + 1 < S.rows ? rr + 1 : rr;
-                s.res.x = gptr(S.resid)[rr];
-                s.res.y = gptr(S.resid)[r1];
-            } else {
-                s.res.x = gptr(S.resid)[rr];
-                s.res.y = 0.0f;
-            }
+            const bool rv = !park && ic == C - 1;
+            const unsigned o0 = oob((unsigned)(r0 * 4), !rv);
+            const unsigned o1 = oob((unsigned)((r0 + 1) * 4), !(rv && RW == 2 && !ab && r0 + 1 < S.rows));
+            const uint8_t* rb = reinterpret_cast<const uint8_t*>(rfl_ptr(S.resid));
+            s.res.x = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(buf_rsrc(rb), o0, 0, 0));
+            s.res.y = RW == 2 && !ab ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(buf_rsrc(rb), o1, 0, 0)) : 0.0f;
         }
-        if (iu < n_units) {
-            if (++ic == C) {
-                ic = 0;
-                if (++iu < n_units) {
+        if (!park && ++ic == C) {
+            ic = 0;
+            if (++iu < n_units) {
 #pragma unroll
-                    for (int r = 0; r < RW; ++r)
+                for (int r = 0; r < RW; ++r)
 #pragma unroll
-                        for (int p = 0; p < 4; ++p) rp[r][p] += step[p];
-                } else {
-                    ic = C - 1;   // parked: every later issue re-reads the last chunk (cache hits)
-                }
+                    for (int p = 0; p < 4; ++p) rp[r][p] += step[p];
             }
         }
     };
+    const int pre = a.pre;
 #pragma unroll
-    for (int k = 0; k < D - 1; ++k) issue(ring[k]);
+    for (int k = 0; k < D - 1; ++k)
+        if (k < pre) issue(ring[k]);
     GV_STAMP(1)
 
     // ---- 3. prologue: the activation into LDS while the weights stream ---------------------------
@@ -352,6 +361,9 @@ __device__ __forceinline__ void gv_body(const GvArgs& a, char* lds) {
         }
     }
     lds_barrier();
+#pragma unroll
+    for (int k = 0; k < D - 1; ++k)
+        if (k >= pre) issue(ring[k]);
     GV_STAMP(2)
 
     // ---- 4. the stream: consume item i while items i+1 .. i+D-1 are in flight -----------------
@@ -443,6 +455,9 @@ __device__ __forceinline__ void gv_body(const GvArgs& a, char* lds) {
         }
     }
     GV_STAMP(4)
+#ifdef MI_STAMPS   // 5: the workgroup's last wave to finish
+    if (a.stamps && lane == 0) atomicMax(a.stamps + blockIdx.x * 8 + 5, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+#endif
 #undef GV_STAMP
 }
 
@@ -636,6 +651,10 @@ void launch_gemv(const GemvParams& p, hipStream_t s, hipEvent_t ev_start, hipEve
     a.head_dim = p.head_dim > 0 ? p.head_dim : 1;
     a.kv_dim = p.kv_dim;
     a.stamps = p.stamps;
+    static const int order = getenv("MI_GEMV_ORDER") ? atoi(getenv("MI_GEMV_ORDER")) : 1;
+    static const int pre = getenv("MI_GEMV_PRE") ? atoi(getenv("MI_GEMV_PRE")) : 8;
+    a.order = order;
+    a.pre = pre;
     for (int i = 0; i < p.nseg; ++i)
         if (p.seg[i].epi == EPI_QKV && (!p.tokpos || (p.n_rot > 0 && p.head_dim <= 0)))
             throw Error("gemv: QKV epilogue needs tokpos and the head geometry");

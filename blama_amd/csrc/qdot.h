@@ -35,6 +35,27 @@ __device__ __forceinline__ T* rfl_ptr(T* p) {
 __device__ __forceinline__ u32x4 ldg16(const uint8_t* p) {
     return __builtin_nontemporal_load(gptr(reinterpret_cast<const u32x4*>(p)));
 }
+// Buffer loads of a wave-uniform base (SGPR descriptor) with the cache policy nt.  An offset at or
+// past GV_OOB is out of the descriptor's range: the load returns zeros without a memory access
+// (the decode GEMV's ring issues such loads once a wave's items run out, so it never waits for a
+// real round trip it does not need).
+constexpr unsigned BUF_OOB = 0xFFFFFF00u;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const uint8_t* base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(base), 0, 0x7FFFFFFF, 0x00020000);
+}
+__device__ __forceinline__ u32x4 bld16(const uint8_t* base, unsigned off) {
+    return __builtin_amdgcn_raw_buffer_load_b128(buf_rsrc(base), off, 0, 2);
+}
+__device__ __forceinline__ unsigned bld8x(const uint8_t* base, unsigned off, unsigned& hi) {
+    typedef unsigned int u32x2_ __attribute__((ext_vector_type(2)));
+    const u32x2_ v = __builtin_amdgcn_raw_buffer_load_b64(buf_rsrc(base), off, 0, 2);
+    hi = v.y;
+    return v.x;
+}
+__device__ __forceinline__ unsigned bld2(const uint8_t* base, unsigned off) {
+    return __builtin_amdgcn_raw_buffer_load_b16(buf_rsrc(base), off, 0, 2);
+}
+__device__ __forceinline__ unsigned oob(unsigned off, bool park) { return park ? BUF_OOB : off; }
 __device__ __forceinline__ float h2f(uint32_t bits) {
     return __half2float(__ushort_as_half(static_cast<unsigned short>(bits & 0xFFFFu)));
 }
@@ -216,6 +237,13 @@ template <> struct Kq<T_Q4_K> {
 #endif
         return l;
     }
+    // buffer-load form (decode GEMV ring): park = the wave has no item left (zeros, no access)
+    __device__ static Ld bload(const uint8_t* const* rp, int sb, int j, bool park) {
+        Ld l;
+        l.qs = bld16(rp[0], oob(sb * 128 + j * 16, park));
+        l.hdr = bld16(rp[1], oob(sb * 16, park));
+        return l;
+    }
     // the activation slice lane (sb, j) needs -- identical for every row
     struct AR { i32x4 alo, ahi; int bs_lo, bs_hi; float dx; };
     __device__ static AR act(const Act& a, int sb, int j) {
@@ -264,6 +292,13 @@ template <> struct Kq<T_Q5_K> {
         l.hdr = ldg16(rp[2] + sb * 16);
         return l;
     }
+    __device__ static Ld bload(const uint8_t* const* rp, int sb, int j, bool park) {
+        Ld l;
+        l.qs = bld16(rp[0], oob(sb * 128 + j * 16, park));
+        l.qh = bld16(rp[1], oob(sb * 32 + (j & 1) * 16, park));
+        l.hdr = bld16(rp[2], oob(sb * 16, park));
+        return l;
+    }
     using AR = Kq<T_Q4_K>::AR;
     __device__ static AR act(const Act& a, int sb, int j) { return Kq<T_Q4_K>::act(a, sb, j); }
     __device__ static float dot(const Ld& l, const AR& r, int j) {
@@ -309,6 +344,15 @@ template <> struct Kq<T_Q6_K> {
         l.sc0 = sc.x;
         l.sc1 = sc.y;
         l.d = __builtin_nontemporal_load(gptr(reinterpret_cast<const unsigned short*>(rp[3] + sb * 2)));
+        return l;
+    }
+    __device__ static Ld bload(const uint8_t* const* rp, int sb, int j, bool park) {
+        Ld l;
+        const int h = j >> 2, half = j & 1;
+        l.ql = bld16(rp[0], oob(sb * 128 + j * 16, park));
+        l.qh = bld16(rp[1], oob(sb * 64 + 32 * h + 16 * half, park));
+        l.sc0 = bld8x(rp[2], oob(sb * 16 + 8 * h, park), l.sc1);
+        l.d = bld2(rp[3], oob(sb * 2, park));
         return l;
     }
     struct AR { i32x4 alo, ahi; int bs_lo, bs_hi; float dx; };
@@ -360,6 +404,13 @@ template <> struct Kq<T_Q8_0> {
         l.q0 = ldg16(rp[0] + sb * 256 + j * 32);
         l.q1 = ldg16(rp[0] + sb * 256 + j * 32 + 16);
         l.d = __builtin_nontemporal_load(gptr(reinterpret_cast<const unsigned short*>(rp[1] + sb * 16 + j * 2)));
+        return l;
+    }
+    __device__ static Ld bload(const uint8_t* const* rp, int sb, int j, bool park) {
+        Ld l;
+        l.q0 = bld16(rp[0], oob(sb * 256 + j * 32, park));
+        l.q1 = bld16(rp[0], oob(sb * 256 + j * 32 + 16, park));
+        l.d = bld2(rp[1], oob(sb * 16 + j * 2, park));
         return l;
     }
     struct AR { i32x4 a0, a1; float d0; };

@@ -43,6 +43,9 @@ def main():
         if not m.any():
             continue   # an unused slab (e.g. the second attention launch in fused mode)
         end = buf[i, :, 4].astype(np.int64)
+        end5 = buf[i, :, 5].astype(np.int64)   # GEMV: last wave of the workgroup (atomic max)
+        if (end5 > 0).any():
+            end = np.where(end5 > 0, end5, end)
         pro = buf[i, :, 2].astype(np.int64)
         pre = buf[i, :, 1].astype(np.int64)
         launches.append((ent[m], end[m & (end > 0)], pro[m & (pro > 0)], pre[m & (pre > 0)]))
@@ -80,6 +83,21 @@ def main():
         # round consumed (first weights landed), 2 stream done + barrier, 4 epilogue done
         print(f"{i:3d} from params-in-LDS: issued {det[0]}  act-quantised {det[1]}  first-weights {det[2]}"
               f"  stream-done {det[3]}  epilogue-done {det[4]}")
+    # GEMV workgroup skew (stamps 6, 7: last wave started / last wave's activation landed, atomic
+    # max over the waves), medians over workgroups, relative to wave 0's entry
+    for i in range(n):
+        d = buf[i, :, :].astype(np.int64)
+        m = (d[:, 0] > 0) & (d[:, 6] > 0)
+        if not m.any():
+            continue
+        e0 = d[m, 0]
+        s6 = np.median(d[m, 6] - e0) / 100.0
+        s7 = np.median(d[m, 7] - e0) / 100.0 if (d[m, 7] > 0).any() else float("nan")
+        s2 = np.median(d[m, 2] - e0) / 100.0
+        s5 = np.median(d[m, 5] - e0) / 100.0 if (d[m, 5] > 0).any() else float("nan")
+        if i < 12:
+            print(f"  launch {i:3d}: last wave started +{s6:5.2f}  last activation landed +{s7:5.2f}  "
+                  f"activation in LDS +{s2:5.2f}  last wave done +{s5:5.2f} us")
     print(f"launches {len(rows)}  first entry -> last end {total:.1f} us;  sum of spans {spans.sum():.1f}"
           f"  sum of gaps {gaps.sum():.1f}")
 
