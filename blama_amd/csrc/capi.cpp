@@ -606,4 +606,84 @@ int32_t mi_op_attention(int32_t device, int32_t n_head, int32_t n_head_kv, int32
     MI_TRY(-1)
 }
 
+int32_t mi_op_gemm(int32_t device, int32_t type, const void* raw, const void* raw_up, int32_t rows, int32_t K,
+                   int32_t ntok, const float* x, float* y) {
+    try {
+        if (!mmq32_supported(type)) throw Error("op_gemm: Q4_K / Q6_K / Q8_0 only");
+        if (ntok < 1 || ntok > UB_MAX) throw Error("op_gemm: 1..512 token rows");
+        if (rows < 1 || K < 256 || K % 256) throw Error("op_gemm: bad shape");
+        MI_HIP(hipSetDevice(device));
+        ensure_attrs(device);
+        std::vector<std::unique_ptr<DevBuf>> keep;
+        QMat A = upload_qmat(type, raw, rows, K, keep);
+        QMat B = A;
+        const bool pair = raw_up != nullptr;
+        if (pair) B = upload_qmat(type, raw_up, rows, K, keep);
+        DevBuf sw(mmq32_copy_bytes(A, pair));
+        launch_mmq32_swizzle(A, pair ? &B : nullptr, sw.as<uint8_t>(), nullptr);
+        A.sw = sw.as<uint8_t>();
+        const int npad = (ntok + 31) / 32 * 32;
+        DevBuf dx((size_t)ntok * K * sizeof(float)), dy((size_t)ntok * rows * sizeof(float));
+        DevBuf dq((size_t)npad * K), ddT((size_t)npad * (K / 32) * sizeof(float)), dbs((size_t)npad * (K / 256) * 16);
+        DevBuf dtp((size_t)ntok * 4 * sizeof(int));
+        MI_HIP(hipMemset(dtp.p, 0, (size_t)ntok * 4 * sizeof(int)));
+        MI_HIP(hipMemcpy(dx.p, x, (size_t)ntok * K * sizeof(float), hipMemcpyHostToDevice));
+        ActQ8 act{dq.as<int8_t>(), ddT.as<float>(), dbs.as<int8_t>(), K, ntok, npad, type == T_Q8_0 ? 1 : 0};
+        launch_quant_act(dx.as<float>(), K, nullptr, 0.0f, act, nullptr);
+        GemmParams p;
+        std::memset(&p, 0, sizeof(p));
+        p.A = A;
+        p.B = B;
+        p.pair = pair ? PAIR_AB : PAIR_ADJ;
+        p.epi = pair ? EPI_SWIGLU : EPI_STORE;
+        p.K = K;
+        p.ntok = ntok;
+        p.tokpos = dtp.as<int>();
+        p.out = dy.as<float>();
+        p.out_stride = rows;
+        launch_mmq32(p, act, nullptr, nullptr);
+        MI_HIP(hipDeviceSynchronize());
+        MI_HIP(hipMemcpy(y, dy.p, (size_t)ntok * rows * sizeof(float), hipMemcpyDeviceToHost));
+        return 0;
+    }
+    MI_TRY(-1)
+}
+
+int32_t mi_op_attention_batch(int32_t device, int32_t n_head, int32_t n_head_kv, int32_t head_dim, int32_t n_cells,
+                              int32_t ntok, const float* q, const uint16_t* k_f16, const uint16_t* v_f16,
+                              const int32_t* cell_pos, const int32_t* tok_cell, const int32_t* tok_pos, float* out) {
+    try {
+        if (n_head <= 0 || n_head_kv <= 0 || n_head % n_head_kv || n_cells <= 0 || ntok <= 0)
+            throw Error("attention_batch: bad shape");
+        if (!attn_mfma_supported(head_dim)) throw Error("attention_batch: head_dim 64 or 128");
+        for (int t = 0; t < ntok; ++t) {
+            if (tok_cell[t] < 0 || tok_cell[t] >= n_cells) throw Error("attention_batch: token cell out of range");
+            if (t && tok_cell[t] <= tok_cell[t - 1]) throw Error("attention_batch: token cells must ascend");
+        }
+        MI_HIP(hipSetDevice(device));
+        const int kv_dim = n_head_kv * head_dim, d = n_head * head_dim;
+        const size_t kvb = (size_t)n_cells * kv_dim * sizeof(uint16_t);
+        DevBuf dq((size_t)ntok * d * sizeof(float)), dk(kvb), dv(kvb), dcp(n_cells * sizeof(int));
+        DevBuf dtp((size_t)ntok * 4 * sizeof(int)), dout((size_t)ntok * d * sizeof(float));
+        std::vector<int> tp((size_t)ntok * 4, 0);
+        for (int t = 0; t < ntok; ++t) {
+            tp[t * 4 + 1] = tok_pos[t];
+            tp[t * 4 + 2] = tok_cell[t];
+        }
+        MI_HIP(hipMemcpy(dq.p, q, (size_t)ntok * d * sizeof(float), hipMemcpyHostToDevice));
+        MI_HIP(hipMemcpy(dk.p, k_f16, kvb, hipMemcpyHostToDevice));
+        MI_HIP(hipMemcpy(dv.p, v_f16, kvb, hipMemcpyHostToDevice));
+        MI_HIP(hipMemcpy(dcp.p, cell_pos, n_cells * sizeof(int), hipMemcpyHostToDevice));
+        MI_HIP(hipMemcpy(dtp.p, tp.data(), tp.size() * sizeof(int), hipMemcpyHostToDevice));
+        AttnParams a{dq.as<float>(), dk.as<__half>(), dv.as<__half>(), dtp.as<int>(), dcp.as<int>(),
+                     nullptr, nullptr, nullptr, n_head, n_head_kv, head_dim, kv_dim,
+                     n_cells, 1.0f / std::sqrt((float)head_dim)};
+        launch_attn_mfma(a, ntok, dout.as<float>(), nullptr);
+        MI_HIP(hipDeviceSynchronize());
+        MI_HIP(hipMemcpy(out, dout.p, (size_t)ntok * d * sizeof(float), hipMemcpyDeviceToHost));
+        return 0;
+    }
+    MI_TRY(-1)
+}
+
 }  // extern "C"

@@ -140,10 +140,32 @@ const GgufTensor* Gguf::tensor(const std::string& name) const {
 
 // ================================================================= model ===
 Model::~Model() {
-    if (arena || mmq_arena) hipSetDevice(device);
+    if (arena || mmq_arena || gelu_tab) hipSetDevice(device);
     if (arena) hipFree(arena);
     if (mmq_arena) hipFree(mmq_arena);
+    if (gelu_tab) hipFree(gelu_tab);
 }
+
+namespace {
+// ggml_table_gelu_f16 (ggml-cpu.c init with GGML_GELU_FP16): fp16(ggml_gelu_f32(fp32(h))) for
+// every f16 bit pattern h, ggml_gelu_f32(x) = 0.5f*x*(1.0f + tanhf(SQRT_2_OVER_PI*x*(1.0f +
+// GELU_COEF_A*x*x))), evaluated on the host with the C library's tanhf (no FMA contraction:
+// -ffp-contract=off), as the reference's CPU build evaluates it.
+std::vector<unsigned short> gelu_table_host() {
+    std::vector<unsigned short> t(65536);
+    const float A = 0.044715f, K = 0.79788456080286535587989211986876f;
+    for (int i = 0; i < 65536; ++i) {
+        const unsigned short h = (unsigned short)i;
+        _Float16 hf;
+        std::memcpy(&hf, &h, 2);
+        const float x = (float)hf;
+        const float g = 0.5f * x * (1.0f + tanhf(K * x * (1.0f + A * x * x)));
+        const _Float16 r = (_Float16)g;
+        std::memcpy(&t[i], &r, 2);
+    }
+    return t;
+}
+}  // namespace
 
 bool Model::ensure_mmq_copies() {
     std::lock_guard<std::mutex> lk(mmq_mu);
@@ -197,8 +219,9 @@ void Model::load(const uint8_t* data, size_t size, const mi_model_params& p) {
     vocab_only = p.vocab_only != 0;
     gguf.parse(data, size);
     const std::string arch = gguf.get_str("general.architecture", "");
-    if (arch != "llama")
-        throw Error("unsupported architecture '" + arch + "' (this backend serves the llama graph)");
+    if (arch != "llama" && arch != "gpt2")
+        throw Error("unsupported architecture '" + arch + "' (this backend serves the llama and gpt2 graphs)");
+    hp.arch = arch == "gpt2" ? ARCH_GPT2 : ARCH_LLAMA;
     auto key = [&](const char* k) { return arch + "." + k; };
     hp.n_embd = (int)gguf.get_int(key("embedding_length"), 0);
     hp.n_layer = (int)gguf.get_int(key("block_count"), 0);
@@ -206,7 +229,8 @@ void Model::load(const uint8_t* data, size_t size, const mi_model_params& p) {
     hp.n_head = (int)gguf.get_int(key("attention.head_count"), 0);
     hp.n_head_kv = (int)gguf.get_int(key("attention.head_count_kv"), hp.n_head);
     hp.n_ctx_train = (int)gguf.get_int(key("context_length"), 2048);
-    hp.eps = (float)gguf.get_float(key("attention.layer_norm_rms_epsilon"), 1e-5);
+    hp.eps = (float)gguf.get_float(key(hp.arch == ARCH_GPT2 ? "attention.layer_norm_epsilon"
+                                                             : "attention.layer_norm_rms_epsilon"), 1e-5);
     hp.rope_base = (float)gguf.get_float(key("rope.freq_base"), 10000.0);
     const double fs = gguf.get_float(key("rope.scale_linear"), 0.0);
     hp.freq_scale = fs > 0.0 ? (float)(1.0 / fs) : 1.0f;
@@ -214,7 +238,8 @@ void Model::load(const uint8_t* data, size_t size, const mi_model_params& p) {
     hp.n_expert_used = (int)gguf.get_int(key("expert_used_count"), 0);
     if (hp.n_embd <= 0 || hp.n_layer <= 0 || hp.n_head <= 0) throw Error("GGUF: missing llama hparams");
     hp.head_dim = hp.n_embd / hp.n_head;
-    hp.n_rot = (int)gguf.get_int(key("rope.dimension_count"), hp.head_dim);
+    hp.n_rot = hp.arch == ARCH_GPT2 ? 0 : (int)gguf.get_int(key("rope.dimension_count"), hp.head_dim);
+    if (hp.arch == ARCH_GPT2 && hp.n_expert) throw Error("gpt2: no MoE");
 
     if (const GgufValue* tv = gguf.get("tokenizer.ggml.tokens")) tokens = tv->arr_s;
     if (const GgufValue* tt = gguf.get("tokenizer.ggml.token_type"))
@@ -293,14 +318,41 @@ void Model::load(const uint8_t* data, size_t size, const mi_model_params& p) {
             off = align256(off + (size_t)kPlanePadSb * plane_sb_bytes(type, k));
         }
     };
-    struct LayerIdx { int an, fn, q, k, v, o, g, u, d, r; std::vector<std::vector<int>> qkv_groups; };
+    struct LayerIdx {
+        int an, fn, q, k, v, o, g, u, d, r;
+        std::vector<std::vector<int>> qkv_groups;
+        int anb = -1, fnb = -1, bqkv = -1, bo = -1, bu = -1, bd = -1;   // GPT-2 biases
+    };
+    const bool gpt2 = hp.arch == ARCH_GPT2;
     const int i_te = add("token_embd.weight", true, 1);
+    const int i_pe = gpt2 ? add("position_embd.weight", true, 1) : -1;
     const int i_on = add("output_norm.weight", true, 1);
+    const int i_onb = gpt2 ? add("output_norm.bias", true, 1) : -1;
     int i_out = add("output.weight", false, 1);
     const int i_rf = add("rope_freqs.weight", false, 1);
     std::vector<LayerIdx> li(hp.n_layer);
     const int E = hp.n_expert > 0 ? hp.n_expert : 1;
-    for (int l = 0; l < hp.n_layer; ++l) {
+    for (int l = 0; l < hp.n_layer && gpt2; ++l) {   // llm_build_gpt2's tensors (LLM_ARCH_GPT2)
+        const std::string b = "blk." + std::to_string(l) + ".";
+        LayerIdx& x = li[l];
+        x.an = add(b + "attn_norm.weight", true, 1);
+        x.anb = add(b + "attn_norm.bias", true, 1);
+        x.fn = add(b + "ffn_norm.weight", true, 1);
+        x.fnb = add(b + "ffn_norm.bias", true, 1);
+        std::vector<int> idx;
+        add_group({b + "attn_qkv.weight"}, idx);   // one fused [3 n_embd] x n_embd matrix
+        x.qkv_groups.push_back(idx);
+        x.q = x.k = x.v = idx[0];
+        x.bqkv = add(b + "attn_qkv.bias", true, 1);
+        x.o = add(b + "attn_output.weight", true, 1);
+        x.bo = add(b + "attn_output.bias", true, 1);
+        x.r = -1;
+        x.g = x.u = add(b + "ffn_up.weight", true, 1);
+        x.bu = add(b + "ffn_up.bias", true, 1);
+        x.d = add(b + "ffn_down.weight", true, 1);
+        x.bd = add(b + "ffn_down.bias", true, 1);
+    }
+    for (int l = 0; l < hp.n_layer && !gpt2; ++l) {
         const std::string b = "blk." + std::to_string(l) + ".";
         LayerIdx& x = li[l];
         x.an = add(b + "attn_norm.weight", true, 1);
@@ -344,7 +396,7 @@ void Model::load(const uint8_t* data, size_t size, const mi_model_params& p) {
     for (const auto& pl : plan) {
         // bytes one decode step streams: an expert tensor contributes the n_expert_used experts
         // the router picks (build_moe_ffn reads only those), not all n_expert of them
-        if (pl.t->name != "token_embd.weight")
+        if (pl.t->name != "token_embd.weight" && pl.t->name != "position_embd.weight")
             weight_bytes += pl.experts > 1 ? (long long)pl.t->nbytes / pl.experts * hp.n_expert_used
                                            : (long long)pl.t->nbytes;
         if (pl.t->type >= 0 && pl.t->type < 32) type_bytes[pl.t->type] += (long long)pl.t->nbytes;
@@ -403,6 +455,8 @@ void Model::load(const uint8_t* data, size_t size, const mi_model_params& p) {
         return reinterpret_cast<float*>(arena + plan[idx].off[0]);
     };
     tok_embd = qm(i_te);
+    if (i_pe >= 0) pos_embd = qm(i_pe);
+    output_norm_b = f32p(i_onb);
     output = i_out >= 0 ? qm(i_out) : qm(i_te);
     if (!is_quant(output.type)) throw Error("output head must be a quantised tensor in this build");
     output_norm = f32p(i_on);
@@ -416,8 +470,22 @@ void Model::load(const uint8_t* data, size_t size, const mi_model_params& p) {
         L.wq = qm(x.q); L.wk = qm(x.k); L.wv = qm(x.v); L.wo = qm(x.o);
         L.gate = qm(x.g); L.up = qm(x.u); L.down = qm(x.d);
         L.router = f32p(x.r);
+        L.attn_norm_b = f32p(x.anb);
+        L.ffn_norm_b = f32p(x.fnb);
+        L.bqkv = f32p(x.bqkv);
+        L.bo = f32p(x.bo);
+        L.bup = f32p(x.bu);
+        L.bdown = f32p(x.bd);
         for (const QMat* m : {&L.wq, &L.wk, &L.wv, &L.wo, &L.gate, &L.up, &L.down})
             if (!is_quant(m->type)) throw Error("layer weights must be quantised (Q4_K/Q5_K/Q6_K/Q8_0)");
+        if (gpt2) {   // the fused QKV rows: n_embd Q rows, n_embd K rows, n_embd V rows
+            L.n_qkv = 1;
+            L.qkv[0] = qm(x.qkv_groups[0][0]);
+            L.qkv_nq[0] = hp.n_embd;
+            L.qkv_nk[0] = hp.n_head_kv * hp.head_dim;
+            if (L.qkv[0].rows != L.qkv_nq[0] + 2 * L.qkv_nk[0]) throw Error("gpt2: attn_qkv must have 3 n_embd rows");
+            continue;
+        }
         L.n_qkv = (int)x.qkv_groups.size();
         int seen = 0;   // Q rows, then K rows, then V rows across the groups
         for (int g = 0; g < L.n_qkv; ++g) {
@@ -435,6 +503,11 @@ void Model::load(const uint8_t* data, size_t size, const mi_model_params& p) {
             L.qkv_nq[g] = nq;
             L.qkv_nk[g] = nk;
         }
+    }
+    if (gpt2) {
+        const std::vector<unsigned short> t = gelu_table_host();
+        MI_HIP(hipMalloc(&gelu_tab, t.size() * sizeof(unsigned short)));
+        MI_HIP(hipMemcpy(gelu_tab, t.data(), t.size() * sizeof(unsigned short), hipMemcpyHostToDevice));
     }
 }
 
@@ -491,7 +564,9 @@ Ctx::Ctx(Model* model, uint32_t nctx, uint32_t nbatch, uint32_t nubatch) : m(mod
     MI_HIP(hipMalloc(&stamps, (size_t)kStampLaunches * kStampWgs * 8 * sizeof(unsigned long long)));
     MI_HIP(hipMemset(stamps, 0, (size_t)kStampLaunches * kStampWgs * 8 * sizeof(unsigned long long)));
 #endif
-    batch_ok = hp.n_expert == 0 && getenv("MI_NO_BATCH") == nullptr;
+    // GPT-2 prompts run token by token (one decode graph each): its batch kernels (LayerNorm,
+    // biases, GELU) are not built
+    batch_ok = hp.n_expert == 0 && hp.arch == ARCH_LLAMA && getenv("MI_NO_BATCH") == nullptr;
     if (batch_ok) {
         // MFMA batch path (decode_ubatch / mmq32) when every layer matrix is Q4_K / Q6_K or every
         // one Q8_0; otherwise prompt chunks on the v_dot4 GEMM (decode_batch)
@@ -600,7 +675,7 @@ void Ctx::enqueue_step(bool with_logits) {
         return stamps + (size_t)(n_launch++) * kStampWgs * 8;
     };
     auto on = [&]() { return seg_filter < 0 || seg_filter == seg; };
-    EmbedParams ep{m->tok_embd, tokpos, x, hp.n_embd};
+    EmbedParams ep{m->tok_embd, tokpos, x, hp.n_embd, m->pos_embd, hp.arch == ARCH_GPT2 ? 1 : 0};
     if (on()) launch_embed(ep, stream);
     const float theta_scale = std::pow(hp.rope_base, -2.0f / (float)hp.n_rot);
     const float kq_scale = 1.0f / std::sqrt((float)hp.head_dim);
@@ -616,6 +691,10 @@ void Ctx::enqueue_step(bool with_logits) {
         base.kv_dim = kv_dim;
         base.eps = hp.eps;
         base.nslots = 1;
+        if (hp.arch == ARCH_GPT2) {   // llm_build_gpt2: LayerNorm, biases, no RoPE, GELU MLP
+            enqueue_layer_gpt2(l, base, kl, vl, kq_scale, stamp);
+            continue;
+        }
         // ---- Q/K/V projections + RoPE + KV append: one launch per pair of row groups ----
         {
             GemvParams p = base;
@@ -720,12 +799,89 @@ void Ctx::enqueue_step(bool with_logits) {
     if (with_logits && on()) enqueue_output(x, stamp());
 }
 
-// final RMSNorm + output head GEMV of one residual row, then the top-k
+// One GPT-2 block (llm_build_gpt2, src/llama-model.cpp b5187) of the decode step:
+//   cur = LayerNorm(x)*attn_norm + attn_norm_b -> wqkv + bqkv -> Q / K / V (no RoPE) -> KV append
+//   attention -> wo + bo + x (residual);  LayerNorm(x)*ffn_norm + ffn_norm_b -> up + bup -> GELU
+//   -> down + bdown + x
+void Ctx::enqueue_layer_gpt2(int l, const GemvParams& base, __half* kl, __half* vl, float kq_scale,
+                             const std::function<unsigned long long*()>& stamp) {
+    const HParams& hp = m->hp;
+    const Layer& L = m->layers[l];
+    auto on = [&]() { return seg_filter < 0; };
+    {
+        GemvParams p = base;
+        p.pro = PRO_LAYERNORM;
+        p.x[0] = x;
+        p.norm_w = L.attn_norm;
+        p.norm_b = L.attn_norm_b;
+        p.K = hp.n_embd;
+        p.n_rot = 0;
+        p.kcache = kl;
+        p.vcache = vl;
+        p.nseg = 1;
+        p.seg[0] = seg_of(L.qkv[0], PAIR_ADJ, EPI_QKV, q);
+        p.seg[0].nq = L.qkv_nq[0];
+        p.seg[0].nk = L.qkv_nk[0];
+        p.seg[0].bias = L.bqkv;
+        p.stamps = stamp();
+        if (on()) launch_gemv(p, stream);
+    }
+    {
+        AttnParams a{q, kl, vl, tokpos, cell_pos, attn_scores, attn_smax, part_o, hp.n_head, hp.n_head_kv, hp.head_dim,
+                     kv_dim, (int)n_ctx, kq_scale};
+        a.fused = attn_fused;
+        a.stamps = stamp();
+        a.stamps2 = stamp();
+        if (on()) launch_attn(a, stream);
+    }
+    {
+        GemvParams p = base;
+        p.pro = PRO_ATTN;
+        p.attn = AttnPartials{part_o, hp.n_head, hp.head_dim};
+        p.attn_nsplit = attn_fused ? 1 : 0;
+        p.K = hp.n_embd;
+        p.nseg = 1;
+        p.seg[0] = seg_of(L.wo, PAIR_ADJ, EPI_ADD, x);
+        p.seg[0].resid = x;
+        p.seg[0].bias = L.bo;
+        p.stamps = stamp();
+        if (on()) launch_gemv(p, stream);
+    }
+    {
+        GemvParams p = base;
+        p.pro = PRO_LAYERNORM;
+        p.x[0] = x;
+        p.norm_w = L.ffn_norm;
+        p.norm_b = L.ffn_norm_b;
+        p.K = hp.n_embd;
+        p.gelu_tab = m->gelu_tab;
+        p.nseg = 1;
+        p.seg[0] = seg_of(L.up, PAIR_ADJ, EPI_GELU, h);
+        p.seg[0].bias = L.bup;
+        p.stamps = stamp();
+        if (on()) launch_gemv(p, stream);
+    }
+    {
+        GemvParams p = base;
+        p.pro = PRO_PLAIN;
+        p.x[0] = h;
+        p.K = hp.n_ff;
+        p.nseg = 1;
+        p.seg[0] = seg_of(L.down, PAIR_ADJ, EPI_ADD, x);
+        p.seg[0].resid = x;
+        p.seg[0].bias = L.bdown;
+        p.stamps = stamp();
+        if (on()) launch_gemv(p, stream);
+    }
+}
+
+// final RMSNorm (GPT-2: LayerNorm) + output head GEMV of one residual row, then the top-k
 void Ctx::enqueue_output(const float* xrow, unsigned long long* stamps_slab) {
     const HParams& hp = m->hp;
     GemvParams p;
     std::memset(&p, 0, sizeof(p));
-    p.pro = PRO_RMSNORM;
+    p.pro = hp.arch == ARCH_GPT2 ? PRO_LAYERNORM : PRO_RMSNORM;
+    p.norm_b = m->output_norm_b;
     p.nslots = 1;
     p.x[0] = xrow;
     p.norm_w = m->output_norm;
@@ -1010,6 +1166,8 @@ int Ctx::decode(const int32_t* tokens, int n, bool all) {
     for (int i = 0; i < n; ++i)
         if (tokens[i] < 0 || tokens[i] >= m->hp.n_vocab) throw Error("decode: token id out of range");
     if (n_cells + n > (int)n_ctx) return 1;   // no KV slot (llama_decode returns 1)
+    if (m->hp.arch == ARCH_GPT2 && pos_max + n >= m->hp.n_ctx_train)
+        throw Error("decode: gpt2 position past the learned position embeddings (n_ctx_train)");
     if (all && n > (int)n_batch) throw Error("decode: MI_OUT_ALL takes at most n_batch tokens");
     out_rows = 0;
     topk_row = -1;

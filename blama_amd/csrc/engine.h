@@ -7,6 +7,7 @@
 #include "kernels.h"
 #include "mi_engine.h"
 
+#include <functional>
 #include <map>
 #include <memory>
 #include <string>
@@ -56,7 +57,9 @@ struct HParams {
     int n_vocab = 0, n_embd = 0, n_layer = 0, n_head = 0, n_head_kv = 0, n_ff = 0, n_ctx_train = 0;
     int n_rot = 0, head_dim = 0, n_expert = 0, n_expert_used = 0;
     float eps = 1e-5f, rope_base = 10000.0f, freq_scale = 1.0f;
+    int arch = 0;                       // ARCH_LLAMA (llm_build_llama) or ARCH_GPT2 (llm_build_gpt2)
 };
+enum { ARCH_LLAMA = 0, ARCH_GPT2 = 1 };
 
 struct Layer {
     float* attn_norm = nullptr;
@@ -70,6 +73,9 @@ struct Layer {
     int n_qkv = 0;
     QMat qkv[3]{};
     int qkv_nq[3] = {0, 0, 0}, qkv_nk[3] = {0, 0, 0};
+    // GPT-2: LayerNorm biases and the projection biases (attn_qkv is the one fused QKV group)
+    float *attn_norm_b = nullptr, *ffn_norm_b = nullptr;
+    float *bqkv = nullptr, *bo = nullptr, *bup = nullptr, *bdown = nullptr;
 };
 
 struct Model {
@@ -101,8 +107,11 @@ struct Model {
     long long type_bytes[32] = {0};
 
     QMat tok_embd{};
+    QMat pos_embd{};                    // GPT-2 learned positions (position_embd.weight)
     QMat output{};
     float* output_norm = nullptr;
+    float* output_norm_b = nullptr;     // GPT-2
+    unsigned short* gelu_tab = nullptr; // GPT-2: ggml_table_gelu_f16 on the device
     float* rope_freqs = nullptr;
     std::vector<Layer> layers;
 
@@ -204,6 +213,8 @@ struct Ctx {
     ~Ctx();
     void enqueue_step(bool with_logits);
     void enqueue_output(const float* xrow, unsigned long long* stamps_slab);
+    void enqueue_layer_gpt2(int l, const GemvParams& base, __half* kl, __half* vl, float kq_scale,
+                            const std::function<unsigned long long*()>& stamp);
     void decode_batch(const int32_t* tokens, int n);
     void decode_ubatch(const int32_t* tokens, int n, bool all);
     ActQ8 ub_act(int K, int ntok) const;

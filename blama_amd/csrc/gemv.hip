@@ -37,6 +37,7 @@ struct GvSeg {
     const uint8_t* b[4];        // PAIR_AB: planes of B
     float* out;
     const float* resid;
+    const float* bias;          // optional per-row bias (GPT-2 projections)
     int units, blk0, nblk, rows;
     int epi, nq, nk, expA, expB, actB;
 };
@@ -45,6 +46,8 @@ struct GvArgs {
     GvSeg seg[2];
     const float* x[2];
     const float* norm_w;
+    const float* norm_b;        // PRO_LAYERNORM
+    const unsigned short* gelu_tab;   // EPI_GELU: ggml_table_gelu_f16
     const float* attn_o;        // PRO_ATTN: split partials [split][attn_stride]
     const int* tokpos;
     int* cell_pos;
@@ -83,7 +86,7 @@ __host__ __device__ inline int gv_red_off(int nb, int nslots, int n_rot) {
     return gv_rope_off(nb, nslots) + (((n_rot / 2) * 8 + 15) & ~15);
 }
 __host__ inline size_t gv_lds_bytes(int nb, int nslots, int n_rot) {
-    return (size_t)gv_red_off(nb, nslots, n_rot) + GV_NW * 8;
+    return (size_t)gv_red_off(nb, nslots, n_rot) + 2 * GV_NW * 8;   // two rounds of per-wave doubles
 }
 
 __device__ __forceinline__ void lds_barrier() {
@@ -146,7 +149,8 @@ template <int T> __host__ __device__ constexpr bool gv_q80() { return T == T_Q8_
 //   KB  activation blocks of 256 per wave held in registers by the prologue: ceil(nb / GV_NW)
 //   D   register ring depth (items in flight per wave)
 // ---------------------------------------------------------------------------------------------
-template <int T, int SI, int RW, int KB, int D>
+//   GX  the GPT-2 extensions (LayerNorm prologue, bias and GELU epilogues) are compiled in
+template <int T, int SI, int RW, int KB, int D, bool GX>
 __device__ __forceinline__ void gv_body(const GvArgs& a, char* lds) {
     using K = Kq<T>;
     constexpr bool Q80 = gv_q80<T>();
@@ -185,8 +189,10 @@ __device__ __forceinline__ void gv_body(const GvArgs& a, char* lds) {
         if (blk < nb) {
             const float* x0 = pro == PRO_ATTN ? a.attn_o : a.x[0];
             xv[i] = gptr(reinterpret_cast<const f32x4*>(x0))[blk * 64 + lane];
-            if (pro == PRO_RMSNORM) wv[i] = gptr(reinterpret_cast<const f32x4*>(a.norm_w))[blk * 64 + lane];
+            if (pro == PRO_RMSNORM || (GX && pro == PRO_LAYERNORM))
+                wv[i] = gptr(reinterpret_cast<const f32x4*>(a.norm_w))[blk * 64 + lane];
             if (dual) yv[i] = gptr(reinterpret_cast<const f32x4*>(a.x[1]))[blk * 64 + lane];
+            else if (GX && pro == PRO_LAYERNORM) yv[i] = gptr(reinterpret_cast<const f32x4*>(a.norm_b))[blk * 64 + lane];
         }
     }
     int e0 = 0, e1 = 0;
@@ -245,10 +251,12 @@ __device__ __forceinline__ void gv_body(const GvArgs& a, char* lds) {
     struct Slot {
         typename K::Ld w[RW];
         float2 res;
+        float2 bia;
     };
     Slot ring[D];
     int iu = 0, ic = 0;                                 // issue cursor: unit index (0..n_units), chunk
     const bool has_res = S.resid != nullptr;
+    const bool has_bias = GX && S.bias != nullptr && !ab;
     auto issue = [&](Slot& s) {
         const int sb0 = ic * 8 + sbl;
         const int sb = sb0 < nb ? sb0 : nb - 1;
@@ -264,6 +272,16 @@ __device__ __forceinline__ void gv_body(const GvArgs& a, char* lds) {
             const uint8_t* rb = reinterpret_cast<const uint8_t*>(rfl_ptr(S.resid));
             s.res.x = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(buf_rsrc(rb), o0, 0, 0));
             s.res.y = RW == 2 && !ab ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(buf_rsrc(rb), o1, 0, 0)) : 0.0f;
+        }
+        if (has_bias) {   // the unit's bias values, with the unit's last chunk
+            const long long u = u_first + (long long)iu * stride;
+            const long long r0 = u * RW;
+            const bool rv = !park && ic == C - 1;
+            const unsigned o0 = oob((unsigned)(r0 * 4), !rv);
+            const unsigned o1 = oob((unsigned)((r0 + 1) * 4), !(rv && RW == 2 && r0 + 1 < S.rows));
+            const uint8_t* bb = reinterpret_cast<const uint8_t*>(rfl_ptr(S.bias));
+            s.bia.x = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(buf_rsrc(bb), o0, 0, 0));
+            s.bia.y = RW == 2 ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(buf_rsrc(bb), o1, 0, 0)) : 0.0f;
         }
         if (!park && ++ic == C) {
             ic = 0;
@@ -304,6 +322,44 @@ __device__ __forceinline__ void gv_body(const GvArgs& a, char* lds) {
         for (int w = 0; w < GV_NW; ++w) tot += red[w];
         scale = 1.0f / sqrtf((float)(tot / (double)a.K) + a.eps);
     }
+    float mean = 0.0f;
+    if (GX && pro == PRO_LAYERNORM) {
+        // ggml_compute_forward_norm_f32: mean from a double sum, then the double sum of the
+        // f32 squares of (x - mean), variance = (float)(sum2 / n)
+        double s = 0.0;
+#pragma unroll
+        for (int i = 0; i < KB; ++i)
+            if (wave + GV_NW * i < nb) {
+                s += (double)xv[i].x;
+                s += (double)xv[i].y;
+                s += (double)xv[i].z;
+                s += (double)xv[i].w;
+            }
+        s = wave_sum63_d(s);
+        if (lane == 63) red[wave] = s;
+        lds_barrier();
+        double tot = 0.0;
+#pragma unroll
+        for (int w = 0; w < GV_NW; ++w) tot += red[w];
+        mean = (float)(tot / (double)a.K);
+        double s2 = 0.0;
+#pragma unroll
+        for (int i = 0; i < KB; ++i)
+            if (wave + GV_NW * i < nb) {
+                const float v0 = xv[i].x - mean, v1 = xv[i].y - mean, v2 = xv[i].z - mean, v3 = xv[i].w - mean;
+                s2 += (double)(v0 * v0);
+                s2 += (double)(v1 * v1);
+                s2 += (double)(v2 * v2);
+                s2 += (double)(v3 * v3);
+            }
+        s2 = wave_sum63_d(s2);
+        if (lane == 63) red[GV_NW + wave] = s2;
+        lds_barrier();
+        double tot2 = 0.0;
+#pragma unroll
+        for (int w = 0; w < GV_NW; ++w) tot2 += red[GV_NW + w];
+        scale = 1.0f / sqrtf((float)(tot2 / (double)a.K) + a.eps);
+    }
     if (pro == PRO_ATTN) {
         // the other splits of the attention partials (contexts past ATTN_SHORT cells), in split order
         int nsplit = a.attn_nsplit;
@@ -330,6 +386,12 @@ __device__ __forceinline__ void gv_body(const GvArgs& a, char* lds) {
             v[1] = (v[1] * scale) * wv[i].y;
             v[2] = (v[2] * scale) * wv[i].z;
             v[3] = (v[3] * scale) * wv[i].w;
+        }
+        if (GX && pro == PRO_LAYERNORM) {        // (x - mean) * scale, then ggml_mul, ggml_add
+            v[0] = ((v[0] - mean) * scale) * wv[i].x + yv[i].x;
+            v[1] = ((v[1] - mean) * scale) * wv[i].y + yv[i].y;
+            v[2] = ((v[2] - mean) * scale) * wv[i].z + yv[i].z;
+            v[3] = ((v[3] - mean) * scale) * wv[i].w + yv[i].w;
         }
         if (Q80)
             quant_q80_block(v, lane, reinterpret_cast<int8_t*>(lds + L.q80 + blk * GV_ASTR),
@@ -396,6 +458,10 @@ __device__ __forceinline__ void gv_body(const GvArgs& a, char* lds) {
                 y[r] = wave_sum63(acc[r]);
                 acc[r] = 0.0f;
             }
+            if (has_bias) {   // ggml_add of the projection bias
+                y[0] += s.bia.x;
+                if (RW == 2) y[RW - 1] += s.bia.y;
+            }
             if (lane == 63) {
                 const long long u = u_first + (long long)cu * stride;
                 const auto out = gptr_w(S.out);
@@ -437,7 +503,14 @@ __device__ __forceinline__ void gv_body(const GvArgs& a, char* lds) {
                             if (r0 + r >= S.rows) break;
                             const float v = r == 0 ? y[0] : y[RW - 1];
                             const float rv = r == 0 ? s.res.x : s.res.y;
-                            out[r0 + r] = epi == EPI_ADD ? v + rv : v;
+                            float o = v;
+                            if (epi == EPI_ADD) o = v + rv;
+                            if (GX && epi == EPI_GELU) {   // ggml_vec_gelu_f32 (GGML_GELU_FP16 table)
+                                const unsigned short hb = __half_as_ushort(__float2half_rn(v));
+                                const float t = __half2float(__ushort_as_half(gptr(a.gelu_tab)[hb]));
+                                o = v <= -10.0f ? 0.0f : (v >= 10.0f ? v : t);
+                            }
+                            out[r0 + r] = o;
                         }
                     }
                 }
@@ -463,12 +536,13 @@ __device__ __forceinline__ void gv_body(const GvArgs& a, char* lds) {
 
 // T1: -1 one segment; -2 two segments of type T0; else the type of segment 1.
 // TAG: 1 for the FFN gate/up launches, so that the roofline kernel has a symbol of its own in
-// kernel traces (the same code as the QKV launches of an all-Q4_K layer).
+// kernel traces (the same code as the QKV launches of an all-Q4_K layer); 2 for the GPT-2
+// launches (LayerNorm / bias / GELU compiled in, kept out of the LLaMA kernels' registers).
 template <int T0, int T1, int RW, int KB, int D, int TAG>
 __global__ __launch_bounds__(GV_NW * 64) void gemv_kernel(const GvArgs a) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
-    if (T1 == -1 || (int)blockIdx.x < a.seg[1].blk0) gv_body<T0, 0, RW, KB, D>(a, lds);
-    else gv_body<(T1 < 0 ? T0 : T1), 1, RW, KB, D>(a, lds);
+    if (T1 == -1 || (int)blockIdx.x < a.seg[1].blk0) gv_body<T0, 0, RW, KB, D, TAG == 2>(a, lds);
+    else gv_body<(T1 < 0 ? T0 : T1), 1, RW, KB, D, TAG == 2>(a, lds);
 }
 
 typedef void (*GvFn)(const GvArgs);
@@ -493,7 +567,8 @@ GvFn gv_fn_kb(int kb) {
 template <int T0, int RW>
 GvFn gv_fn_pair(int t1, int kb, int tag) {
     switch (t1) {
-    case -1: return tag && RW == 2 ? gv_fn_kb<T0, -1, RW, 1>(kb) : gv_fn_kb<T0, -1, RW, 0>(kb);
+    case -1: return tag == 2 ? gv_fn_kb<T0, -1, RW, 2>(kb)
+                  : tag && RW == 2 ? gv_fn_kb<T0, -1, RW, 1>(kb) : gv_fn_kb<T0, -1, RW, 0>(kb);
     case -2: return gv_fn_kb<T0, -2, RW, 0>(kb);
     case T_Q6_K: return gv_fn_kb<T0, T_Q6_K, RW, 0>(kb);
     case T_Q8_0: return gv_fn_kb<T0, T_Q8_0, RW, 0>(kb);
@@ -562,7 +637,7 @@ void init_kernel_attributes() {
         for (int kb : {1, 2, 4})
             for (int t0 : types)
                 for (int t1 : {-1, t0, (int)T_Q6_K, (int)T_Q8_0}) {
-                    for (int tag = 0; tag <= 1; ++tag) {
+                    for (int tag = 0; tag <= 2; ++tag) {
                         GvFn f = t1 < 0 ? gv_fn(1, t0, t0, rw, kb, tag) : gv_fn(2, t0, t1, rw, kb, tag);
                         if (f)
                             MI_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(f),
@@ -585,14 +660,20 @@ void launch_gemv(const GemvParams& p, hipStream_t s, hipEvent_t ev_start, hipEve
         if ((g.epi == EPI_SWIGLU || g.epi == EPI_MOE_DOWN) != (g.pair == PAIR_AB))
             throw Error("gemv: SwiGLU / MoE-down epilogues take a PAIR_AB segment");
         if ((g.epi == EPI_ADD || g.epi == EPI_MOE_DOWN) && !g.resid) throw Error("gemv: residual epilogue without resid");
+        if (g.epi == EPI_GELU && (!p.gelu_tab || g.pair == PAIR_AB)) throw Error("gemv: GELU epilogue needs the table, one matrix");
+        if (g.bias && g.pair == PAIR_AB) throw Error("gemv: no bias on a PAIR_AB segment");
     }
     if (p.nseg == 2 && !gemv_pair_supported(p.seg[0].A.type, p.seg[1].A.type))
         throw Error("gemv: unsupported pair of segment types");
     if (p.pro == PRO_ATTN && (p.attn.n_head * p.attn.head_dim != p.K)) throw Error("gemv: attention combine needs K == n_head*head_dim");
-    if (p.nslots == 2 && p.pro == PRO_RMSNORM) throw Error("gemv: a second activation slot is plain");
+    if (p.nslots == 2 && (p.pro == PRO_RMSNORM || p.pro == PRO_LAYERNORM)) throw Error("gemv: a second activation slot is plain");
+    if (p.pro == PRO_LAYERNORM && (!p.norm_w || !p.norm_b)) throw Error("gemv: layer norm needs its weight and bias");
     const int kb = gv_kb(p.K);
+    bool gx = p.pro == PRO_LAYERNORM;
+    for (int i = 0; i < p.nseg; ++i) gx = gx || p.seg[i].bias || p.seg[i].epi == EPI_GELU;
+    if (gx && p.nseg != 1) throw Error("gemv: LayerNorm / bias / GELU launches take one segment");
     GvFn fn = gv_fn(p.nseg, p.seg[0].A.type, p.seg[p.nseg - 1].A.type, rw2 ? 2 : 1, kb,
-                    p.nseg == 1 && p.seg[0].epi == EPI_SWIGLU ? 1 : 0);
+                    gx ? 2 : (p.nseg == 1 && p.seg[0].epi == EPI_SWIGLU ? 1 : 0));
     if (!fn) throw Error("gemv: no kernel for this type / shape");
 
     GvArgs a;
@@ -611,6 +692,7 @@ void launch_gemv(const GemvParams& p, hipStream_t s, hipEvent_t ev_start, hipEve
         }
         o.out = g.out;
         o.resid = g.resid;
+        o.bias = g.bias;
         o.rows = g.A.rows;
         const int rw = rw2 ? 2 : 1;
         o.units = g.pair == PAIR_AB ? g.A.rows : (g.A.rows + rw - 1) / rw;
@@ -631,6 +713,8 @@ void launch_gemv(const GemvParams& p, hipStream_t s, hipEvent_t ev_start, hipEve
     a.x[0] = p.x[0];
     a.x[1] = p.nslots > 1 ? p.x[1] : p.x[0];
     a.norm_w = p.norm_w;
+    a.norm_b = p.norm_b;
+    a.gelu_tab = p.gelu_tab;
     a.attn_o = p.attn.o;
     a.tokpos = p.tokpos;
     a.cell_pos = p.cell_pos;

@@ -19,11 +19,15 @@ enum Epi {
     EPI_V = 7,        //   -> f16 V cache
     EPI_SWIGLU = 5,   // out[u] = silu(yA) * yB            (LLM_FFN_SILU + LLM_FFN_PAR)
     EPI_MOE_DOWN = 6, // out[u] = (yA*wA + yB*wB) + resid[u] (build_moe_ffn aggregation)
+    EPI_GELU = 8,     // out[r] = gelu(y + bias[r])       (llm_build_gpt2 FFN: LLM_FFN_GELU, LLM_FFN_SEQ)
 };
+// Every epilogue but SwiGLU / MoE-down adds GemvSeg::bias[r] to y first when it is set (the
+// ggml_add of a GPT-2 projection bias, before RoPE-less KV append, residual add or GELU).
 enum Pro {
     PRO_PLAIN = 0,    // activation = x[0] (and x[1] for a second slot)
     PRO_RMSNORM = 1,  // activation = rms_norm(x[0]) * norm_w
     PRO_ATTN = 2,     // activation = the attention partials of the splits, added in split order
+    PRO_LAYERNORM = 3,// activation = layer_norm(x[0]) * norm_w + norm_b  (build_norm LLM_NORM)
 };
 
 struct GemvSeg {
@@ -34,6 +38,7 @@ struct GemvSeg {
     int actB;             // activation slot of the B rows (MoE down: 1)
     float* out;
     const float* resid;   // EPI_ADD / EPI_MOE_DOWN (may alias out)
+    const float* bias;    // optional per-row bias (GPT-2), added before the epilogue
 };
 
 // Attention split over cells: split s of q head h holds the partial sum
@@ -70,8 +75,10 @@ struct GemvParams {
     int nslots;               // 1, or 2 (MoE down: x[1] feeds the B rows)
     const float* x[2];
     const float* norm_w;
+    const float* norm_b;      // PRO_LAYERNORM bias
     float eps;
     int K;                    // activation length (multiple of 256, <= 14336)
+    const unsigned short* gelu_tab;   // EPI_GELU: ggml_table_gelu_f16 (65536 f16 bit patterns)
     // RoPE / KV cache (EPI_QKV)
     const int* tokpos;        // {token, pos, cell, -}
     int* cell_pos;            // cell -> position (written with the K rows)
@@ -137,6 +144,8 @@ struct EmbedParams {
     const int* tokpos;
     float* out;
     int n_embd;
+    QMat P;                    // GPT-2: learned position embedding (row = the token's position),
+    int has_pos;               // added to the token row (ggml_add of the two get_rows)
 };
 void launch_embed(const EmbedParams& p, hipStream_t s);
 

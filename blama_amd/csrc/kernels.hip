@@ -335,17 +335,25 @@ __device__ float dequant_elem(const QMat& M, long long row, int col) {
     }
 }
 
+// get_rows(tok_embd, token) (+ get_rows(position_embd, pos) for GPT-2, llm_build_gpt2's
+// inpL = ggml_add(tok rows, pos rows))
 __global__ void embed_kernel(const EmbedParams P) {
     const long long tok = P.tokpos[0];
-    for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < P.n_embd; c += gridDim.x * blockDim.x)
-        P.out[c] = dequant_elem(P.E, tok, c);
+    const long long pos = P.tokpos[1];
+    for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < P.n_embd; c += gridDim.x * blockDim.x) {
+        const float e = dequant_elem(P.E, tok, c);
+        P.out[c] = P.has_pos ? e + dequant_elem(P.P, pos, c) : e;
+    }
 }
 
 __global__ void embed_multi_kernel(const EmbedParams P) {
     const long long tok = P.tokpos[blockIdx.y * 4];
+    const long long pos = P.tokpos[blockIdx.y * 4 + 1];
     float* out = P.out + (long long)blockIdx.y * P.n_embd;
-    for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < P.n_embd; c += gridDim.x * blockDim.x)
-        out[c] = dequant_elem(P.E, tok, c);
+    for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < P.n_embd; c += gridDim.x * blockDim.x) {
+        const float e = dequant_elem(P.E, tok, c);
+        out[c] = P.has_pos ? e + dequant_elem(P.P, pos, c) : e;
+    }
 }
 
 void launch_embed_multi(const EmbedParams& p, int ntok, hipStream_t s) {

@@ -93,6 +93,9 @@ _SIGS = {
                                     C.c_int32, _P]),
     "mi_op_gemv_bench": (C.c_int32, [C.c_int32, C.c_int32, _P, C.c_int32, C.c_int32, C.c_int32,
                                      C.POINTER(C.c_float)]),
+    "mi_op_gemm": (C.c_int32, [C.c_int32, C.c_int32, _P, _P, C.c_int32, C.c_int32, C.c_int32, _P, _P]),
+    "mi_op_attention_batch": (C.c_int32, [C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
+                                          _P, _P, _P, _P, _P, _P, _P]),
 }
 
 
@@ -368,3 +371,35 @@ def op_attention(q: np.ndarray, k16: np.ndarray, v16: np.ndarray, n_head_kv: int
     _check(lib().mi_op_attention(device, n_head, n_head_kv, hd, n, _ptr(q), _ptr(k16), _ptr(v16), _ptr(cp), pos,
                                  _ptr(out)), "op_attention")
     return out.reshape(n_head, hd)
+
+
+def op_gemm(type_: int, raw: np.ndarray, rows: int, K: int, x: np.ndarray, raw_up=None,
+            device: int = 0) -> np.ndarray:
+    """Prompt-batch GEMM (mmq32) of x (ntok, K) f32 -> (ntok, rows); with raw_up the gate/up
+    SwiGLU pair silu(gate . x) * (up . x)."""
+    raw = np.ascontiguousarray(raw, np.uint8)
+    x = np.ascontiguousarray(x, np.float32)
+    ntok = x.shape[0]
+    up = None if raw_up is None else np.ascontiguousarray(raw_up, np.uint8)
+    y = np.empty((ntok, rows), np.float32)
+    _check(lib().mi_op_gemm(device, type_, _ptr(raw), None if up is None else _ptr(up), rows, K, ntok, _ptr(x),
+                            _ptr(y)), "op_gemm")
+    return y
+
+
+def op_attention_batch(q: np.ndarray, k16: np.ndarray, v16: np.ndarray, n_head_kv: int, tok_cell, tok_pos=None,
+                       cell_pos=None, device: int = 0) -> np.ndarray:
+    """q: (ntok, n_head, hd) f32; k16/v16: (n_cells, n_head_kv*hd) f16; token t in cell tok_cell[t] at
+    position tok_pos[t] (default: its cell) -> (ntok, n_head, hd) f32 (attn_mfma)."""
+    q = np.ascontiguousarray(q, np.float32)
+    ntok, n_head, hd = q.shape
+    k16 = np.ascontiguousarray(k16, np.float16)
+    v16 = np.ascontiguousarray(v16, np.float16)
+    n = k16.shape[0]
+    cp = np.ascontiguousarray(np.arange(n) if cell_pos is None else cell_pos, np.int32)
+    tc = np.ascontiguousarray(tok_cell, np.int32)
+    tpos = np.ascontiguousarray(tc if tok_pos is None else tok_pos, np.int32)
+    out = np.empty((ntok, n_head, hd), np.float32)
+    _check(lib().mi_op_attention_batch(device, n_head, n_head_kv, hd, n, ntok, _ptr(q), _ptr(k16), _ptr(v16),
+                                       _ptr(cp), _ptr(tc), _ptr(tpos), _ptr(out)), "op_attention_batch")
+    return out

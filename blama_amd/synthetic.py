@@ -40,6 +40,7 @@ class LlamaConfig:
     ftype: str            # "Q4_K_M", "Q5_K_M", "Q6_K", "Q8_0", "Q4_K"...
     n_expert: int = 0
     n_expert_used: int = 0
+    arch: str = "llama"   # "llama" or "gpt2" (llm_build_gpt2)
 
     @property
     def head_dim(self):
@@ -64,6 +65,14 @@ CONFIGS = {
     "tiny1-q4_k_m": LlamaConfig("tiny1", 512, 256, 1, 4, 2, 512, 256, 10000.0, 1e-5, "Q4_K_M"),
     "tiny-moe-q5_k_m": LlamaConfig("tiny-moe", 512, 256, 2, 4, 2, 512, 256, 1e6, 1e-5,
                                     "Q5_K_M", n_expert=4, n_expert_used=2),
+    # the reference's own KAT model shape (gpt2-117m-q6_k, t-integration.cpp:25): 12 x 768,
+    # 12 heads of 64, n_ff 3072, V 50257, 1024 positions, every matrix Q6_K, tied output head
+    "gpt2-117m-q6_k": LlamaConfig("GPT-2-117M", 50257, 768, 12, 12, 12, 3072, 1024, 10000.0, 1e-5,
+                                  "Q6_K", arch="gpt2"),
+    "tiny-gpt2-q6_k": LlamaConfig("tiny-gpt2", 700, 256, 2, 4, 4, 768, 128, 10000.0, 1e-5, "Q6_K",
+                                  arch="gpt2"),
+    "tiny-gpt2-q8_0": LlamaConfig("tiny-gpt2", 600, 512, 2, 8, 8, 1024, 128, 10000.0, 1e-5, "Q8_0",
+                                  arch="gpt2"),
 }
 
 
@@ -72,10 +81,49 @@ def use_more_bits(i: int, n: int) -> bool:
     return i < n // 8 or i >= 7 * n // 8 or (i - n // 8) % 3 == 2
 
 
+def _gpt2_types(cfg, base) -> dict:
+    """llm_build_gpt2's tensors (LLM_ARCH_GPT2 in src/llama-arch.cpp): every matrix of the
+    file type, LayerNorm weights / biases and the matrix biases F32, no output.weight (the
+    head is token_embd, TENSOR_DUPLICATED in llama-model.cpp)."""
+    t = {"token_embd.weight": base, "position_embd.weight": base,
+         "output_norm.weight": F32, "output_norm.bias": F32}
+    for i in range(cfg.n_layer):
+        p = f"blk.{i}."
+        for n in ("attn_norm", "ffn_norm"):
+            t[p + n + ".weight"] = F32
+            t[p + n + ".bias"] = F32
+        for n in ("attn_qkv", "attn_output", "ffn_up", "ffn_down"):
+            t[p + n + ".weight"] = base
+            t[p + n + ".bias"] = F32
+    return t
+
+
+def _gpt2_shapes(cfg) -> dict:
+    d = cfg.n_embd
+    s = {"token_embd.weight": (d, cfg.n_vocab), "position_embd.weight": (d, cfg.n_ctx_train),
+         "output_norm.weight": (d,), "output_norm.bias": (d,)}
+    for i in range(cfg.n_layer):
+        p = f"blk.{i}."
+        for n in ("attn_norm", "ffn_norm"):
+            s[p + n + ".weight"] = (d,)
+            s[p + n + ".bias"] = (d,)
+        s[p + "attn_qkv.weight"] = (d, 3 * d)
+        s[p + "attn_qkv.bias"] = (3 * d,)
+        s[p + "attn_output.weight"] = (d, d)
+        s[p + "attn_output.bias"] = (d,)
+        s[p + "ffn_up.weight"] = (d, cfg.n_ff)
+        s[p + "ffn_up.bias"] = (cfg.n_ff,)
+        s[p + "ffn_down.weight"] = (cfg.n_ff, d)
+        s[p + "ffn_down.bias"] = (d,)
+    return s
+
+
 def tensor_types(cfg: LlamaConfig) -> dict:
     """name -> ggml type for every weight (the Q*_K_M mixes of llama_tensor_get_type)."""
     base = {"Q4_K_M": Q4_K, "Q5_K_M": Q5_K, "Q6_K": Q6_K, "Q8_0": Q8_0, "Q4_K": Q4_K,
             "Q5_K": Q5_K}[cfg.ftype]
+    if cfg.arch == "gpt2":
+        return _gpt2_types(cfg, base)
     mixed = cfg.ftype in ("Q4_K_M", "Q5_K_M")
     t = {"token_embd.weight": base, "output_norm.weight": F32,
          "output.weight": Q8_0 if base == Q8_0 else Q6_K}
@@ -110,6 +158,8 @@ def tensor_types(cfg: LlamaConfig) -> dict:
 
 def tensor_shapes(cfg: LlamaConfig) -> dict:
     """name -> ggml ne shape (ne0 = input dim K)."""
+    if cfg.arch == "gpt2":
+        return _gpt2_shapes(cfg)
     d, kv = cfg.n_embd, cfg.n_head_kv * cfg.head_dim
     s = {"token_embd.weight": (d, cfg.n_vocab), "output_norm.weight": (d,),
          "output.weight": (d, cfg.n_vocab)}
@@ -324,6 +374,8 @@ def _init_params(cfg):
     env = dict(kv.split("=") for kv in os.environ.get("BLAMA_SYNTH_INIT", "").split(",") if kv)
     p = {"base": 0.03, "qk": 0.01, "resid": 0.03 / np.sqrt(2.0 * cfg.n_layer), "embd": 8.0,
          "alpha": 0.01, "nsucc": 10}
+    if cfg.arch == "gpt2":
+        p["embd"] = 1.0   # the embedding is also the (tied) output head: logits O(sqrt(d))
     for k, v in env.items():
         p[k] = float(v)
     return p
@@ -429,7 +481,7 @@ def build_gguf(cfg: LlamaConfig, seed: int = 0, header_only: bool = False, vocab
     metadata + tensor table, enough for a vocab-only or no_upload replica load).
     vocab: a byte-level BPE vocabulary from bpe_vocab() instead of the SPM one."""
     w = gguf.GGUFWriter()
-    arch = "llama"
+    arch = cfg.arch
     w.add_str("general.architecture", arch)
     w.add_str("general.name", f"synthetic {cfg.name} {cfg.ftype}")
     w.add_u32("general.file_type", {"Q8_0": 7, "Q4_K_M": 15, "Q5_K_M": 17, "Q6_K": 18,
@@ -439,10 +491,13 @@ def build_gguf(cfg: LlamaConfig, seed: int = 0, header_only: bool = False, vocab
     w.add_u32(f"{arch}.block_count", cfg.n_layer)
     w.add_u32(f"{arch}.feed_forward_length", cfg.n_ff)
     w.add_u32(f"{arch}.attention.head_count", cfg.n_head)
-    w.add_u32(f"{arch}.attention.head_count_kv", cfg.n_head_kv)
-    w.add_f32(f"{arch}.attention.layer_norm_rms_epsilon", cfg.eps)
-    w.add_f32(f"{arch}.rope.freq_base", cfg.rope_base)
-    w.add_u32(f"{arch}.rope.dimension_count", cfg.head_dim)
+    if arch == "gpt2":   # LLM_KV_ATTENTION_LAYERNORM_EPS; no RoPE keys
+        w.add_f32(f"{arch}.attention.layer_norm_epsilon", cfg.eps)
+    else:
+        w.add_u32(f"{arch}.attention.head_count_kv", cfg.n_head_kv)
+        w.add_f32(f"{arch}.attention.layer_norm_rms_epsilon", cfg.eps)
+        w.add_f32(f"{arch}.rope.freq_base", cfg.rope_base)
+        w.add_u32(f"{arch}.rope.dimension_count", cfg.head_dim)
     w.add_u32(f"{arch}.vocab_size", cfg.n_vocab)
     if cfg.n_expert:
         w.add_u32(f"{arch}.expert_count", cfg.n_expert)
@@ -467,7 +522,7 @@ def build_gguf(cfg: LlamaConfig, seed: int = 0, header_only: bool = False, vocab
         w.add_u32("tokenizer.ggml.bos_token_id", vocab["bos"])
         w.add_u32("tokenizer.ggml.eos_token_id", vocab["eos"])
         w.add_u32("tokenizer.ggml.eot_token_id", vocab["eot"])
-    w.add_bool("tokenizer.ggml.add_bos_token", True)
+    w.add_bool("tokenizer.ggml.add_bos_token", arch != "gpt2")
     types = tensor_types(cfg)
     shapes = tensor_shapes(cfg)
     for name in types:
@@ -485,6 +540,11 @@ def build_gguf(cfg: LlamaConfig, seed: int = 0, header_only: bool = False, vocab
         if name.endswith("norm.weight"):
             v = view.view(np.float32)
             v[:] = rng.uniform(0.8, 1.2, v.size).astype(np.float32)
+        elif name.endswith(".bias"):
+            v = view.view(np.float32)
+            v[:] = (rng.standard_normal(v.size) * 0.02).astype(np.float32)
+        elif name == "position_embd.weight":
+            fill_quant(view, t, rng, std=0.1)
         elif name.endswith("ffn_gate_inp.weight"):
             fill_quant(view, t, rng, std=0.05)
         else:

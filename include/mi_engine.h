@@ -166,6 +166,21 @@ int32_t mi_op_topk(int32_t device, const float* logits, int32_t n, int32_t k, in
 int32_t mi_op_attention(int32_t device, int32_t n_head, int32_t n_head_kv, int32_t head_dim, int32_t n_cells,
                         const float* q, const uint16_t* k_f16, const uint16_t* v_f16, const int32_t* cell_pos,
                         int32_t pos, float* out);
+/* The prompt-batch GEMM (mmq32: int8 MFMA, Session.cpp:381-392's n_ubatch physical batches) of
+ * ntok <= 512 token rows x[ntok][K] against a rows x K Q4_K / Q6_K / Q8_0 matrix: each row's
+ * activation is quantised to Q8_K (Q8_0 for Q8_0 weights) as the CPU graph does, then
+ * y[t][r] = vec_dot(W_r, q(x_t)).  With raw_up non-NULL the launch is the FFN gate/up pair
+ * (raw_blocks = gate): y[t][r] = silu(gate_r . q(x_t)) * (up_r . q(x_t)).  y: [ntok][rows]. */
+int32_t mi_op_gemm(int32_t device, int32_t type, const void* raw_blocks, const void* raw_up, int32_t rows,
+                   int32_t K, int32_t ntok, const float* x, float* y);
+/* The prompt-batch attention (attn_mfma: f16 MFMA) of ntok query tokens q[ntok][n_head*head_dim]
+ * over an f16 cache of n_cells cells: token t sits in cell tok_cell[t] at position tok_pos[t] and
+ * sees the cells c <= tok_cell[t] whose cell_pos[c] <= tok_pos[t] (llm_build_llama's kq_mask).
+ * tok_cell must be ascending.  out: [ntok][n_head*head_dim]. */
+int32_t mi_op_attention_batch(int32_t device, int32_t n_head, int32_t n_head_kv, int32_t head_dim,
+                              int32_t n_cells, int32_t ntok, const float* q, const uint16_t* k_f16,
+                              const uint16_t* v_f16, const int32_t* cell_pos, const int32_t* tok_cell,
+                              const int32_t* tok_pos, float* out);
 /* Median device time (us) of `iters` launches of the GEMV above (micro-benchmark). */
 int32_t mi_op_gemv_bench(int32_t device, int32_t type, const void* raw_blocks, int32_t rows, int32_t K,
                          int32_t iters, float* median_us);

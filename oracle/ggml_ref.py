@@ -13,7 +13,8 @@ this container.  The functions below restate the published
 algorithms of that tag's CPU backend (``ggml/src/ggml-quants.c``,
 ``ggml/src/ggml-cpu/ggml-cpu-quants.c``, ``ggml/src/ggml-cpu/ops`` in
 ``ggml-cpu.c``) and of ``src/llama-graph.cpp`` / ``src/llama-model.cpp``
-(``llm_build_llama``) and are anchored on the reference's call sites:
+(``llm_build_llama``, and ``llm_build_gpt2`` for SURVEY.md §8 row f4) and are anchored
+on the reference's call sites:
 
 * ``Model::Params{.gpu=false}`` selects this CPU path
   (``inference/code/llama/Model.cpp:13-16,28``);
@@ -27,7 +28,7 @@ Pinning
 -------
 The only golden vector the reference holds that runs without model files is
 the LogitComparer known-answer test ``inference/test/t-LogitComparer.cpp:13-39``
-(pinned in ``tests/test_oracle_golden.py``).  The quant formats, the integer
+(pinned in ``tests/test_oracle.py``).  The quant formats, the integer
 dot products and the llama graph are **parity unpinned**: no reference test
 covers Q4_K/Q5_K/Q6_K/Q8_0 LLaMA arithmetic, and ggml itself cannot be built
 here.  Parity for those rows rests on this restatement,
@@ -348,6 +349,58 @@ def rms_norm(x: np.ndarray, eps: float) -> np.ndarray:
     return (x * np.float32(scale)).astype(np.float32)
 
 
+def layer_norm(x: np.ndarray, eps: float) -> np.ndarray:
+    """ggml_compute_forward_norm_f32 (ggml-cpu.c, b5187): sum in double, mean = (float)(sum/n);
+    v = x - mean (f32), y = v, sum2 += (double)(v*v) (the square rounded to f32 first);
+    variance = (float)(sum2/n); y *= 1.0f/sqrtf(variance + eps).  build_norm (LLM_NORM) then
+    multiplies by the weight and adds the bias as separate f32 ops (ggml_mul, ggml_add)."""
+    x = np.asarray(x, np.float32)
+    n = x.shape[-1]
+    mean = np.float32(np.sum(x.astype(np.float64)) / n)
+    v = (x - mean).astype(np.float32)
+    sum2 = np.sum((v * v).astype(np.float32).astype(np.float64))
+    var = np.float32(sum2 / n)
+    scale = np.float32(1.0) / np.sqrt(np.float32(var + np.float32(eps)), dtype=np.float32)
+    return (v * scale).astype(np.float32)
+
+
+_GELU_TAB = None
+
+
+def gelu_table() -> np.ndarray:
+    """ggml_table_gelu_f16 (ggml-cpu.c init, GGML_GELU_FP16 is defined in b5187): for every f16
+    bit pattern u, fp16(ggml_gelu_f32(fp32(u))) with ggml_gelu_f32(x) =
+    0.5f*x*(1.0f + tanhf(SQRT_2_OVER_PI*x*(1.0f + GELU_COEF_A*x*x))), evaluated in f32 with the C
+    library's tanhf (the same call the reference's x86 build makes).  Returns uint16[65536]."""
+    global _GELU_TAB
+    if _GELU_TAB is None:
+        import ctypes
+        libm = ctypes.CDLL("libm.so.6")
+        libm.tanhf.restype = ctypes.c_float
+        libm.tanhf.argtypes = [ctypes.c_float]
+        xs = np.arange(65536, dtype=np.uint16).view(np.float16).astype(np.float32)
+        xs = np.where(np.isfinite(xs), xs, np.float32(0.0)).astype(np.float32)   # inf/nan rows: unused
+        a = np.float32(0.044715)
+        k = np.float32(0.79788456080286535587989211986876)
+        inner = (k * xs).astype(np.float32) * ((np.float32(1.0) + (a * xs).astype(np.float32) * xs)
+                                               .astype(np.float32))
+        inner = inner.astype(np.float32)
+        th = np.array([libm.tanhf(float(v)) if np.isfinite(v) else (1.0 if v > 0 else -1.0) for v in inner],
+                      np.float32)
+        y = ((np.float32(0.5) * xs).astype(np.float32) * (np.float32(1.0) + th).astype(np.float32)).astype(np.float32)
+        with np.errstate(invalid="ignore", over="ignore"):
+            _GELU_TAB = y.astype(np.float16).view(np.uint16)
+    return _GELU_TAB
+
+
+def gelu(x: np.ndarray) -> np.ndarray:
+    """ggml_vec_gelu_f32 with GGML_GELU_FP16: x <= -10 -> 0, x >= 10 -> x, else the f16 table at
+    fp16(x)."""
+    x = np.asarray(x, np.float32)
+    t = gelu_table()[x.astype(np.float16).view(np.uint16)].view(np.float16).astype(np.float32)
+    return np.where(x <= -10.0, np.float32(0.0), np.where(x >= 10.0, x, t)).astype(np.float32)
+
+
 def silu(x: np.ndarray) -> np.ndarray:
     """ggml_silu_f32: x/(1+expf(-x)) (ggml's SIMD expf differs by <=1-2 ulp)."""
     x = np.asarray(x, np.float32)
@@ -542,6 +595,7 @@ class HParams:
     n_rot: int
     n_expert: int = 0
     n_expert_used: int = 0
+    arch: str = "llama"      # "llama" (llm_build_llama) or "gpt2" (llm_build_gpt2)
 
     @property
     def head_dim(self):
@@ -638,8 +692,66 @@ class LlamaOracle:
         if neg:
             self.kv_seq_rm(-(1 << 30), 0)
 
+    def _row(self, name, r):
+        t = self.tensors[name]
+        rb = row_bytes(t.type, t.shape[0])
+        return dequantize(t.data.reshape(-1)[r * rb:(r + 1) * rb], t.type)
+
+    def _vec(self, name):
+        return self._w(name).astype(np.float32)
+
+    def _norm(self, x, name):
+        """build_norm(LLM_NORM): layer_norm, * weight, + bias (separate f32 ops)."""
+        y = (layer_norm(x, self.hp.eps) * self._vec(name + ".weight")).astype(np.float32)
+        return (y + self._vec(name + ".bias")).astype(np.float32)
+
+    def _decode_one_gpt2(self, token: int) -> np.ndarray:
+        """llm_build_gpt2 (src/llama-model.cpp, b5187) for one token: token + learned position
+        embedding; per layer LayerNorm -> fused QKV + bias -> attention (no RoPE) -> WO + bias
+        -> residual; LayerNorm -> up + bias -> GELU -> down + bias -> residual; final LayerNorm
+        and the output head (tied to token_embd when output.weight is absent)."""
+        hp = self.hp
+        hd = hp.head_dim
+        d = hp.n_embd
+        pos = (max(self.cell_pos) + 1) if self.n_past else 0
+        cell = self.n_past
+        assert cell < self.n_ctx and pos < hp.n_ctx_train
+        x = (self._row("token_embd.weight", token) + self._row("position_embd.weight", pos)).astype(np.float32)
+        scale = np.float32(1.0) / np.sqrt(np.float32(hd), dtype=np.float32)
+        for il in range(hp.n_layer):
+            b = f"blk.{il}."
+            cur = self._norm(x, b + "attn_norm")
+            qkv = (self._mm(b + "attn_qkv.weight", cur) + self._vec(b + "attn_qkv.bias")).astype(np.float32)
+            q = qkv[:d].reshape(hp.n_head, hd)
+            k = qkv[d:2 * d]
+            v = qkv[2 * d:3 * d]
+            self.kcache[il][cell] = f32_to_f16(k)
+            self.vcache[il][cell] = f32_to_f16(v)
+            vis = [c for c in range(cell + 1) if c == cell or self.cell_pos[c] <= pos]
+            Kc = self.kcache[il][vis].reshape(len(vis), hp.n_head_kv, hd)
+            Vc = self.vcache[il][vis].reshape(len(vis), hp.n_head_kv, hd)
+            ratio = hp.n_head // hp.n_head_kv
+            att = np.empty((hp.n_head, hd), np.float32)
+            for h in range(hp.n_head):
+                att[h] = attention_head(q[h], Kc[:, h // ratio], Vc[:, h // ratio], scale)
+            cur = (self._mm(b + "attn_output.weight", att.reshape(-1)) + self._vec(b + "attn_output.bias")).astype(np.float32)
+            x = (cur + x).astype(np.float32)
+            cur = self._norm(x, b + "ffn_norm")
+            u = (self._mm(b + "ffn_up.weight", cur) + self._vec(b + "ffn_up.bias")).astype(np.float32)
+            hh = gelu(u)
+            cur = (self._mm(b + "ffn_down.weight", hh) + self._vec(b + "ffn_down.bias")).astype(np.float32)
+            x = (cur + x).astype(np.float32)
+        cur = self._norm(x, "output_norm")
+        out = self.tensors.get("output.weight", self.tensors["token_embd.weight"])
+        logits = mul_mat_vec(out.data, out.type, out.shape[0], cur)
+        self.cell_pos.append(pos)
+        self.n_past += 1
+        return logits
+
     def decode_one(self, token: int) -> np.ndarray:
         """One llama_decode of a single token at position max(pos)+1; returns logits f32[V]."""
+        if self.hp.arch == "gpt2":
+            return self._decode_one_gpt2(token)
         hp = self.hp
         hd = hp.head_dim
         pos = (max(self.cell_pos) + 1) if self.n_past else 0

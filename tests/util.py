@@ -28,10 +28,11 @@ def oracle_from_gguf(buf, n_ctx: int = 0) -> R.LlamaOracle:
         n_vocab=int(te.shape[1]), n_embd=n_embd, n_layer=int(kv[f"{a}.block_count"]),
         n_head=n_head, n_head_kv=int(kv.get(f"{a}.attention.head_count_kv", n_head)),
         n_ff=int(kv[f"{a}.feed_forward_length"]), n_ctx_train=int(kv[f"{a}.context_length"]),
-        eps=float(kv[f"{a}.attention.layer_norm_rms_epsilon"]),
+        eps=float(kv.get(f"{a}.attention.layer_norm_rms_epsilon", kv.get(f"{a}.attention.layer_norm_epsilon", 1e-5))),
         rope_base=float(kv.get(f"{a}.rope.freq_base", 10000.0)),
         n_rot=int(kv.get(f"{a}.rope.dimension_count", n_embd // n_head)),
-        n_expert=int(kv.get(f"{a}.expert_count", 0)), n_expert_used=int(kv.get(f"{a}.expert_used_count", 0)))
+        n_expert=int(kv.get(f"{a}.expert_count", 0)), n_expert_used=int(kv.get(f"{a}.expert_used_count", 0)),
+        arch=a)
     tens = {k: R.Tensor(v.type, v.shape, v.data) for k, v in rd.tensors.items()}
     return R.LlamaOracle(hp, tens, n_ctx=n_ctx)
 
