@@ -549,17 +549,19 @@ std::vector<Token> Vocab::tokenize(std::string_view text, bool addSpecial, bool 
 // ---------------------------------------------------------------- Sampler ---
 Sampler::Sampler(Model& model, const Params& params)
     : m_model(model), m_params(params), m_mu(2.0f * params.mirostat.tau), m_xtcRng(params.rngSeed), m_rng(params.rngSeed) {
-    if (!params.grammar.empty()) BL_THROW("grammar-constrained sampling is not served by this build");
     if (params.mirostat.ver > 2) BL_THROW("Unsupported mirostat version");   // Sampler.cpp:67-69
+    if (!params.grammar.empty()) m_grammar = std::make_unique<Grammar>(params.grammar, "root");
 }
 
-void Sampler::accept(Token id, bool) {
+void Sampler::accept(Token id, bool acceptGrammar) {
+    if (acceptGrammar && m_grammar) m_grammar->accept(m_model.vocab(), id);   // Sampler.cpp:100-106
     m_prev.push_back(id);
     const size_t w = (size_t)std::max(0, m_params.repetitionPenalty.numTokens);
     if (m_prev.size() > w) m_prev.erase(m_prev.begin(), m_prev.end() - (std::ptrdiff_t)w);
 }
 
 void Sampler::reset() {
+    if (m_grammar) m_grammar->reset();
     m_prev.clear();
     m_rng.seed(m_params.rngSeed);   // llama_sampler_dist reset re-seeds
     m_xtcRng.seed(m_params.rngSeed);
@@ -785,7 +787,34 @@ Token Sampler::applyMirostat(std::vector<Candidate>& cur) {
     return cur[idx].id;
 }
 
-Token Sampler::sample(mi_ctx* ctx) {
+Token Sampler::sample(mi_ctx* ctx, int idx, bool grammarFirst) {
+    if (m_grammar && grammarFirst) return sampleGrammarFirst(ctx, idx);
+    const Token id = sampleChain(ctx, idx);
+    if (!m_grammar || m_grammar->allows(m_model.vocab(), id)) return id;
+    // resampling: the grammar on the whole vocabulary first, then the chain (Sampler.cpp:158-172)
+    return sampleGrammarFirst(ctx, idx);
+}
+
+Token Sampler::sampleGrammarFirst(mi_ctx* ctx, int idx) {
+    const float* lg = mi_logits(ctx, idx);
+    if (!lg) BL_THROW("sampling: " << last_error());
+    const int32_t n = mi_model_n_vocab(m_model.mmodel());
+    std::vector<int32_t> ids((size_t)n);
+    std::vector<float> v(lg, lg + n);
+    for (int32_t i = 0; i < n; ++i) ids[(size_t)i] = i;
+    m_grammar->apply(m_model.vocab(), ids.data(), v.data(), (size_t)n);
+    std::vector<Candidate> cur((size_t)n);
+    bool any = false;
+    for (int32_t i = 0; i < n; ++i) {
+        cur[(size_t)i] = {i, v[(size_t)i], 0.0f};
+        any = any || v[(size_t)i] != -INFINITY;
+    }
+    if (!any) BL_THROW("no selected token during re-sampling - check your sampling configuration");
+    std::stable_sort(cur.begin(), cur.end(), [](auto& a, auto& b) { return a.logit > b.logit; });
+    return applyChain(cur);
+}
+
+Token Sampler::sampleChain(mi_ctx* ctx, int idx) {
     std::vector<Candidate> cur;
     // The GPU top-k may stand in for the vocabulary only when nothing before top_k in the chain
     // (logit_bias, penalties: Sampler.cpp:30-41) can move a token across the top-k boundary.
@@ -796,10 +825,10 @@ Token Sampler::sample(mi_ctx* ctx) {
         const int k = m_params.topK;
         std::vector<int32_t> ids(k);
         std::vector<float> lg(k);
-        if (mi_topk(ctx, -1, k, ids.data(), lg.data()) < 0) BL_THROW("sampling: " << last_error());
+        if (mi_topk(ctx, idx, k, ids.data(), lg.data()) < 0) BL_THROW("sampling: " << last_error());
         for (int i = 0; i < k; ++i) cur.push_back({ids[i], lg[i], 0.0f});
     } else {   // full vocabulary: the chain does not start with a top-k the engine can serve
-        const float* lg = mi_logits(ctx, -1);
+        const float* lg = mi_logits(ctx, idx);
         if (!lg) BL_THROW("sampling: " << last_error());
         const int32_t n = mi_model_n_vocab(m_model.mmodel());
         cur.resize((size_t)n);

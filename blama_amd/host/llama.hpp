@@ -32,6 +32,8 @@
 #include <unordered_map>
 #include <vector>
 
+#include "grammar.hpp"
+
 struct mi_model;
 struct mi_ctx;
 
@@ -181,9 +183,13 @@ public:
     // candidate set (ties broken by id, which std::sort leaves unspecified).  Otherwise bias and
     // penalties can move tokens across the top-k boundary, so the chain runs on the full
     // vocabulary, as the reference's does (Sampler.cpp:30-41).
-    Token sample(mi_ctx* ctx);
+    // With a grammar (Params::grammar, GBNF, root rule "root"): the chain's pick is checked
+    // against the grammar and, when it does not fit, the full vocabulary is resampled with the
+    // grammar applied first (Sampler.cpp:126-173); grammarFirst applies it first always.
+    Token sample(mi_ctx* ctx, int idx = -1, bool grammarFirst = false);
     void accept(Token id, bool acceptGrammar);
     void reset();
+    const Grammar* grammar() const noexcept { return m_grammar.get(); }
 
     // The chain applied to a candidate list sorted by logit descending (exposed for tests).
     struct Candidate { Token id; float logit; float p; };
@@ -197,6 +203,9 @@ private:
     std::mt19937 m_xtcRng;                 // llama_sampler_init_xtc's own generator
     std::mt19937 m_rng;
     std::vector<Token> m_prev;          // penalty window
+    std::unique_ptr<Grammar> m_grammar;    // null: no grammar (llama_sampler_init_grammar of "")
+    Token sampleChain(mi_ctx* ctx, int idx);
+    Token sampleGrammarFirst(mi_ctx* ctx, int idx);
 };
 
 class Instance;

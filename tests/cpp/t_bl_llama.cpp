@@ -267,6 +267,117 @@ TEST_CASE_G("vocab only", "cpu") {   // t-integration.cpp:25-43
     CHECK(back == " \xc3\xa9");
 }
 
+// GBNF grammars (llama-grammar.cpp b5187 restated in blama_amd/host/grammar.cpp; parity unpinned):
+// the language of each construct, the parser's errors, and the token-level filter the Sampler
+// applies (Sampler.cpp:126-173) with partial UTF-8 across byte tokens.
+TEST_CASE_G("grammar", "cpu") {
+    {
+        Grammar g("root ::= \"a\" [0-9]+ (\"x\" | \"yz\")?\n");
+        CHECK(g.acceptsComplete("a12"));
+        CHECK(g.acceptsComplete("a1x"));
+        CHECK(g.acceptsComplete("a1yz"));
+        CHECK_FALSE(g.acceptsComplete("a"));
+        CHECK(g.acceptsPrefix("a"));
+        CHECK(g.acceptsPrefix("a1y"));
+        CHECK_FALSE(g.acceptsComplete("a1y"));
+        CHECK_FALSE(g.acceptsPrefix("b"));
+        CHECK_FALSE(g.acceptsPrefix("a1xy"));
+    }
+    {   // bounded repetitions: S{m}, S{m,}, S{m,n}
+        Grammar g("root ::= \"ab\"{2,3} c\nc ::= [c]{1} d{2,}\nd ::= \"d\"");
+        CHECK(g.acceptsComplete("ababcdd"));
+        CHECK(g.acceptsComplete("abababcddddd"));
+        CHECK_FALSE(g.acceptsComplete("abcdd"));
+        CHECK_FALSE(g.acceptsPrefix("abababab"));
+        CHECK_FALSE(g.acceptsComplete("ababcd"));
+    }
+    {   // classes, negation, any char, escapes, comments, unicode ranges, multi-line alternates
+        Grammar g("# a comment\nroot ::= item (\",\" item)*   # trailing comment\n"
+                  "item ::= [^,\\x5D\\n]+ | \"\\u00e9\" [\\u03b1-\\u03c9] |\n    \"<\" . \">\"\n");
+        CHECK(g.acceptsComplete("abc,d e"));
+        CHECK(g.acceptsComplete("\xc3\xa9\xce\xb2"));       // "é" then a greek small letter
+        CHECK(g.acceptsComplete("\xc3\xa9" "A"));           // ... and by the first alternative
+        CHECK_FALSE(g.acceptsComplete("\n"));
+        CHECK(g.acceptsComplete("<,>,x"));                   // "." takes the comma inside <>
+        CHECK_FALSE(g.acceptsPrefix("a]"));
+        CHECK_FALSE(g.acceptsComplete("a,"));
+    }
+    // parser errors (llama_sampler_init_grammar yields no grammar for these)
+    auto throws = [](const char* txt) {
+        try { Grammar g(txt); } catch (const std::runtime_error&) { return true; }
+        return false;
+    };
+    CHECK(throws("root ::= foo\n"));                     // undefined rule
+    CHECK(throws("root ::= root \"a\" | \"b\"\n"));      // left recursion
+    CHECK(throws("item ::= \"a\"\n"));                   // no root
+    CHECK(throws("root ::= \"\\q\"\n"));                 // unknown escape
+    CHECK(throws("root ::= \"a\" {,2}\n"));              // expecting an int
+    CHECK(throws("root ::= ( \"a\"\n"));                 // unbalanced group
+    CHECK(throws("root ::= * \"a\"\n"));                 // repetition without an item
+
+    // token level over the test vocabulary
+    REQUIRE(!g_vocab.empty());
+    Model model(g_vocab, {.vocabOnly = true});
+    auto& voc = model.vocab();
+    const Token hello = voc.tokenize("hello", false, true).back(), world = voc.tokenize("world", false, true).back();
+    REQUIRE(voc.tokenToString(hello) == " hello");
+    {
+        Grammar g("root ::= \" hello\" \" world\"\n");
+        CHECK(g.allows(voc, hello));
+        CHECK_FALSE(g.allows(voc, world));
+        CHECK_FALSE(g.allows(voc, voc.eos()));               // EOG only once a stack is complete
+        std::vector<int32_t> ids = {hello, world, voc.eos()};
+        std::vector<float> lg = {1.0f, 2.0f, 3.0f};
+        g.apply(voc, ids.data(), lg.data(), ids.size());
+        CHECK(lg[0] == 1.0f && lg[1] == -INFINITY && lg[2] == -INFINITY);
+        g.accept(voc, hello);
+        CHECK(g.allows(voc, world));
+        CHECK_FALSE(g.allows(voc, hello));
+        g.accept(voc, world);
+        CHECK(g.allows(voc, voc.eos()));
+        CHECK_FALSE(g.allows(voc, hello));                   // a complete stack takes nothing more
+        bool threw = false;
+        try { g.accept(voc, hello); } catch (const std::runtime_error&) { threw = true; }
+        CHECK(threw);                                        // "Unexpected empty grammar stack"
+        g.reset();
+        CHECK(g.allows(voc, hello) && !g.allows(voc, world));
+    }
+    {   // a two-byte character split over byte-fallback tokens (partial UTF-8 state)
+        const auto by = voc.tokenize("\xc3\xa9", false, false);
+        REQUIRE(by.size() >= 2);
+        const Token b0 = by[by.size() - 2], b1 = by[by.size() - 1];
+        REQUIRE(voc.tokenToString(b0) == "\xc3" && voc.tokenToString(b1) == "\xa9");
+        Grammar g("root ::= \"\\u00e9\"\n");
+        CHECK(g.allows(voc, b0));                            // 0xC3 can still complete to U+00E9
+        CHECK_FALSE(g.allows(voc, b1));                      // a continuation byte cannot start
+        g.accept(voc, b0);
+        CHECK(g.allows(voc, b1));
+        CHECK_FALSE(g.allows(voc, b0));                      // 0xC3 does not continue 0xC3
+        CHECK_FALSE(g.allows(voc, voc.eos()));
+        g.accept(voc, b1);
+        CHECK(g.allows(voc, voc.eos()));
+        Grammar h("root ::= [a-z]\n");
+        CHECK_FALSE(h.allows(voc, b0));                      // U+00C0..U+00FF is past [a-z]
+    }
+    {   // the Sampler: generated tokens advance the grammar, prompt tokens do not; reset rewinds
+        Sampler::Params p;
+        p.grammar = "root ::= \" hello\" \" world\"";
+        Sampler s(model, p);
+        REQUIRE(s.grammar() != nullptr);
+        s.accept(world, false);                              // prompt token: grammar untouched
+        CHECK(s.grammar()->allows(voc, hello));
+        s.accept(hello, true);
+        CHECK(s.grammar()->allows(voc, world));
+        s.reset();
+        CHECK(s.grammar()->allows(voc, hello));
+        Sampler::Params bad;
+        bad.grammar = "root ::= nope";
+        bool threw = false;
+        try { Sampler t(model, bad); } catch (const std::runtime_error&) { threw = true; }
+        CHECK(threw);
+    }
+}
+
 // tests/test_tokenizer_bpe.py: tokenise every line of --in (hex-encoded UTF-8) with the vocab-only
 // model --vocab (parseSpecial, no BOS) and write the ids, one line per text, to --out
 TEST_CASE_G("tokenize file", "tok") {
@@ -483,6 +594,40 @@ TEST_CASE_G("sampler stages on the logits", "gpu") {   // Sampler.cpp:47-96 over
     Sampler::Params p;                    // a near-zero target surprise: mirostat v2 is greedy
     p.mirostat = {2, 0.0f, 0.1f};
     CHECK(Sampler(model, p).sample(inst.mctx()) == top);
+}
+
+TEST_CASE_G("grammar sampling", "gpu") {   // Sampler.cpp:126-173 / Session.cpp:374-377 over a real context
+    Model model(g_model, {});
+    Instance inst(model, {});
+    auto& voc = model.vocab();
+    // the synthetic vocabulary's pieces are " t<i>" (and byte tokens): a finite language, so the
+    // generation must spell one of its strings and then end on end-of-generation
+    const std::string gram = "root ::= \" t1\" [0-9] [0-9] \" t2\" [0-9] [0-9]";
+    Grammar check(gram);
+    for (uint32_t seed : {5u, 6u}) {
+        Session::InitParams ip;
+        ip.seed = seed;
+        ip.grammar = gram;
+        auto& s = inst.startSession(ip);
+        s.setInitialPrompt(kPrompt);
+        auto p = s.complete({.maxTokens = 12});
+        std::string text;
+        for (auto& tp : p) text += voc.tokenToString(tp.token);
+        CHECK(p.size() < 12);                 // stopped on EOG, the only token a complete grammar allows
+        CHECK(check.acceptsComplete(text));
+        inst.stopSession();
+    }
+    {   // without a grammar the same session samples outside that set
+        Session::InitParams ip;
+        ip.seed = 5;
+        auto& s = inst.startSession(ip);
+        s.setInitialPrompt(kPrompt);
+        auto p = s.complete({.maxTokens = 6});
+        bool outside = false;
+        for (auto& tp : p) outside = outside || voc.tokenToString(tp.token).rfind(" t1", 0) != 0;
+        CHECK(outside);
+        inst.stopSession();
+    }
 }
 
 TEST_CASE_G("filling ctx", "gpu") {   // t-integration.cpp:219-248: bit-identical verification
