@@ -16,7 +16,7 @@ import pytest
 
 import ggml_ref as R
 from blama_amd import engine, synthetic
-from util import oracle_from_gguf
+from util import oracle_from_gguf, oracle_ulp_floor
 
 pytestmark = pytest.mark.gpu
 
@@ -24,6 +24,10 @@ LOGIT_TOL = 2e-3
 
 
 def _check(cfg, steps, prompt, n_ctx=64, seed=5, tol=LOGIT_TOL):
+    """Decode `prompt` then `steps` random tokens on the engine and the oracle.  Every output
+    must be within tol x rms element-wise with identical top-10 -- or, at a step where it is not,
+    within twice the oracle's own 1-ulp floor there (util.oracle_ulp_floor: a rounding boundary
+    the CPU algorithm itself flips on), with the top-10 equal up to near ties."""
     buf = synthetic.build_gguf(cfg, seed=seed)
     m = engine.Model(buf)
     ctx = engine.Context(m, n_ctx=n_ctx)
@@ -32,18 +36,28 @@ def _check(cfg, steps, prompt, n_ctx=64, seed=5, tol=LOGIT_TOL):
     ref = orc.decode(prompt)
     outs = [(ctx.logits(), ref, ctx.topk(10))]
     rng = np.random.default_rng(2)
+    toks = []
     for _ in range(steps):
         t = int(rng.integers(0, cfg.n_vocab))
+        toks.append(t)
         ctx.decode([t])
         outs.append((ctx.logits(), orc.decode_one(t), ctx.topk(10)))
+    floor = None
     agg = R.MetricsAggregator()
     sims = []
-    for got, ref, (ids, vals) in outs:
+    for s, (got, ref, (ids, vals)) in enumerate(outs):
         rms = float(np.sqrt(np.mean(ref.astype(np.float64) ** 2)))
         err = float(np.max(np.abs(got - ref)))
-        print(f"{cfg.name}: max|dlogit|/rms = {err / rms:.2e}")
-        assert err <= tol * rms
-        assert [int(i) for i in ids] == [i for i, _ in R.topk(ref, 10)]
+        print(f"{cfg.name} step {s}: max|dlogit|/rms = {err / rms:.2e}")
+        if err <= tol * rms:
+            assert [int(i) for i in ids] == [i for i, _ in R.topk(ref, 10)]
+        else:
+            if floor is None:
+                floor = oracle_ulp_floor(buf, n_ctx, prompt, toks)[1]
+            print(f"  oracle 1-ulp floor at step {s}: {floor[s] / rms:.2e} x rms")
+            assert err <= 2 * floor[s], (s, err / rms, floor[s] / rms)
+            ref_sorted = np.sort(ref)[::-1][:10]
+            assert np.all(np.abs(ref[ids.astype(np.int64)] - ref_sorted) <= 2 * err + 1e-6)
         a = [(int(i), float(v)) for i, v in zip(ids, vals)]
         cm = R.compare(a, R.gather(ref, [i for i, _ in a]))
         assert cm.top1Match == 1.0

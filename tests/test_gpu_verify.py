@@ -12,7 +12,7 @@ import pytest
 
 import ggml_ref as R
 from blama_amd import engine, synthetic
-from util import oracle_from_gguf
+from util import c_alt_floor, oracle_from_gguf
 
 pytestmark = pytest.mark.gpu
 LOGIT_TOL = 2e-3
@@ -84,27 +84,30 @@ def test_out_all_batch_vs_serial(gpu_lib, monkeypatch):
     b.decode(prompt)
     b.decode(claimed, all_logits=True)
     # both paths against the oracle row by row, and against each other through the
-    # reference's gate (identical top-1, LogitComparer score)
-    orc = oracle_from_gguf(buf, n_ctx=64)
-    orc.decode(prompt)
+    # reference's gate (identical top-1, LogitComparer score).  The serial path is the decode
+    # graphs (LOGIT_TOL).  A batch row outside LOGIT_TOL must sit where the CPU algorithm itself
+    # moves as far under another fp32 sum order (util.c_alt_floor: a Q8_K quantum on its
+    # rounding boundary; r02 measured one row of 33 at 4.6e-3 x rms).
+    base, floor = c_alt_floor(buf, 64, prompt, claimed)
     agg = R.MetricsAggregator()
     errs = []
     for i, t in enumerate(claimed):
-        ref = orc.decode_one(t)
-        rms = float(np.sqrt(np.mean(ref.astype(np.float64) ** 2)))
+        ref = base[i + 1]
+        rms = float(np.sqrt(np.mean(ref ** 2)))
         la, lb = a.logits(row=i), b.logits(row=i)
-        errs.append((float(np.max(np.abs(la - ref))) / rms, float(np.max(np.abs(lb - ref))) / rms))
-        # the serial path is the decode graphs (LOGIT_TOL); a batch row may carry one Q8_K
-        # rounding flip from the GEMM's fp32 order (measured: one row of 33 at 4.6e-3)
-        assert _close(lb, ref) and _close(la, ref, 5 * LOGIT_TOL), (i, errs[-1])
+        ea, eb = float(np.max(np.abs(la - ref))), float(np.max(np.abs(lb - ref)))
+        errs.append((ea / rms, eb / rms, floor[i + 1] / rms))
+        assert eb <= LOGIT_TOL * rms, (i, errs[-1])
+        assert ea <= LOGIT_TOL * rms or ea <= 2 * floor[i + 1], (i, errs[-1])
         ia, va = a.topk(10, row=i)
         ib, vb = b.topk(10, row=i)
         assert ia[0] == ib[0]
         score = agg.push_and_verify([R.compare([(int(x), float(v)) for x, v in zip(ia, va)],
                                                [(int(x), float(v)) for x, v in zip(ib, vb)])])
-    print("max |dlogit|/rms per row (batch, serial):", max(e[0] for e in errs), max(e[1] for e in errs))
-    assert sum(e[0] > LOGIT_TOL for e in errs) <= len(errs) // 16
+    print("max |dlogit|/rms per row (batch, serial, cpu floor):", [max(e[k] for e in errs) for k in range(3)])
     assert score >= 0.99
+    orc = oracle_from_gguf(buf, n_ctx=64)
+    orc.decode(prompt + claimed)
     for t in [5, 6]:   # caches written by the batch serve later steps
         a.decode([t])
         b.decode([t])
@@ -145,7 +148,13 @@ def test_long_prompt_batches_match_cpu_oracle(gpu_lib):
     assert _close(ctx.logits(), ref)
     assert [int(i) for i in ctx.topk(10)[0]] == [j for j, _ in R.topk(ref, 10)]
     ctx.decode(claimed, all_logits=True)
-    for i, t in enumerate(claimed):
-        ref = orc.decode_one(t)
-        assert _close(ctx.logits(row=i), ref, 5 * LOGIT_TOL), i
-        assert int(ctx.topk(1, row=i)[0][0]) == R.topk(ref, 1)[0][0], i
+    orc.close()
+    # a row outside LOGIT_TOL must sit on a rounding boundary of the CPU algorithm itself (the
+    # C oracle in the reversed lane order moves at least half as far there)
+    base, floor = c_alt_floor(buf, 1200, prompt, claimed)
+    for i in range(len(claimed)):
+        ref = base[i + 1]
+        rms = float(np.sqrt(np.mean(ref ** 2)))
+        err = float(np.max(np.abs(ctx.logits(row=i) - ref)))
+        assert err <= LOGIT_TOL * rms or err <= 2 * floor[i + 1], (i, err / rms, floor[i + 1] / rms)
+        assert int(ctx.topk(1, row=i)[0][0]) == int(np.argmax(ref)), i

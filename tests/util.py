@@ -37,6 +37,62 @@ def oracle_from_gguf(buf, n_ctx: int = 0) -> R.LlamaOracle:
     return R.LlamaOracle(hp, tens, n_ctx=n_ctx)
 
 
+def oracle_ulp_floor(buf, n_ctx, prompt, tokens, runs=4, seed=100):
+    """The live rounding floor of the CPU algorithm at each output of a decode run.
+
+    The oracle is re-run `runs` times with every GEMV output moved by -1, 0 or +1 ulp at random:
+    an fp32 summation order exactly as valid as ggml's (its AVX2 and generic paths differ in
+    it).  Returns base outputs and, per output (the prompt's last token, then each of `tokens`),
+    the largest max|perturbed - base| over the runs.  A step where the HIP engine differs from the
+    oracle by more than the element-wise tolerance is still at parity when the oracle itself moves
+    that far under a 1-ulp change: a Q8_K / Q8_0 activation quantum or an f16 rounding (GELU
+    table index, attention weight) sat on its boundary and flipped (measured for tiny-gpt2 step 7:
+    1.2e-2 x rms in 3 of 4 perturbed runs, every other step <= 3e-6)."""
+    orig = R.mul_mat_vec
+
+    def run(rng):
+        if rng is not None:
+            def mm(raw, t, K, x):
+                y = orig(raw, t, K, x)
+                k = rng.integers(-1, 2, y.size).astype(np.int32)
+                return (y.view(np.int32) + k).view(np.float32)
+            R.mul_mat_vec = mm
+        try:
+            orc = oracle_from_gguf(buf, n_ctx=n_ctx)
+            outs = [orc.decode(prompt).astype(np.float64)]
+            outs += [orc.decode_one(t).astype(np.float64) for t in tokens]
+        finally:
+            R.mul_mat_vec = orig
+        return outs
+
+    base = run(None)
+    floor = np.zeros(len(base))
+    for r in range(runs):
+        for i, o in enumerate(run(np.random.default_rng(seed + r))):
+            floor[i] = max(floor[i], float(np.max(np.abs(o - base[i]))))
+    return base, floor
+
+
+def c_alt_floor(buf, n_ctx, prompt, tokens):
+    """As oracle_ulp_floor, with the C oracle (LLaMA graphs) and one perturbation: the 8 float
+    lanes of every k-quant dot summed in the reverse order (ORC_ALT).  Returns (base outputs,
+    per-output max|alt - base|)."""
+    import ggml_cpu
+    a, b = ggml_cpu.Model(buf, n_ctx=n_ctx), ggml_cpu.Model(buf, n_ctx=n_ctx)
+    try:
+        base = [a.decode(prompt).astype(np.float64)]
+        for t in prompt:
+            alt = b.decode_one(t, alt=True)
+        floor = [float(np.max(np.abs(alt - base[0])))]
+        for t in tokens:
+            base.append(a.decode_one(t).astype(np.float64))
+            floor.append(float(np.max(np.abs(b.decode_one(t, alt=True) - base[-1]))))
+    finally:
+        a.close()
+        b.close()
+    return base, np.array(floor)
+
+
 def parse_state(st: bytes, n_layer: int, kv_dim: int):
     """Split an mi_state_get() blob: (cell_pos, K[n_layer][n_cells][kv_dim], V[...])."""
     import struct
