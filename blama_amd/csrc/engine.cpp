@@ -515,6 +515,21 @@ void Model::load(const uint8_t* data, size_t size, const mi_model_params& p) {
 namespace {
 std::vector<int> g_attr_done(64, 0);
 
+namespace {
+struct DevChain {
+    std::mutex mu;
+    hipEvent_t ev = nullptr;   // the last persistent step enqueued on the device
+};
+DevChain& dev_chain(int device) {
+    static std::mutex mu;
+    static std::map<int, std::unique_ptr<DevChain>> chains;
+    std::lock_guard<std::mutex> lk(mu);
+    auto& c = chains[device];
+    if (!c) c.reset(new DevChain());
+    return *c;
+}
+}  // namespace
+
 GemvSeg seg_of(const QMat& A, int pair, int epi, float* out) {
     GemvSeg g;
     std::memset(&g, 0, sizeof(g));
@@ -567,6 +582,9 @@ Ctx::Ctx(Model* model, uint32_t nctx, uint32_t nbatch, uint32_t nubatch) : m(mod
     // GPT-2 prompts run token by token (one decode graph each): its batch kernels (LayerNorm,
     // biases, GELU) are not built
     batch_ok = hp.n_expert == 0 && hp.arch == ARCH_LLAMA && getenv("MI_NO_BATCH") == nullptr;
+    // the persistent step is opt-in (MI_PERSIST=1): measured slower than the graph
+    persist_ok = hp.n_expert == 0 && hp.arch == ARCH_LLAMA && use_graphs && getenv("MI_PERSIST") != nullptr &&
+                 getenv("MI_NO_PERSIST") == nullptr;
     if (batch_ok) {
         // MFMA batch path (decode_ubatch / mmq32) when every layer matrix is Q4_K / Q6_K or every
         // one Q8_0; otherwise prompt chunks on the v_dot4 GEMM (decode_batch)
@@ -631,6 +649,11 @@ Ctx::~Ctx() {
     hipSetDevice(device);
     if (stream) hipStreamSynchronize(stream);
     invalidate_graphs();
+    for (PersistStep*& p : pst) {
+        persist_free(p);
+        p = nullptr;
+    }
+    if (pbuf) hipFree(pbuf);
     for (auto e : prof_ev) if (e) hipEventDestroy(e);
     for (void* p : {(void*)kcache, (void*)vcache, (void*)kv_scratch, (void*)cell_pos, (void*)tokpos, (void*)x,
                     (void*)q, (void*)attn, (void*)h, (void*)h2, (void*)logits, (void*)cand, (void*)topk_ids,
@@ -663,11 +686,128 @@ long long Ctx::ffn_bytes() const {
     return w + act;   // weights + x and norm weight read + h written
 }
 
+// The ops of one llm_build_llama layer for the token in tokpos, as launch parameters handed to
+// `gemv` (role: 0 QKV, 1 WO, 2 FFN gate/up, 3 FFN down), `attn` and `router`.  The buffers are
+// the graph path's (the residual updated in place) or the persistent step's (every output a
+// buffer of its own, written once per step).
+void Ctx::layer_ops(int l, const LayerBufs& B, const std::function<void(const GemvParams&, int)>& gemv,
+                    const std::function<void(const AttnParams&)>& attn,
+                    const std::function<void(const RouterParams&)>& router) {
+    const HParams& hp = m->hp;
+    const Layer& L = m->layers[l];
+    __half* kl = kcache + (size_t)l * n_ctx * kv_dim;
+    __half* vl = vcache + (size_t)l * n_ctx * kv_dim;
+    const float theta_scale = std::pow(hp.rope_base, -2.0f / (float)hp.n_rot);
+    const float kq_scale = 1.0f / std::sqrt((float)hp.head_dim);
+    GemvParams base;
+    std::memset(&base, 0, sizeof(base));
+    base.tokpos = tokpos;
+    base.cell_pos = cell_pos;
+    base.head_dim = hp.head_dim;
+    base.kv_dim = kv_dim;
+    base.eps = hp.eps;
+    base.nslots = 1;
+    // ---- Q/K/V projections + RoPE + KV append: one launch per pair of row groups ----
+    {
+        GemvParams p = base;
+        p.pro = PRO_RMSNORM;
+        p.x[0] = B.x_in;
+        p.norm_w = L.attn_norm;
+        p.K = hp.n_embd;
+        p.theta_scale = theta_scale;
+        p.freq_scale = hp.freq_scale;
+        p.n_rot = hp.n_rot;
+        p.freq_factors = m->rope_freqs;
+        p.kcache = kl;
+        p.vcache = vl;
+        for (int g = 0; g < L.n_qkv;) {
+            p.nseg = 0;
+            for (; g < L.n_qkv && p.nseg < GEMV_MAX_SEG; ++g) {
+                if (p.nseg == 1 && !gemv_pair_supported(p.seg[0].A.type, L.qkv[g].type)) break;
+                GemvSeg& sg = p.seg[p.nseg++];
+                sg = seg_of(L.qkv[g], PAIR_ADJ, EPI_QKV, B.q);
+                sg.nq = L.qkv_nq[g];
+                sg.nk = L.qkv_nk[g];
+            }
+            gemv(p, 0);
+        }
+    }
+    // ---- attention ----
+    {
+        AttnParams a{B.q, kl, vl, tokpos, cell_pos, attn_scores, attn_smax, B.po, hp.n_head, hp.n_head_kv, hp.head_dim,
+                     kv_dim, (int)n_ctx, kq_scale};
+        a.fused = attn_fused;
+        attn(a);
+    }
+    // ---- output projection + residual (prologue: the attention splits combined) ----
+    {
+        GemvParams p = base;
+        p.pro = PRO_ATTN;
+        p.attn = AttnPartials{B.po, hp.n_head, hp.head_dim};
+        p.attn_nsplit = attn_fused ? 1 : 0;   // the split graph reads the count from the cell count
+        p.K = hp.n_embd;
+        p.nseg = 1;
+        p.seg[0] = seg_of(L.wo, PAIR_ADJ, EPI_ADD, B.xa);
+        p.seg[0].resid = B.x_in;
+        gemv(p, 1);
+    }
+    if (hp.n_expert > 0) {
+        RouterParams rp{B.xa, L.ffn_norm, hp.eps, L.router, hp.n_embd, hp.n_expert, hp.n_expert_used, sel, selw};
+        router(rp);
+    }
+    // ---- FFN gate/up + SwiGLU ----
+    {
+        GemvParams p = base;
+        p.pro = PRO_RMSNORM;
+        p.x[0] = B.xa;
+        p.norm_w = L.ffn_norm;
+        p.K = hp.n_embd;
+        const int nsl = hp.n_expert > 0 ? 2 : 1;
+        if (hp.n_expert > 0) {   // expert ids/weights: only MoE launches wait for them
+            p.sel = sel;
+            p.selw = selw;
+        }
+        p.nseg = nsl;
+        for (int k = 0; k < nsl; ++k) {
+            p.seg[k] = seg_of(L.gate, PAIR_AB, EPI_SWIGLU, k == 0 ? B.h : B.h2);
+            p.seg[k].B = L.up;
+            if (hp.n_expert > 0) p.seg[k].expA = p.seg[k].expB = k;
+        }
+        gemv(p, 2);
+    }
+    // ---- FFN down + residual ----
+    {
+        GemvParams p = base;
+        p.pro = PRO_PLAIN;
+        p.x[0] = B.h;
+        p.K = hp.n_ff;
+        p.nseg = 1;
+        if (hp.n_expert > 0) {
+            p.sel = sel;
+            p.selw = selw;
+            p.nslots = 2;
+            p.x[1] = B.h2;
+            p.seg[0] = seg_of(L.down, PAIR_AB, EPI_MOE_DOWN, B.xf);
+            p.seg[0].expA = 0;
+            p.seg[0].expB = 1;
+            p.seg[0].actB = 1;
+        } else {
+            p.seg[0] = seg_of(L.down, PAIR_ADJ, EPI_ADD, B.xf);
+        }
+        p.seg[0].resid = B.xa;
+        gemv(p, 3);
+    }
+}
+
 // One decode step for the token in tokpos (batch 1): the llm_build_llama graph.
 // With seg_filter >= 0 only the ops of that profiling segment are enqueued
 // (0: up to layer prof_layer's FFN gate/up, 1: that launch, 2: the rest).
 void Ctx::enqueue_step(bool with_logits) {
     const HParams& hp = m->hp;
+    if (attn_fused && persist_step(with_logits)) {
+        enqueue_step_persist(with_logits);
+        return;
+    }
     int seg = 0;
     int n_launch = 0;   // diagnostic stamps (MI_STAMPS builds only): one slab per launch
     auto stamp = [&]() -> unsigned long long* {
@@ -677,126 +817,136 @@ void Ctx::enqueue_step(bool with_logits) {
     auto on = [&]() { return seg_filter < 0 || seg_filter == seg; };
     EmbedParams ep{m->tok_embd, tokpos, x, hp.n_embd, m->pos_embd, hp.arch == ARCH_GPT2 ? 1 : 0};
     if (on()) launch_embed(ep, stream);
-    const float theta_scale = std::pow(hp.rope_base, -2.0f / (float)hp.n_rot);
     const float kq_scale = 1.0f / std::sqrt((float)hp.head_dim);
     for (int l = 0; l < hp.n_layer; ++l) {
-        const Layer& L = m->layers[l];
-        __half* kl = kcache + (size_t)l * n_ctx * kv_dim;
-        __half* vl = vcache + (size_t)l * n_ctx * kv_dim;
-        GemvParams base;
-        std::memset(&base, 0, sizeof(base));
-        base.tokpos = tokpos;
-        base.cell_pos = cell_pos;
-        base.head_dim = hp.head_dim;
-        base.kv_dim = kv_dim;
-        base.eps = hp.eps;
-        base.nslots = 1;
         if (hp.arch == ARCH_GPT2) {   // llm_build_gpt2: LayerNorm, biases, no RoPE, GELU MLP
-            enqueue_layer_gpt2(l, base, kl, vl, kq_scale, stamp);
+            GemvParams base;
+            std::memset(&base, 0, sizeof(base));
+            base.tokpos = tokpos;
+            base.cell_pos = cell_pos;
+            base.head_dim = hp.head_dim;
+            base.kv_dim = kv_dim;
+            base.eps = hp.eps;
+            base.nslots = 1;
+            enqueue_layer_gpt2(l, base, kcache + (size_t)l * n_ctx * kv_dim, vcache + (size_t)l * n_ctx * kv_dim,
+                               kq_scale, stamp);
             continue;
         }
-        // ---- Q/K/V projections + RoPE + KV append: one launch per pair of row groups ----
-        {
-            GemvParams p = base;
-            p.pro = PRO_RMSNORM;
-            p.x[0] = x;
-            p.norm_w = L.attn_norm;
-            p.K = hp.n_embd;
-            p.theta_scale = theta_scale;
-            p.freq_scale = hp.freq_scale;
-            p.n_rot = hp.n_rot;
-            p.freq_factors = m->rope_freqs;
-            p.kcache = kl;
-            p.vcache = vl;
-            for (int g = 0; g < L.n_qkv;) {
-                p.nseg = 0;
-                for (; g < L.n_qkv && p.nseg < GEMV_MAX_SEG; ++g) {
-                    if (p.nseg == 1 && !gemv_pair_supported(p.seg[0].A.type, L.qkv[g].type)) break;
-                    GemvSeg& sg = p.seg[p.nseg++];
-                    sg = seg_of(L.qkv[g], PAIR_ADJ, EPI_QKV, q);
-                    sg.nq = L.qkv_nq[g];
-                    sg.nk = L.qkv_nk[g];
-                }
+        const LayerBufs B{x, q, part_o, x, h, h2, x};
+        layer_ops(
+            l, B,
+            [&](const GemvParams& p0, int role) {
+                GemvParams p = p0;
                 p.stamps = stamp();
-                if (on()) launch_gemv(p, stream);
-            }
-        }
-        // ---- attention ----
-        {
-            AttnParams a{q, kl, vl, tokpos, cell_pos, attn_scores, attn_smax, part_o, hp.n_head, hp.n_head_kv, hp.head_dim,
-                         kv_dim, (int)n_ctx, kq_scale};
-            a.fused = attn_fused;
-            a.stamps = stamp();
-            a.stamps2 = stamp();
-            if (on()) launch_attn(a, stream);
-        }
-        // ---- output projection + residual (prologue: the attention splits combined) ----
-        {
-            GemvParams p = base;
-            p.pro = PRO_ATTN;
-            p.attn = AttnPartials{part_o, hp.n_head, hp.head_dim};
-            p.attn_nsplit = attn_fused ? 1 : 0;   // the split graph reads the count from the cell count
-            p.K = hp.n_embd;
-            p.nseg = 1;
-            p.seg[0] = seg_of(L.wo, PAIR_ADJ, EPI_ADD, x);
-            p.seg[0].resid = x;
-            p.stamps = stamp();
-            if (on()) launch_gemv(p, stream);
-        }
-        if (hp.n_expert > 0) {
-            RouterParams rp{x, L.ffn_norm, hp.eps, L.router, hp.n_embd, hp.n_expert, hp.n_expert_used, sel, selw};
-            if (on()) launch_router(rp, stream);
-        }
-        // ---- FFN gate/up + SwiGLU ----
-        {
-            GemvParams p = base;
-            p.pro = PRO_RMSNORM;
-            p.x[0] = x;
-            p.norm_w = L.ffn_norm;
-            p.K = hp.n_embd;
-            const int nsl = hp.n_expert > 0 ? 2 : 1;
-            if (hp.n_expert > 0) {   // expert ids/weights: only MoE launches wait for them
-                p.sel = sel;
-                p.selw = selw;
-            }
-            p.nseg = nsl;
-            for (int k = 0; k < nsl; ++k) {
-                p.seg[k] = seg_of(L.gate, PAIR_AB, EPI_SWIGLU, k == 0 ? h : h2);
-                p.seg[k].B = L.up;
-                if (hp.n_expert > 0) p.seg[k].expA = p.seg[k].expB = k;
-            }
-            p.stamps = stamp();
-            if (l == prof_layer) seg = 1;
-            // the profiled launch (segment 1, always eager) carries the event pair
-            const bool timed = l == prof_layer && seg_filter == 1;
-            if (on()) launch_gemv(p, stream, timed ? prof_ev[0] : nullptr, timed ? prof_ev[1] : nullptr);
-            if (l == prof_layer) seg = 2;
-        }
-        // ---- FFN down + residual ----
-        {
-            GemvParams p = base;
-            p.pro = PRO_PLAIN;
-            p.x[0] = h;
-            p.K = hp.n_ff;
-            p.nseg = 1;
-            if (hp.n_expert > 0) {
-                p.sel = sel;
-                p.selw = selw;
-                p.nslots = 2;
-                p.x[1] = h2;
-                p.seg[0] = seg_of(L.down, PAIR_AB, EPI_MOE_DOWN, x);
-                p.seg[0].expA = 0;
-                p.seg[0].expB = 1;
-                p.seg[0].actB = 1;
-            } else {
-                p.seg[0] = seg_of(L.down, PAIR_ADJ, EPI_ADD, x);
-            }
-            p.seg[0].resid = x;
-            p.stamps = stamp();
-            if (on()) launch_gemv(p, stream);
-        }
+                if (role != 2) {
+                    if (on()) launch_gemv(p, stream);
+                    return;
+                }
+                if (l == prof_layer) seg = 1;
+                // the profiled launch (segment 1, always eager) carries the event pair
+                const bool timed = l == prof_layer && seg_filter == 1;
+                if (on()) launch_gemv(p, stream, timed ? prof_ev[0] : nullptr, timed ? prof_ev[1] : nullptr);
+                if (l == prof_layer) seg = 2;
+            },
+            [&](const AttnParams& a0) {
+                AttnParams a = a0;
+                a.stamps = stamp();
+                a.stamps2 = stamp();
+                if (on()) launch_attn(a, stream);
+            },
+            [&](const RouterParams& rp) {
+                if (on()) launch_router(rp, stream);
+            });
     }
     if (with_logits && on()) enqueue_output(x, stamp());
+}
+
+// The persistent form of a step (contexts within ATTN_SHORT cells): the embedding, ONE launch of
+// the layers and the output head (gemv.hip decode_step_kernel), the top-k.  Profiling segments:
+// 0 the embedding, 1 the persistent launch (eager, with the event pair), 2 the top-k.
+void Ctx::enqueue_step_persist(bool with_logits) {
+    const HParams& hp = m->hp;
+    auto on = [&](int seg) { return seg_filter < 0 || seg_filter == seg; };
+    EmbedParams ep{m->tok_embd, tokpos, x, hp.n_embd, m->pos_embd, 0};
+    if (on(0)) launch_embed(ep, stream);
+    const bool timed = seg_filter == 1 && prof_layer >= 0;
+    if (on(1)) persist_launch(pst[with_logits], stream, timed ? prof_ev[0] : nullptr, timed ? prof_ev[1] : nullptr);
+    if (with_logits && on(2)) {
+        TopkParams tp{logits, hp.n_vocab, cand, topk_ids, topk_vals, d_h_topk_ids, d_h_topk_vals};
+        launch_topk(tp, stream);
+    }
+}
+
+// Builds the persistent stage table of a step on first use; false when the step has no
+// persistent form (not opted in, MoE, GPT-2, a quant type mix outside the compiled classes).
+bool Ctx::persist_step(bool with_logits) {
+    if (!persist_ok) return false;
+    if (pst[with_logits]) return true;
+    const HParams& hp = m->hp;
+    const size_t hq = (size_t)hp.n_head * hp.head_dim;
+    const size_t per_layer = 2 * hq + 2 * (size_t)hp.n_embd + (size_t)hp.n_ff;
+    if (!pbuf) {
+        MI_HIP(hipSetDevice(device));
+        MI_HIP(hipMalloc(&pbuf, per_layer * hp.n_layer * sizeof(float)));
+    }
+    PersistStep* p = persist_new(device);
+    bool ok = p != nullptr;
+    try {
+        const float* xin = x;
+        for (int l = 0; ok && l < hp.n_layer; ++l) {
+            float* b = pbuf + per_layer * l;
+            const LayerBufs B{xin, b, b + hq, b + 2 * hq, b + 2 * hq + 2 * hp.n_embd, nullptr, b + 2 * hq + hp.n_embd};
+            const int saved = attn_fused;
+            attn_fused = 1;
+            layer_ops(
+                l, B, [&](const GemvParams& g, int) { ok = ok && persist_add_gemv(p, g); },
+                [&](const AttnParams& a) { ok = ok && persist_add_attn(p, a, B.po); },
+                [&](const RouterParams&) { ok = false; });
+            attn_fused = saved;
+            xin = B.xf;
+        }
+        if (ok && with_logits) {
+            GemvParams g;
+            std::memset(&g, 0, sizeof(g));
+            g.pro = PRO_RMSNORM;
+            g.nslots = 1;
+            g.x[0] = xin;
+            g.norm_w = m->output_norm;
+            g.eps = hp.eps;
+            g.K = hp.n_embd;
+            g.tokpos = tokpos;
+            g.nseg = 1;
+            g.seg[0] = seg_of(m->output, PAIR_ADJ, EPI_STORE, logits);
+            ok = persist_add_gemv(p, g);
+        }
+        ok = ok && persist_finalize(p);
+    } catch (const std::exception&) {
+        ok = false;
+    }
+    if (!ok) {
+        persist_free(p);
+        persist_ok = false;
+        return false;
+    }
+    pst[with_logits] = p;
+    return true;
+}
+
+// A persistent step whose grid barrier timed out (its grid was not co-resident: another
+// process's persistent kernel on the same GPU) left garbage behind: reject it and stop using
+// the persistent form in this context.
+void Ctx::check_persist() {
+    for (PersistStep* p : pst)
+        if (persist_aborted(p)) {
+            for (PersistStep* r : pst)
+                if (r) persist_reset(r, stream);
+            persist_ok = false;
+            invalidate_graphs();
+            logits_valid = false;
+            throw Error("persistent decode step aborted (its grid was not co-resident; another process's "
+                        "persistent kernel on this GPU?): the step's results are invalid; persistent steps are "
+                        "off for this context (MI_NO_PERSIST=1 disables them everywhere)");
+        }
 }
 
 // One GPT-2 block (llm_build_gpt2, src/llama-model.cpp b5187) of the decode step:
@@ -898,6 +1048,7 @@ void Ctx::enqueue_output(const float* xrow, unsigned long long* stamps_slab) {
 
 hipGraphExec_t Ctx::build_graph(bool with_logits, int seg) {
     hipGraph_t g = nullptr;
+    if (attn_fused) persist_step(with_logits);   // allocations and uploads cannot be captured
     seg_filter = seg;
     MI_HIP(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
     try {
@@ -1219,12 +1370,29 @@ int Ctx::decode(const int32_t* tokens, int n, bool all) {
                 }
             }
             prof_pending = true;
+            if (attn_fused && pst[1]) {   // the persistent launch: every weight, the KV rows read
+                const HParams& hp = m->hp;
+                prof_bytes = m->weight_bytes + 2LL * hp.n_layer * (cell + 1) * kv_dim * 2;
+            } else {
+                prof_bytes = ffn_bytes();
+            }
         } else if (!use_graphs) {
             enqueue_step(last);
         } else {
             hipGraphExec_t& g = last ? g_full[attn_fused] : g_nolog[attn_fused];
             if (!g) g = build_graph(last, -1);
-            MI_HIP(hipGraphLaunch(g, stream));
+            if (attn_fused && pst[last]) {
+                // persistent steps of the contexts on one device run one at a time (two grids of
+                // one workgroup per CU at once would not be co-resident)
+                DevChain& dc = dev_chain(device);
+                std::lock_guard<std::mutex> lk(dc.mu);
+                if (dc.ev) MI_HIP(hipStreamWaitEvent(stream, dc.ev, 0));
+                else MI_HIP(hipEventCreateWithFlags(&dc.ev, hipEventDisableTiming));
+                MI_HIP(hipGraphLaunch(g, stream));
+                MI_HIP(hipEventRecord(dc.ev, stream));
+            } else {
+                MI_HIP(hipGraphLaunch(g, stream));
+            }
         }
         if (all)   // this token's logits -> row i
             MI_HIP(hipMemcpyAsync(logits_all + (size_t)i * m->hp.n_vocab, logits, (size_t)m->hp.n_vocab * sizeof(float),
@@ -1241,6 +1409,7 @@ int Ctx::decode(const int32_t* tokens, int n, bool all) {
 void Ctx::sync() {
     MI_HIP(hipSetDevice(device));
     MI_HIP(hipStreamSynchronize(stream));
+    check_persist();
 }
 
 const float* Ctx::out_row(int row) const {

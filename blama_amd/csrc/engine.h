@@ -205,9 +205,27 @@ struct Ctx {
     int prof_layer = -1;
     hipEvent_t prof_ev[2] = {nullptr, nullptr};
     bool prof_pending = false;
+    long long prof_bytes = 0;            // algorithmic bytes of the timed launch (mi_prof_bytes)
     int seg_filter = -1;                // -1: enqueue everything; else only ops of this segment
 
     static constexpr int kTokRing = 8192;
+
+    // persistent decode step (gemv.hip decode_step_kernel) for contexts within ATTN_SHORT cells:
+    // stage tables without / with the output head, built on first use; per-layer activation
+    // buffers (q, attention, residual after WO, FFN, residual after down) written once per step
+    PersistStep* pst[2] = {nullptr, nullptr};
+    bool persist_ok = false;            // opt-in (MI_PERSIST=1): dense LLaMA graph with graphs on
+    float* pbuf = nullptr;
+    bool persist_step(bool with_logits);
+    void enqueue_step_persist(bool with_logits);
+    void check_persist();
+    struct LayerBufs {
+        const float* x_in;              // residual stream into the layer
+        float *q, *po, *xa, *h, *h2, *xf;   // q, attention output, residual after WO, FFN (2nd expert), after down
+    };
+    void layer_ops(int l, const LayerBufs& B, const std::function<void(const GemvParams&, int)>& gemv,
+                   const std::function<void(const AttnParams&)>& attn,
+                   const std::function<void(const RouterParams&)>& router);
 
     Ctx(Model* model, uint32_t n_ctx, uint32_t n_batch, uint32_t n_ubatch);
     ~Ctx();

@@ -106,6 +106,27 @@ bool gemv_pair_supported(int t1, int t2);
 int gemv_grid(const GemvParams& p);
 void init_gemm_attributes();     // the batch GEMMs' LDS limits (kernels.hip)
 
+// ---- persistent decode step (gemv.hip): a table of stages -- the GEMV launches above and the
+// short-context attention -- run by ONE launch of one 16-wave workgroup per CU, with a grid
+// barrier between stages that the next stage's weight prefetch overlaps.  Dense LLaMA graphs
+// whose matrices fall in one compiled type class (Q4_K+Q6_K, Q5_K+Q6_K, Q6_K, Q8_0). ----
+struct PersistStep;
+struct AttnParams;
+PersistStep* persist_new(int device);                 // nullptr: no compute units reported
+void persist_free(PersistStep* p);
+// append a stage; false: the launch has no persistent form (the caller keeps the graph path).
+// Outputs a later stage reads must be buffers written once per step.
+bool persist_add_gemv(PersistStep* p, const GemvParams& g);
+bool persist_add_attn(PersistStep* p, const AttnParams& a, float* out);   // <= ATTN_SHORT cells
+bool persist_finalize(PersistStep* p);                // false: no compiled class covers the stages
+int persist_stages(const PersistStep* p);
+void persist_launch(PersistStep* p, hipStream_t s, hipEvent_t ev_start = nullptr, hipEvent_t ev_stop = nullptr);
+bool persist_aborted(const PersistStep* p);           // a grid barrier timed out (not co-resident)
+void persist_reset(PersistStep* p, hipStream_t s);    // zero the barrier state after an abort
+// diagnostics (MI_PERSIST_STAMPS=1 at the first step): the last launch's s_memrealtime stamps,
+// [stage][workgroup][4] = entry, barrier start, barrier end, stage end; returns the count copied
+size_t persist_read_stamps(PersistStep* p, unsigned long long* out, size_t n);
+
 // ---- batched quantised GEMM over up to GEMM_NT tokens (prompt ingestion) ----
 // The GEMV's integer arithmetic per token (Q8_K / Q8_0 activations, per-block integer
 // dots), with every weight load used for GEMM_NT tokens: a prompt of n tokens streams

@@ -47,22 +47,37 @@ def oracle_ulp_floor(buf, n_ctx, prompt, tokens, runs=4, seed=100):
     oracle by more than the element-wise tolerance is still at parity when the oracle itself moves
     that far under a 1-ulp change: a Q8_K / Q8_0 activation quantum or an f16 rounding (GELU
     table index, attention weight) sat on its boundary and flipped (measured for tiny-gpt2 step 7:
-    1.2e-2 x rms in 3 of 4 perturbed runs, every other step <= 3e-6)."""
+    1.2e-2 x rms in 3 of 4 perturbed runs, every other step <= 3e-6).  The perturbed runs also
+    accumulate the attention dots (KQ, KQV) in f32 as ggml's AVX2 ggml_vec_dot_f16 does, where
+    the base oracle sums in double, and move every score and head output by -1/0/+1 ulp: the synthetic GPT-2 models have large, flat attention scores
+    past ~500 cells, where that alone moves the oracle's logits by 7.7e-3 x rms
+    (tiny-gpt2-q8_0, 520 cells)."""
     orig = R.mul_mat_vec
+    orig_attn = R.attention_head
+
+    def ulp(y, rng):
+        y = np.ascontiguousarray(y, np.float32)
+        return (y.view(np.int32) + rng.integers(-1, 2, y.size).astype(np.int32).reshape(y.shape)).view(np.float32)
 
     def run(rng):
         if rng is not None:
+            def attn32(q, K16, V16, scale):
+                q16 = R.f32_to_f16(q).astype(np.float32)
+                s = ulp((K16.astype(np.float32) @ q16).astype(np.float32), rng)
+                p16 = R.f32_to_f16(R.soft_max(s, scale)).astype(np.float32)
+                return ulp((p16 @ V16.astype(np.float32)).astype(np.float32), rng)
+
             def mm(raw, t, K, x):
-                y = orig(raw, t, K, x)
-                k = rng.integers(-1, 2, y.size).astype(np.int32)
-                return (y.view(np.int32) + k).view(np.float32)
+                return ulp(orig(raw, t, K, x), rng)
             R.mul_mat_vec = mm
+            R.attention_head = attn32
         try:
             orc = oracle_from_gguf(buf, n_ctx=n_ctx)
             outs = [orc.decode(prompt).astype(np.float64)]
             outs += [orc.decode_one(t).astype(np.float64) for t in tokens]
         finally:
             R.mul_mat_vec = orig
+            R.attention_head = orig_attn
         return outs
 
     base = run(None)
