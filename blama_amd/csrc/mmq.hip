@@ -215,11 +215,14 @@ __device__ __forceinline__ void q4k_scales(const u32x4 hd, int sc[8], int mn[8])
 // MFMA-order weight copy: one 32-row x superblock tile (lane = h*32 + c holds row c's bytes of
 // k-half h; rows of a gate/up pair tile: c < 16 gate row 16*rt + c, c >= 16 up row 16*rt + c - 16)
 //   Q4_K  [p 4][lane 64][16] qs bytes 32p + 16h.. | [c 32][16] header                       4608 B
-//   Q6_K  [hf 2][cc 2][lane 64][16] ql bytes 64hf + 32cc + 16h.. | [hf 2][lane 64][16] qh bytes
-//         32hf + 16h.. | [c 32][16] scales | [c 32][2] d                                     6720 B
+//   Q6_K  the scaled weights w = (q - 32) * scale (|w| <= 4096, exact in int16) as two int8 MFMA
+//         operands w = 64*hi + lo (hi -64..64, lo 0..63): [s 8][lane 64][16] hi of span s (superblock
+//         elements 32s + 16h..) | the same for lo | [c 32][2] d                              16448 B
+//         (a 32-element span holds two 16-element scale groups, one per k-half: with the scale
+//         folded into the operand, one MFMA per span and operand carries the exact integer sum)
 //   Q8_0  [j 8][lane 64][16] qs bytes 32j + 16h.. | [c 32][8 f16] d                            8704 B
 __host__ __device__ constexpr int mmq32_tile_bytes_d(int type) {
-    return type == T_Q4_K ? 4608 : type == T_Q6_K ? 6720 : type == T_Q8_0 ? 8704 : 0;
+    return type == T_Q4_K ? 4608 : type == T_Q6_K ? 16448 : type == T_Q8_0 ? 8704 : 0;
 }
 
 __global__ void swizzle_kernel(const QMat A, const QMat B, int pair, uint8_t* dst) {
@@ -244,18 +247,24 @@ __global__ void swizzle_kernel(const QMat A, const QMat B, int pair, uint8_t* ds
             } else {
                 plane = 1; c = (off - 4096) >> 4; byte = (off - 4096) & 15;
             }
-        } else {
-            if (off < 4096) {
-                const int f = off >> 10, ln = (off >> 4) & 63, e = off & 15;
-                plane = 0; c = ln & 31; byte = 64 * (f >> 1) + 32 * (f & 1) + 16 * (ln >> 5) + e;
-            } else if (off < 6144) {
-                const int f = (off - 4096) >> 10, ln = ((off - 4096) >> 4) & 63, e = off & 15;
-                plane = 1; c = ln & 31; byte = 32 * f + 16 * (ln >> 5) + e;
-            } else if (off < 6656) {
-                plane = 2; c = (off - 6144) >> 4; byte = (off - 6144) & 15;
-            } else {
-                plane = 3; c = (off - 6656) >> 1; byte = (off - 6656) & 1;
+        } else {   // Q6_K
+            if (off < 16384) {   // w = (q - 32) * scale of element 32s + 16h + e (dequantize_row_q6_K)
+                const int lo = off >= 8192, o2 = off & 8191;
+                const int sp = o2 >> 10, ln = (o2 >> 4) & 63, e = o2 & 15;
+                const int cc = ln & 31, h = ln >> 5, l = 16 * h + e, hf = sp >> 2, qq = sp & 3;
+                const QMat& M = (pair && cc >= 16) ? B : A;
+                long long row = pair ? 16LL * rt + (cc & 15) : 32LL * rt + cc;
+                if (row >= M.rows) row = M.rows - 1;
+                const long long b = row * nb + sb;
+                const int ql = M.p[0][b * 128 + 64 * hf + l + 32 * (qq & 1)];
+                const int qh = M.p[1][b * 64 + 32 * hf + l];
+                const int sc = (int)(signed char)M.p[2][b * 16 + 8 * hf + 2 * qq + h];
+                const int q = ((qq >= 2 ? ql >> 4 : ql & 0xF) | (((qh >> (2 * qq)) & 3) << 4)) - 32;
+                const int w = q * sc;
+                o[off] = (uint8_t)(lo ? (w & 63) : (w >> 6));
+                continue;
             }
+            plane = 3; c = (off - 16384) >> 1; byte = (off - 16384) & 1;
         }
         const QMat& M = (pair && c >= 16) ? B : A;
         long long row = pair ? 16LL * rt + (c & 15) : 32LL * rt + c;
@@ -369,49 +378,26 @@ __global__ __launch_bounds__(256, OCC) void mmq32_t(const GemmParams P, const Ac
                         y[r] = fmaf(-dm, (float)(64 * x1[r] + x2[r]), fmaf(d, (float)S[r], y[r]));
                     }
                 }
-            } else {   // Q6_K: ql[128] qh[64] scales[16] d
-                const u32x4 scw = *gp(reinterpret_cast<const u32x4*>(wt + 6144 + col * 16));
-                const unsigned scv[4] = {scw.x, scw.y, scw.z, scw.w};
+            } else {   // Q6_K: sum of the 8 spans of w = 64*hi + lo, each operand accumulated by the MFMA
+                v16i ah = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, al = ah;
 #pragma unroll
-                for (int hf = 0; hf < 2; ++hf) {
-                    const u32x4 H = *gp(reinterpret_cast<const u32x4*>(wt + 4096 + hf * 1024 + lane * 16));
-#pragma unroll
-                    for (int c = 0; c < 2; ++c) {
-                        const u32x4 L = *gp(reinterpret_cast<const u32x4*>(wt + (2 * hf + c) * 1024 + lane * 16));
-#pragma unroll
-                        for (int nib = 0; nib < 2; ++nib) {
-                            // span (hf, qq): elements 128hf + 32qq + l; this lane's l = 16h + e
-                            const int qq = c + 2 * nib, s = 4 * hf + qq;
-                            const unsigned ls = 4 * nib, hs = 2 * qq;
-                            const unsigned lw[4] = {L.x, L.y, L.z, L.w}, hw[4] = {H.x, H.y, H.z, H.w};
-                            int v[4];
-#pragma unroll
-                            for (int k = 0; k < 4; ++k) {
-                                const unsigned u = ((lw[k] >> ls) & 0x0F0F0F0Fu) | (((hw[k] >> hs) & 0x03030303u) << 4);
-                                v[k] = (int)(((u | 0x80808080u) - 0x20202020u) ^ 0x80808080u);   // q - 32 per byte
-                            }
-                            const v4i bf = v4i{v[0], v[1], v[2], v[3]};
-                            const v4i z = {0, 0, 0, 0};
-                            const int is = 2 * s;   // the span's scale groups 2s (k-half 0), 2s+1 (k-half 1)
-                            const int g0 = (int)(signed char)((scv[is >> 2] >> (8 * (is & 3))) & 0xFF);
-                            const int g1 = (int)(signed char)((scv[is >> 2] >> (8 * (is & 3) + 8)) & 0xFF);
-                            const v4i a = *gp(reinterpret_cast<const v4i*>(aq + s * 1024));
-                            const v16i d0 = mfma(a, h == 0 ? bf : z);
-#pragma unroll
-                            for (int r = 0; r < 16; ++r) S[r] = __mul24(g0, d0[r]) + S[r];
-                            const v16i d1 = mfma(a, h == 1 ? bf : z);
-#pragma unroll
-                            for (int r = 0; r < 16; ++r) S[r] = __mul24(g1, d1[r]) + S[r];
-                        }
-                    }
+                for (int sp = 0; sp < 8; ++sp) {
+                    const v4i a = *gp(reinterpret_cast<const v4i*>(aq + sp * 1024));
+                    const v4i bh = *gp(reinterpret_cast<const v4i*>(wt + sp * 1024 + lane * 16));
+                    const v4i bl = *gp(reinterpret_cast<const v4i*>(wt + 8192 + sp * 1024 + lane * 16));
+                    ah = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bh, ah, 0, 0, 0);
+                    al = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bl, al, 0, 0, 0);
                 }
-                const float dr = h2f(*gp(reinterpret_cast<const unsigned short*>(wt + 6656 + col * 2)));
+                const float dr = h2f(*gp(reinterpret_cast<const unsigned short*>(wt + 16384 + col * 2)));
 #pragma unroll
                 for (int g = 0; g < 4; ++g) {
                     const f32x4 dx4 = *gp(reinterpret_cast<const f32x4*>(dT + 8 * g));
                     const float dx[4] = {dx4.x, dx4.y, dx4.z, dx4.w};
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) y[4 * g + i] = fmaf(dr * dx[i], (float)S[4 * g + i], y[4 * g + i]);
+                    for (int i = 0; i < 4; ++i) {
+                        const int r = 4 * g + i;
+                        y[r] = fmaf(dr * dx[i], (float)(ah[r] * 64 + al[r]), y[r]);   // the exact sumi of the superblock
+                    }
                 }
             }
         }

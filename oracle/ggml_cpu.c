@@ -209,7 +209,11 @@ static float dot_q6_K(const uint8_t* row, int K, const q8k_t* y) {   /* ggml_vec
 
 static float dot_q8_0(const uint8_t* row, int K, const q80_t* y) {   /* ggml_vec_dot_q8_0_q8_0 */
     float sumf = 0;
-    for (int b = 0; b < K / 32; ++b) {
+    const int nb = K / 32;
+    /* ORC_ALT: the blocks summed last to first -- an fp32 order as valid as the generic loop's
+       (the AVX2 path keeps 8 running sums; ggml-cpu's block order differs between its paths) */
+    for (int bi = 0; bi < nb; ++bi) {
+        const int b = alt_order() ? nb - 1 - bi : bi;
         const uint8_t* blk = row + (size_t)b * 34;
         const int8_t* q = (const int8_t*)(blk + 2);
         int sumi = 0;

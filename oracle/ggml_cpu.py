@@ -82,8 +82,9 @@ class Model:
             lib().orc_set_tensor(self.h, name.encode(), t.type, data.ctypes.data, ne[0], ne[1], ne[2])
 
     def decode_one(self, token: int, alt: bool = False) -> np.ndarray:
-        """alt: the same algorithm with the 8 float lanes of every k-quant dot summed in the
-        reverse order -- an equally valid fp32 order (measures the CPU path's own noise floor)."""
+        """alt: the same algorithm with the 8 float lanes of every k-quant dot (the blocks of a
+        Q8_0 row) summed in the reverse order -- an equally valid fp32 order (measures the CPU
+        path's own noise floor)."""
         out = np.empty(self.hp.n_vocab, np.float32)
         lib().orc_set_alt(1 if alt else 0)
         try:
