@@ -623,7 +623,7 @@ int32_t mi_op_attention(int32_t device, int32_t n_head, int32_t n_head_kv, int32
 int32_t mi_op_gemm(int32_t device, int32_t type, const void* raw, const void* raw_up, int32_t rows, int32_t K,
                    int32_t ntok, const float* x, float* y) {
     try {
-        if (!mmq32_supported(type)) throw Error("op_gemm: Q4_K / Q6_K / Q8_0 only");
+        if (!mmq32_supported(type)) throw Error("op_gemm: Q4_K / Q5_K / Q6_K / Q8_0 only");
         if (ntok < 1 || ntok > UB_MAX) throw Error("op_gemm: 1..512 token rows");
         if (rows < 1 || K < 256 || K % 256) throw Error("op_gemm: bad shape");
         MI_HIP(hipSetDevice(device));

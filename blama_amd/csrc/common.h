@@ -60,6 +60,8 @@ struct QMat {                // device view of one (expert of a) quantised matri
     // none): [row tile of 32][superblock][tile bytes], for a gate/up pair on the gate matrix with
     // 16 gate + 16 up rows per tile.
     const uint8_t* sw;
+    long long sw_expert_stride;  // bytes between the experts' MFMA-order copies (MoE)
+    int n_exp;                   // experts stacked in the planes (MoE *_exps tensors), else 1
 };
 
 struct Error : std::runtime_error { using std::runtime_error::runtime_error; };

@@ -167,11 +167,21 @@ std::vector<unsigned short> gelu_table_host() {
 }
 }  // namespace
 
+// Expert e of a MoE tensor as a matrix of its own (planes and MFMA-order copy offset).
+QMat expert_view(const QMat& q, int e) {
+    QMat v = q;
+    for (int k = 0; k < 4; ++k)
+        if (v.p[k]) v.p[k] += e * q.expert_stride[k];
+    if (v.sw) v.sw += e * q.sw_expert_stride;
+    return v;
+}
+
 bool Model::ensure_mmq_copies() {
     std::lock_guard<std::mutex> lk(mmq_mu);
     if (mmq_arena) return true;
     MI_HIP(hipSetDevice(device));
-    // every Q4_K / Q6_K projection (gate and up as one pair copy) and the output head
+    // every mmq32-capable projection (gate and up as one pair copy; MoE: one copy per expert,
+    // expert e at sw + e * sw_expert_stride) and the output head
     std::vector<std::pair<QMat*, QMat*>> todo;
     for (Layer& L : layers) {
         for (QMat* q : {&L.wq, &L.wk, &L.wv, &L.wo, &L.down})
@@ -179,11 +189,13 @@ bool Model::ensure_mmq_copies() {
         if (mmq32_supported(L.gate.type) && L.up.type == L.gate.type) todo.push_back({&L.gate, &L.up});
     }
     if (mmq32_supported(output.type)) todo.push_back({&output, nullptr});
+    auto experts = [](const QMat& q) { return std::max(1, q.n_exp); };
     size_t total = 0;
     std::vector<size_t> offs;
     for (auto& t : todo) {
         offs.push_back(total);
-        total = (total + mmq32_copy_bytes(*t.first, t.second != nullptr) + 255) & ~size_t(255);
+        const size_t one = mmq32_copy_bytes(*t.first, t.second != nullptr);
+        total = (total + one * experts(*t.first) + 255) & ~size_t(255);
     }
     if (!total) return true;
     if (hipMalloc(&mmq_arena, total) != hipSuccess) {
@@ -193,8 +205,14 @@ bool Model::ensure_mmq_copies() {
     }
     mmq_bytes = total;
     for (size_t i = 0; i < todo.size(); ++i) {
-        launch_mmq32_swizzle(*todo[i].first, todo[i].second, mmq_arena + offs[i], nullptr);
-        todo[i].first->sw = mmq_arena + offs[i];
+        QMat& A = *todo[i].first;
+        const size_t one = mmq32_copy_bytes(A, todo[i].second != nullptr);
+        for (int e = 0; e < experts(A); ++e) {   // expert e's planes -> its own copy
+            QMat a = expert_view(A, e), b = todo[i].second ? expert_view(*todo[i].second, e) : QMat{};
+            launch_mmq32_swizzle(a, todo[i].second ? &b : nullptr, mmq_arena + offs[i] + one * e, nullptr);
+        }
+        A.sw = mmq_arena + offs[i];
+        A.sw_expert_stride = (long long)one;
     }
     MI_HIP(hipDeviceSynchronize());
     return true;
@@ -439,6 +457,7 @@ void Model::load(const uint8_t* data, size_t size, const mi_model_params& p) {
         m.K = pl.K;
         m.nb = pl.K / 256;
         m.rows = (int)(pl.rows / pl.experts);
+        m.n_exp = pl.experts;
         if (is_quant(m.type)) {
             for (int k = 0; k < plane_count(m.type); ++k) {
                 m.p[k] = arena + pl.off[k];
@@ -581,46 +600,62 @@ Ctx::Ctx(Model* model, uint32_t nctx, uint32_t nbatch, uint32_t nubatch) : m(mod
 #endif
     // GPT-2 prompts run token by token (one decode graph each): its batch kernels (LayerNorm,
     // biases, GELU) are not built
-    batch_ok = hp.n_expert == 0 && hp.arch == ARCH_LLAMA && getenv("MI_NO_BATCH") == nullptr;
+    batch_ok = hp.arch == ARCH_LLAMA && getenv("MI_NO_BATCH") == nullptr;
     // the persistent step is opt-in (MI_PERSIST=1): measured slower than the graph
     persist_ok = hp.n_expert == 0 && hp.arch == ARCH_LLAMA && use_graphs && getenv("MI_PERSIST") != nullptr &&
                  getenv("MI_NO_PERSIST") == nullptr;
     if (batch_ok) {
-        // MFMA batch path (decode_ubatch / mmq32) when every layer matrix is Q4_K / Q6_K or every
-        // one Q8_0; otherwise prompt chunks on the v_dot4 GEMM (decode_batch)
+        // MFMA batch path (decode_ubatch / mmq32) when every layer matrix is mmq32-capable (each
+        // matrix reads the activation format of its type: Q8_0 activations for Q8_0 weights, Q8_K
+        // for the k-quants); otherwise prompt chunks on the v_dot4 GEMM (decode_batch, dense only)
         mmq_ok = getenv("MI_NO_MMQ") == nullptr;
+        bool any_k = false, any_0 = false;
         for (const Layer& L : m->layers)
-            for (const QMat* q : {&L.wq, &L.wk, &L.wv, &L.wo, &L.gate, &L.up, &L.down})
+            for (const QMat* q : {&L.wq, &L.wk, &L.wv, &L.wo, &L.gate, &L.up, &L.down}) {
                 mmq_ok = mmq_ok && mmq32_supported(q->type);
+                (q->type == T_Q8_0 ? any_0 : any_k) = true;
+            }
         // the gate/up pair shares one MFMA-order copy (16 gate + 16 up rows per tile)
         for (const Layer& L : m->layers)
             mmq_ok = mmq_ok && L.gate.type == L.up.type && L.gate.rows == L.up.rows;
         const int NB = kBatchRows;
+        const int hrows = hp.n_expert > 0 ? NB * hp.n_expert_used : NB;   // MoE: a row per (token, slot)
         MI_HIP(hipMalloc(&xb, (size_t)NB * hp.n_embd * sizeof(float)));
         MI_HIP(hipMalloc(&qb, (size_t)NB * hp.n_embd * sizeof(float)));
         MI_HIP(hipMalloc(&attnb, (size_t)NB * hp.n_embd * sizeof(float)));
-        MI_HIP(hipMalloc(&hb, (size_t)NB * hp.n_ff * sizeof(float)));
+        MI_HIP(hipMalloc(&hb, (size_t)hrows * hp.n_ff * sizeof(float)));
         MI_HIP(hipMalloc(&tokpos_b, (size_t)NB * 4 * sizeof(int)));
         MI_HIP(hipHostMalloc(&h_tokpos_b, (size_t)kTokbRing * NB * 4 * sizeof(int)));
         const int kmax = std::max(hp.n_embd, hp.n_ff);
-        // physical batches on mmq32: every layer matrix Q4_K / Q6_K (the output head too for
-        // batched logits of every token)
         if (mmq_ok) {
-            // one activation format per model: every layer matrix a k-quant (Q8_K activations)
-            // or every one Q8_0 (Q8_0 activations)
-            ub_q80 = m->layers[0].wq.type == T_Q8_0;
-            for (const Layer& L : m->layers)
-                for (const QMat* q : {&L.wq, &L.wk, &L.wv, &L.wo, &L.gate, &L.up, &L.down})
-                    mmq_ok = mmq_ok && mmq32_supported(q->type) && ((q->type == T_Q8_0) == ub_q80);
+            // ub_q / ub_dT / ub_bsb: the k-quant (Q8_K) activations, or the Q8_0 ones when every
+            // matrix is Q8_0; a model mixing both (Mixtral's Q8_0 attn_k / attn_v) has a second
+            // set ub_q0 / ub_dT0 for Q8_0
+            ub_q80 = !any_k;
             // no room for the copy: prompt batches fall back to the v_dot4 GEMM
-            if (mmq_ok) mmq_ok = m->ensure_mmq_copies();
+            mmq_ok = m->ensure_mmq_copies();
             out_mmq = mmq_ok && mmq32_supported(m->output.type);
             attn_mfma = attn_mfma_supported(hp.head_dim) && getenv("MI_ATTN_VALU") == nullptr;
             MI_HIP(hipMalloc(&ub_q, (size_t)UB_MAX * kmax));
             MI_HIP(hipMalloc(&ub_dT, (size_t)UB_MAX * (kmax / 32) * sizeof(float)));   // Q8_0: per 32
             MI_HIP(hipMalloc(&ub_bsb, (size_t)UB_MAX * (kmax / 256) * 16));
+            if (any_k && any_0) {
+                MI_HIP(hipMalloc(&ub_q0, (size_t)UB_MAX * kmax));
+                MI_HIP(hipMalloc(&ub_dT0, (size_t)UB_MAX * (kmax / 32) * sizeof(float)));
+            }
+            if (hp.n_expert > 0) {   // routing of a physical batch, expert down outputs
+                const int ns = NB * hp.n_expert_used;
+                MI_HIP(hipMalloc(&yb, (size_t)ns * hp.n_embd * sizeof(float)));
+                MI_HIP(hipMalloc(&sel_b, (size_t)ns * sizeof(int)));
+                MI_HIP(hipMalloc(&selw_b, (size_t)ns * sizeof(float)));
+                MI_HIP(hipMalloc(&moe_rows, (size_t)ns * sizeof(int)));
+                MI_HIP(hipMalloc(&moe_pos, (size_t)ns * sizeof(int)));
+                MI_HIP(hipHostMalloc(&h_moe, (size_t)3 * ns * sizeof(int)));
+            }
             MI_HIP(hipMalloc(&ub_rope, (size_t)UB_MAX * std::max(1, hp.n_rot / 2) * sizeof(float2)));
         }
+        // MoE prompts need the MFMA path (the v_dot4 GEMM has no routed-expert form)
+        if (hp.n_expert > 0 && !mmq_ok) batch_ok = false;
     }
     MI_HIP(hipMalloc(&attn_smax, (size_t)ATTN_SMAX * hp.n_head * sizeof(float)));
     MI_HIP(hipMalloc(&attn_scores, (size_t)hp.n_head * n_ctx * sizeof(float)));
@@ -660,10 +695,11 @@ Ctx::~Ctx() {
                     (void*)topk_vals, (void*)sel, (void*)selw, (void*)gather_ids, (void*)gather_out,
                     (void*)cell_delta, (void*)move_src, (void*)part_o, (void*)attn_smax, (void*)attn_scores, (void*)stamps,
                     (void*)xb, (void*)qb, (void*)attnb, (void*)hb, (void*)tokpos_b, (void*)ub_q, (void*)ub_dT, (void*)ub_bsb, (void*)ub_rope,
+                    (void*)ub_q0, (void*)ub_dT0, (void*)yb, (void*)sel_b, (void*)selw_b, (void*)moe_rows, (void*)moe_pos,
                     (void*)logits_all, (void*)grows_ids, (void*)grows_out})
         if (p) hipFree(p);
     for (void* p : {(void*)h_tokpos, (void*)h_topk_ids, (void*)h_topk_vals, (void*)h_logits, (void*)h_gather, (void*)h_grows,
-                    (void*)h_tokpos_b})
+                    (void*)h_tokpos_b, (void*)h_moe})
         if (p) hipHostFree(p);
     if (stream) hipStreamDestroy(stream);
 }
@@ -752,7 +788,7 @@ void Ctx::layer_ops(int l, const LayerBufs& B, const std::function<void(const Ge
         gemv(p, 1);
     }
     if (hp.n_expert > 0) {
-        RouterParams rp{B.xa, L.ffn_norm, hp.eps, L.router, hp.n_embd, hp.n_expert, hp.n_expert_used, sel, selw};
+        RouterParams rp{B.xa, L.ffn_norm, hp.eps, L.router, hp.n_embd, hp.n_expert, hp.n_expert_used, sel, selw, 0};
         router(rp);
     }
     // ---- FFN gate/up + SwiGLU ----
@@ -1178,15 +1214,82 @@ void Ctx::decode_batch(const int32_t* tokens, int n) {
     logits_valid = true;
 }
 
-ActQ8 Ctx::ub_act(int K, int ntok) const {
+// build_moe_ffn (src/llama-graph.cpp, b5187: softmax gating, top-2, weights normalised) over a
+// physical batch: the router of every token (the decode step's router_kernel), the (token, slot)
+// picks grouped by expert on the host (one readback per layer), each expert's gate/up + SwiGLU and
+// down over its own tokens (mmq32 on the expert's MFMA-order copy), then every token's
+// x += w0*y0 + w1*y1 in slot order (launch_moe_combine, the decode GEMV's EPI_MOE_DOWN arithmetic).
+void Ctx::moe_ffn_batch(int l, int nt) {
+    const HParams& hp = m->hp;
+    const Layer& L = m->layers[l];
+    const int U = hp.n_expert_used, E = hp.n_expert;
+    RouterParams rp{xb, L.ffn_norm, hp.eps, L.router, hp.n_embd, E, U, sel_b, selw_b, hp.n_embd};
+    launch_router_multi(rp, nt, stream);
+    int* hs = h_moe;                         // [token][slot] -> expert
+    int* hrows = h_moe + (size_t)nt * U;     // row -> source token (rows grouped by expert)
+    int* hpos = h_moe + (size_t)2 * nt * U;  // [token][slot] -> row
+    MI_HIP(hipMemcpyAsync(hs, sel_b, (size_t)nt * U * sizeof(int), hipMemcpyDeviceToHost, stream));
+    MI_HIP(hipStreamSynchronize(stream));
+    std::vector<int> off(E + 1, 0);
+    for (int i = 0; i < nt * U; ++i) {
+        if (hs[i] < 0 || hs[i] >= E) throw Error("moe: router picked an expert out of range");
+        ++off[hs[i] + 1];
+    }
+    for (int e = 0; e < E; ++e) off[e + 1] += off[e];
+    std::vector<int> fill(off.begin(), off.end() - 1);
+    for (int t = 0; t < nt; ++t)   // tokens ascending within an expert
+        for (int k = 0; k < U; ++k) {
+            const int r = fill[hs[t * U + k]]++;
+            hrows[r] = t;
+            hpos[t * U + k] = r;
+        }
+    MI_HIP(hipMemcpyAsync(moe_rows, hrows, (size_t)nt * U * sizeof(int), hipMemcpyHostToDevice, stream));
+    MI_HIP(hipMemcpyAsync(moe_pos, hpos, (size_t)nt * U * sizeof(int), hipMemcpyHostToDevice, stream));
+    for (int e = 0; e < E; ++e) {
+        const int c = off[e + 1] - off[e];
+        if (c == 0) continue;
+        GemmParams p;
+        std::memset(&p, 0, sizeof(p));
+        p.ntok = c;
+        p.tokpos = tokpos_b;
+        // gate/up + SwiGLU: rms_norm(x) * ffn_norm of the expert's tokens
+        const ActQ8 act = ub_act(hp.n_embd, c, L.gate.type);
+        launch_quant_act(xb, hp.n_embd, L.ffn_norm, hp.eps, act, stream, moe_rows + off[e]);
+        p.A = expert_view(L.gate, e);
+        p.B = expert_view(L.up, e);
+        p.pair = PAIR_AB;
+        p.epi = EPI_SWIGLU;
+        p.K = hp.n_embd;
+        p.out = hb + (size_t)off[e] * hp.n_ff;
+        p.out_stride = hp.n_ff;
+        launch_mmq32(p, act, ub_rope, stream);
+        // down: this expert's rows of the FFN output, stored (weighted and summed by the combine)
+        const ActQ8 a2 = ub_act(hp.n_ff, c, L.down.type);
+        launch_quant_act(hb + (size_t)off[e] * hp.n_ff, hp.n_ff, nullptr, hp.eps, a2, stream);
+        GemmParams d = p;
+        d.A = expert_view(L.down, e);
+        std::memset(&d.B, 0, sizeof(d.B));
+        d.pair = PAIR_ADJ;
+        d.epi = EPI_STORE;
+        d.K = hp.n_ff;
+        d.out = yb + (size_t)off[e] * hp.n_embd;
+        d.out_stride = hp.n_embd;
+        launch_mmq32(d, a2, ub_rope, stream);
+    }
+    launch_moe_combine(yb, moe_pos, selw_b, xb, nt, hp.n_embd, stream);
+}
+
+ActQ8 Ctx::ub_act(int K, int ntok, int type) const {
+    const bool q80 = type == T_Q8_0;
+    const bool second = q80 && !ub_q80 && ub_q0;   // the Q8_0 set of a mixed model
     ActQ8 a;
-    a.q = ub_q;
-    a.dT = ub_dT;
+    a.q = second ? ub_q0 : ub_q;
+    a.dT = second ? ub_dT0 : ub_dT;
     a.bsb = ub_bsb;
     a.K = K;
     a.ntok = ntok;
     a.npad = (ntok + 31) / 32 * 32;
-    a.q80 = ub_q80 ? 1 : 0;
+    a.q80 = q80 ? 1 : 0;
     return a;
 }
 
@@ -1217,7 +1320,6 @@ void Ctx::decode_ubatch(const int32_t* tokens, int n, bool all) {
         EmbedParams ep{m->tok_embd, tokpos_b, xb, hp.n_embd};
         launch_embed_multi(ep, nt, stream);
         launch_rope_table(tokpos_b, nt, hp.n_rot, theta_scale, hp.freq_scale, m->rope_freqs, ub_rope, stream);
-        const ActQ8 a_embd = ub_act(hp.n_embd, nt), a_ff = ub_act(hp.n_ff, nt);
         for (int l = 0; l < hp.n_layer; ++l) {
             const Layer& L = m->layers[l];
             __half* kl = kcache + (size_t)l * n_ctx * kv_dim;
@@ -1234,34 +1336,45 @@ void Ctx::decode_ubatch(const int32_t* tokens, int n, bool all) {
             b.kv_dim = kv_dim;
             b.K = hp.n_embd;
             b.out_stride = hp.n_embd;
-            // Q / K / V (+ RoPE, KV append) over one quantisation of rms_norm(x) * attn_norm
-            launch_quant_act(xb, hp.n_embd, L.attn_norm, hp.eps, a_embd, stream);
+            // Q / K / V (+ RoPE, KV append) over one quantisation of rms_norm(x) * attn_norm per
+            // activation format the three matrices read
             const QMat* mats[3] = {&L.wq, &L.wk, &L.wv};
             const int epis[3] = {EPI_ROPE_Q, EPI_ROPE_K, EPI_V};
+            for (int f = 0; f < 2; ++f) {
+                bool need = false;
+                for (const QMat* q : mats) need = need || (q->type == T_Q8_0) == (f == 1);
+                if (need) launch_quant_act(xb, hp.n_embd, L.attn_norm, hp.eps, ub_act(hp.n_embd, nt, f ? T_Q8_0 : T_Q4_K), stream);
+            }
             for (int i = 0; i < 3; ++i) {
                 GemmParams p = b;
                 p.A = *mats[i];
                 p.pair = PAIR_ADJ;
                 p.epi = epis[i];
                 p.out = qb;
-                launch_mmq32(p, a_embd, ub_rope, stream);
+                launch_mmq32(p, ub_act(hp.n_embd, nt, mats[i]->type), ub_rope, stream);
             }
             AttnParams a{qb, kl, vl, tokpos_b, cell_pos, attn_scores, attn_smax, attnb, hp.n_head, hp.n_head_kv,
                          hp.head_dim, kv_dim, (int)n_ctx, kq_scale};
             if (attn_mfma) launch_attn_mfma(a, nt, attnb, stream);
             else launch_attn_multi(a, nt, attnb, stream);
             {   // output projection + residual
-                launch_quant_act(attnb, hp.n_embd, nullptr, hp.eps, a_embd, stream);
+                const ActQ8 act = ub_act(hp.n_embd, nt, L.wo.type);
+                launch_quant_act(attnb, hp.n_embd, nullptr, hp.eps, act, stream);
                 GemmParams p = b;
                 p.A = L.wo;
                 p.pair = PAIR_ADJ;
                 p.epi = EPI_ADD;
                 p.out = xb;
                 p.resid = xb;
-                launch_mmq32(p, a_embd, ub_rope, stream);
+                launch_mmq32(p, act, ub_rope, stream);
+            }
+            if (hp.n_expert > 0) {   // routed experts (build_moe_ffn) + residual
+                moe_ffn_batch(l, nt);
+                continue;
             }
             {   // FFN gate/up + SwiGLU
-                launch_quant_act(xb, hp.n_embd, L.ffn_norm, hp.eps, a_embd, stream);
+                const ActQ8 act = ub_act(hp.n_embd, nt, L.gate.type);
+                launch_quant_act(xb, hp.n_embd, L.ffn_norm, hp.eps, act, stream);
                 GemmParams p = b;
                 p.A = L.gate;
                 p.B = L.up;
@@ -1269,10 +1382,11 @@ void Ctx::decode_ubatch(const int32_t* tokens, int n, bool all) {
                 p.epi = EPI_SWIGLU;
                 p.out = hb;
                 p.out_stride = hp.n_ff;
-                launch_mmq32(p, a_embd, ub_rope, stream);
+                launch_mmq32(p, act, ub_rope, stream);
             }
             {   // FFN down + residual
-                launch_quant_act(hb, hp.n_ff, nullptr, hp.eps, a_ff, stream);
+                const ActQ8 act = ub_act(hp.n_ff, nt, L.down.type);
+                launch_quant_act(hb, hp.n_ff, nullptr, hp.eps, act, stream);
                 GemmParams p = b;
                 p.A = L.down;
                 p.pair = PAIR_ADJ;
@@ -1280,12 +1394,11 @@ void Ctx::decode_ubatch(const int32_t* tokens, int n, bool all) {
                 p.K = hp.n_ff;
                 p.out = xb;
                 p.resid = xb;
-                launch_mmq32(p, a_ff, ub_rope, stream);
+                launch_mmq32(p, act, ub_rope, stream);
             }
         }
         if (all) {   // final norm + output head over every token of the batch
-            ActQ8 a_out = a_embd;
-            a_out.q80 = m->output.type == T_Q8_0 ? 1 : 0;   // the head's own activation format
+            const ActQ8 a_out = ub_act(hp.n_embd, nt, m->output.type);   // the head's own activation format
             launch_quant_act(xb, hp.n_embd, m->output_norm, hp.eps, a_out, stream);
             GemmParams p;
             std::memset(&p, 0, sizeof(p));
@@ -1330,7 +1443,7 @@ int Ctx::decode(const int32_t* tokens, int n, bool all) {
     }
     // prompt ingestion through the batched GEMM when the context stays within the fused
     // attention's reach (dense models; MI_NO_BATCH=1 forces token-by-token decode)
-    const bool fits = n >= 2 && batch_ok && n_cells + n <= ATTN_SHORT && prof_layer < 0;
+    const bool fits = n >= 2 && batch_ok && hp_dense() && n_cells + n <= ATTN_SHORT && prof_layer < 0;
     // the MFMA batch path attends over any number of cells with the MFMA attention kernel
     const bool ub = n >= 2 && batch_ok && mmq_ok && prof_layer < 0 && (attn_mfma || n_cells + n <= ATTN_SHORT);
     if (ub && (!all || out_mmq)) {

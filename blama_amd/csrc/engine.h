@@ -235,7 +235,21 @@ struct Ctx {
                             const std::function<unsigned long long*()>& stamp);
     void decode_batch(const int32_t* tokens, int n);
     void decode_ubatch(const int32_t* tokens, int n, bool all);
-    ActQ8 ub_act(int K, int ntok) const;
+    ActQ8 ub_act(int K, int ntok, int type) const;   // the activation format `type`'s matrices read
+    bool hp_dense() const { return m->hp.n_expert == 0; }
+    // a second activation set (Q8_0) for a model mixing Q8_0 and k-quant matrices
+    int8_t* ub_q0 = nullptr;
+    float* ub_dT0 = nullptr;
+    // MoE prompt batches: router picks and weights [token][n_used], the tokens grouped by expert
+    // (moe_rows: source token of each (expert, token) row; moe_pos: the row of each (token, slot)),
+    // the experts' down outputs [row][n_embd]; h_moe: pinned staging
+    float* yb = nullptr;
+    int* sel_b = nullptr;
+    float* selw_b = nullptr;
+    int* moe_rows = nullptr;
+    int* moe_pos = nullptr;
+    int* h_moe = nullptr;
+    void moe_ffn_batch(int l, int nt);
     const float* out_row(int row) const;   // device logits of output row `row` (-1: the last)
     hipGraphExec_t build_graph(bool with_logits, int seg);
     void invalidate_graphs();

@@ -223,10 +223,18 @@ struct RouterParams {
     float eps;
     const float* w;            // F32 [n_expert][n_embd]
     int n_embd, n_expert, n_used;
-    int* sel;
+    int* sel;                  // [token][n_used]
     float* selw;
+    long long x_stride;        // elements between token rows (launch_router_multi)
 };
 void launch_router(const RouterParams& p, hipStream_t s);
+// the router of ntok token rows x[t * x_stride] -> sel/selw [t][n_used] (one workgroup each)
+void launch_router_multi(const RouterParams& p, int ntok, hipStream_t s);
+// build_moe_ffn's aggregation over a physical batch: x[t] = (y[pos[t][0]]*w[t][0] + y[pos[t][1]]*w[t][1])
+// + x[t] (ggml_mul by the weights, ggml_add of the slots in slot order, then the residual add);
+// y holds the experts' down outputs in compact rows (grouped by expert)
+void launch_moe_combine(const float* y, const int* pos, const float* w, float* x, int ntok, int n_embd,
+                        hipStream_t s);
 
 // ---- load-time repack of GGUF blocks into planes ----
 void launch_repack(const uint8_t* raw, int type, long long rows, int K, uint8_t* const planes[4],
@@ -273,7 +281,9 @@ struct ActQ8 {
     int ntok, npad;            // tokens; rows allocated (ntok rounded up to 32, <= UB_MAX)
     int q80;                   // 1: Q8_0 activations (for Q8_0 weights): dT is [K/32][npad] f16-rounded d, no bsb
 };
-void launch_quant_act(const float* x, int x_stride, const float* norm_w, float eps, const ActQ8& a, hipStream_t s);
+// rows (optional): token t of the batch reads row rows[t] of x (the tokens routed to one expert)
+void launch_quant_act(const float* x, int x_stride, const float* norm_w, float eps, const ActQ8& a, hipStream_t s,
+                      const int* rows = nullptr);
 // ggml_rope_cache_init per token of the batch: out [ntok][n_rot/2] (cos, sin)
 void launch_rope_table(const int* tokpos, int ntok, int n_rot, float theta_scale, float freq_scale,
                        const float* freq_factors, float2* out, hipStream_t s);

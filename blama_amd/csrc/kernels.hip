@@ -1001,9 +1001,14 @@ void launch_gather(const float* logits, const int* ids, int n, float* out, hipSt
 // ---------------------------------------------------------------------------
 // MoE router (build_moe_ffn, softmax gating, norm_w): one workgroup.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void router_kernel(const RouterParams P) {
+__global__ __launch_bounds__(256) void router_kernel(const RouterParams P0) {
     __shared__ double redd[4];
     __shared__ float logit[64];
+    // token blockIdx.x of a batch (launch_router_multi); one token for the decode step
+    RouterParams P = P0;
+    P.x += (long long)blockIdx.x * P.x_stride;
+    P.sel += blockIdx.x * P.n_used;
+    P.selw += blockIdx.x * P.n_used;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     double s = 0.0;
     for (int i = tid; i < P.n_embd; i += 256) s += (double)(P.x[i] * P.x[i]);
@@ -1042,9 +1047,29 @@ __global__ __launch_bounds__(256) void router_kernel(const RouterParams P) {
     }
 }
 
-void launch_router(const RouterParams& p, hipStream_t s) {
+void launch_router(const RouterParams& p, hipStream_t s) { launch_router_multi(p, 1, s); }
+
+void launch_router_multi(const RouterParams& p, int ntok, hipStream_t s) {
     if (p.n_expert > 64) throw Error("router: too many experts");
-    hipLaunchKernelGGL(router_kernel, dim3(1), dim3(256), 0, s, p);
+    if (ntok < 1) return;
+    hipLaunchKernelGGL(router_kernel, dim3(ntok), dim3(256), 0, s, p);
+    MI_HIP(hipGetLastError());
+}
+
+__global__ void moe_combine_kernel(const float* y, const int* pos, const float* w, float* x, int n_embd) {
+    const int t = blockIdx.y;
+    const float* y0 = y + (long long)pos[2 * t] * n_embd;
+    const float* y1 = y + (long long)pos[2 * t + 1] * n_embd;
+    const float w0 = w[2 * t], w1 = w[2 * t + 1];
+    float* xr = x + (long long)t * n_embd;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n_embd; i += gridDim.x * blockDim.x)
+        xr[i] = (y0[i] * w0 + y1[i] * w1) + xr[i];   // as the decode GEMV's EPI_MOE_DOWN
+}
+
+void launch_moe_combine(const float* y, const int* pos, const float* w, float* x, int ntok, int n_embd,
+                        hipStream_t s) {
+    if (ntok < 1) return;
+    hipLaunchKernelGGL(moe_combine_kernel, dim3((n_embd + 255) / 256, ntok), dim3(256), 0, s, y, pos, w, x, n_embd);
     MI_HIP(hipGetLastError());
 }
 

@@ -77,7 +77,7 @@ __device__ __forceinline__ float wave_max_pos(float v) {
 // sum_j m_j*bsum_j = 64*sum m_j hi_j + sum m_j lo_j exactly.  Rows ntok..npad-1 are zero.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void quant_act_kernel(const float* x, int x_stride, const float* norm_w,
-                                                        float eps, ActQ8 a) {
+                                                        float eps, ActQ8 a, const int* rows) {
     const int t = blockIdx.x;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int nb = a.K >> 8;
@@ -97,7 +97,7 @@ __global__ __launch_bounds__(256) void quant_act_kernel(const float* x, int x_st
         }
         return;
     }
-    const f32x4* x4 = reinterpret_cast<const f32x4*>(x + (long long)t * x_stride);
+    const f32x4* x4 = reinterpret_cast<const f32x4*>(x + (long long)(rows ? rows[t] : t) * x_stride);
     float scale = 1.0f;
     if (norm_w) {   // ggml_compute_forward_rms_norm_f32: sum of squares in double
         double sacc = 0.0;
@@ -221,8 +221,9 @@ __device__ __forceinline__ void q4k_scales(const u32x4 hd, int sc[8], int mn[8])
 //         (a 32-element span holds two 16-element scale groups, one per k-half: with the scale
 //         folded into the operand, one MFMA per span and operand carries the exact integer sum)
 //   Q8_0  [j 8][lane 64][16] qs bytes 32j + 16h.. | [c 32][8 f16] d                            8704 B
+//   Q5_K  as Q4_K, plus [lane 64][16] qh bytes 16h..: [p 4][lane][16] qs | qh | [c 32][16] header 5632 B
 __host__ __device__ constexpr int mmq32_tile_bytes_d(int type) {
-    return type == T_Q4_K ? 4608 : type == T_Q6_K ? 16448 : type == T_Q8_0 ? 8704 : 0;
+    return type == T_Q4_K ? 4608 : type == T_Q5_K ? 5632 : type == T_Q6_K ? 16448 : type == T_Q8_0 ? 8704 : 0;
 }
 
 __global__ void swizzle_kernel(const QMat A, const QMat B, int pair, uint8_t* dst) {
@@ -247,6 +248,16 @@ __global__ void swizzle_kernel(const QMat A, const QMat B, int pair, uint8_t* ds
             } else {
                 plane = 1; c = (off - 4096) >> 4; byte = (off - 4096) & 15;
             }
+        } else if (A.type == T_Q5_K) {
+            if (off < 4096) {
+                const int p = off >> 10, ln = (off >> 4) & 63, e = off & 15;
+                plane = 0; c = ln & 31; byte = 32 * p + 16 * (ln >> 5) + e;
+            } else if (off < 5120) {
+                const int ln = (off - 4096) >> 4, e = off & 15;
+                plane = 1; c = ln & 31; byte = 16 * (ln >> 5) + e;
+            } else {
+                plane = 2; c = (off - 5120) >> 4; byte = (off - 5120) & 15;
+            }
         } else {   // Q6_K
             if (off < 16384) {   // w = (q - 32) * scale of element 32s + 16h + e (dequantize_row_q6_K)
                 const int lo = off >= 8192, o2 = off & 8191;
@@ -270,7 +281,9 @@ __global__ void swizzle_kernel(const QMat A, const QMat B, int pair, uint8_t* ds
         long long row = pair ? 16LL * rt + (c & 15) : 32LL * rt + c;
         if (row >= M.rows) row = M.rows - 1;
         const int pb = A.type == T_Q8_0 ? (plane == 0 ? 256 : 16)
-                     : A.type == T_Q4_K ? (plane == 0 ? 128 : 16) : (plane == 0 ? 128 : plane == 1 ? 64 : plane == 2 ? 16 : 2);
+                     : A.type == T_Q4_K ? (plane == 0 ? 128 : 16)
+                     : A.type == T_Q5_K ? (plane == 0 ? 128 : plane == 1 ? 32 : 16)
+                                        : (plane == 0 ? 128 : plane == 1 ? 64 : plane == 2 ? 16 : 2);
         o[off] = M.p[plane][(row * nb + sb) * pb + byte];
     }
 }
@@ -336,18 +349,26 @@ __global__ __launch_bounds__(256, OCC) void mmq32_t(const GemmParams P, const Ac
                 }
                 continue;
             }
-            if (T == T_Q4_K) {
-                // qs[32p + l]: low nibble = sub-block 2p element l, high nibble = sub-block 2p+1
-                const u32x4 hd = *gp(reinterpret_cast<const u32x4*>(wt + 4096 + col * 16));
+            if (T == T_Q4_K || T == T_Q5_K) {
+                // qs[32p + l]: low nibble = sub-block 2p element l, high nibble = sub-block 2p+1;
+                // Q5_K: + 16 * bit 2p / 2p+1 of qh[l] (dequantize_row_q5_K)
+                const u32x4 hd = *gp(reinterpret_cast<const u32x4*>(wt + (T == T_Q5_K ? 5120 : 4096) + col * 16));
+                u32x4 qh = {0u, 0u, 0u, 0u};
+                if (T == T_Q5_K) qh = *gp(reinterpret_cast<const u32x4*>(wt + 4096 + lane * 16));
                 int sc[8], mn[8];
                 q4k_scales(hd, sc, mn);
 #pragma unroll
                 for (int p = 0; p < 4; ++p) {
                     const u32x4 wq = *gp(reinterpret_cast<const u32x4*>(wt + p * 1024 + lane * 16));
-                    const v4i blo = v4i{(int)(wq.x & 0x0F0F0F0Fu), (int)(wq.y & 0x0F0F0F0Fu), (int)(wq.z & 0x0F0F0F0Fu),
-                                        (int)(wq.w & 0x0F0F0F0Fu)};
-                    const v4i bhi = v4i{(int)((wq.x >> 4) & 0x0F0F0F0Fu), (int)((wq.y >> 4) & 0x0F0F0F0Fu),
-                                        (int)((wq.z >> 4) & 0x0F0F0F0Fu), (int)((wq.w >> 4) & 0x0F0F0F0Fu)};
+                    const unsigned sl = 2 * p, sh = 2 * p + 1;
+                    const v4i blo = v4i{(int)((wq.x & 0x0F0F0F0Fu) | (((qh.x >> sl) & 0x01010101u) << 4)),
+                                        (int)((wq.y & 0x0F0F0F0Fu) | (((qh.y >> sl) & 0x01010101u) << 4)),
+                                        (int)((wq.z & 0x0F0F0F0Fu) | (((qh.z >> sl) & 0x01010101u) << 4)),
+                                        (int)((wq.w & 0x0F0F0F0Fu) | (((qh.w >> sl) & 0x01010101u) << 4))};
+                    const v4i bhi = v4i{(int)(((wq.x >> 4) & 0x0F0F0F0Fu) | (((qh.x >> sh) & 0x01010101u) << 4)),
+                                        (int)(((wq.y >> 4) & 0x0F0F0F0Fu) | (((qh.y >> sh) & 0x01010101u) << 4)),
+                                        (int)(((wq.z >> 4) & 0x0F0F0F0Fu) | (((qh.z >> sh) & 0x01010101u) << 4)),
+                                        (int)(((wq.w >> 4) & 0x0F0F0F0Fu) | (((qh.w >> sh) & 0x01010101u) << 4))};
                     const v4i a0 = *gp(reinterpret_cast<const v4i*>(aq + (2 * p) * 1024));
                     const v4i a1 = *gp(reinterpret_cast<const v4i*>(aq + (2 * p + 1) * 1024));
                     const v16i d0 = mfma(a0, blo);
@@ -468,10 +489,11 @@ __device__ __forceinline__ void mmq_epilogue(const GemmParams& P, const ActQ8& a
 
 }  // namespace mmq
 
-void launch_quant_act(const float* x, int x_stride, const float* norm_w, float eps, const ActQ8& a, hipStream_t s) {
+void launch_quant_act(const float* x, int x_stride, const float* norm_w, float eps, const ActQ8& a, hipStream_t s,
+                      const int* rows) {
     if (a.K % 256) throw Error("quant_act: K must be a multiple of 256");
     if (a.npad % 32 || a.ntok > a.npad || a.npad > UB_MAX) throw Error("quant_act: bad token count");
-    hipLaunchKernelGGL(mmq::quant_act_kernel, dim3(a.npad), dim3(256), 0, s, x, x_stride, norm_w, eps, a);
+    hipLaunchKernelGGL(mmq::quant_act_kernel, dim3(a.npad), dim3(256), 0, s, x, x_stride, norm_w, eps, a, rows);
     MI_HIP(hipGetLastError());
 }
 
@@ -483,7 +505,7 @@ void launch_rope_table(const int* tokpos, int ntok, int n_rot, float theta_scale
     MI_HIP(hipGetLastError());
 }
 
-bool mmq32_supported(int type) { return type == T_Q4_K || type == T_Q6_K || type == T_Q8_0; }
+bool mmq32_supported(int type) { return type == T_Q4_K || type == T_Q5_K || type == T_Q6_K || type == T_Q8_0; }
 
 int mmq32_tile_bytes(int type) { return mmq::mmq32_tile_bytes_d(type); }
 
@@ -493,7 +515,7 @@ size_t mmq32_copy_bytes(const QMat& A, bool pair) {
 }
 
 void launch_mmq32_swizzle(const QMat& A, const QMat* B, uint8_t* dst, hipStream_t s) {
-    if (!mmq32_supported(A.type)) throw Error("mmq32 swizzle: Q4_K / Q6_K / Q8_0 only");
+    if (!mmq32_supported(A.type)) throw Error("mmq32 swizzle: Q4_K / Q5_K / Q6_K / Q8_0 only");
     if (B && (B->type != A.type || B->rows != A.rows || B->K != A.K)) throw Error("mmq32 swizzle: bad pair");
     const long long nrt = B ? (A.rows + 15) / 16 : (A.rows + 31) / 32;
     hipLaunchKernelGGL(mmq::swizzle_kernel, dim3((unsigned)(nrt * A.nb)), dim3(256), 0, s, A, B ? *B : A, B ? 1 : 0, dst);
@@ -501,7 +523,7 @@ void launch_mmq32_swizzle(const QMat& A, const QMat* B, uint8_t* dst, hipStream_
 }
 
 void launch_mmq32(const GemmParams& p, const ActQ8& act, const float2* rope, hipStream_t s) {
-    if (!mmq32_supported(p.A.type)) throw Error("mmq32: Q4_K / Q6_K / Q8_0 only");
+    if (!mmq32_supported(p.A.type)) throw Error("mmq32: Q4_K / Q5_K / Q6_K / Q8_0 only");
     if ((p.A.type == T_Q8_0) != (act.q80 != 0)) throw Error("mmq32: Q8_0 weights take Q8_0 activations, k-quants Q8_K");
     if (act.K != p.K || p.A.K != p.K) throw Error("mmq32: activation length differs from K");
     const bool ab = p.pair == PAIR_AB;
@@ -522,6 +544,7 @@ void launch_mmq32(const GemmParams& p, const ActQ8& act, const float2* rope, hip
     decltype(&mmq::mmq32_t<T_Q4_K, false, 4, 2>) fn;
 #define MMQ_PICK(KS_, OCC_)                                                                              \
     fn = p.A.type == T_Q4_K ? (ab ? mmq::mmq32_t<T_Q4_K, true, KS_, OCC_> : mmq::mmq32_t<T_Q4_K, false, KS_, OCC_>) \
+       : p.A.type == T_Q5_K ? (ab ? mmq::mmq32_t<T_Q5_K, true, KS_, OCC_> : mmq::mmq32_t<T_Q5_K, false, KS_, OCC_>) \
        : p.A.type == T_Q6_K ? (ab ? mmq::mmq32_t<T_Q6_K, true, KS_, OCC_> : mmq::mmq32_t<T_Q6_K, false, KS_, OCC_>) \
                             : (ab ? mmq::mmq32_t<T_Q8_0, true, KS_, OCC_> : mmq::mmq32_t<T_Q8_0, false, KS_, OCC_>)
     if (var == 1) MMQ_PICK(1, 2);

@@ -103,13 +103,17 @@ def _check_gemm(t, rows, K, ntok, pair, seed):
     assert bad.size == 0, (R.TYPE_NAME[t], rows, K, ntok, len(bad), bad[:5].tolist(), float((err / lim).max()))
 
 
-# (type, rows, K, token counts, gate/up pair): the 7B / Llama-3-8B / TinyLlama projection shapes,
+# (type, rows, K, token counts, gate/up pair): the 7B / Llama-3-8B / Mixtral (Q5_K experts) /
+# TinyLlama projection shapes,
 # 33 tokens (one full 32-token tile + a 1-token padded tile), 128, and a whole 512-token batch
 GEMM_CASES = [
     (R.Q4_K, 4096, 4096, (33, 128, 512), False),
     (R.Q4_K, 11008, 4096, (33, 512), True),
     (R.Q4_K, 4096, 11008, (128, 512), False),
     (R.Q4_K, 14336, 4096, (128,), False),
+    (R.Q5_K, 4096, 4096, (33, 512), False),
+    (R.Q5_K, 14336, 4096, (128,), True),
+    (R.Q5_K, 4096, 14336, (128,), False),
     (R.Q6_K, 4096, 4096, (33, 512), False),
     (R.Q6_K, 4096, 11008, (512,), False),
     (R.Q6_K, 14336, 4096, (128,), True),
@@ -134,6 +138,7 @@ def test_mmq32_rows_not_multiple_of_tile(gpu_lib):
     _check_gemm(R.Q4_K, 1000, 2048, 40, False, seed=7)
     _check_gemm(R.Q4_K, 1000, 2048, 40, True, seed=8)
     _check_gemm(R.Q6_K, 77, 1024, 5, False, seed=9)
+    _check_gemm(R.Q5_K, 77, 1024, 5, True, seed=10)
 
 
 def attn_batch_ref(q, k16, v16, n_head_kv, tok_cell, tok_pos, cell_pos):

@@ -10,7 +10,8 @@ compare the HIP engine with the C restatement of the ggml CPU path (oracle/ggml_
                       16-wave FFN gate/up over 11008 rows, Q6_K output over 32000 rows
   Llama-3-8B Q6_K     R=4, hd=128, V=128256 (the top-k over 126 blocks)
   Mixtral Q5_K_M      8 experts (so attn_k/attn_v are Q8_0, llama_tensor_get_type's
-                      8-expert rule), top-2 routing, R=4; n_ff cut to 1024 to bound the file
+                      8-expert rule), top-2 routing, R=4; n_ff cut to 1024, and once at the
+                      real 14336 (the real expert GEMV / GEMM shapes and expert stride)
   TinyLlama Q8_0      R=8, hd=64, Q8_0 everywhere
 
 Tolerance.  At these widths the CPU algorithm is not stable to its own fp32 summation order:
@@ -46,6 +47,8 @@ FULL = {
     "llama2-7b-q4_k_m": dict(n_layer=2),
     "llama3-8b-q6_k": dict(n_layer=2),
     "mixtral-8x7b-q5_k_m": dict(n_layer=2, n_ff=1024),
+    # the real 14336 x 4096 Q5_K experts (8 per layer, ~1 GB a layer) at the real expert stride
+    "mixtral-8x7b-q5_k_m-ff14336": dict(base="mixtral-8x7b-q5_k_m", n_layer=2),
     "tinyllama-1.1b-q8_0": dict(n_layer=2),
 }
 
@@ -55,7 +58,8 @@ _cache = {}
 def full_model(name):
     """(cfg, gguf image, engine model) -- built once per test session."""
     if name not in _cache:
-        cfg = synthetic.small_config(name, **FULL[name])
+        kw = dict(FULL[name])
+        cfg = synthetic.small_config(kw.pop("base", name), **kw)
         buf = synthetic.build_gguf(cfg, seed=3)
         _cache[name] = (cfg, buf, engine.Model(buf))
     return _cache[name]
@@ -145,10 +149,13 @@ def test_fullwidth_7b_crosses_512_cells(gpu_lib):
         orc.close()
 
 
-@pytest.mark.parametrize("name", ["llama2-7b-q4_k_m", "llama3-8b-q6_k", "tinyllama-1.1b-q8_0"])
+@pytest.mark.parametrize("name", ["llama2-7b-q4_k_m", "llama3-8b-q6_k", "tinyllama-1.1b-q8_0",
+                                  "mixtral-8x7b-q5_k_m-ff14336"])
 def test_fullwidth_batched_verification_matches_oracle(gpu_lib, name):
     """MI_OUT_ALL at real widths: 24 claimed tokens after a 20-token prompt in one batched pass
-    (mmq32 for every projection and the output head, MFMA attention); every row against the C
+    (mmq32 for every projection and the output head, MFMA attention; Mixtral: the router per
+    token, each expert's GEMMs over the tokens routed to it, Q8_0 attn_k / attn_v on their own
+    Q8_0 activations); every row against the C
     oracle decoding the same tokens one at a time, with this file's tolerances and the
     reference gate, and the claimed ids gathered per row (mi_gather_rows) as fillCtx does."""
     cfg, buf, m = full_model(name)
@@ -178,7 +185,9 @@ def test_fullwidth_batched_verification_matches_oracle(gpu_lib, name):
             assert np.all(np.abs(ref[ids.astype(np.int64)] - ref_sorted) <= 2 * dmax + 1e-6), (name, i)
             a = [(int(x), float(v)) for x, v in zip(ids, vals)]
             cm = R.compare(a, R.gather(ref.astype(np.float32), [x for x, _ in a]))
-            top1.append(cm.top1Match)
+            # top-1 as the reference gate demands, or the oracle's own top two within 2 max|dlogit|
+            # (a near tie the CPU algorithm's rounding floor decides either way)
+            top1.append(1.0 if cm.top1Match == 1.0 or ref_sorted[0] - ref[int(ids[0])] <= 2 * dmax else 0.0)
             score = agg.push_and_verify([cm])
             sims.append(R.logit_similarity(a, R.gather(ref.astype(np.float32), [x for x, _ in a])))
         g = ctx.gather_rows(0, ids_rows)

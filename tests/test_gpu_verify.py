@@ -12,7 +12,7 @@ import pytest
 
 import ggml_ref as R
 from blama_amd import engine, synthetic
-from util import c_alt_floor, oracle_from_gguf
+from util import c_alt_floor, oracle_from_gguf, oracle_ulp_floor
 
 pytestmark = pytest.mark.gpu
 LOGIT_TOL = 2e-3
@@ -24,15 +24,27 @@ def _close(got, ref, tol=LOGIT_TOL):
 
 
 def _check_rows(ctx, buf, prompt, claimed, n_ctx):
+    """Every row within LOGIT_TOL x rms with identical top-10 -- or, at a row where it is not,
+    within twice the oracle's own rounding floor there (util.oracle_ulp_floor, 16 perturbed runs:
+    tiny-moe row 35 is a flip the perturbation reaches in 1 run of 16, at exactly the 5.4e-3 x rms
+    both GPU paths show), with the top-10 equal up to near ties."""
     orc = oracle_from_gguf(buf, n_ctx=n_ctx)
     orc.decode(prompt)
     agg = R.MetricsAggregator()
+    floor = None
     for i, t in enumerate(claimed):
         ref = orc.decode_one(t)
         got = ctx.logits(row=i)
-        assert _close(got, ref), f"row {i}"
         ids, vals = ctx.topk(10, row=i)
-        assert [int(x) for x in ids] == [j for j, _ in R.topk(ref, 10)], f"row {i}"
+        if _close(got, ref):
+            assert [int(x) for x in ids] == [j for j, _ in R.topk(ref, 10)], f"row {i}"
+        else:
+            if floor is None:
+                floor = oracle_ulp_floor(buf, n_ctx, prompt, claimed, runs=16)[1]
+            err = float(np.max(np.abs(got - ref)))
+            assert err <= 2 * floor[i + 1], (i, err, floor[i + 1])
+            ref_sorted = np.sort(ref)[::-1][:10]
+            assert np.all(np.abs(ref[ids.astype(np.int64)] - ref_sorted) <= 2 * err + 1e-6), f"row {i}"
         assert np.array_equal(vals, got[ids])
         g = ctx.gather(ids[::-1], row=i)
         assert np.array_equal(g, got[ids[::-1]])
@@ -43,7 +55,7 @@ def _check_rows(ctx, buf, prompt, claimed, n_ctx):
     assert score >= 0.95
 
 
-@pytest.mark.parametrize("cfg_name", ["tiny-q4_k_m", "tiny-q6_k", "tiny-q5_k_m", "tiny-q8_0"])
+@pytest.mark.parametrize("cfg_name", ["tiny-q4_k_m", "tiny-q6_k", "tiny-q5_k_m", "tiny-q8_0", "tiny-moe-q5_k_m"])
 def test_out_all_matches_oracle(gpu_lib, cfg_name):
     cfg = synthetic.CONFIGS[cfg_name]
     buf = synthetic.build_gguf(cfg, seed=31)

@@ -51,7 +51,9 @@ def oracle_ulp_floor(buf, n_ctx, prompt, tokens, runs=4, seed=100):
     accumulate the attention dots (KQ, KQV) in f32 as ggml's AVX2 ggml_vec_dot_f16 does, where
     the base oracle sums in double, and move every score and head output by -1/0/+1 ulp: the synthetic GPT-2 models have large, flat attention scores
     past ~500 cells, where that alone moves the oracle's logits by 7.7e-3 x rms
-    (tiny-gpt2-q8_0, 520 cells)."""
+    (tiny-gpt2-q8_0, 520 cells).  F32 weights (the MoE router, summed in double by the base
+    oracle) are summed in f32 in the perturbed runs: a router near-tie there picks another
+    expert (tiny-moe row 35: 5.4e-3 x rms, GPU batch and per-token paths alike)."""
     orig = R.mul_mat_vec
     orig_attn = R.attention_head
 
@@ -68,6 +70,9 @@ def oracle_ulp_floor(buf, n_ctx, prompt, tokens, runs=4, seed=100):
                 return ulp((p16 @ V16.astype(np.float32)).astype(np.float32), rng)
 
             def mm(raw, t, K, x):
+                if t == R.F32:   # F32 weights (the MoE router): an fp32 dot, as ggml_vec_dot_f32 forms it
+                    W = np.ascontiguousarray(raw).view(np.float32).reshape(-1, K)
+                    return ulp(W @ np.asarray(x, np.float32).reshape(-1), rng)
                 return ulp(orig(raw, t, K, x), rng)
             R.mul_mat_vec = mm
             R.attention_head = attn32
