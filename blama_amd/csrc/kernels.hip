@@ -416,7 +416,10 @@ void launch_quantize_q8k(const float* x, int K, int8_t* q, float* d, int* bsums,
 // Lane layout: LPC = head_dim/8 lanes hold one cache row (8 halves = one
 // 16-byte load each); a wave covers CPW = 64/LPC cells per step.
 // ---------------------------------------------------------------------------
-template <int R, int LPC>
+// U: cell steps whose cache loads are in flight together.  The first step's loads are issued at
+// entry, ahead of the loads the arithmetic waits on first (q; the split maxima and scores), so
+// the cache round trip overlaps them.
+template <int R, int LPC, int U>
 __global__ __launch_bounds__(256) void attn_scores_kernel(const AttnParams P) {
     constexpr int CPW = 64 / LPC;
     constexpr int HD = LPC * 8;
@@ -435,6 +438,19 @@ __global__ __launch_bounds__(256) void attn_scores_kernel(const AttnParams P) {
     const int c0 = s * chunk, c1 = min(ncell, c0 + chunk);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int L = lane % LPC, G = lane / LPC;
+    const long long row_off = (long long)g * HD + L * 8;
+    u32x4 kk[U];
+    int cpos[U];
+    auto fetch = [&](int cb) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            int c = cb + u * 4 * CPW + G;
+            c = c < c1 ? c : c1 - 1;
+            kk[u] = *reinterpret_cast<const u32x4*>(P.kcache + (long long)c * P.kv_dim + row_off);
+            cpos[u] = P.cell_pos[c];
+        }
+    };
+    fetch(c0 + wave * CPW);
     float q[R][8];
 #pragma unroll
     for (int t = 0; t < R; ++t) {
@@ -447,18 +463,8 @@ __global__ __launch_bounds__(256) void attn_scores_kernel(const AttnParams P) {
     float mx[R];
 #pragma unroll
     for (int t = 0; t < R; ++t) mx[t] = -INFINITY;
-    const long long row_off = (long long)g * HD + L * 8;
-    constexpr int U = 4;   // steps whose K loads are issued together
     for (int cb = c0 + wave * CPW; cb < c1; cb += 4 * CPW * U) {
-        u32x4 kk[U];
-        int cpos[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            int c = cb + u * 4 * CPW + G;
-            c = c < c1 ? c : c1 - 1;
-            kk[u] = *reinterpret_cast<const u32x4*>(P.kcache + (long long)c * P.kv_dim + row_off);
-            cpos[u] = P.cell_pos[c];
-        }
+        if (cb != c0 + wave * CPW) fetch(cb);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int c = cb + u * 4 * CPW + G;
@@ -499,7 +505,7 @@ __global__ __launch_bounds__(256) void attn_scores_kernel(const AttnParams P) {
 #endif
 }
 
-template <int R, int LPC>
+template <int R, int LPC, int U>
 __global__ __launch_bounds__(256) void attn_pv_kernel(const AttnParams P) {
     constexpr int CPW = 64 / LPC;
     constexpr int HD = LPC * 8;
@@ -521,6 +527,16 @@ __global__ __launch_bounds__(256) void attn_pv_kernel(const AttnParams P) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int L = lane % LPC, G = lane / LPC;
     const long long row_off = (long long)g * HD + L * 8;
+    u32x4 vv[U];
+    auto fetch = [&](int cb) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            int c = cb + u * 4 * CPW + G;
+            c = c < c1 ? c : c1 - 1;
+            vv[u] = *reinterpret_cast<const u32x4*>(P.vcache + (long long)c * P.kv_dim + row_off);
+        }
+    };
+    fetch(c0 + wave * CPW);   // in flight while the softmax statistics are formed
     // global max of every head of the group
     float M[R];
 #pragma unroll
@@ -550,16 +566,14 @@ __global__ __launch_bounds__(256) void attn_pv_kernel(const AttnParams P) {
     for (int t = 0; t < R; ++t)
 #pragma unroll
         for (int e = 0; e < 8; ++e) o[t][e] = 0.0f;
-    constexpr int U = 4;
     for (int cb = c0 + wave * CPW; cb < c1; cb += 4 * CPW * U) {
-        u32x4 vv[U];
+        if (cb != c0 + wave * CPW) fetch(cb);
         float pw[U][R];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             int c = cb + u * 4 * CPW + G;
             const bool in = c < c1;
             c = in ? c : c1 - 1;
-            vv[u] = *reinterpret_cast<const u32x4*>(P.vcache + (long long)c * P.kv_dim + row_off);
 #pragma unroll
             for (int t = 0; t < R; ++t) {
                 const float w = P.scores[(long long)(gq + t) * P.n_ctx + c];
@@ -787,13 +801,29 @@ __global__ __launch_bounds__(256) void attn_fused_kernel(const AttnParams P) {
 }
 
 typedef void (*AttnFn)(const AttnParams);
+// MI_ATTN_U=<4|8>: cell steps per wave whose cache loads the split kernels issue together
+static int attn_u() {
+    static const int u = getenv("MI_ATTN_U") ? atoi(getenv("MI_ATTN_U")) : 4;
+    return u == 8 ? 8 : 4;
+}
+template <int R, int LPC>
+static void attn_fns_l(AttnFn& a, AttnFn& b, AttnFn& f) {
+    if (attn_u() == 8) {
+        a = attn_scores_kernel<R, LPC, 8>;
+        b = attn_pv_kernel<R, LPC, 8>;
+    } else {
+        a = attn_scores_kernel<R, LPC, 4>;
+        b = attn_pv_kernel<R, LPC, 4>;
+    }
+    f = attn_fused_kernel<R, LPC>;
+}
 template <int R>
 static void attn_fns_r(int hd, AttnFn& a, AttnFn& b, AttnFn& f) {
     switch (hd) {
-    case 32: a = attn_scores_kernel<R, 4>; b = attn_pv_kernel<R, 4>; f = attn_fused_kernel<R, 4>; break;
-    case 64: a = attn_scores_kernel<R, 8>; b = attn_pv_kernel<R, 8>; f = attn_fused_kernel<R, 8>; break;
-    case 128: a = attn_scores_kernel<R, 16>; b = attn_pv_kernel<R, 16>; f = attn_fused_kernel<R, 16>; break;
-    case 256: a = attn_scores_kernel<R, 32>; b = attn_pv_kernel<R, 32>; f = attn_fused_kernel<R, 32>; break;
+    case 32: attn_fns_l<R, 4>(a, b, f); break;
+    case 64: attn_fns_l<R, 8>(a, b, f); break;
+    case 128: attn_fns_l<R, 16>(a, b, f); break;
+    case 256: attn_fns_l<R, 32>(a, b, f); break;
     default: a = b = f = nullptr; break;
     }
 }
