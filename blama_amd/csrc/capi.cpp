@@ -611,6 +611,15 @@ int32_t mi_op_attention(int32_t device, int32_t n_head, int32_t n_head_kv, int32
                      dsc.as<float>(), dsm.as<float>(), dpo.as<float>(), n_head, n_head_kv, head_dim, kv_dim,
                      n_cells, 1.0f / std::sqrt((float)head_dim)};
         a.fused = n_cells <= ATTN_SHORT ? 1 : 0;   // the decode graph's choice for this cell count
+        // the decode graph's single-launch long-context kernel (exchange buffers zeroed, step 0)
+        DevBuf dxf((size_t)n_head * ATTN_SMAX * 32 * sizeof(unsigned)), dxm((size_t)n_head * ATTN_SMAX * sizeof(float));
+        DevBuf dxs((size_t)n_head * ATTN_SMAX * sizeof(double)), dst(16);
+        MI_HIP(hipMemset(dxf.p, 0, (size_t)n_head * ATTN_SMAX * 32 * sizeof(unsigned)));
+        MI_HIP(hipMemset(dst.p, 0, 16));
+        a.xflags = dxf.as<unsigned>();
+        a.xmax = dxm.as<float>();
+        a.xsum = dxs.as<double>();
+        a.step = dst.as<unsigned>();
         launch_attn(a, nullptr);
         launch_attn_combine(AttnPartials{dpo.as<float>(), n_head, head_dim}, dtp.as<int>(), dout.as<float>(), nullptr);
         MI_HIP(hipDeviceSynchronize());

@@ -659,6 +659,15 @@ Ctx::Ctx(Model* model, uint32_t nctx, uint32_t nbatch, uint32_t nubatch) : m(mod
     }
     MI_HIP(hipMalloc(&attn_smax, (size_t)ATTN_SMAX * hp.n_head * sizeof(float)));
     MI_HIP(hipMalloc(&attn_scores, (size_t)hp.n_head * n_ctx * sizeof(float)));
+    MI_HIP(hipMalloc(&attn_xflags, (size_t)hp.n_head * ATTN_SMAX * 32 * sizeof(unsigned)));
+    MI_HIP(hipMemset(attn_xflags, 0, (size_t)hp.n_head * ATTN_SMAX * 32 * sizeof(unsigned)));
+    MI_HIP(hipMalloc(&attn_xmax, (size_t)hp.n_head * ATTN_SMAX * sizeof(float)));
+    MI_HIP(hipMalloc(&attn_xsum, (size_t)hp.n_head * ATTN_SMAX * sizeof(double)));
+    MI_HIP(hipMalloc(&step_ctr, 16));
+    MI_HIP(hipMemset(step_ctr, 0, 16));
+    MI_HIP(hipHostMalloc(&h_attn_xerr, 16, hipHostMallocMapped | hipHostMallocCoherent));
+    *h_attn_xerr = 0;
+    MI_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&d_attn_xerr), h_attn_xerr, 0));
     MI_HIP(hipMalloc(&topk_ids, TOPK_MAX * sizeof(int)));
     MI_HIP(hipMalloc(&topk_vals, TOPK_MAX * sizeof(float)));
     MI_HIP(hipMalloc(&sel, 64 * sizeof(int)));
@@ -694,12 +703,13 @@ Ctx::~Ctx() {
                     (void*)q, (void*)attn, (void*)h, (void*)h2, (void*)logits, (void*)cand, (void*)topk_ids,
                     (void*)topk_vals, (void*)sel, (void*)selw, (void*)gather_ids, (void*)gather_out,
                     (void*)cell_delta, (void*)move_src, (void*)part_o, (void*)attn_smax, (void*)attn_scores, (void*)stamps,
+                    (void*)attn_xflags, (void*)attn_xmax, (void*)attn_xsum, (void*)step_ctr,
                     (void*)xb, (void*)qb, (void*)attnb, (void*)hb, (void*)tokpos_b, (void*)ub_q, (void*)ub_dT, (void*)ub_bsb, (void*)ub_rope,
                     (void*)ub_q0, (void*)ub_dT0, (void*)yb, (void*)sel_b, (void*)selw_b, (void*)moe_rows, (void*)moe_pos,
                     (void*)logits_all, (void*)grows_ids, (void*)grows_out})
         if (p) hipFree(p);
     for (void* p : {(void*)h_tokpos, (void*)h_topk_ids, (void*)h_topk_vals, (void*)h_logits, (void*)h_gather, (void*)h_grows,
-                    (void*)h_tokpos_b, (void*)h_moe})
+                    (void*)h_tokpos_b, (void*)h_moe, (void*)h_attn_xerr})
         if (p) hipHostFree(p);
     if (stream) hipStreamDestroy(stream);
 }
@@ -773,6 +783,12 @@ void Ctx::layer_ops(int l, const LayerBufs& B, const std::function<void(const Ge
         AttnParams a{B.q, kl, vl, tokpos, cell_pos, attn_scores, attn_smax, B.po, hp.n_head, hp.n_head_kv, hp.head_dim,
                      kv_dim, (int)n_ctx, kq_scale};
         a.fused = attn_fused;
+        a.xflags = attn_xflags;   // contexts past ATTN_SHORT: one launch (attn_long_kernel)
+        a.xmax = attn_xmax;
+        a.xsum = attn_xsum;
+        a.step = step_ctr;
+        a.layer = l;
+        a.xerr = d_attn_xerr;
         attn(a);
     }
     // ---- output projection + residual (prologue: the attention splits combined) ----
@@ -851,7 +867,7 @@ void Ctx::enqueue_step(bool with_logits) {
         return stamps + (size_t)(n_launch++) * kStampWgs * 8;
     };
     auto on = [&]() { return seg_filter < 0 || seg_filter == seg; };
-    EmbedParams ep{m->tok_embd, tokpos, x, hp.n_embd, m->pos_embd, hp.arch == ARCH_GPT2 ? 1 : 0};
+    EmbedParams ep{m->tok_embd, tokpos, x, hp.n_embd, m->pos_embd, hp.arch == ARCH_GPT2 ? 1 : 0, step_ctr};
     if (on()) launch_embed(ep, stream);
     const float kq_scale = 1.0f / std::sqrt((float)hp.head_dim);
     for (int l = 0; l < hp.n_layer; ++l) {
@@ -903,7 +919,7 @@ void Ctx::enqueue_step(bool with_logits) {
 void Ctx::enqueue_step_persist(bool with_logits) {
     const HParams& hp = m->hp;
     auto on = [&](int seg) { return seg_filter < 0 || seg_filter == seg; };
-    EmbedParams ep{m->tok_embd, tokpos, x, hp.n_embd, m->pos_embd, 0};
+    EmbedParams ep{m->tok_embd, tokpos, x, hp.n_embd, m->pos_embd, 0, step_ctr};
     if (on(0)) launch_embed(ep, stream);
     const bool timed = seg_filter == 1 && prof_layer >= 0;
     if (on(1)) persist_launch(pst[with_logits], stream, timed ? prof_ev[0] : nullptr, timed ? prof_ev[1] : nullptr);
@@ -1523,6 +1539,12 @@ void Ctx::sync() {
     MI_HIP(hipSetDevice(device));
     MI_HIP(hipStreamSynchronize(stream));
     check_persist();
+    if (h_attn_xerr && *h_attn_xerr) {   // an attention exchange gave up: the step's logits are invalid
+        *h_attn_xerr = 0;
+        logits_valid = false;
+        throw Error("long-context attention: the splits of a head were not co-resident (exchange timed out); "
+                    "MI_ATTN_SPLIT2=1 selects the two-launch kernels");
+    }
 }
 
 const float* Ctx::out_row(int row) const {

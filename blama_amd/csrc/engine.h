@@ -148,6 +148,13 @@ struct Ctx {
     float* part_o = nullptr;            // split-K attention partials [ATTN_SMAX][n_head][hd]
     float* attn_smax = nullptr;         // [ATTN_SMAX][n_head] split maxima
     float* attn_scores = nullptr;       // [n_head][n_ctx] scaled KQ
+    // the single-launch long-context attention's exchange (attn_long_kernel) and the step counter
+    unsigned* attn_xflags = nullptr;    // [n_head][ATTN_SMAX][32]
+    float* attn_xmax = nullptr;
+    double* attn_xsum = nullptr;
+    unsigned* step_ctr = nullptr;       // decode steps so far (incremented by the embedding launch)
+    unsigned* h_attn_xerr = nullptr;    // host-mapped: an exchange timed out
+    unsigned* d_attn_xerr = nullptr;
     // batched prompt ingestion (dense models): GEMM_NT rows of residual / q / attention / FFN
     bool batch_ok = false;
     float *xb = nullptr, *qb = nullptr, *attnb = nullptr, *hb = nullptr;

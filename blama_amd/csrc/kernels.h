@@ -167,6 +167,7 @@ struct EmbedParams {
     int n_embd;
     QMat P;                    // GPT-2: learned position embedding (row = the token's position),
     int has_pos;               // added to the token row (ggml_add of the two get_rows)
+    unsigned* step;            // optional: incremented once per launch (decode step counter)
 };
 void launch_embed(const EmbedParams& p, hipStream_t s);
 
@@ -188,6 +189,14 @@ struct AttnParams {
     unsigned long long* stamps2;
     int fused;                     // 1: the single-launch kernel (the context has <= ATTN_SHORT cells)
     int qsplit;                    // fused kernel: 0 = a workgroup per kv head; R = a workgroup per q head
+    // contexts past ATTN_SHORT cells in ONE launch (attn_long_kernel): the splits of a q head
+    // exchange their maxima and partial sums through these (null: the two-launch split kernels)
+    unsigned* xflags;              // [n_head][ATTN_SMAX][32]: the exchange's flag lines
+    float* xmax;                   // [n_head][ATTN_SMAX]
+    double* xsum;                  // [n_head][ATTN_SMAX]
+    const unsigned* step;          // decode steps so far (the embedding launch counts them)
+    int layer;                     // this layer (the exchange's epoch: step * 256 + 2 * layer + phase)
+    unsigned* xerr;                // host-mapped: an exchange timed out (the step is invalid)
 };
 void launch_attn(const AttnParams& p, hipStream_t s);
 // Combine the partials into out[n_head*hd] (tests / the eager debug path).

@@ -340,6 +340,7 @@ __device__ float dequant_elem(const QMat& M, long long row, int col) {
 __global__ void embed_kernel(const EmbedParams P) {
     const long long tok = P.tokpos[0];
     const long long pos = P.tokpos[1];
+    if (P.step && blockIdx.x == 0 && threadIdx.x == 0) *P.step += 1u;
     for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < P.n_embd; c += gridDim.x * blockDim.x) {
         const float e = dequant_elem(P.E, tok, c);
         P.out[c] = P.has_pos ? e + dequant_elem(P.P, pos, c) : e;
@@ -621,6 +622,194 @@ __global__ __launch_bounds__(256) void attn_pv_kernel(const AttnParams P) {
 #endif
 }
 
+// Contexts past ATTN_SHORT cells in ONE launch: grid (n_head, ATTN_SMAX), one q head per
+// workgroup row, split s of the head's cells per column (attn_split's chunks).  The split keeps its
+// scaled scores in LDS; the splits of a head exchange their maxima, then their partial sums of
+// expf(w - M) in double, through flag lines (agent-scope stores, bounded polls), so every split
+// rounds p = f16(expf(w - M) * (1/S)) with the head's global M and S -- the CPU graph's softmax --
+// without the scores' round trip through global memory and the second launch of
+// attn_scores_kernel / attn_pv_kernel.  The V chunk's loads are issued before the exchange.
+// The splits of one head are co-resident (n_head * 16 workgroups of 4 waves fit the chip many
+// times over); a poll gives up after 2 s and flags the step invalid (xerr) instead of hanging.
+__device__ __forceinline__ unsigned ld_ag(const unsigned* p) {
+    return __hip_atomic_load(const_cast<unsigned*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <int LPC>
+__global__ __launch_bounds__(256) void attn_long_kernel(const AttnParams P) {
+    constexpr int CPW = 64 / LPC;
+    constexpr int HD = LPC * 8;
+    constexpr int U = 4;
+    extern __shared__ __attribute__((aligned(16))) float sw[];   // [chunk] scaled scores
+    __shared__ float redm[4];
+    __shared__ double dred[4];
+    __shared__ float stat[2];                                     // M, inv
+    __shared__ float red_o[4][HD];
+    const int h = blockIdx.x, s = blockIdx.y;
+    const int g = h / (P.n_head / P.n_head_kv);
+    const int ncell = P.tokpos[2] + 1, qpos = P.tokpos[1];
+    int chunk, nsplit;
+    attn_split(ncell, chunk, nsplit);
+    if (s >= nsplit) return;
+    const int c0 = s * chunk, c1 = min(ncell, c0 + chunk);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int L = lane % LPC, G = lane / LPC;
+    const long long row_off = (long long)g * HD + L * 8;
+    const unsigned epoch = *P.step * 256u + 2u * (unsigned)P.layer;
+    unsigned* const fl = P.xflags + (long long)h * ATTN_SMAX * 32;
+    u32x4 kk[U];
+    int cpos[U];
+    auto fetch_k = [&](int cb) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            int c = cb + u * 4 * CPW + G;
+            c = c < c1 ? c : c1 - 1;
+            kk[u] = *reinterpret_cast<const u32x4*>(P.kcache + (long long)c * P.kv_dim + row_off);
+            cpos[u] = P.cell_pos[c];
+        }
+    };
+    fetch_k(c0 + wave * CPW);
+    float q[8];
+    {
+        const float4* qp = reinterpret_cast<const float4*>(P.q + (long long)h * HD + L * 8);
+        const float4 a = qp[0], b = qp[1];
+        const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) q[e] = __half2float(__float2half_rn(v[e]));
+    }
+    // 1. scaled KQ of the split's cells into LDS, the split's max
+    float mx = -INFINITY;
+    for (int cb = c0 + wave * CPW; cb < c1; cb += 4 * CPW * U) {
+        if (cb != c0 + wave * CPW) fetch_k(cb);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int c = cb + u * 4 * CPW + G;
+            const bool valid = c < c1 && cpos[u] <= qpos;
+            const unsigned kw[4] = {kk[u].x, kk[u].y, kk[u].z, kk[u].w};
+            float d = 0.0f;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                d = fmaf(q[2 * e], h2f(kw[e]), d);
+                d = fmaf(q[2 * e + 1], h2f(kw[e] >> 16), d);
+            }
+#pragma unroll
+            for (int off = LPC / 2; off > 0; off >>= 1) d += __shfl_xor(d, off, 64);
+            const float w = valid ? d * P.scale : -INFINITY;
+            mx = fmaxf(mx, w);
+            if (L == 0 && c < c1) sw[c - c0] = w;
+        }
+    }
+    // the V chunk a wave reads first: waves 1-3 issue it before the exchange; wave 0, which polls,
+    // after it (vmcnt retires in issue order: a flag load would wait behind it)
+    u32x4 vv[U];
+    auto fetch_v = [&](int cb) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            int c = cb + u * 4 * CPW + G;
+            c = c < c1 ? c : c1 - 1;
+            vv[u] = *reinterpret_cast<const u32x4*>(P.vcache + (long long)c * P.kv_dim + row_off);
+        }
+    };
+    mx = wave_max(mx);
+    if (lane == 0) redm[wave] = mx;
+    __syncthreads();
+    // publish this split's value of phase ph (stored by thread 0 before), then wait for every
+    // split's (wave 0); false after a timeout
+    auto exchange = [&](int ph) -> bool {
+        bool ok = true;
+        if (wave == 0) {
+            const unsigned tgt = epoch + 1u + (unsigned)ph;
+            if (lane == 0) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the value's store completed
+                __hip_atomic_store(fl + s * 32, tgt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+            for (;;) {
+                const unsigned f = lane < nsplit ? ld_ag(fl + lane * 32) : tgt;
+                if (__all((int)(f - tgt) >= 0)) break;
+                if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {
+                    ok = false;
+                    if (lane == 0 && P.xerr) __hip_atomic_store(P.xerr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    break;
+                }
+            }
+            asm volatile("" ::: "memory");
+        }
+        return ok;
+    };
+    if (tid == 0) {
+        const float m = fmaxf(fmaxf(redm[0], redm[1]), fmaxf(redm[2], redm[3]));
+        __hip_atomic_store(P.xmax + h * ATTN_SMAX + s, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (wave != 0) fetch_v(c0 + wave * CPW);
+    exchange(0);
+    if (wave == 0) {
+        float m = lane < nsplit ? __hip_atomic_load(P.xmax + h * ATTN_SMAX + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                : -INFINITY;
+        m = wave_max(m);
+        if (lane == 0) stat[0] = m;
+    }
+    __syncthreads();
+    const float M = stat[0];
+    // 2. the split's sum of expf(w - M) in double; the head's sum in split order
+    double acc = 0.0;
+    for (int c = c0 + tid; c < c1; c += 256) acc += (double)expf(sw[c - c0] - M);
+    acc = wave_sum_d(acc);
+    if (lane == 0) dred[wave] = acc;
+    __syncthreads();
+    if (tid == 0) {
+        const double ss = ((dred[0] + dred[1]) + dred[2]) + dred[3];
+        __hip_atomic_store(P.xsum + h * ATTN_SMAX + s, ss, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    exchange(1);
+    if (tid == 0) {
+        double v[ATTN_SMAX];
+#pragma unroll
+        for (int k = 0; k < ATTN_SMAX; ++k)
+            v[k] = k < nsplit ? __hip_atomic_load(P.xsum + h * ATTN_SMAX + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
+        double tot = 0.0;
+        for (int k = 0; k < nsplit; ++k) tot += v[k];
+        stat[1] = (float)(1.0 / tot);
+    }
+    if (wave == 0) fetch_v(c0 + wave * CPW);
+    __syncthreads();
+    const float inv = stat[1];
+    // 3. sum over the split's cells of f16(p_c) v_c
+    float o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = 0.0f;
+    for (int cb = c0 + wave * CPW; cb < c1; cb += 4 * CPW * U) {
+        if (cb != c0 + wave * CPW) fetch_v(cb);
+        float pw[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int c = cb + u * 4 * CPW + G;
+            const bool in = c < c1;
+            const float p = expf(sw[(in ? c : c1 - 1) - c0] - M) * inv;   // ggml_vec_soft_max_f32, f16 vec_dot_type
+            pw[u] = in ? __half2float(__float2half_rn(p)) : 0.0f;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const unsigned vw[4] = {vv[u].x, vv[u].y, vv[u].z, vv[u].w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                o[2 * e] = fmaf(pw[u], h2f(vw[e]), o[2 * e]);
+                o[2 * e + 1] = fmaf(pw[u], h2f(vw[e] >> 16), o[2 * e + 1]);
+            }
+        }
+    }
+#pragma unroll
+    for (int off = LPC; off < 64; off <<= 1)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] += __shfl_xor(o[e], off, 64);
+    if (G == 0) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) red_o[wave][L * 8 + e] = o[e];
+    }
+    __syncthreads();
+    for (int d = tid; d < HD; d += 256)
+        P.part_o[((long long)s * P.n_head + h) * HD + d] = ((red_o[0][d] + red_o[1][d]) + red_o[2][d]) + red_o[3][d];
+}
+
 // Short contexts (<= ATTN_SHORT cells): the same arithmetic as the two kernels above with a
 // single split, in one launch.  One workgroup per kv head keeps its scores in LDS, so no
 // other workgroup's result is needed between the softmax statistics and the PV sum.
@@ -853,6 +1042,16 @@ void launch_attn(const AttnParams& p, hipStream_t s) {
         hipLaunchKernelGGL(ff, dim3(p.n_head_kv), dim3(256), 0, s, p);
         MI_HIP(hipGetLastError());
         return;
+    }
+    if (p.xflags && p.step && (p.head_dim == 64 || p.head_dim == 128) && getenv("MI_ATTN_SPLIT2") == nullptr) {
+        // one launch, the splits of a q head exchanging their softmax statistics
+        const size_t lds = (size_t)std::max(64, ((p.n_ctx + ATTN_SMAX - 1) / ATTN_SMAX + 63) / 64 * 64) * sizeof(float);
+        if (lds <= 64 * 1024) {
+            auto fn = p.head_dim == 128 ? attn_long_kernel<16> : attn_long_kernel<8>;
+            hipLaunchKernelGGL(fn, dim3(p.n_head, ATTN_SMAX), dim3(256), lds, s, p);
+            MI_HIP(hipGetLastError());
+            return;
+        }
     }
     if (r > 1 && p.n_head_kv < 16) {   // few kv heads: one workgroup per q head and split
         AttnFn f1 = nullptr, a1 = nullptr, b1 = nullptr;
