@@ -504,24 +504,27 @@ __device__ __forceinline__ void gv_body(const GvArgs& a, char* lds, Wait&& wait 
             int chunk;
             attn_split(__builtin_amdgcn_readfirstlane(tp.z) + 1, chunk, nsplit);
         }
-        // four splits' loads in flight together, then added in split order
-        for (int sp0 = 1; sp0 < nsplit; sp0 += 4) {
-            f32x4 t4[4][KB];
+        if constexpr (KB == 1) {
+            // four splits' loads in flight together, then added in split order
+            for (int sp0 = 1; sp0 < nsplit; sp0 += 4) {
+                f32x4 t4[4];
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
+                for (int j = 0; j < 4; ++j)
+                    if (wave < nb && sp0 + j < nsplit)
+                        t4[j] = gptr(reinterpret_cast<const f32x4*>(a.attn_o + (long long)(sp0 + j) * a.attn_stride))[wave * 64 + lane];
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if (wave < nb && sp0 + j < nsplit) xv[0] += t4[j];
+            }
+        } else {   // wider activations: no extra registers (they would cost the GEMV ring its occupancy)
+            for (int sp = 1; sp < nsplit; ++sp) {
 #pragma unroll
                 for (int i = 0; i < KB; ++i) {
                     const int blk = wave + GV_NW * i;
-                    if (blk < nb && sp0 + j < nsplit)
-                        t4[j][i] = gptr(reinterpret_cast<const f32x4*>(a.attn_o + (long long)(sp0 + j) * a.attn_stride))[blk * 64 + lane];
+                    if (blk < nb)
+                        xv[i] += gptr(reinterpret_cast<const f32x4*>(a.attn_o + (long long)sp * a.attn_stride))[blk * 64 + lane];
                 }
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-#pragma unroll
-                for (int i = 0; i < KB; ++i) {
-                    const int blk = wave + GV_NW * i;
-                    if (blk < nb && sp0 + j < nsplit) xv[i] += t4[j][i];
-                }
+            }
         }
     }
 #pragma unroll
