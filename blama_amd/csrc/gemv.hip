@@ -400,7 +400,11 @@ __device__ __forceinline__ void gv_body(const GvArgs& a, char* lds, Wait&& wait 
     for (int i = 0; i < KB; ++i) {
         const int blk = wave + GV_NW * i;
         if (blk < nb) {
-            const float* x0 = pro == PRO_ATTN ? a.attn_o : a.x[0];
+            // (values made opaque: a select of two addresses into the parameter copy would put it in scratch)
+            const float* xo = a.attn_o;
+            const float* xs = a.x[0];
+            asm volatile("" : "+s"(xo), "+s"(xs));
+            const float* x0 = pro == PRO_ATTN ? xo : xs;
             xv[i] = gptr(reinterpret_cast<const f32x4*>(x0))[blk * 64 + lane];
             if (pro == PRO_RMSNORM || (GX && pro == PRO_LAYERNORM))
                 wv[i] = gptr(reinterpret_cast<const f32x4*>(a.norm_w))[blk * 64 + lane];
@@ -690,9 +694,28 @@ __device__ __forceinline__ void gv_body(const GvArgs& a, char* lds, Wait&& wait 
 // TAG: 1 for the FFN gate/up launches, so that the roofline kernel has a symbol of its own in
 // kernel traces (the same code as the QKV launches of an all-Q4_K layer); 2 for the GPT-2
 // launches (LayerNorm / bias / GELU compiled in, kept out of the LLaMA kernels' registers).
+// The parameter block is read with ONE vector load per lane and spread to scalars with
+// v_readlane: the compiler's kernarg scalar loads came in ~7 dependent rounds (each a scalar
+// cache miss), ~2.4 us from entry to the first weight request (scripts/timeline.py).
+__device__ __forceinline__ GvArgs gv_args_fetch(const GvArgs& ka) {
+    constexpr int NW = (int)(sizeof(GvArgs) / 4);
+    static_assert(sizeof(GvArgs) % 4 == 0 && NW <= 4 * 64, "parameter block layout");
+    int lane = threadIdx.x & 63;
+    asm volatile("" : "+v"(lane));
+    const u32x4* src = reinterpret_cast<const u32x4*>(&ka);
+    u32x4 v = {0u, 0u, 0u, 0u};
+    if (lane < (NW + 3) / 4) v = src[lane];
+    GvArgs l;
+    unsigned* dst = reinterpret_cast<unsigned*>(&l);
+#pragma unroll
+    for (int i = 0; i < NW; ++i) dst[i] = __builtin_amdgcn_readlane(v[i & 3], i >> 2);
+    return l;
+}
+
 template <int T0, int T1, int RW, int KB, int D, int TAG>
-__global__ __launch_bounds__(GV_NW * 64) void gemv_kernel(const GvArgs a) {
+__global__ __launch_bounds__(GV_NW * 64) void gemv_kernel(const GvArgs ka) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
+    const GvArgs a = gv_args_fetch(ka);
     if (T1 == -1 || (int)blockIdx.x < a.seg[1].blk0) gv_body<T0, 0, RW, KB, D, TAG == 2>(a, lds);
     else gv_body<(T1 < 0 ? T0 : T1), 1, RW, KB, D, TAG == 2>(a, lds);
 }
