@@ -920,7 +920,7 @@ static void gv_prepare(const GemvParams& p, int cap, GvArgs& a, int& grid_out, G
     a.head_dim = p.head_dim > 0 ? p.head_dim : 1;
     a.kv_dim = p.kv_dim;
     a.stamps = p.stamps;
-    static const int order = getenv("MI_GEMV_ORDER") ? atoi(getenv("MI_GEMV_ORDER")) : 1;
+    static const int order = getenv("MI_GEMV_ORDER") ? atoi(getenv("MI_GEMV_ORDER")) : 0;
     static const int pre = getenv("MI_GEMV_PRE") ? atoi(getenv("MI_GEMV_PRE")) : 8;
     a.order = order;
     a.pre = pre;
