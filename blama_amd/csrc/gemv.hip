@@ -729,7 +729,12 @@ typedef void (*GvFn)(const GvArgs);
 #ifndef MI_GV_DEEP
 #define MI_GV_DEEP 0   // A/B builds: one more ring item per wave
 #endif
-template <int T, int RW> struct GvD { static constexpr int D = (RW == 1 ? 4 : (T == T_Q4_K ? 3 : 2)) + MI_GV_DEEP; };
+#ifndef MI_GV_DEEP_Q4
+#define MI_GV_DEEP_Q4 0   // A/B builds: one more item for the two-row Q4_K and one-row rings only
+#endif
+template <int T, int RW> struct GvD {
+    static constexpr int D = (RW == 1 ? 4 + MI_GV_DEEP_Q4 : (T == T_Q4_K ? 3 + MI_GV_DEEP_Q4 : 2)) + MI_GV_DEEP;
+};
 
 template <int T0, int T1, int RW, int TAG>
 GvFn gv_fn_kb(int kb) {
