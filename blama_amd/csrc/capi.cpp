@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <vector>
 
@@ -187,7 +188,32 @@ int32_t mi_model_arena(const mi_model* m, void** dev_ptr, size_t* bytes) {
 }
 
 
+// One line per replication stage on stderr: a start-up that dies inside RCCL or HIP says where.
+static void replicate_log(const std::string& what) {
+    std::fprintf(stderr, "mi_engine: replicate: %s\n", what.c_str());
+    std::fflush(stderr);
+}
+
 int32_t mi_model_replicate(mi_model* const* models, int32_t n) {
+    int caller_dev = -1;
+    (void)hipGetDevice(&caller_dev);
+    // communicators and streams are released on every path (a throw after ncclCommInitAll included)
+    struct Guard {
+        std::vector<ncclComm_t> comms;
+        std::vector<std::pair<int, hipStream_t>> streams;
+        int dev;
+        ~Guard() {
+            for (auto& [d, s] : streams) {
+                if (!s) continue;
+                (void)hipSetDevice(d);
+                (void)hipStreamSynchronize(s);
+                (void)hipStreamDestroy(s);
+            }
+            for (ncclComm_t c : comms)
+                if (c && rccl().destroy) rccl().destroy(c);
+            if (dev >= 0) (void)hipSetDevice(dev);
+        }
+    } guard{{}, {}, caller_dev};
     try {
         if (!models || n < 1 || !models[0]) throw Error("replicate: no source model");
         const Model& src = models[0]->impl;
@@ -205,7 +231,7 @@ int32_t mi_model_replicate(mi_model* const* models, int32_t n) {
         // also sends the first same-device replica through a one-rank broadcast (exercises the path on
         // a single GPU)
         std::vector<int> devs = {src.device}, recv = {0};
-        static const bool force = getenv("MI_REPLICATE_RCCL") != nullptr;
+        const bool force = getenv("MI_REPLICATE_RCCL") != nullptr;
         for (int i = 1; i < n; ++i) {
             const int dv = models[i]->impl.device;
             if (std::find(devs.begin(), devs.end(), dv) == devs.end()) {
@@ -217,31 +243,38 @@ int32_t mi_model_replicate(mi_model* const* models, int32_t n) {
         if (force && devs.size() == 1)
             for (int i = 1; i < n && self_recv < 0; ++i)
                 if (models[i]->impl.device == src.device) self_recv = i;
+        replicate_log(std::to_string(n) + " models, " + std::to_string(src.arena_bytes) + " B arena, " +
+                      std::to_string(devs.size()) + " device(s)" + (self_recv > 0 ? ", one-rank RCCL broadcast forced" : ""));
         if (devs.size() > 1 || self_recv > 0) {
             const Rccl& R = rccl();
-            if (!R.init || !R.bcast || !R.gstart || !R.gend || !R.destroy) throw Error("replicate: librccl not found");
+            if (!R.init || !R.bcast || !R.gstart || !R.gend || !R.destroy)
+                throw Error(std::string("replicate: librccl not usable: ") + (dlerror() ? dlerror() : "missing symbols"));
             const int nd = (int)devs.size();
-            std::vector<ncclComm_t> comms(nd);
-            nccl_ck(R.init(comms.data(), nd, devs.data()), "ncclCommInitAll");
-            std::vector<hipStream_t> st(nd);
+            guard.comms.assign(nd, nullptr);
+            replicate_log("ncclCommInitAll over " + std::to_string(nd) + " device(s)");
+            nccl_ck(R.init(guard.comms.data(), nd, devs.data()), "ncclCommInitAll");
+            replicate_log("communicators ready");
             for (int r = 0; r < nd; ++r) {
                 MI_HIP(hipSetDevice(devs[r]));
-                MI_HIP(hipStreamCreateWithFlags(&st[r], hipStreamNonBlocking));
+                hipStream_t s = nullptr;
+                MI_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+                guard.streams.emplace_back(devs[r], s);
             }
+            replicate_log("ncclBroadcast of the arena");
             nccl_ck(R.gstart(), "ncclGroupStart");
             for (int r = 0; r < nd; ++r) {
                 MI_HIP(hipSetDevice(devs[r]));
                 uint8_t* dst = r == 0 ? (self_recv > 0 ? models[self_recv]->impl.arena : src.arena)
                                       : models[recv[r]]->impl.arena;
-                nccl_ck(R.bcast(src.arena, dst, src.arena_bytes, ncclUint8, 0, comms[r], st[r]), "ncclBroadcast");
+                nccl_ck(R.bcast(src.arena, dst, src.arena_bytes, ncclUint8, 0, guard.comms[r], guard.streams[r].second),
+                        "ncclBroadcast");
             }
             nccl_ck(R.gend(), "ncclGroupEnd");
-            for (int r = 0; r < nd; ++r) {
-                MI_HIP(hipSetDevice(devs[r]));
-                MI_HIP(hipStreamSynchronize(st[r]));
-                MI_HIP(hipStreamDestroy(st[r]));
-                R.destroy(comms[r]);
+            for (auto& [d, s] : guard.streams) {
+                MI_HIP(hipSetDevice(d));
+                MI_HIP(hipStreamSynchronize(s));
             }
+            replicate_log("broadcast complete");
             for (int r = 1; r < nd; ++r) filled[recv[r]] = 1;
             if (self_recv > 0) filled[self_recv] = 1;
         }
@@ -253,6 +286,8 @@ int32_t mi_model_replicate(mi_model* const* models, int32_t n) {
             int from_dev = src.device;
             for (int j = 0; j < n; ++j)
                 if (filled[j] && models[j]->impl.device == d.device) { from = models[j]->impl.arena; from_dev = d.device; break; }
+            replicate_log("replica " + std::to_string(i) + ": device copy " + std::to_string(from_dev) + " -> " +
+                          std::to_string(d.device));
             MI_HIP(hipSetDevice(d.device));
             if (from_dev == d.device) MI_HIP(hipMemcpy(d.arena, from, src.arena_bytes, hipMemcpyDeviceToDevice));
             else MI_HIP(hipMemcpyPeer(d.arena, d.device, from, from_dev, src.arena_bytes));
@@ -262,6 +297,7 @@ int32_t mi_model_replicate(mi_model* const* models, int32_t n) {
             MI_HIP(hipSetDevice(models[i]->impl.device));
             MI_HIP(hipDeviceSynchronize());
         }
+        replicate_log("done");
         return 0;
     }
     MI_TRY(-1)

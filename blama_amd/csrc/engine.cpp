@@ -10,6 +10,8 @@
 //   llama_state_*               /root/reference/inference/code/llama/Session.cpp:291-304
 #include "engine.h"
 
+#include <atomic>
+
 #include <algorithm>
 #include <climits>
 #include <cmath>
@@ -538,6 +540,7 @@ namespace {
 struct DevChain {
     std::mutex mu;
     hipEvent_t ev = nullptr;   // the last persistent step enqueued on the device
+    std::atomic<int> nctx{0};  // live contexts on the device (attention co-residency budget)
 };
 DevChain& dev_chain(int device) {
     static std::mutex mu;
@@ -687,9 +690,11 @@ Ctx::Ctx(Model* model, uint32_t nctx, uint32_t nbatch, uint32_t nubatch) : m(mod
     MI_HIP(hipHostMalloc(&h_logits, (size_t)hp.n_vocab * sizeof(float)));
     MI_HIP(hipHostMalloc(&h_gather, 4096 * sizeof(float)));
     h_cell_pos.assign(n_ctx, 0);
+    dev_chain(device).nctx++;
 }
 
 Ctx::~Ctx() {
+    dev_chain(device).nctx--;
     hipSetDevice(device);
     if (stream) hipStreamSynchronize(stream);
     invalidate_graphs();
@@ -788,7 +793,10 @@ void Ctx::layer_ops(int l, const LayerBufs& B, const std::function<void(const Ge
         a.xsum = attn_xsum;
         a.step = step_ctr;
         a.layer = l;
+        a.n_layer = hp.n_layer;
         a.xerr = d_attn_xerr;
+        a.long_share = dev_chain(device).nctx.load();
+        a.long_off = attn_long_off ? 1 : 0;
         attn(a);
     }
     // ---- output projection + residual (prologue: the attention splits combined) ----
@@ -1443,6 +1451,11 @@ void Ctx::decode_ubatch(const int32_t* tokens, int n, bool all) {
 int Ctx::decode(const int32_t* tokens, int n, bool all) {
     MI_HIP(hipSetDevice(device));
     if (n <= 0) throw Error("decode: empty batch");
+    if (!unsynced) {   // the state a failed long-context exchange rolls back to
+        undo_cells = n_cells;
+        undo_pos = pos_max;
+    }
+    unsynced = true;
     for (int i = 0; i < n; ++i)
         if (tokens[i] < 0 || tokens[i] >= m->hp.n_vocab) throw Error("decode: token id out of range");
     if (n_cells + n > (int)n_ctx) return 1;   // no KV slot (llama_decode returns 1)
@@ -1539,11 +1552,21 @@ void Ctx::sync() {
     MI_HIP(hipSetDevice(device));
     MI_HIP(hipStreamSynchronize(stream));
     check_persist();
+    const bool was_unsynced = unsynced;
+    unsynced = false;
     if (h_attn_xerr && *h_attn_xerr) {   // an attention exchange gave up: the step's logits are invalid
         *h_attn_xerr = 0;
         logits_valid = false;
+        // the cells decoded since the last good sync hold KV rows built from a wrong attention
+        // output: drop them, and use the two-launch split kernels from now on
+        if (was_unsynced) {
+            n_cells = undo_cells;
+            pos_max = undo_pos;
+        }
+        attn_long_off = true;
+        invalidate_graphs();
         throw Error("long-context attention: the splits of a head were not co-resident (exchange timed out); "
-                    "MI_ATTN_SPLIT2=1 selects the two-launch kernels");
+                    "the step was rolled back and this context now uses the two-launch kernels");
     }
 }
 

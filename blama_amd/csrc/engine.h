@@ -209,6 +209,9 @@ struct Ctx {
     hipGraphExec_t g_full[2] = {nullptr, nullptr}, g_nolog[2] = {nullptr, nullptr};
     hipGraphExec_t g_seg[2][3] = {{nullptr, nullptr, nullptr}, {nullptr, nullptr, nullptr}};
     int attn_fused = 0;                 // mode of the step being enqueued
+    bool attn_long_off = false;         // an exchange of attn_long_kernel timed out: split kernels only
+    bool unsynced = false;              // decodes enqueued since the last sync()
+    int undo_cells = 0, undo_pos = -1;  // n_cells / pos_max at the last sync (xerr rollback)
     int prof_layer = -1;
     hipEvent_t prof_ev[2] = {nullptr, nullptr};
     bool prof_pending = false;

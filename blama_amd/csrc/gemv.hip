@@ -60,7 +60,13 @@ struct GvArgs {
     float eps, theta_scale, freq_scale;
     int K, pro, nslots, attn_nsplit, attn_stride, n_rot, head_dim, kv_dim;
     int order;                    // 0: weights right after the activation requests; 1: after a
-                                  // workgroup barrier; 2: after this wave's activation landed
+                                  // workgroup barrier; 2: after this wave's activation landed;
+                                  // 4: waves [0, npro) build the activation (staged by LDS-DMA)
+                                  // while the others stream, then stream themselves
+    int npro;                     // order 4: prologue waves
+    int touch;                    // order 4: wave npro prefetches the workgroup's share into L2
+    int stage_off;                // order 4: LDS byte offset of the staged activation arrays
+    int flag_off;                 // order 4: LDS byte offset of the [2][GV_NW] flag words
     int pre;                      // ring items issued before the prologue (the rest after it)
     unsigned long long* stamps;   // MI_STAMPS builds: [grid][8] s_memrealtime per workgroup
 };
@@ -89,7 +95,14 @@ __host__ __device__ inline int gv_red_off(int nb, int nslots, int n_rot) {
 __host__ inline size_t gv_lds_bytes(int nb, int nslots, int n_rot) {
     return (size_t)gv_red_off(nb, nslots, n_rot) + 2 * GV_NW * 8;   // two rounds of per-wave doubles
 }
+// order 4: the fp32 arrays the prologue waves stage (x, then the norm weight or the second
+// slot), 1 KiB per 256-block each, after the rest; then the flag words
+constexpr size_t GV_LDS_MAX = 160 * 1024;
+__host__ inline int gv_stage_arrays(int pro, int nslots) {
+    return 1 + ((pro == PRO_RMSNORM || nslots > 1) ? 1 : 0);
+}
 
+__device__ __forceinline__ int readfirstlane_i(int v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ void lds_barrier() {
     __builtin_amdgcn_s_waitcnt((0xF) | (0x3 << 14) | (0x7 << 4));   // lgkmcnt(0): LDS writes done; vmcnt untouched
     __builtin_amdgcn_s_barrier();
@@ -218,8 +231,12 @@ __device__ __forceinline__ void gv_body(const GvArgs& a, char* lds, Wait&& wait 
                    // 2 activation in LDS, 3 first item consumed, 4 end
 #define GV_STAMP(k) \
     if (a.stamps && threadIdx.x == 0) a.stamps[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime();
+    // order 4: the stamps of the last wave (a streaming wave) instead of wave 0's
+#define GV_STAMPL(k) \
+    if (a.stamps && threadIdx.x == (GV_NW - 1) * 64) a.stamps[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime();
 #else
 #define GV_STAMP(k)
+#define GV_STAMPL(k)
 #endif
     GV_STAMP(0)
 #ifdef MI_STAMPS   // 6: the workgroup's last wave to start
@@ -394,196 +411,358 @@ __device__ __forceinline__ void gv_body(const GvArgs& a, char* lds, Wait&& wait 
     const bool qkv = epi == EPI_QKV;
     const bool need_tp = qkv || (pro == PRO_ATTN && a.attn_nsplit == 0);
     i32x4 tp = {0, 0, 0, 0};
-    if (need_tp) tp = *gptr(reinterpret_cast<const i32x4*>(a.tokpos));
-    f32x4 xv[KB], wv[KB], yv[KB];
-#pragma unroll
-    for (int i = 0; i < KB; ++i) {
-        const int blk = wave + GV_NW * i;
-        if (blk < nb) {
-            // (values made opaque: a select of two addresses into the parameter copy would put it in scratch)
-            const float* xo = a.attn_o;
-            const float* xs = a.x[0];
-            asm volatile("" : "+s"(xo), "+s"(xs));
-            const float* x0 = pro == PRO_ATTN ? xo : xs;
-            xv[i] = gptr(reinterpret_cast<const f32x4*>(x0))[blk * 64 + lane];
-            if (pro == PRO_RMSNORM || (GX && pro == PRO_LAYERNORM))
-                wv[i] = gptr(reinterpret_cast<const f32x4*>(a.norm_w))[blk * 64 + lane];
-            if (dual) yv[i] = gptr(reinterpret_cast<const f32x4*>(a.x[1]))[blk * 64 + lane];
-            else if (GX && pro == PRO_LAYERNORM) yv[i] = gptr(reinterpret_cast<const f32x4*>(a.norm_b))[blk * 64 + lane];
-        }
-    }
-    float ff0 = 1.0f, ff1 = 1.0f;
-    const bool rope_wave = qkv && a.n_rot > 0 && wave == GV_NW - 1;
-    if (rope_wave && a.freq_factors) {
-        if (lane < a.n_rot / 2) ff0 = gptr(a.freq_factors)[lane];
-        if (lane + 64 < a.n_rot / 2) ff1 = gptr(a.freq_factors)[lane + 64];
-    }
-    if (P) {   // the residuals of the prefilled items (item k = unit k / C, chunk k % C)
-        if (has_res) {
-#pragma unroll
-            for (int k = 0; k < D - 1; ++k) res_load(ring[k], k / C, k % C, k / C >= n_units);
-        }
-    } else {
-        // the activation requests ahead of the weight requests (a.order, measured: DESIGN.md §4)
-        if (a.order == 1) __builtin_amdgcn_s_barrier();
-        if (a.order == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#ifdef MI_STAMPS   // 7 (order 2): the workgroup's last wave whose activation landed
-        if (a.stamps && lane == 0 && a.order == 2)
-            atomicMax(a.stamps + blockIdx.x * 8 + 7, (unsigned long long)__builtin_amdgcn_s_memrealtime());
-#endif
-    }
-    const int pre = P ? D - 1 : a.pre;
-    if (!P) {
-#pragma unroll
-        for (int k = 0; k < D - 1; ++k)
-            if (k < pre) issue(ring[k], false);
-    }
-    GV_STAMP(1)
-
-    // ---- 3. prologue: the activation into LDS while the weights stream ---------------------------
+    const bool order4 = !P && a.order == 4;
+    if (need_tp && !order4) tp = *gptr(reinterpret_cast<const i32x4*>(a.tokpos));
     double* red = reinterpret_cast<double*>(lds + gv_red_off(nb, a.nslots, a.n_rot));
     float* rope = reinterpret_cast<float*>(lds + gv_rope_off(nb, a.nslots));
-    float scale = 1.0f;
-    if (pro == PRO_RMSNORM) {
-        // ggml_compute_forward_rms_norm_f32: sum of float squares in double
-        double s = 0.0;
-#pragma unroll
-        for (int i = 0; i < KB; ++i)
-            if (wave + GV_NW * i < nb) {
-                s += (double)(xv[i].x * xv[i].x);
-                s += (double)(xv[i].y * xv[i].y);
-                s += (double)(xv[i].z * xv[i].z);
-                s += (double)(xv[i].w * xv[i].w);
-            }
-        s = wave_sum63_d(s);
-        if (lane == 63) red[wave] = s;
-        lds_barrier();
-        double tot = 0.0;
-#pragma unroll
-        for (int w = 0; w < GV_NW; ++w) tot += red[w];
-        scale = 1.0f / sqrtf((float)(tot / (double)a.K) + a.eps);
-    }
-    float mean = 0.0f;
-    if (GX && pro == PRO_LAYERNORM) {
-        // ggml_compute_forward_norm_f32: mean from a double sum, then the double sum of the
-        // f32 squares of (x - mean), variance = (float)(sum2 / n)
-        double s = 0.0;
-#pragma unroll
-        for (int i = 0; i < KB; ++i)
-            if (wave + GV_NW * i < nb) {
-                s += (double)xv[i].x;
-                s += (double)xv[i].y;
-                s += (double)xv[i].z;
-                s += (double)xv[i].w;
-            }
-        s = wave_sum63_d(s);
-        if (lane == 63) red[wave] = s;
-        lds_barrier();
-        double tot = 0.0;
-#pragma unroll
-        for (int w = 0; w < GV_NW; ++w) tot += red[w];
-        mean = (float)(tot / (double)a.K);
-        double s2 = 0.0;
-#pragma unroll
-        for (int i = 0; i < KB; ++i)
-            if (wave + GV_NW * i < nb) {
-                const float v0 = xv[i].x - mean, v1 = xv[i].y - mean, v2 = xv[i].z - mean, v3 = xv[i].w - mean;
-                s2 += (double)(v0 * v0);
-                s2 += (double)(v1 * v1);
-                s2 += (double)(v2 * v2);
-                s2 += (double)(v3 * v3);
-            }
-        s2 = wave_sum63_d(s2);
-        if (lane == 63) red[GV_NW + wave] = s2;
-        lds_barrier();
-        double tot2 = 0.0;
-#pragma unroll
-        for (int w = 0; w < GV_NW; ++w) tot2 += red[GV_NW + w];
-        scale = 1.0f / sqrtf((float)(tot2 / (double)a.K) + a.eps);
-    }
-    if (pro == PRO_ATTN) {
-        // the other splits of the attention partials (contexts past ATTN_SHORT cells), in split order
-        int nsplit = a.attn_nsplit;
-        if (nsplit == 0) {
-            int chunk;
-            attn_split(__builtin_amdgcn_readfirstlane(tp.z) + 1, chunk, nsplit);
-        }
-        if constexpr (KB == 1) {
-            // four splits' loads in flight together, then added in split order
-            for (int sp0 = 1; sp0 < nsplit; sp0 += 4) {
-                f32x4 t4[4];
-#pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    if (wave < nb && sp0 + j < nsplit)
-                        t4[j] = gptr(reinterpret_cast<const f32x4*>(a.attn_o + (long long)(sp0 + j) * a.attn_stride))[wave * 64 + lane];
-#pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    if (wave < nb && sp0 + j < nsplit) xv[0] += t4[j];
-            }
-        } else {   // wider activations: no extra registers (they would cost the GEMV ring its occupancy)
-            for (int sp = 1; sp < nsplit; ++sp) {
-#pragma unroll
-                for (int i = 0; i < KB; ++i) {
-                    const int blk = wave + GV_NW * i;
-                    if (blk < nb)
-                        xv[i] += gptr(reinterpret_cast<const f32x4*>(a.attn_o + (long long)sp * a.attn_stride))[blk * 64 + lane];
-                }
-            }
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < KB; ++i) {
-        const int blk = wave + GV_NW * i;
-        if (blk >= nb) continue;
-        float v[4] = {xv[i].x, xv[i].y, xv[i].z, xv[i].w};
-        if (pro == PRO_RMSNORM) {
-            v[0] = (v[0] * scale) * wv[i].x;   // ggml_vec_scale_f32 then ggml_mul
-            v[1] = (v[1] * scale) * wv[i].y;
-            v[2] = (v[2] * scale) * wv[i].z;
-            v[3] = (v[3] * scale) * wv[i].w;
-        }
-        if (GX && pro == PRO_LAYERNORM) {        // (x - mean) * scale, then ggml_mul, ggml_add
-            v[0] = ((v[0] - mean) * scale) * wv[i].x + yv[i].x;
-            v[1] = ((v[1] - mean) * scale) * wv[i].y + yv[i].y;
-            v[2] = ((v[2] - mean) * scale) * wv[i].z + yv[i].z;
-            v[3] = ((v[3] - mean) * scale) * wv[i].w + yv[i].w;
-        }
-        if (Q80)
-            quant_q80_block(v, lane, reinterpret_cast<int8_t*>(lds + L.q80 + blk * GV_ASTR),
-                            reinterpret_cast<float*>(lds + L.d0) + blk * 8);
-        else
-            quant_q8k_block(v, lane, reinterpret_cast<int8_t*>(lds + L.q8k + blk * GV_ASTR),
-                            reinterpret_cast<int*>(lds + L.bsum) + blk * 16, reinterpret_cast<float*>(lds + L.dk) + blk);
-        if (dual) {
-            float y[4] = {yv[i].x, yv[i].y, yv[i].z, yv[i].w};
-            char* s1 = lds + slot_bytes;
-            if (Q80)
-                quant_q80_block(y, lane, reinterpret_cast<int8_t*>(s1 + L.q80 + blk * GV_ASTR),
-                                reinterpret_cast<float*>(s1 + L.d0) + blk * 8);
-            else
-                quant_q8k_block(y, lane, reinterpret_cast<int8_t*>(s1 + L.q8k + blk * GV_ASTR),
-                                reinterpret_cast<int*>(s1 + L.bsum) + blk * 16, reinterpret_cast<float*>(s1 + L.dk) + blk);
-        }
-    }
-    const int pos = __builtin_amdgcn_readfirstlane(tp.y);
-    const int cell = __builtin_amdgcn_readfirstlane(tp.z);
-    if (rope_wave) {   // ggml_rope_cache_init for this token's position (ext_factor 0, mscale 1)
+    // ggml_rope_cache_init for this token's position (ext_factor 0, mscale 1) into LDS
+    auto rope_table = [&](int pos_, float ff0_, float ff1_) {
         for (int i = lane; i < a.n_rot / 2; i += 64) {
-            float theta = (float)pos;
+            float theta = (float)pos_;
             for (int k = 0; k < i; ++k) theta = theta * a.theta_scale;
-            const float ff = i < 64 ? ff0 : ff1;
+            const float ff = i < 64 ? ff0_ : ff1_;
             const float th = a.freq_scale * (theta / ff);
             rope[2 * i] = cosf(th);
             rope[2 * i + 1] = sinf(th);
         }
-    }
-    lds_barrier();
+    };
+    unsigned touch_sink = 0;   // order 4 + touch: the VGPR the L2 prefetch loads write
+    if (order4) {
+        // ---- prologue waves (order 4) ----------------------------------------------------------
+        // A wave that has issued its weight ring cannot run the prologue: its later instructions
+        // wait behind the ring's requests in the CU's memory pipeline (back-pressure, ~4 us at a
+        // decode launch's ~100 KB in flight per CU; in-kernel stamps).  So waves
+        // [0, npro) build the activation -- their x / norm-weight blocks by LDS-DMA into a stage,
+        // the RMSNorm partials exchanged through LDS flag words, then the Q8_K / Q8_0 blocks --
+        // and issue their rings after it; the other waves issue their rings at once and wait for
+        // the prologue waves' flags (and the RoPE wave's) before the first dot product.
+        const int npro = a.npro;
+        const bool pw = wave < npro;
+        const bool need_w = pro == PRO_RMSNORM;
+        char* const stage = lds + a.stage_off;
+        // [2][GV_NW] flag words, through an LDS-typed pointer (a generic one would make them flat_*)
+        volatile __attribute__((address_space(3))) int* const flg = (volatile __attribute__((address_space(3))) int*)(lds + a.flag_off);
+        if (wave == 0 && lane < 2 * GV_NW) flg[lane] = 0;
+        if (pw) {
+            const float* xo = a.attn_o;
+            const float* xs = a.x[0];
+            asm volatile("" : "+s"(xo), "+s"(xs));
+            const float* x0 = pro == PRO_ATTN ? xo : xs;
+            for (int blk = wave; blk < nb; blk += npro) {
+                __builtin_amdgcn_global_load_lds(gptr(x0 + blk * 256 + lane * 4),
+                                                 (__attribute__((address_space(3))) void*)(stage + blk * 1024), 16, 0, 0);
+                if (need_w)
+                    __builtin_amdgcn_global_load_lds(gptr(a.norm_w + blk * 256 + lane * 4),
+                                                     (__attribute__((address_space(3))) void*)(stage + (size_t)(nb + blk) * 1024), 16, 0, 0);
+                if (dual)
+                    __builtin_amdgcn_global_load_lds(gptr(a.x[1] + blk * 256 + lane * 4),
+                                                     (__attribute__((address_space(3))) void*)(stage + (size_t)(nb + blk) * 1024), 16, 0, 0);
+            }
+        }
+        float ff0 = 1.0f, ff1 = 1.0f;
+        const bool rope_wave = qkv && a.n_rot > 0 && wave == GV_NW - 1;
+        // the token position: prologue waves and the RoPE wave now, the other waves behind their ring
+        if (need_tp && (pw || rope_wave)) tp = *gptr(reinterpret_cast<const i32x4*>(a.tokpos));
+        if (rope_wave && a.freq_factors) {
+            if (lane < a.n_rot / 2) ff0 = gptr(a.freq_factors)[lane];
+            if (lane + 64 < a.n_rot / 2) ff1 = gptr(a.freq_factors)[lane + 64];
+        }
+        lds_barrier();   // the flag words are zero (the LDS-DMA stays in flight across it)
+        // wait until flags[round][w] are set for every wave w in `mask` (one lane per wave)
+        auto wait_flags = [&](int round, unsigned mask) {
+            for (;;) {
+                const bool ok = !((mask >> lane) & 1u) || flg[round * GV_NW + (lane & (GV_NW - 1))] != 0;
+                if (__all(ok)) break;
+                __builtin_amdgcn_s_sleep(1);
+            }
+        };
+        const unsigned pmask = (1u << npro) - 1u;
+        if (!pw) {
+            if (a.touch && wave == npro) {
+                // L2 prefetch of the workgroup's whole share (every row of its units, one dword
+                // per 128-byte line), ahead of this wave's ring: the later ring requests of every
+                // wave then hit L2.  The touch loads are invisible to the compiler (one pinned
+                // VGPR, written in order); they precede every load this wave waits for, so its
+                // vmcnt waits cover them.
+                const int M = S.units > wg ? (S.units - wg + S.nblk - 1) / S.nblk : 0;
 #pragma unroll
-    for (int k = 0; k < D - 1; ++k)
-        if (k >= pre) issue(ring[k], false);
-    GV_STAMP(2)
-    if (P) wait.mark();
+                for (int pl = 0; pl < 4; ++pl) {
+                    constexpr int bpa[4] = {PlaneBytes<T>::b[0], PlaneBytes<T>::b[1], PlaneBytes<T>::b[2], PlaneBytes<T>::b[3]};
+                    if (bpa[pl] == 0) continue;
+                    const long long rowb = (long long)nb * bpa[pl];
+                    const int Lp = (int)((rowb + 127) / 128);
+                    const long long ex = (long long)S.rows * rowb;
+#pragma unroll
+                    for (int r = 0; r < RW; ++r) {
+                        const bool isB = ab && r == 1;
+                        const uint8_t* base = isB ? S.b[pl] + eB * ex : S.a[pl] + eA * ex;
+                        const __amdgpu_buffer_rsrc_t rs = buf_rsrc(rfl_ptr(base));
+                        for (int i = lane; i < M * Lp; i += 64) {
+                            const int m = i / Lp, l = i - m * Lp;
+                            const long long u = wg + (long long)m * S.nblk;
+                            long long row = ab ? u : u * RW + r;
+                            if (row >= S.rows) row = S.rows - 1;
+                            const unsigned off = (unsigned)(row * rowb + (long long)l * 128);
+                            asm volatile("buffer_load_dword %0, %1, %2, 0 offen" : "+v"(touch_sink) : "v"(off), "s"(rs) : "memory");
+                        }
+                    }
+                }
+            }
+            if (rope_wave) {   // before its ring: the table is on the critical path of the epilogue
+                rope_table(readfirstlane_i(tp.y), ff0, ff1);
+                __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the table is written
+                if (lane == 0) flg[GV_NW + wave] = 1;
+            }
+#pragma unroll
+            for (int k = 0; k < D - 1; ++k) issue(ring[k], false);
+            if (need_tp && !rope_wave) tp = *gptr(reinterpret_cast<const i32x4*>(a.tokpos));
+            GV_STAMPL(1)
+        } else {
+            wait_vm<0>();   // this wave's staged blocks landed
+            float scale = 1.0f;
+            if (pro == PRO_RMSNORM) {
+                // ggml_compute_forward_rms_norm_f32: sum of float squares in double
+                double sq = 0.0;
+                for (int blk = wave; blk < nb; blk += npro) {
+                    const f32x4 v = *reinterpret_cast<const f32x4*>(stage + blk * 1024 + lane * 16);
+                    sq += (double)(v.x * v.x);
+                    sq += (double)(v.y * v.y);
+                    sq += (double)(v.z * v.z);
+                    sq += (double)(v.w * v.w);
+                }
+                sq = wave_sum63_d(sq);
+                if (lane == 63) red[wave] = sq;
+                __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the partial is written
+                if (lane == 63) flg[wave] = 1;
+                wait_flags(0, pmask);
+                double tot = 0.0;
+                for (int w = 0; w < npro; ++w) tot += red[w];
+                scale = 1.0f / sqrtf((float)(tot / (double)a.K) + a.eps);
+            }
+            for (int blk = wave; blk < nb; blk += npro) {
+                const f32x4 xv = *reinterpret_cast<const f32x4*>(stage + blk * 1024 + lane * 16);
+                float v[4] = {xv.x, xv.y, xv.z, xv.w};
+                if (pro == PRO_RMSNORM) {
+                    const f32x4 wv = *reinterpret_cast<const f32x4*>(stage + (size_t)(nb + blk) * 1024 + lane * 16);
+                    v[0] = (v[0] * scale) * wv.x;   // ggml_vec_scale_f32 then ggml_mul
+                    v[1] = (v[1] * scale) * wv.y;
+                    v[2] = (v[2] * scale) * wv.z;
+                    v[3] = (v[3] * scale) * wv.w;
+                }
+                if (Q80)
+                    quant_q80_block(v, lane, reinterpret_cast<int8_t*>(lds + L.q80 + blk * GV_ASTR),
+                                    reinterpret_cast<float*>(lds + L.d0) + blk * 8);
+                else
+                    quant_q8k_block(v, lane, reinterpret_cast<int8_t*>(lds + L.q8k + blk * GV_ASTR),
+                                    reinterpret_cast<int*>(lds + L.bsum) + blk * 16, reinterpret_cast<float*>(lds + L.dk) + blk);
+                if (dual) {
+                    const f32x4 yv = *reinterpret_cast<const f32x4*>(stage + (size_t)(nb + blk) * 1024 + lane * 16);
+                    float y[4] = {yv.x, yv.y, yv.z, yv.w};
+                    char* s1 = lds + slot_bytes;
+                    if (Q80)
+                        quant_q80_block(y, lane, reinterpret_cast<int8_t*>(s1 + L.q80 + blk * GV_ASTR),
+                                        reinterpret_cast<float*>(s1 + L.d0) + blk * 8);
+                    else
+                        quant_q8k_block(y, lane, reinterpret_cast<int8_t*>(s1 + L.q8k + blk * GV_ASTR),
+                                        reinterpret_cast<int*>(s1 + L.bsum) + blk * 16, reinterpret_cast<float*>(s1 + L.dk) + blk);
+                }
+            }
+            __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this wave's blocks are written
+            if (lane == 0) flg[GV_NW + wave] = 1;
+#ifdef MI_STAMPS   // 7 (order 4): the workgroup's last prologue wave done
+            if (a.stamps && lane == 0) atomicMax(a.stamps + blockIdx.x * 8 + 7, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+#endif
+#pragma unroll
+            for (int k = 0; k < D - 1; ++k) issue(ring[k], false);
+            GV_STAMP(1)
+        }
+        wait_flags(1, pmask | (rope_wave || (qkv && a.n_rot > 0) ? (1u << (GV_NW - 1)) : 0u));
+        GV_STAMPL(2)
+    } else {
+        // ---- 3. entry loads: token position, the activation slices ---------------------------------
+        const bool qkv = epi == EPI_QKV;
+        const bool need_tp = qkv || (pro == PRO_ATTN && a.attn_nsplit == 0);
+        i32x4 tp = {0, 0, 0, 0};
+        if (need_tp) tp = *gptr(reinterpret_cast<const i32x4*>(a.tokpos));
+        f32x4 xv[KB], wv[KB], yv[KB];
+    #pragma unroll
+        for (int i = 0; i < KB; ++i) {
+            const int blk = wave + GV_NW * i;
+            if (blk < nb) {
+                // (values made opaque: a select of two addresses into the parameter copy would put it in scratch)
+                const float* xo = a.attn_o;
+                const float* xs = a.x[0];
+                asm volatile("" : "+s"(xo), "+s"(xs));
+                const float* x0 = pro == PRO_ATTN ? xo : xs;
+                xv[i] = gptr(reinterpret_cast<const f32x4*>(x0))[blk * 64 + lane];
+                if (pro == PRO_RMSNORM || (GX && pro == PRO_LAYERNORM))
+                    wv[i] = gptr(reinterpret_cast<const f32x4*>(a.norm_w))[blk * 64 + lane];
+                if (dual) yv[i] = gptr(reinterpret_cast<const f32x4*>(a.x[1]))[blk * 64 + lane];
+                else if (GX && pro == PRO_LAYERNORM) yv[i] = gptr(reinterpret_cast<const f32x4*>(a.norm_b))[blk * 64 + lane];
+            }
+        }
+        float ff0 = 1.0f, ff1 = 1.0f;
+        const bool rope_wave = qkv && a.n_rot > 0 && wave == GV_NW - 1;
+        if (rope_wave && a.freq_factors) {
+            if (lane < a.n_rot / 2) ff0 = gptr(a.freq_factors)[lane];
+            if (lane + 64 < a.n_rot / 2) ff1 = gptr(a.freq_factors)[lane + 64];
+        }
+        if (P) {   // the residuals of the prefilled items (item k = unit k / C, chunk k % C)
+            if (has_res) {
+    #pragma unroll
+                for (int k = 0; k < D - 1; ++k) res_load(ring[k], k / C, k % C, k / C >= n_units);
+            }
+        } else {
+            // the activation requests ahead of the weight requests (a.order, measured: DESIGN.md §4)
+            if (a.order == 1) __builtin_amdgcn_s_barrier();
+            if (a.order == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    #ifdef MI_STAMPS   // 7 (order 2): the workgroup's last wave whose activation landed
+            if (a.stamps && lane == 0 && a.order == 2)
+                atomicMax(a.stamps + blockIdx.x * 8 + 7, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    #endif
+        }
+        const int pre = P ? D - 1 : a.pre;
+        if (!P) {
+    #pragma unroll
+            for (int k = 0; k < D - 1; ++k)
+                if (k < pre) issue(ring[k], false);
+        }
+        GV_STAMP(1)
 
+        // ---- 3. prologue: the activation into LDS while the weights stream ---------------------------
+        float scale = 1.0f;
+        if (pro == PRO_RMSNORM) {
+            // ggml_compute_forward_rms_norm_f32: sum of float squares in double
+            double s = 0.0;
+    #pragma unroll
+            for (int i = 0; i < KB; ++i)
+                if (wave + GV_NW * i < nb) {
+                    s += (double)(xv[i].x * xv[i].x);
+                    s += (double)(xv[i].y * xv[i].y);
+                    s += (double)(xv[i].z * xv[i].z);
+                    s += (double)(xv[i].w * xv[i].w);
+                }
+            s = wave_sum63_d(s);
+            if (lane == 63) red[wave] = s;
+            lds_barrier();
+            double tot = 0.0;
+    #pragma unroll
+            for (int w = 0; w < GV_NW; ++w) tot += red[w];
+            scale = 1.0f / sqrtf((float)(tot / (double)a.K) + a.eps);
+        }
+        float mean = 0.0f;
+        if (GX && pro == PRO_LAYERNORM) {
+            // ggml_compute_forward_norm_f32: mean from a double sum, then the double sum of the
+            // f32 squares of (x - mean), variance = (float)(sum2 / n)
+            double s = 0.0;
+    #pragma unroll
+            for (int i = 0; i < KB; ++i)
+                if (wave + GV_NW * i < nb) {
+                    s += (double)xv[i].x;
+                    s += (double)xv[i].y;
+                    s += (double)xv[i].z;
+                    s += (double)xv[i].w;
+                }
+            s = wave_sum63_d(s);
+            if (lane == 63) red[wave] = s;
+            lds_barrier();
+            double tot = 0.0;
+    #pragma unroll
+            for (int w = 0; w < GV_NW; ++w) tot += red[w];
+            mean = (float)(tot / (double)a.K);
+            double s2 = 0.0;
+    #pragma unroll
+            for (int i = 0; i < KB; ++i)
+                if (wave + GV_NW * i < nb) {
+                    const float v0 = xv[i].x - mean, v1 = xv[i].y - mean, v2 = xv[i].z - mean, v3 = xv[i].w - mean;
+                    s2 += (double)(v0 * v0);
+                    s2 += (double)(v1 * v1);
+                    s2 += (double)(v2 * v2);
+                    s2 += (double)(v3 * v3);
+                }
+            s2 = wave_sum63_d(s2);
+            if (lane == 63) red[GV_NW + wave] = s2;
+            lds_barrier();
+            double tot2 = 0.0;
+    #pragma unroll
+            for (int w = 0; w < GV_NW; ++w) tot2 += red[GV_NW + w];
+            scale = 1.0f / sqrtf((float)(tot2 / (double)a.K) + a.eps);
+        }
+        if (pro == PRO_ATTN) {
+            // the other splits of the attention partials (contexts past ATTN_SHORT cells), in split order
+            int nsplit = a.attn_nsplit;
+            if (nsplit == 0) {
+                int chunk;
+                attn_split(__builtin_amdgcn_readfirstlane(tp.z) + 1, chunk, nsplit);
+            }
+            if constexpr (KB == 1) {
+                // four splits' loads in flight together, then added in split order
+                for (int sp0 = 1; sp0 < nsplit; sp0 += 4) {
+                    f32x4 t4[4];
+    #pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        if (wave < nb && sp0 + j < nsplit)
+                            t4[j] = gptr(reinterpret_cast<const f32x4*>(a.attn_o + (long long)(sp0 + j) * a.attn_stride))[wave * 64 + lane];
+    #pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        if (wave < nb && sp0 + j < nsplit) xv[0] += t4[j];
+                }
+            } else {   // wider activations: no extra registers (they would cost the GEMV ring its occupancy)
+                for (int sp = 1; sp < nsplit; ++sp) {
+    #pragma unroll
+                    for (int i = 0; i < KB; ++i) {
+                        const int blk = wave + GV_NW * i;
+                        if (blk < nb)
+                            xv[i] += gptr(reinterpret_cast<const f32x4*>(a.attn_o + (long long)sp * a.attn_stride))[blk * 64 + lane];
+                    }
+                }
+            }
+        }
+    #pragma unroll
+        for (int i = 0; i < KB; ++i) {
+            const int blk = wave + GV_NW * i;
+            if (blk >= nb) continue;
+            float v[4] = {xv[i].x, xv[i].y, xv[i].z, xv[i].w};
+            if (pro == PRO_RMSNORM) {
+                v[0] = (v[0] * scale) * wv[i].x;   // ggml_vec_scale_f32 then ggml_mul
+                v[1] = (v[1] * scale) * wv[i].y;
+                v[2] = (v[2] * scale) * wv[i].z;
+                v[3] = (v[3] * scale) * wv[i].w;
+            }
+            if (GX && pro == PRO_LAYERNORM) {        // (x - mean) * scale, then ggml_mul, ggml_add
+                v[0] = ((v[0] - mean) * scale) * wv[i].x + yv[i].x;
+                v[1] = ((v[1] - mean) * scale) * wv[i].y + yv[i].y;
+                v[2] = ((v[2] - mean) * scale) * wv[i].z + yv[i].z;
+                v[3] = ((v[3] - mean) * scale) * wv[i].w + yv[i].w;
+            }
+            if (Q80)
+                quant_q80_block(v, lane, reinterpret_cast<int8_t*>(lds + L.q80 + blk * GV_ASTR),
+                                reinterpret_cast<float*>(lds + L.d0) + blk * 8);
+            else
+                quant_q8k_block(v, lane, reinterpret_cast<int8_t*>(lds + L.q8k + blk * GV_ASTR),
+                                reinterpret_cast<int*>(lds + L.bsum) + blk * 16, reinterpret_cast<float*>(lds + L.dk) + blk);
+            if (dual) {
+                float y[4] = {yv[i].x, yv[i].y, yv[i].z, yv[i].w};
+                char* s1 = lds + slot_bytes;
+                if (Q80)
+                    quant_q80_block(y, lane, reinterpret_cast<int8_t*>(s1 + L.q80 + blk * GV_ASTR),
+                                    reinterpret_cast<float*>(s1 + L.d0) + blk * 8);
+                else
+                    quant_q8k_block(y, lane, reinterpret_cast<int8_t*>(s1 + L.q8k + blk * GV_ASTR),
+                                    reinterpret_cast<int*>(s1 + L.bsum) + blk * 16, reinterpret_cast<float*>(s1 + L.dk) + blk);
+            }
+        }
+        if (rope_wave) rope_table(readfirstlane_i(tp.y), ff0, ff1);
+        lds_barrier();
+    #pragma unroll
+        for (int k = 0; k < D - 1; ++k)
+            if (k >= pre) issue(ring[k], false);
+        GV_STAMP(2)
+        if (P) wait.mark();
+
+    }
+    const int pos = readfirstlane_i(tp.y);
+    const int cell = readfirstlane_i(tp.z);
     // ---- 4. the stream: consume item i while items i+1 .. i+D-1 are in flight -----------------
     const char* act0 = lds;
     const char* actB = (dual && S.actB == 1) ? lds + slot_bytes : lds;
@@ -680,9 +859,12 @@ __device__ __forceinline__ void gv_body(const GvArgs& a, char* lds, Wait&& wait 
         for (int k = 0; k < D; ++k) {
             issue(ring[(k + D - 1) % D], false);
             if (base + k < n_items) consume(ring[k]);
-            if (base + k == 0) { GV_STAMP(3) }
+            if (base + k == 0) {
+                if (order4) { GV_STAMPL(3) } else { GV_STAMP(3) }
+            }
         }
     }
+    asm volatile("" ::"v"(touch_sink));   // pinned to the end (no other value may take the VGPR)
     GV_STAMP(4)
 #ifdef MI_STAMPS   // 5: the workgroup's last wave to finish
     if (a.stamps && lane == 0) atomicMax(a.stamps + blockIdx.x * 8 + 5, (unsigned long long)__builtin_amdgcn_s_memrealtime());
@@ -789,6 +971,13 @@ long long seg_bytes(const GemvSeg& s) {
     return s.pair == PAIR_AB ? mb(s.A) + mb(s.B) : mb(s.A);
 }
 
+// dynamic LDS of a launch: the activation slots, RoPE table and reductions (+ the staged arrays)
+size_t gv_lds_total(const GvArgs& a, int nb, int pro) {
+    size_t b = gv_lds_bytes(nb, a.nslots, a.n_rot);
+    if (a.order == 4) b = (size_t)a.flag_off + 2 * GV_NW * sizeof(int);
+    return b;
+}
+
 // cap on workgroups: the weight ring keeps D items x RW rows in flight per wave
 int gv_grid_cap() {
     static const int cap = getenv("MI_GEMV_GRID") ? std::max(1, atoi(getenv("MI_GEMV_GRID"))) : 256;
@@ -824,7 +1013,7 @@ void init_kernel_attributes() {
                         GvFn f = t1 < 0 ? gv_fn(1, t0, t0, rw, kb, tag) : gv_fn(2, t0, t1, rw, kb, tag);
                         if (f)
                             MI_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(f),
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024));
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)GV_LDS_MAX));
                     }
                 }
 }
@@ -932,10 +1121,24 @@ static void gv_prepare(const GemvParams& p, int cap, GvArgs& a, int& grid_out, G
     static const int pre = getenv("MI_GEMV_PRE") ? atoi(getenv("MI_GEMV_PRE")) : 8;
     a.order = order;
     a.pre = pre;
+    // order 4 (prologue waves): not for the GPT-2 launches (LayerNorm) nor a WO launch that adds
+    // the splits of a long-context attention; too wide to stage -> order 0
+    if (a.order == 4 && (key.tag == 2 || p.pro == PRO_LAYERNORM || (p.pro == PRO_ATTN && p.attn_nsplit != 1))) a.order = 0;
+    {
+        static const int npro_env = getenv("MI_GEMV_NPRO") ? atoi(getenv("MI_GEMV_NPRO")) : 0;
+        const int nb = p.K / 256;
+        a.npro = npro_env > 0 ? npro_env : (nb + 3) / 4;
+        a.npro = std::max(1, std::min(a.npro, std::min(8, nb)));
+        static const int touch_env = getenv("MI_GEMV_TOUCH") ? atoi(getenv("MI_GEMV_TOUCH")) : 0;
+        a.touch = touch_env;
+    }
+    a.stage_off = (int)((gv_lds_bytes(p.K / 256, a.nslots, p.n_rot) + 15) & ~(size_t)15);
+    a.flag_off = a.stage_off + gv_stage_arrays(p.pro, a.nslots) * (p.K / 256) * 1024;
+    if (a.order == 4 && gv_lds_total(a, p.K / 256, p.pro) > GV_LDS_MAX) a.order = 0;
     for (int i = 0; i < p.nseg; ++i)
         if (p.seg[i].epi == EPI_QKV && (!p.tokpos || (p.n_rot > 0 && p.head_dim <= 0)))
             throw Error("gemv: QKV epilogue needs tokpos and the head geometry");
-    if (gv_lds_bytes(p.K / 256, a.nslots, p.n_rot) > 96 * 1024) throw Error("gemv: activation too large for LDS");
+    if (gv_lds_total(a, p.K / 256, p.pro) > GV_LDS_MAX) throw Error("gemv: activation too large for LDS");
     grid_out = blk;
 }
 
@@ -946,7 +1149,7 @@ void launch_gemv(const GemvParams& p, hipStream_t s, hipEvent_t ev_start, hipEve
     gv_prepare(p, gv_grid_cap(), a, grid, key);
     GvFn fn = gv_fn(key.nseg, key.t0, key.t1, key.rw, key.kb, key.tag);
     if (!fn) throw Error("gemv: no kernel for this type / shape");
-    const size_t smem = gv_lds_bytes(p.K / 256, a.nslots, p.n_rot);
+    const size_t smem = gv_lds_total(a, p.K / 256, p.pro);
     if (ev_start || ev_stop)
         hipExtLaunchKernelGGL(fn, dim3(grid), dim3(GV_NW * 64), smem, s, ev_start, ev_stop, 0, a);
     else

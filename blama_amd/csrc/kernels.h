@@ -195,8 +195,13 @@ struct AttnParams {
     float* xmax;                   // [n_head][ATTN_SMAX]
     double* xsum;                  // [n_head][ATTN_SMAX]
     const unsigned* step;          // decode steps so far (the embedding launch counts them)
-    int layer;                     // this layer (the exchange's epoch: step * 256 + 2 * layer + phase)
+    int layer;                     // this layer (the exchange's epoch: step * (2 * n_layer + 2) + 2 * layer + phase)
+    int n_layer;                   // layers per step (the epoch's stride; 0 = one layer)
     unsigned* xerr;                // host-mapped: an exchange timed out (the step is invalid)
+    // contexts that may run attention on this device at once: the single launch is used only when
+    // that many grids of n_head * ATTN_SMAX workgroups are co-resident (occupancy x CUs)
+    int long_share;
+    int long_off;                  // 1: never the single launch (an exchange timed out before)
 };
 void launch_attn(const AttnParams& p, hipStream_t s);
 // Combine the partials into out[n_head*hd] (tests / the eager debug path).

@@ -654,7 +654,8 @@ __global__ __launch_bounds__(256) void attn_long_kernel(const AttnParams P) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int L = lane % LPC, G = lane / LPC;
     const long long row_off = (long long)g * HD + L * 8;
-    const unsigned epoch = *P.step * 256u + 2u * (unsigned)P.layer;
+    // strictly increasing over (step, layer, phase) for any depth
+    const unsigned epoch = *P.step * (2u * (unsigned)max(P.n_layer, 1) + 2u) + 2u * (unsigned)P.layer;
     unsigned* const fl = P.xflags + (long long)h * ATTN_SMAX * 32;
     u32x4 kk[U];
     int cpos[U];
@@ -990,6 +991,15 @@ __global__ __launch_bounds__(256) void attn_fused_kernel(const AttnParams P) {
 }
 
 typedef void (*AttnFn)(const AttnParams);
+// Can `need` workgroups of attn_long_kernel (256 threads, `lds` dynamic LDS) be resident on the
+// current device at once?  The splits of a head spin on each other, so they all must be.
+static bool attn_long_resident(const void* fn, size_t lds, long long need) {
+    int dev = 0, cus = 0, per_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return false;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return false;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, lds) != hipSuccess) return false;
+    return (long long)per_cu * cus >= need;
+}
 // MI_ATTN_U=<4|8>: cell steps per wave whose cache loads the split kernels issue together
 static int attn_u() {
     static const int u = getenv("MI_ATTN_U") ? atoi(getenv("MI_ATTN_U")) : 4;
@@ -1043,11 +1053,11 @@ void launch_attn(const AttnParams& p, hipStream_t s) {
         MI_HIP(hipGetLastError());
         return;
     }
-    if (p.xflags && p.step && (p.head_dim == 64 || p.head_dim == 128) && getenv("MI_ATTN_SPLIT2") == nullptr) {
+    if (p.xflags && p.step && !p.long_off && (p.head_dim == 64 || p.head_dim == 128) && getenv("MI_ATTN_SPLIT2") == nullptr) {
         // one launch, the splits of a q head exchanging their softmax statistics
         const size_t lds = (size_t)std::max(64, ((p.n_ctx + ATTN_SMAX - 1) / ATTN_SMAX + 63) / 64 * 64) * sizeof(float);
-        if (lds <= 64 * 1024) {
-            auto fn = p.head_dim == 128 ? attn_long_kernel<16> : attn_long_kernel<8>;
+        auto fn = p.head_dim == 128 ? attn_long_kernel<16> : attn_long_kernel<8>;
+        if (lds <= 64 * 1024 && attn_long_resident(reinterpret_cast<const void*>(fn), lds, (long long)p.n_head * ATTN_SMAX * std::max(1, p.long_share))) {
             hipLaunchKernelGGL(fn, dim3(p.n_head, ATTN_SMAX), dim3(256), lds, s, p);
             MI_HIP(hipGetLastError());
             return;

@@ -19,6 +19,7 @@
 // - /chat/completions and /chat/verify_completion return 501: chat templating is out of scope.
 // - A malformed request head or Content-Length gets a 400, a body over 64 MB a 413.
 #include <arpa/inet.h>
+#include <execinfo.h>
 #include <net/if.h>
 #include <netinet/in.h>
 #include <signal.h>
@@ -26,6 +27,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <charconv>
 #include <cstdio>
 #include <cstdlib>
@@ -186,11 +188,47 @@ std::string modelFromEnv() {
 
 int serve();
 
+namespace {
+std::atomic<bool> g_listening{false};
+
+// A fatal signal before or while serving: name it and print a backtrace on stderr, then die of
+// the same signal (the parent sees the signal number as the exit status).
+void crash_handler(int sig) {
+    char msg[64];
+    int n = 0;
+    for (const char* p = "blama-http-server: fatal signal "; *p; ++p) msg[n++] = *p;
+    char d[8];
+    int k = 0;
+    for (int v = sig; v > 0 && k < 8; v /= 10) d[k++] = char('0' + v % 10);
+    while (k > 0) msg[n++] = d[--k];
+    msg[n++] = '\n';
+    (void)!::write(2, msg, n);
+    void* frames[64];
+    const int nf = ::backtrace(frames, 64);
+    ::backtrace_symbols_fd(frames, nf, 2);
+    ::signal(sig, SIG_DFL);
+    ::raise(sig);
+}
+
+void install_crash_handlers() {
+    void* warm[1];
+    ::backtrace(warm, 1);   // loads libgcc's unwinder now, not inside the handler
+    for (int sig : {SIGSEGV, SIGBUS, SIGILL, SIGFPE, SIGABRT}) ::signal(sig, crash_handler);
+    // a library calling exit() during start-up (before "Listening") says so
+    std::atexit([] {
+        if (!g_listening.load()) std::cerr << "blama-http-server: exit() called before the server was listening" << std::endl;
+    });
+}
+}  // namespace
+
 int main() {
+    std::setvbuf(stdout, nullptr, _IOLBF, 0);   // stage lines reach a log file as they happen
+    install_crash_handlers();
     try {
         return serve();
     } catch (const std::exception& e) {   // configuration errors: message and a non-zero exit
         std::cerr << "blama-http-server: " << e.what() << std::endl;
+        g_listening = true;   // a reported configuration error, not a silent exit
         return 1;
     }
 }
@@ -262,7 +300,11 @@ int serve() {
             at = comma + 1;
         }
     }
-    Server server(bl::llama::Model::loadReplicas(modelGguf, devices));
+    std::cerr << "blama-http-server: loading " << devices.size() << " replica(s)" << std::endl;
+    auto replicas = bl::llama::Model::loadReplicas(modelGguf, devices);
+    std::cerr << "blama-http-server: weights resident on every replica; creating instances" << std::endl;
+    Server server(std::move(replicas));
+    std::cerr << "blama-http-server: instances ready" << std::endl;
 
     const int lfd = ::socket(ss.ss_family, SOCK_STREAM, 0);
     const int one = 1;
@@ -277,6 +319,7 @@ int serve() {
     ::getsockname(lfd, (sockaddr*)&ss, &alen);
     const uint16_t bound = ss.ss_family == AF_INET ? reinterpret_cast<sockaddr_in*>(&ss)->sin_port
                                                    : reinterpret_cast<sockaddr_in6*>(&ss)->sin6_port;
+    g_listening = true;
     std::cout << "Listening on port " << ntohs(bound) << std::endl;
     for (;;) {
         const int fd = ::accept(lfd, nullptr, nullptr);

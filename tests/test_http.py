@@ -12,6 +12,7 @@ GPU: a synthetic model served on 127.0.0.1.
   - Non-POST gives 400, an unknown path 404, a malformed body 500."""
 import json
 import os
+import re
 import subprocess
 import time
 import urllib.error
@@ -91,6 +92,46 @@ def served(tmp_path):
     yield from _serve(tmp_path, synthetic.CONFIGS["tiny-q4_k_m"])
 
 
+def _start_server(env, log_dir, limit=300):
+    """Start blama-http-server with stdout+stderr going to `log_dir`/server.log (a file, so a chatty
+    server can never block on a full pipe) and wait for its "Listening on port" line.  If the
+    server exits or the limit passes first, fail with its return code (negative = the signal
+    that ended it) and everything it wrote: the stage log, RCCL's WARN lines, a backtrace."""
+    log_path = os.path.join(str(log_dir), "server.log")
+    log = open(log_path, "w")
+    env = dict(env)
+    env.setdefault("NCCL_DEBUG", "WARN")
+    proc = subprocess.Popen([_binary()], env=env, stdout=log, stderr=subprocess.STDOUT)
+    log.close()
+    t0 = time.time()
+    port, text = None, ""
+    while time.time() - t0 < limit:
+        with open(log_path, errors="replace") as f:
+            text = f.read()
+        m = re.search(r"^Listening on port (\d+)$", text, re.M)
+        if m:
+            port = int(m.group(1))
+            break
+        if proc.poll() is not None:
+            break
+        time.sleep(0.1)
+    if not port:
+        rc = proc.poll()
+        if rc is None:
+            proc.kill()      # the exact child we started
+            proc.wait(timeout=30)
+        with open(log_path, errors="replace") as f:
+            text = f.read()
+        raise AssertionError(f"server did not start (returncode {rc}, after {time.time() - t0:.1f} s); "
+                             f"its output:\n{text[-6000:]}")
+    return proc, port
+
+
+def _stop_server(proc):
+    proc.kill()              # the exact child we started
+    proc.wait(timeout=30)
+
+
 def _serve(tmp_path, cfg, devices=None):
     buf = synthetic.build_gguf(cfg, seed=5)
     path = str(tmp_path / "model.gguf")
@@ -98,23 +139,11 @@ def _serve(tmp_path, cfg, devices=None):
     env = dict(os.environ, BLAMA_MODEL=path, BLAMA_HOST="127.0.0.1", BLAMA_PORT="0")
     if devices:
         env["BLAMA_DEVICES"] = devices
-    proc = subprocess.Popen([_binary()], env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
-                            text=True)
-    port = None
-    t0 = time.time()
+    proc, port = _start_server(env, tmp_path)
     try:
-        while time.time() - t0 < 90:
-            line = proc.stdout.readline()
-            if not line:
-                break
-            if line.startswith("Listening on port "):
-                port = int(line.split()[-1])
-                break
-        assert port, "server did not start: " + proc.stderr.read()[-2000:]
         yield port, buf
     finally:
-        proc.kill()          # the exact child we started
-        proc.wait(timeout=30)
+        _stop_server(proc)
 
 
 @pytest.mark.gpu
@@ -276,21 +305,7 @@ def llama3_bpe_model(tmp_path_factory):
 
 def _serve_path(path, env_extra):
     env = dict(os.environ, BLAMA_MODEL=path, BLAMA_HOST="127.0.0.1", BLAMA_PORT="0", **env_extra)
-    proc = subprocess.Popen([_binary()], env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
-    port = None
-    t0 = time.time()
-    while time.time() - t0 < 180:
-        line = proc.stdout.readline()
-        if not line:
-            break
-        if line.startswith("Listening on port "):
-            port = int(line.split()[-1])
-            break
-    if not port:
-        proc.kill()
-        proc.wait(timeout=30)
-        raise AssertionError("server did not start: " + proc.stderr.read()[-2000:])
-    return proc, port
+    return _start_server(env, os.path.dirname(path))
 
 
 @pytest.mark.gpu
@@ -350,8 +365,7 @@ def test_http_llama3_width_concurrent_verify_on_replicas(llama3_bpe_model):
         assert all(r is not None and r >= 0.999 for r in results[:7]), results
         assert results[7] < 0.95, results
     finally:
-        proc.kill()
-        proc.wait(timeout=30)
+        _stop_server(proc)
     # the CPU oracle verifies each completion on its own session (prompt: BOS + BPE ids)
     orc = ggml_cpu.Model(buf, n_ctx=64)
     try:
