@@ -6,17 +6,22 @@
 // kernels of kernels.hip: q rounded to f16 (the f16 vec_dot_type), KQ = sum f16(q) k in f32,
 // w = KQ * scale, masked to -inf where the cell is after the token (cell_pos > pos, or a later
 // cell); soft_max with the exact global max, the sum of expf(w - max) in double and
-// p = expf(w - max) * (float)(1/sum); KQV = sum f16(p) v in f32.  The softmax is therefore
-// three passes over the cells (max, sum, weighted V) -- an online softmax would round p
-// before the sum is known.  Only fp32 summation orders differ from the CPU.
+// p = expf(w - max) * (float)(1/sum); KQV = sum f16(p) v in f32.  The softmax needs the max
+// before any exponential and the whole sum before any p (an online softmax would round p
+// before the sum is known); only fp32 / double summation orders differ from the CPU.
 //
-// Geometry.  A workgroup is one query head x 64 tokens (2 waves, a 32-token tile each); the
-// 32-cell chunks of K and V are staged once per workgroup in LDS (V transposed) and shared,
-// the next chunk's loads in flight while the current one is computed.
-// S^T = K Q^T per chunk (D: lane = token, registers = cells), so a token's softmax statistics
-// are lane-local, and S^T's registers are directly the B operand of O^T = V^T P^T (the
-// accumulator-as-operand idiom: element j of k-step s = register 8s + j = cell
-// 16s + 8(j>>2) + 4h + (j&3), which the V^T operand reads at the same cells).
+// Geometry.  A workgroup is one query head x one 32-token tile, 8 waves; the tile's 32-cell
+// chunks are dealt to the waves round-robin (chunk c -> wave c % 8), so every wave holds its
+// chunks' scores in registers:
+//   S^T = K Q^T per chunk (D: lane = token, register r = cell (r&3) + 8(r>>2) + 4h), K straight
+//   from the cache into the A operand (16 B per lane and k-step), so a token's softmax
+//   statistics are lane-local; the waves' maxima and double sums are combined through LDS in
+//   wave order.  O^T = V^T P^T: P^T is the S^T accumulator itself (registers 8s..8s+7 are the
+//   B operand of k-step s, k-permuted), V^T comes from the wave's V chunk staged row-major in
+//   LDS (XOR-swizzled 256-B rows) and read with ds_read_b64_tr_b16.  The 8 waves' O^T
+//   partials are added in a fixed tree order through LDS.
+// Up to 8 * CPR chunks (CPR per wave) the scores are computed once and kept in registers over
+// the three softmax passes; past that the passes recompute them, CPR chunks at a time.
 #include "kernels.h"
 #include <hip/hip_runtime.h>
 
@@ -24,12 +29,15 @@ namespace mi {
 namespace amf {
 
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef __fp16 trv4 __attribute__((__vector_size__(4 * sizeof(__fp16))));   // ds_read_tr16_b64 result
 typedef float f16x16 __attribute__((ext_vector_type(16)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int WT = 2;          // token tiles (waves) per workgroup
+constexpr int NW = 8;          // waves per workgroup (cell groups of one token tile)
 constexpr int CH = 32;         // cells per chunk
+constexpr int CPR = 2;         // chunks per wave whose scores stay in registers
 
 __device__ __forceinline__ unsigned pack2(float a, float b) {
     const unsigned lo = __half_as_ushort(__float2half_rn(a)), hi = __half_as_ushort(__float2half_rn(b));
@@ -37,36 +45,45 @@ __device__ __forceinline__ unsigned pack2(float a, float b) {
 }
 __device__ __forceinline__ half8 as_h8(u32x4 v) { return __builtin_bit_cast(half8, v); }
 
+// byte offset of 16-B chunk `ch` (0..HD/8-1) of row `row` in a [CH][HD] f16 image of 2*HD-byte
+// rows, XOR-swizzled so that the transposed reads of the PV operand are conflict-free
+// (cdna_hip_programming.md T10 layout (b), generalised to HD/8 chunks per row)
 template <int HD>
-__global__ __launch_bounds__(64 * WT) void attn_mfma_kernel(const AttnParams P, int ntok, float* out) {
+__device__ __forceinline__ int vimg_off(int row, int ch) {
+    constexpr int NCH = HD / 8;
+    const int x = (((row & 3) << 2) | ((row >> 2) & 3)) & (NCH - 1);
+    return row * (2 * HD) + 16 * (ch ^ x);
+}
+
+template <int HD>
+__global__ __launch_bounds__(64 * NW) void attn_mfma_kernel(const AttnParams P, int ntok, float* out) {
     constexpr int KS = HD / 16;          // k-steps of KQ
     constexpr int HB = HD / 32;          // 32-wide output blocks
-    constexpr int KST = HD + 8;          // K row stride (halfs): 16-B aligned, staggered banks
-    constexpr int VST = CH + 4;          // V^T row stride (halfs): 72 B
-    __shared__ __attribute__((aligned(16))) _Float16 ks[CH * KST];
-    __shared__ __attribute__((aligned(16))) _Float16 vt[HD * VST];
-    __shared__ int cps[CH];
-    __shared__ int last_cell;
+    constexpr int VPL = CH * HD / 8 / 64;   // 16-B pieces of a V chunk per lane
+    constexpr int VIMG = CH * HD * 2;    // bytes of one V chunk image
+    // LDS (dynamic, NW * VIMG bytes): one V chunk image per wave, reused for the partial-output
+    // tree; then the exchanges
+    extern __shared__ __attribute__((aligned(16))) char vimg[];
+    __shared__ float xmax[NW][32];
+    __shared__ double xsum[NW][32];
     const int hq = blockIdx.x;                      // query head
     const int R = P.n_head / P.n_head_kv;
     const int g = hq / R;                           // its kv head
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int col = lane & 31, h = lane >> 5;
-    const int t0 = blockIdx.y * (32 * WT) + 32 * w;   // this wave's token tile
+    const int t0 = blockIdx.y * 32;                 // the token tile
     const int tok = t0 + col;                       // this lane's query token (D column)
     const bool tv = tok < ntok;
     const int qcell = tv ? P.tokpos[tok * 4 + 2] : -1;
     const int qpos = tv ? P.tokpos[tok * 4 + 1] : 0;
-    // the workgroup's last cell (its last valid token's) and this wave's
-    if (tid == 0) {
-        const int lt = min(ntok, (int)(blockIdx.y + 1) * 32 * WT) - 1;
-        last_cell = P.tokpos[lt * 4 + 2];
-    }
-    int wlast = -1;
-    {
-        const int lt = min(ntok, t0 + 32) - 1;
-        if (lt >= t0) wlast = P.tokpos[lt * 4 + 2];
-    }
+    // the tile's last cell (its last valid token's): the causal end of every token in it
+    const int wlast = __builtin_amdgcn_readfirstlane(P.tokpos[(min(ntok, t0 + 32) - 1) * 4 + 2]);
+    const int nch = wlast / CH + 1;                 // chunks of the tile
+    const int myn = nch > w ? (nch - w + NW - 1) / NW : 0;   // this wave's chunks: w, w+8, ...
+    const int nround = (myn + CPR - 1) / CPR;
+    const bool keep = nround <= 1;                  // scores computed once, kept in registers
+
     // Q^T fragments (B operand): lane (token col, half h), k-step s: q[tok][16s + 8h .. +7] as f16
     u32x4 qf[KS];
     {
@@ -79,124 +96,187 @@ __global__ __launch_bounds__(64 * WT) void attn_mfma_kernel(const AttnParams P, 
                        : u32x4{0u, 0u, 0u, 0u};
         }
     }
+    const __half* kbase = P.kcache + (long long)g * HD;
+    const __half* vbase = P.vcache + (long long)g * HD;
+    // scores of chunk c into st: masked, scaled w (lane = token, register r = cell (r&3)+8(r>>2)+4h)
+    auto scores = [&](int c, f16x16& st) {
+        const int c0 = c * CH;
+        const int cr = min(c0 + col, P.n_ctx - 1);  // the A operand row this lane supplies
+        u32x4 kf[KS];
+#pragma unroll
+        for (int s = 0; s < KS; ++s) kf[s] = *reinterpret_cast<const u32x4*>(kbase + (long long)cr * P.kv_dim + 16 * s + 8 * h);
+        i32x4 cp[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int cb = c0 + 8 * q + 4 * h;
+            if (cb + 3 < P.n_ctx) {
+                cp[q] = *reinterpret_cast<const i32x4*>(P.cell_pos + cb);
+            } else {   // the cache's last cells (cells past n_ctx are masked by cell <= qcell)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) cp[q][e] = P.cell_pos[min(cb + e, P.n_ctx - 1)];
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) st[r] = 0.0f;
+#pragma unroll
+        for (int s = 0; s < KS; ++s) st = __builtin_amdgcn_mfma_f32_32x32x16_f16(as_h8(kf[s]), as_h8(qf[s]), st, 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int cell = c0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            const int pos = cp[r >> 2][r & 3];
+            const bool ok = tv && cell <= qcell && pos <= qpos;
+            st[r] = ok ? st[r] * P.scale : -INFINITY;
+        }
+    };
+
+    // ---- pass 1: the token's max over every cell ------------------------------------------------
+    f16x16 st[CPR];
+    float mx = -INFINITY;
+    for (int rd = 0; rd < nround; ++rd) {
+#pragma unroll
+        for (int i = 0; i < CPR; ++i) {
+            const int k = rd * CPR + i;
+            if (k < myn) {
+                scores(w + NW * k, st[i]);
+#pragma unroll
+                for (int r = 0; r < 16; ++r) mx = fmaxf(mx, st[i][r]);
+            }
+        }
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));         // the token's other half of the cells
+    if (h == 0) xmax[w][col] = mx;
     __syncthreads();
-    const int ncell = last_cell + 1;
-    float mx = -INFINITY, inv = 0.0f;
+    float M = xmax[0][col];
+#pragma unroll
+    for (int k = 1; k < NW; ++k) M = fmaxf(M, xmax[k][col]);
+
+    // ---- pass 2: the sum of expf(w - M) in double, waves added in order ------------------------
     double sum = 0.0;
+    for (int rd = 0; rd < nround; ++rd) {
+#pragma unroll
+        for (int i = 0; i < CPR; ++i) {
+            const int k = rd * CPR + i;
+            if (k < myn) {
+                if (!keep) scores(w + NW * k, st[i]);
+#pragma unroll
+                for (int r = 0; r < 16; ++r) sum += (double)expf(st[i][r] - M);
+            }
+        }
+    }
+    {
+        const long long b = __double_as_longlong(sum);
+        const int lo = __shfl_xor((int)b, 32, 64), hi = __shfl_xor((int)(b >> 32), 32, 64);
+        const double other = __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+        sum = h == 0 ? sum + other : other + sum;   // same order in both halves
+    }
+    if (h == 0) xsum[w][col] = sum;
+    __syncthreads();
+    double tot = 0.0;
+#pragma unroll
+    for (int k = 0; k < NW; ++k) tot += xsum[k][col];
+    const float inv = (float)(1.0 / tot);
+
+    // ---- pass 3: O^T += V^T P^T over the wave's chunks --------------------------------------------
     f16x16 o[HB];
 #pragma unroll
     for (int b = 0; b < HB; ++b)
 #pragma unroll
         for (int r = 0; r < 16; ++r) o[b][r] = 0.0f;
-
-    constexpr int SEG = HD / 8;                     // 16-B pieces per cell row
-    constexpr int NPC = CH * SEG / (64 * WT);       // pieces per thread per chunk
-    static_assert(CH * SEG % (64 * WT) == 0, "chunk pieces split evenly over the threads");
-    for (int pass = 0; pass < 3; ++pass) {
-        // the next chunk's K (and V) in registers, issued before the current chunk is computed
-        u32x4 kr[NPC], vr_[NPC];
-        int cpr = 0;
-        auto fetch = [&](int c0) {
+    char* const vw = vimg + w * VIMG;
+    // V chunk c: piece i of this lane = row (lane + 64 i) / (HD/8), chunk (lane + 64 i) % (HD/8);
+    // rows past the tile's last cell are zero (p = 0 there, and 0 * stale bits could be NaN)
+    u32x4 vr[VPL];
+    auto vload = [&](int c) {
 #pragma unroll
-            for (int i = 0; i < NPC; ++i) {
-                const int pc = tid + 64 * WT * i;
-                const int cl = pc / SEG, sg = pc % SEG;
-                const int c = min(c0 + cl, P.n_ctx - 1);
-                const long long ga = (long long)c * P.kv_dim + (long long)g * HD + sg * 8;
-                kr[i] = *reinterpret_cast<const u32x4*>(P.kcache + ga);
-                if (pass == 2) {   // cells past the batch's last are zero (p = 0 there; 0 * stale bits)
-                    const u32x4 z = {0u, 0u, 0u, 0u};
-                    vr_[i] = c0 + cl <= last_cell ? *reinterpret_cast<const u32x4*>(P.vcache + ga) : z;
+        for (int i = 0; i < VPL; ++i) {
+            const int pc = lane + 64 * i;
+            const int row = pc / (HD / 8), ch = pc % (HD / 8);
+            const int cell = c * CH + row;
+            const u32x4 z = {0u, 0u, 0u, 0u};
+            vr[i] = cell <= wlast ? *reinterpret_cast<const u32x4*>(vbase + (long long)min(cell, P.n_ctx - 1) * P.kv_dim + 8 * ch) : z;
+        }
+    };
+    if (myn > 0) vload(w);
+    for (int rd = 0; rd < nround; ++rd) {
+#pragma unroll
+        for (int i = 0; i < CPR; ++i) {
+            const int k = rd * CPR + i;
+            if (k < myn) {
+                const int c = w + NW * k;
+                if (!keep) scores(c, st[i]);
+                // stage this chunk's V (wave-private image; the previous chunk's reads are done:
+                // ds ops of one wave complete in order)
+#pragma unroll
+                for (int j = 0; j < VPL; ++j) {
+                    const int pc = lane + 64 * j;
+                    *reinterpret_cast<u32x4*>(vw + vimg_off<HD>(pc / (HD / 8), pc % (HD / 8))) = vr[j];
                 }
-            }
-            if (tid < CH) cpr = P.cell_pos[min(c0 + tid, P.n_ctx - 1)];
-        };
-        fetch(0);
-        for (int c0 = 0; c0 < ncell; c0 += CH) {
-            // ---- stage K (and V^T in the last pass) of cells c0 .. c0+31, and their positions
-            __syncthreads();
-#pragma unroll
-            for (int i = 0; i < NPC; ++i) {
-                const int pc = tid + 64 * WT * i;
-                const int cl = pc / SEG, sg = pc % SEG;
-                *reinterpret_cast<u32x4*>(&ks[cl * KST + sg * 8]) = kr[i];
-                if (pass == 2) {
-                    const unsigned vw[4] = {vr_[i].x, vr_[i].y, vr_[i].z, vr_[i].w};
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        vt[(sg * 8 + 2 * e) * VST + cl] = __ushort_as_half((unsigned short)(vw[e] & 0xFFFFu));
-                        vt[(sg * 8 + 2 * e + 1) * VST + cl] = __ushort_as_half((unsigned short)(vw[e] >> 16));
-                    }
-                }
-            }
-            if (tid < CH) cps[tid] = cpr;
-            __syncthreads();
-            if (c0 + CH < ncell) fetch(c0 + CH);
-            if (c0 > wlast) continue;                   // wave-uniform: nothing of this tile here
-            // ---- S^T = K Q^T: lane = token, register r = cell c0 + (r&3) + 8(r>>2) + 4h
-            f16x16 st;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) st[r] = 0.0f;
-#pragma unroll
-            for (int s = 0; s < KS; ++s) {
-                const u32x4 kf = *reinterpret_cast<const u32x4*>(&ks[col * KST + 16 * s + 8 * h]);
-                st = __builtin_amdgcn_mfma_f32_32x32x16_f16(as_h8(kf), as_h8(qf[s]), st, 0, 0, 0);
-            }
-            float wv[16];
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int cl = (r & 3) + 8 * (r >> 2) + 4 * h;
-                const int c = c0 + cl;
-                const bool ok = tv && c <= qcell && cps[cl] <= qpos;
-                wv[r] = ok ? st[r] * P.scale : -INFINITY;
-            }
-            if (pass == 0) {
-#pragma unroll
-                for (int r = 0; r < 16; ++r) mx = fmaxf(mx, wv[r]);
-            } else if (pass == 1) {
-#pragma unroll
-                for (int r = 0; r < 16; ++r) sum += (double)expf(wv[r] - mx);
-            } else {
-                // p = f16(expf(w - max) * inv): the B operand of k-steps 0 (registers 0-7), 1 (8-15)
+                if (k + 1 < myn) vload(c + NW);     // the next chunk's V in flight during this one
+                // p = f16(expf(w - M) * inv): the B operand of k-steps 0 (registers 0-7), 1 (8-15)
                 u32x4 pf[2];
 #pragma unroll
                 for (int s = 0; s < 2; ++s) {
                     float p[8];
 #pragma unroll
-                    for (int j = 0; j < 8; ++j) p[j] = tv ? expf(wv[8 * s + j] - mx) * inv : 0.0f;
+                    for (int j = 0; j < 8; ++j) p[j] = tv ? expf(st[i][8 * s + j] - M) * inv : 0.0f;
                     pf[s] = u32x4{pack2(p[0], p[1]), pack2(p[2], p[3]), pack2(p[4], p[5]), pack2(p[6], p[7])};
                 }
+                __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the V image is written
 #pragma unroll
                 for (int b = 0; b < HB; ++b) {
 #pragma unroll
                     for (int s = 0; s < 2; ++s) {
-                        // V^T operand: row hd = 32b + col, cells 16s + 4h + 0..3 and 16s + 8 + 4h + 0..3
-                        const _Float16* vr = &vt[(32 * b + col) * VST + 16 * s + 4 * h];
-                        const u32x2 lo = *reinterpret_cast<const u32x2*>(vr);
-                        const u32x2 hi = *reinterpret_cast<const u32x2*>(vr + 8);
+                        // V^T operand of lane (hd row 32b + col, half h), k-step s: cells
+                        // 16s + 4h + 0..3 (elements 0-3) and 16s + 8 + 4h + 0..3 (elements 4-7),
+                        // two transposed reads of 4 rows x 16 columns per 16-lane group
+                        const int gq = (lane >> 2) & 3, gp = lane & 3;       // lane 4q+p of its group
+                        const int colb = 32 * b + 16 * ((lane >> 4) & 1) + 4 * gp;   // first hd of the lane's address
+                        const int r0 = 16 * s + 4 * h + gq, r1 = r0 + 8;
+                        const int o0 = vimg_off<HD>(r0, colb >> 3) + 2 * (colb & 7);
+                        const int o1 = vimg_off<HD>(r1, colb >> 3) + 2 * (colb & 7);
+                        const u32x2 lo = __builtin_bit_cast(u32x2, __builtin_amdgcn_ds_read_tr16_b64_v4f16(
+                            (__attribute__((address_space(3))) trv4*)(vw + o0)));
+                        const u32x2 hi = __builtin_bit_cast(u32x2, __builtin_amdgcn_ds_read_tr16_b64_v4f16(
+                            (__attribute__((address_space(3))) trv4*)(vw + o1)));
                         const u32x4 vf = {lo.x, lo.y, hi.x, hi.y};
                         o[b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(as_h8(vf), as_h8(pf[s]), o[b], 0, 0, 0);
                     }
                 }
             }
         }
-        if (pass == 0) {
-            mx = fmaxf(mx, __shfl_xor(mx, 32, 64));   // the token's other half of the cells
-        } else if (pass == 1) {
-            const long long b = __double_as_longlong(sum);
-            const int lo = __shfl_xor((int)b, 32, 64), hi = __shfl_xor((int)(b >> 32), 32, 64);
-            const double other = __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-            const double tot = h == 0 ? sum + other : other + sum;   // same order in both halves
-            inv = (float)(1.0 / tot);
+    }
+
+    // ---- the waves' partials, added in a fixed tree: ((0+4)+(2+6)) + ((1+5)+(3+7)) ----------------
+    // each partial is [HB][16 registers][64 lanes] f32 = HD * 128 B, inside the writer's V images
+    __syncthreads();   // every wave is done with its V image
+    float* const red = reinterpret_cast<float*>(vimg);
+    for (int hw = NW / 2; hw >= 1; hw >>= 1) {
+        if (w >= hw && w < 2 * hw) {
+            float* dst = red + (w - hw) * (HD * 32);
+#pragma unroll
+            for (int b = 0; b < HB; ++b)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) dst[(b * 16 + r) * 64 + lane] = o[b][r];
         }
+        __syncthreads();
+        if (w < hw) {
+            const float* src = red + w * (HD * 32);
+#pragma unroll
+            for (int b = 0; b < HB; ++b)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) o[b][r] += src[(b * 16 + r) * 64 + lane];
+        }
+        __syncthreads();
     }
     // ---- O^T: lane = token, register r of block b = hd 32b + (r&3) + 8(r>>2) + 4h
-    if (!tv) return;
+    if (w != 0 || !tv) return;
     float* orow = out + (long long)tok * P.n_head * HD + (long long)hq * HD;
 #pragma unroll
     for (int b = 0; b < HB; ++b)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) orow[32 * b + (r & 3) + 8 * (r >> 2) + 4 * h] = o[b][r];
+        for (int q = 0; q < 4; ++q)
+            *reinterpret_cast<float4*>(orow + 32 * b + 8 * q + 4 * h) =
+                float4{o[b][4 * q], o[b][4 * q + 1], o[b][4 * q + 2], o[b][4 * q + 3]};
 }
 
 }  // namespace amf
@@ -206,9 +286,17 @@ bool attn_mfma_supported(int head_dim) { return head_dim == 64 || head_dim == 12
 void launch_attn_mfma(const AttnParams& p, int ntok, float* out, hipStream_t s) {
     if (ntok < 1) return;
     if (p.n_head % p.n_head_kv) throw Error("attn_mfma: n_head must be a multiple of n_head_kv");
-    const dim3 grid(p.n_head, (ntok + 32 * amf::WT - 1) / (32 * amf::WT));
-    if (p.head_dim == 128) hipLaunchKernelGGL(amf::attn_mfma_kernel<128>, grid, dim3(64 * amf::WT), 0, s, p, ntok, out);
-    else if (p.head_dim == 64) hipLaunchKernelGGL(amf::attn_mfma_kernel<64>, grid, dim3(64 * amf::WT), 0, s, p, ntok, out);
+    if (p.n_ctx < 4) throw Error("attn_mfma: n_ctx must be at least 4");
+    const dim3 grid(p.n_head, (ntok + 31) / 32);
+    const size_t lds = (size_t)amf::NW * amf::CH * p.head_dim * 2;
+    static bool attr = false;
+    if (!attr) {
+        MI_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(amf::attn_mfma_kernel<128>), hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024));
+        MI_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(amf::attn_mfma_kernel<64>), hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024));
+        attr = true;
+    }
+    if (p.head_dim == 128) hipLaunchKernelGGL(amf::attn_mfma_kernel<128>, grid, dim3(64 * amf::NW), lds, s, p, ntok, out);
+    else if (p.head_dim == 64) hipLaunchKernelGGL(amf::attn_mfma_kernel<64>, grid, dim3(64 * amf::NW), lds, s, p, ntok, out);
     else throw Error("attn_mfma: head_dim 64 or 128");
     MI_HIP(hipGetLastError());
 }

@@ -6,17 +6,20 @@
 // Numerics: every per-block integer dot is ggml b5187's vec_dot_q*_K_q8_K / vec_dot_q8_0_q8_0
 // bit for bit (qdot.h); only the fp32 sum order across superblocks differs from the CPU's.
 //
-// Structure (measured, scripts/exp_gemv2.cpp):
+// Structure (measured, scripts/exp_gemv2.cpp, in-kernel stamps):
 //  * A workgroup of GV_NW waves serves one segment.  A wave walks "items" -- one 8-superblock
 //    chunk of the RW rows of one unit -- through a D-deep register ring: one aligned 16-byte load
 //    per lane of the main quant plane (+ side planes), the next items in flight while one is
 //    reduced against the activation in LDS.
-//  * Activation requests go out first: every wave issues its x slices, then a workgroup barrier
-//    that waits for no counter, and only then any weight request.  Without it the CU's x requests
-//    queue behind its weight stream (a decode launch has ~100 KB in flight per CU: x landed
-//    3-6 us after entry, in-kernel stamps); with it x lands while the first weights stream.
-//  * The whole parameter block is ~0.5 KB of kernarg read by independent scalar loads; a
-//    workgroup's segment is a compile-time index (no dependent kernarg reads).
+//  * Request order (GvArgs::order).  Order 0: each wave issues its activation slices, then its
+//    weight ring at once (no workgroup barrier: the barrier waited for the workgroup's last wave
+//    to start), then builds its share of the activation.  Order 4: waves [0, npro) stage the
+//    activation by LDS-DMA and build it while the other waves issue their rings; a wave that has
+//    issued its ring runs its later instructions only as fast as the CU's memory pipeline drains
+//    (back-pressure), so the prologue is kept off those waves.  Orders 1 and 2 (barrier / wait for
+//    the own slice first) are A/B knobs.
+//  * The ~0.5 KB parameter block is read with one vector load per lane and spread to scalars by
+//    v_readlane; a workgroup's segment is a compile-time index (no dependent kernarg reads).
 #include "qdot.h"
 #include <hip/hip_ext.h>
 
@@ -208,7 +211,8 @@ template <bool P> __device__ __forceinline__ void gst(int* p, int v) {
 //   P   persistent step kernel (decode_step_kernel): the ring prefill is issued before `wait`
 //       (the grid barrier that publishes the previous stage's outputs), the activation and the
 //       residuals are loaded after it, and every output is stored write-through (agent scope)
-template <int T, int SI, int RW, int KB, int D, bool GX, bool P = false, typename Wait = GvNoWait>
+//   ND  the launch has one activation slot (the FFN gate/up launch): no second-slot paths
+template <int T, int SI, int RW, int KB, int D, bool GX, bool P = false, typename Wait = GvNoWait, bool ND = false>
 __device__ __forceinline__ void gv_body(const GvArgs& a, char* lds, Wait&& wait = Wait()) {
     using K = Kq<T>;
     constexpr bool Q80 = gv_q80<T>();
@@ -224,7 +228,7 @@ __device__ __forceinline__ void gv_body(const GvArgs& a, char* lds, Wait&& wait 
     const int C = (nb + 7) >> 3;                       // 8-superblock chunks per row
     const int pro = a.pro;
     const int epi = S.epi;
-    const bool dual = a.nslots > 1;
+    const bool dual = !ND && a.nslots > 1;
     const GvLds L = gv_lds(nb);
     const int slot_bytes = L.slot;
 #ifdef MI_STAMPS   // diagnostic build only (scripts/timeline.py): 0 entry, 1 prefill issued,
@@ -898,8 +902,8 @@ template <int T0, int T1, int RW, int KB, int D, int TAG>
 __global__ __launch_bounds__(GV_NW * 64) void gemv_kernel(const GvArgs ka) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     const GvArgs a = gv_args_fetch(ka);
-    if (T1 == -1 || (int)blockIdx.x < a.seg[1].blk0) gv_body<T0, 0, RW, KB, D, TAG == 2>(a, lds);
-    else gv_body<(T1 < 0 ? T0 : T1), 1, RW, KB, D, TAG == 2>(a, lds);
+    if (T1 == -1 || (int)blockIdx.x < a.seg[1].blk0) gv_body<T0, 0, RW, KB, D, TAG == 2, false, GvNoWait, TAG == 1>(a, lds);
+    else gv_body<(T1 < 0 ? T0 : T1), 1, RW, KB, D, TAG == 2, false, GvNoWait, TAG == 1>(a, lds);
 }
 
 typedef void (*GvFn)(const GvArgs);
@@ -1053,7 +1057,7 @@ static void gv_prepare(const GemvParams& p, int cap, GvArgs& a, int& grid_out, G
     key.t1 = p.seg[p.nseg - 1].A.type;
     key.rw = rw2 ? 2 : 1;
     key.kb = kb;
-    key.tag = gx ? 2 : (p.nseg == 1 && p.seg[0].epi == EPI_SWIGLU ? 1 : 0);
+    key.tag = gx ? 2 : (p.nseg == 1 && p.seg[0].epi == EPI_SWIGLU && p.nslots <= 1 ? 1 : 0);
 
     std::memset(&a, 0, sizeof(a));
     // workgroups per segment in proportion to its bytes (at least one each)

@@ -258,7 +258,6 @@ template <> struct Kq<T_Q4_K> {
         return r;
     }
     __device__ static float dot(const Ld& l, const AR& r, int j) {
-        const int g = j >> 1;
         const i32x4 alo = r.alo, ahi = r.ahi;
         int dlo = 0, dhi = 0;
         dlo = dot4(l.qs.x & 0x0F0F0F0F, alo.x, dlo);
@@ -269,15 +268,32 @@ template <> struct Kq<T_Q4_K> {
         dhi = dot4((l.qs.y >> 4) & 0x0F0F0F0F, ahi.y, dhi);
         dhi = dot4((l.qs.z >> 4) & 0x0F0F0F0F, ahi.z, dhi);
         dhi = dot4((l.qs.w >> 4) & 0x0F0F0F0F, ahi.w, dhi);
-        // get_scale_min_k4 for sub-blocks 2g, 2g+1 (bytes 2(g&1), 2(g&1)+1 of each header dword)
-        const unsigned sh = (g & 1) * 16;
-        const unsigned Y = l.hdr.y >> sh, Z = l.hdr.z >> sh, W = l.hdr.w >> sh;
-        const unsigned SC = g < 2 ? (Y & 0x3F3Fu) : ((W & 0x0F0Fu) | ((Y >> 2) & 0x3030u));
-        const unsigned MM = g < 2 ? (Z & 0x3F3Fu) : (((W >> 4) & 0x0F0Fu) | ((Z >> 2) & 0x3030u));
-        const int S = (int)(SC & 0xFF) * dlo + (int)((SC >> 8) & 0xFF) * dhi;
-        const int M = (int)(MM & 0xFF) * r.bs_lo + (int)((MM >> 8) & 0xFF) * r.bs_hi;
-        const float d = h2f(l.hdr.x) * r.dx;
-        const float dm = h2f(l.hdr.x >> 16) * r.dx;
+        return finish(l.hdr, ScaleSel(j), dlo, dhi, r);
+    }
+    // get_scale_min_k4 for the lane's sub-blocks 2g, 2g+1 (g = j >> 1) without a lane-dependent
+    // branch: bytes 2(g&1), 2(g&1)+1 of each header dword, then per-lane masks pick the g < 2
+    // form (6 low bits of scales[is] / scales[is+4]) or the g >= 2 form (4 bits of scales[is+4]
+    // | the top 2 bits of scales[is-4] / scales[is] << 4).  The masks depend on the lane only.
+    struct ScaleSel {
+        unsigned sh, lo6, lo4, hi2;
+        __device__ explicit ScaleSel(int j) {
+            const int g = j >> 1;
+            sh = (unsigned)(g & 1) * 16;
+            lo6 = g < 2 ? 0x3F3Fu : 0u;
+            lo4 = g < 2 ? 0u : 0x0F0Fu;
+            hi2 = g < 2 ? 0u : 0x3030u;
+        }
+    };
+    // d * sum(sc * q.a) - dmin * sum(m * bsum), the scale products in 24-bit multiplies
+    // (|dlo|, |dhi| <= 32*31*127, scales and mins 6-bit, |bsum| <= 16*127: exact)
+    __device__ static float finish(const u32x4& hdr, const ScaleSel& q, int dlo, int dhi, const AR& r) {
+        const unsigned Y = hdr.y >> q.sh, Z = hdr.z >> q.sh, W = hdr.w >> q.sh;
+        const unsigned SC = (Y & q.lo6) | (W & q.lo4) | ((Y >> 2) & q.hi2);
+        const unsigned MM = (Z & q.lo6) | ((W >> 4) & q.lo4) | ((Z >> 2) & q.hi2);
+        const int S = __mul24((int)(SC & 0xFF), dlo) + __mul24((int)((SC >> 8) & 0xFF), dhi);
+        const int M = __mul24((int)(MM & 0xFF), r.bs_lo) + __mul24((int)((MM >> 8) & 0xFF), r.bs_hi);
+        const float d = h2f(hdr.x) * r.dx;
+        const float dm = h2f(hdr.x >> 16) * r.dx;
         return d * (float)S - dm * (float)M;
     }
 };
@@ -318,15 +334,7 @@ template <> struct Kq<T_Q5_K> {
         dhi = dot4((int)Q5H(w), ahi.w, dhi);
 #undef Q5L
 #undef Q5H
-        const unsigned sh = (g & 1) * 16;
-        const unsigned Y = l.hdr.y >> sh, Z = l.hdr.z >> sh, W = l.hdr.w >> sh;
-        const unsigned SC = g < 2 ? (Y & 0x3F3Fu) : ((W & 0x0F0Fu) | ((Y >> 2) & 0x3030u));
-        const unsigned MM = g < 2 ? (Z & 0x3F3Fu) : (((W >> 4) & 0x0F0Fu) | ((Z >> 2) & 0x3030u));
-        const int S = (int)(SC & 0xFF) * dlo + (int)((SC >> 8) & 0xFF) * dhi;
-        const int M = (int)(MM & 0xFF) * r.bs_lo + (int)((MM >> 8) & 0xFF) * r.bs_hi;
-        const float d = h2f(l.hdr.x) * r.dx;
-        const float dm = h2f(l.hdr.x >> 16) * r.dx;
-        return d * (float)S - dm * (float)M;
+        return Kq<T_Q4_K>::finish(l.hdr, Kq<T_Q4_K>::ScaleSel(j), dlo, dhi, r);
     }
 };
 

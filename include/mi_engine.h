@@ -182,7 +182,7 @@ int32_t mi_op_attention(int32_t device, int32_t n_head, int32_t n_head_kv, int32
                         const float* q, const uint16_t* k_f16, const uint16_t* v_f16, const int32_t* cell_pos,
                         int32_t pos, float* out);
 /* The prompt-batch GEMM (mmq32: int8 MFMA, Session.cpp:381-392's n_ubatch physical batches) of
- * ntok <= 512 token rows x[ntok][K] against a rows x K Q4_K / Q6_K / Q8_0 matrix: each row's
+ * ntok <= 512 token rows x[ntok][K] against a rows x K Q4_K / Q5_K / Q6_K / Q8_0 matrix: each row's
  * activation is quantised to Q8_K (Q8_0 for Q8_0 weights) as the CPU graph does, then
  * y[t][r] = vec_dot(W_r, q(x_t)).  With raw_up non-NULL the launch is the FFN gate/up pair
  * (raw_blocks = gate): y[t][r] = silu(gate_r . q(x_t)) * (up_r . q(x_t)).  y: [ntok][rows]. */

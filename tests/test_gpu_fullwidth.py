@@ -37,6 +37,7 @@ import pytest
 import ggml_cpu
 import ggml_ref as R
 from blama_amd import engine, synthetic
+from util import c_alt_floor
 
 pytestmark = pytest.mark.gpu
 
@@ -169,7 +170,7 @@ def test_fullwidth_batched_verification_matches_oracle(gpu_lib, name):
         orc.decode(prompt)
         assert ctx.decode(claimed, all_logits=True) == 0
         agg = R.MetricsAggregator()
-        sims, top1 = [], []
+        sims, top1, ties = [], [], []
         score = None
         ids_rows = np.zeros((len(claimed), 10), np.int32)
         refs = []
@@ -185,14 +186,27 @@ def test_fullwidth_batched_verification_matches_oracle(gpu_lib, name):
             assert np.all(np.abs(ref[ids.astype(np.int64)] - ref_sorted) <= 2 * dmax + 1e-6), (name, i)
             a = [(int(x), float(v)) for x, v in zip(ids, vals)]
             cm = R.compare(a, R.gather(ref.astype(np.float32), [x for x, _ in a]))
-            # top-1 as the reference gate demands, or the oracle's own top two within 2 max|dlogit|
-            # (a near tie the CPU algorithm's rounding floor decides either way)
-            top1.append(1.0 if cm.top1Match == 1.0 or ref_sorted[0] - ref[int(ids[0])] <= 2 * dmax else 0.0)
+            # top-1 on every row, as the reference gate demands (t-LogitComparer.cpp:76-78); a
+            # mismatch is re-examined below against the CPU algorithm's own floor at that row
+            if cm.top1Match != 1.0:
+                ties.append((i, int(ids[0]), int(np.argmax(ref)), float(ref.max() - ref[int(ids[0])])))
+            top1.append(cm.top1Match)
             score = agg.push_and_verify([cm])
             sims.append(R.logit_similarity(a, R.gather(ref.astype(np.float32), [x for x, _ in a])))
         g = ctx.gather_rows(0, ids_rows)
         for i in range(len(claimed)):
             assert np.array_equal(g[i], ctx.logits(row=i)[ids_rows[i]])
+        if ties:
+            # A top-1 mismatch passes only as a genuine CPU-side tie: the oracle's own margin
+            # between its top id and the GPU's is within the live floor at that row (the same
+            # C oracle with the 8 lanes of every k-quant dot summed in reverse, an equally valid
+            # ggml order: util.c_alt_floor), i.e. the CPU algorithm itself ranks them either way.
+            _, floor = c_alt_floor(buf, 64, prompt, claimed)
+            for i, gid, cid, margin in ties:
+                print(f"{name} row {i}: GPU top-1 {gid}, CPU {cid}, CPU margin {margin:.3e}, "
+                      f"CPU reorder floor {floor[i + 1]:.3e}")
+                assert margin <= floor[i + 1], (name, i, gid, cid, margin, floor[i + 1])
+                top1[i] = 1.0
         assert score >= 0.95 and float(np.mean(sims)) >= 0.98 and min(top1) == 1.0, (score, np.mean(sims))
     finally:
         ctx.close()
