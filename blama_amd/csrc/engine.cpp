@@ -622,7 +622,8 @@ Ctx::Ctx(Model* model, uint32_t nctx, uint32_t nbatch, uint32_t nubatch) : m(mod
         for (const Layer& L : m->layers)
             mmq_ok = mmq_ok && L.gate.type == L.up.type && L.gate.rows == L.up.rows;
         const int NB = kBatchRows;
-        const int hrows = hp.n_expert > 0 ? NB * hp.n_expert_used : NB;   // MoE: a row per (token, slot)
+        // MoE: a row per (token, slot), each expert's rows padded to whole 32-row tiles
+        const int hrows = hp.n_expert > 0 ? moe_rows_cap(NB * hp.n_expert_used, hp.n_expert) : NB;
         MI_HIP(hipMalloc(&xb, (size_t)NB * hp.n_embd * sizeof(float)));
         MI_HIP(hipMalloc(&qb, (size_t)NB * hp.n_embd * sizeof(float)));
         MI_HIP(hipMalloc(&attnb, (size_t)NB * hp.n_embd * sizeof(float)));
@@ -646,14 +647,20 @@ Ctx::Ctx(Model* model, uint32_t nctx, uint32_t nbatch, uint32_t nubatch) : m(mod
                 MI_HIP(hipMalloc(&ub_q0, (size_t)UB_MAX * kmax));
                 MI_HIP(hipMalloc(&ub_dT0, (size_t)UB_MAX * (kmax / 32) * sizeof(float)));
             }
-            if (hp.n_expert > 0) {   // routing of a physical batch, expert down outputs
+            if (hp.n_expert > 0) {   // routing of a physical batch, grouped rows, expert down outputs
+                if (hp.n_expert > MOE_GROUP_MAXE) throw Error("MoE prompt batches: at most 16 experts");
                 const int ns = NB * hp.n_expert_used;
-                MI_HIP(hipMalloc(&yb, (size_t)ns * hp.n_embd * sizeof(float)));
+                const int cap = moe_rows_cap(ns, hp.n_expert);
+                MI_HIP(hipMalloc(&yb, (size_t)cap * hp.n_embd * sizeof(float)));
                 MI_HIP(hipMalloc(&sel_b, (size_t)ns * sizeof(int)));
                 MI_HIP(hipMalloc(&selw_b, (size_t)ns * sizeof(float)));
-                MI_HIP(hipMalloc(&moe_rows, (size_t)ns * sizeof(int)));
+                MI_HIP(hipMalloc(&moe_rows, (size_t)cap * sizeof(int)));
+                MI_HIP(hipMalloc(&moe_rowsel, (size_t)cap * sizeof(int)));
                 MI_HIP(hipMalloc(&moe_pos, (size_t)ns * sizeof(int)));
-                MI_HIP(hipHostMalloc(&h_moe, (size_t)3 * ns * sizeof(int)));
+                MI_HIP(hipMalloc(&moe_grp, (size_t)(2 * MOE_GROUP_MAXE + 1) * sizeof(int)));
+                MI_HIP(hipMalloc(&moe_q, (size_t)cap * kmax));
+                MI_HIP(hipMalloc(&moe_dT, (size_t)cap * (kmax / 32) * sizeof(float)));
+                MI_HIP(hipMalloc(&moe_bsb, (size_t)cap * (kmax / 256) * 16));
             }
             MI_HIP(hipMalloc(&ub_rope, (size_t)UB_MAX * std::max(1, hp.n_rot / 2) * sizeof(float2)));
         }
@@ -711,10 +718,11 @@ Ctx::~Ctx() {
                     (void*)attn_xflags, (void*)attn_xmax, (void*)attn_xsum, (void*)step_ctr,
                     (void*)xb, (void*)qb, (void*)attnb, (void*)hb, (void*)tokpos_b, (void*)ub_q, (void*)ub_dT, (void*)ub_bsb, (void*)ub_rope,
                     (void*)ub_q0, (void*)ub_dT0, (void*)yb, (void*)sel_b, (void*)selw_b, (void*)moe_rows, (void*)moe_pos,
+                    (void*)moe_rowsel, (void*)moe_grp, (void*)moe_q, (void*)moe_dT, (void*)moe_bsb,
                     (void*)logits_all, (void*)grows_ids, (void*)grows_out})
         if (p) hipFree(p);
     for (void* p : {(void*)h_tokpos, (void*)h_topk_ids, (void*)h_topk_vals, (void*)h_logits, (void*)h_gather, (void*)h_grows,
-                    (void*)h_tokpos_b, (void*)h_moe, (void*)h_attn_xerr})
+                    (void*)h_tokpos_b, (void*)h_attn_xerr})
         if (p) hipHostFree(p);
     if (stream) hipStreamDestroy(stream);
 }
@@ -1239,67 +1247,62 @@ void Ctx::decode_batch(const int32_t* tokens, int n) {
 }
 
 // build_moe_ffn (src/llama-graph.cpp, b5187: softmax gating, top-2, weights normalised) over a
-// physical batch: the router of every token (the decode step's router_kernel), the (token, slot)
-// picks grouped by expert on the host (one readback per layer), each expert's gate/up + SwiGLU and
-// down over its own tokens (mmq32 on the expert's MFMA-order copy), then every token's
-// x += w0*y0 + w1*y1 in slot order (launch_moe_combine, the decode GEMV's EPI_MOE_DOWN arithmetic).
+// physical batch, all on the device: the router of every token (the decode step's router_kernel),
+// the (token, slot) picks grouped by expert (launch_moe_group: tokens ascending within an expert,
+// each expert's rows whole 32-row MFMA tiles), one quantisation of every row, ONE grouped mmq32
+// launch for the experts' gate/up + SwiGLU and one for their down projections (a workgroup per
+// (expert, row tile) over that expert's token tiles), then every token's x += w0*y0 + w1*y1 in
+// slot order (launch_moe_combine, the decode GEMV's EPI_MOE_DOWN arithmetic).  No host round trip.
 void Ctx::moe_ffn_batch(int l, int nt) {
     const HParams& hp = m->hp;
     const Layer& L = m->layers[l];
     const int U = hp.n_expert_used, E = hp.n_expert;
     RouterParams rp{xb, L.ffn_norm, hp.eps, L.router, hp.n_embd, E, U, sel_b, selw_b, hp.n_embd};
     launch_router_multi(rp, nt, stream);
-    int* hs = h_moe;                         // [token][slot] -> expert
-    int* hrows = h_moe + (size_t)nt * U;     // row -> source token (rows grouped by expert)
-    int* hpos = h_moe + (size_t)2 * nt * U;  // [token][slot] -> row
-    MI_HIP(hipMemcpyAsync(hs, sel_b, (size_t)nt * U * sizeof(int), hipMemcpyDeviceToHost, stream));
-    MI_HIP(hipStreamSynchronize(stream));
-    std::vector<int> off(E + 1, 0);
-    for (int i = 0; i < nt * U; ++i) {
-        if (hs[i] < 0 || hs[i] >= E) throw Error("moe: router picked an expert out of range");
-        ++off[hs[i] + 1];
-    }
-    for (int e = 0; e < E; ++e) off[e + 1] += off[e];
-    std::vector<int> fill(off.begin(), off.end() - 1);
-    for (int t = 0; t < nt; ++t)   // tokens ascending within an expert
-        for (int k = 0; k < U; ++k) {
-            const int r = fill[hs[t * U + k]]++;
-            hrows[r] = t;
-            hpos[t * U + k] = r;
-        }
-    MI_HIP(hipMemcpyAsync(moe_rows, hrows, (size_t)nt * U * sizeof(int), hipMemcpyHostToDevice, stream));
-    MI_HIP(hipMemcpyAsync(moe_pos, hpos, (size_t)nt * U * sizeof(int), hipMemcpyHostToDevice, stream));
-    for (int e = 0; e < E; ++e) {
-        const int c = off[e + 1] - off[e];
-        if (c == 0) continue;
-        GemmParams p;
-        std::memset(&p, 0, sizeof(p));
-        p.ntok = c;
-        p.tokpos = tokpos_b;
-        // gate/up + SwiGLU: rms_norm(x) * ffn_norm of the expert's tokens
-        const ActQ8 act = ub_act(hp.n_embd, c, L.gate.type);
-        launch_quant_act(xb, hp.n_embd, L.ffn_norm, hp.eps, act, stream, moe_rows + off[e]);
-        p.A = expert_view(L.gate, e);
-        p.B = expert_view(L.up, e);
-        p.pair = PAIR_AB;
-        p.epi = EPI_SWIGLU;
-        p.K = hp.n_embd;
-        p.out = hb + (size_t)off[e] * hp.n_ff;
-        p.out_stride = hp.n_ff;
-        launch_mmq32(p, act, ub_rope, stream);
-        // down: this expert's rows of the FFN output, stored (weighted and summed by the combine)
-        const ActQ8 a2 = ub_act(hp.n_ff, c, L.down.type);
-        launch_quant_act(hb + (size_t)off[e] * hp.n_ff, hp.n_ff, nullptr, hp.eps, a2, stream);
-        GemmParams d = p;
-        d.A = expert_view(L.down, e);
-        std::memset(&d.B, 0, sizeof(d.B));
-        d.pair = PAIR_ADJ;
-        d.epi = EPI_STORE;
-        d.K = hp.n_ff;
-        d.out = yb + (size_t)off[e] * hp.n_embd;
-        d.out_stride = hp.n_embd;
-        launch_mmq32(d, a2, ub_rope, stream);
-    }
+    const int cap = moe_rows_cap(nt * U, E);
+    launch_moe_group(sel_b, nt * U, U, E, moe_grp, moe_rows, moe_rowsel, moe_pos, cap, stream);
+    auto act_of = [&](int K, int type) {
+        ActQ8 a;
+        a.q = moe_q;
+        a.dT = moe_dT;
+        a.bsb = moe_bsb;
+        a.K = K;
+        a.ntok = cap;
+        a.npad = cap;
+        a.q80 = type == T_Q8_0 ? 1 : 0;
+        return a;
+    };
+    GemmParams p;
+    std::memset(&p, 0, sizeof(p));
+    p.ntok = cap;
+    p.tokpos = tokpos_b;
+    p.grp = moe_grp;
+    p.grp_n = E;
+    // gate/up + SwiGLU: rms_norm(x) * ffn_norm of each row's token
+    const ActQ8 act = act_of(hp.n_embd, L.gate.type);
+    launch_quant_act(xb, hp.n_embd, L.ffn_norm, hp.eps, act, stream, moe_rows);
+    p.A = L.gate;
+    p.B = L.up;
+    p.pair = PAIR_AB;
+    p.epi = EPI_SWIGLU;
+    p.K = hp.n_embd;
+    p.out = hb;
+    p.out_stride = hp.n_ff;
+    p.grp_stride = L.gate.sw_expert_stride;
+    launch_mmq32(p, act, ub_rope, stream);
+    // down: every row of the FFN output, stored (weighted and summed by the combine)
+    const ActQ8 a2 = act_of(hp.n_ff, L.down.type);
+    launch_quant_act(hb, hp.n_ff, nullptr, hp.eps, a2, stream, moe_rowsel);
+    GemmParams d = p;
+    d.A = L.down;
+    std::memset(&d.B, 0, sizeof(d.B));
+    d.pair = PAIR_ADJ;
+    d.epi = EPI_STORE;
+    d.K = hp.n_ff;
+    d.out = yb;
+    d.out_stride = hp.n_embd;
+    d.grp_stride = L.down.sw_expert_stride;
+    launch_mmq32(d, a2, ub_rope, stream);
     launch_moe_combine(yb, moe_pos, selw_b, xb, nt, hp.n_embd, stream);
 }
 

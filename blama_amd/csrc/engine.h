@@ -250,15 +250,19 @@ struct Ctx {
     // a second activation set (Q8_0) for a model mixing Q8_0 and k-quant matrices
     int8_t* ub_q0 = nullptr;
     float* ub_dT0 = nullptr;
-    // MoE prompt batches: router picks and weights [token][n_used], the tokens grouped by expert
-    // (moe_rows: source token of each (expert, token) row; moe_pos: the row of each (token, slot)),
-    // the experts' down outputs [row][n_embd]; h_moe: pinned staging
+    // MoE prompt batches: router picks and weights [token][n_used], the tokens grouped by expert on
+    // the device (moe_rows: source token of each (expert, token) row, -1 for padding; moe_pos: the
+    // row of each (token, slot)), the experts' down outputs [row][n_embd]
     float* yb = nullptr;
     int* sel_b = nullptr;
     float* selw_b = nullptr;
     int* moe_rows = nullptr;
     int* moe_pos = nullptr;
-    int* h_moe = nullptr;
+    int* moe_rowsel = nullptr;          // row r or -1 (padding): the down projection's input rows
+    int* moe_grp = nullptr;             // launch_moe_group's {offsets, counts}
+    int8_t* moe_q = nullptr;            // the rows' Q8_K / Q8_0 activations (moe_rows_cap rows)
+    float* moe_dT = nullptr;
+    int8_t* moe_bsb = nullptr;
     void moe_ffn_batch(int l, int nt);
     const float* out_row(int row) const;   // device logits of output row `row` (-1: the last)
     hipGraphExec_t build_graph(bool with_logits, int seg);

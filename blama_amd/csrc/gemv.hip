@@ -236,11 +236,13 @@ __device__ __forceinline__ void gv_body(const GvArgs& a, char* lds, Wait&& wait 
 #define GV_STAMP(k) \
     if (a.stamps && threadIdx.x == 0) a.stamps[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime();
     // order 4: the stamps of the last wave (a streaming wave) instead of wave 0's
-#define GV_STAMPL(k) \
-    if (a.stamps && threadIdx.x == (GV_NW - 1) * 64) a.stamps[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime();
+#define GV_STAMPL(k)
+#define GV_STAMPP(k) \
+    if (a.stamps && threadIdx.x == 0) a.stamps[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime();
 #else
 #define GV_STAMP(k)
 #define GV_STAMPL(k)
+#define GV_STAMPP(k)
 #endif
     GV_STAMP(0)
 #ifdef MI_STAMPS   // 6: the workgroup's last wave to start
@@ -523,6 +525,7 @@ __device__ __forceinline__ void gv_body(const GvArgs& a, char* lds, Wait&& wait 
             GV_STAMPL(1)
         } else {
             wait_vm<0>();   // this wave's staged blocks landed
+            GV_STAMPP(1)
             float scale = 1.0f;
             if (pro == PRO_RMSNORM) {
                 // ggml_compute_forward_rms_norm_f32: sum of float squares in double
@@ -539,6 +542,7 @@ __device__ __forceinline__ void gv_body(const GvArgs& a, char* lds, Wait&& wait 
                 __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the partial is written
                 if (lane == 63) flg[wave] = 1;
                 wait_flags(0, pmask);
+                GV_STAMPP(3)
                 double tot = 0.0;
                 for (int w = 0; w < npro; ++w) tot += red[w];
                 scale = 1.0f / sqrtf((float)(tot / (double)a.K) + a.eps);
@@ -572,13 +576,14 @@ __device__ __forceinline__ void gv_body(const GvArgs& a, char* lds, Wait&& wait 
                 }
             }
             __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this wave's blocks are written
+            GV_STAMPP(2)
             if (lane == 0) flg[GV_NW + wave] = 1;
 #ifdef MI_STAMPS   // 7 (order 4): the workgroup's last prologue wave done
             if (a.stamps && lane == 0) atomicMax(a.stamps + blockIdx.x * 8 + 7, (unsigned long long)__builtin_amdgcn_s_memrealtime());
 #endif
 #pragma unroll
             for (int k = 0; k < D - 1; ++k) issue(ring[k], false);
-            GV_STAMP(1)
+            // (diag) no stamp
         }
         wait_flags(1, pmask | (rope_wave || (qkv && a.n_rot > 0) ? (1u << (GV_NW - 1)) : 0u));
         GV_STAMPL(2)
@@ -1121,7 +1126,8 @@ static void gv_prepare(const GemvParams& p, int cap, GvArgs& a, int& grid_out, G
     a.head_dim = p.head_dim > 0 ? p.head_dim : 1;
     a.kv_dim = p.kv_dim;
     a.stamps = p.stamps;
-    static const int order = getenv("MI_GEMV_ORDER") ? atoi(getenv("MI_GEMV_ORDER")) : 0;
+    // default: prologue waves (order 4; +2 % decode over order 0 on two boxes)
+    static const int order = getenv("MI_GEMV_ORDER") ? atoi(getenv("MI_GEMV_ORDER")) : 4;
     static const int pre = getenv("MI_GEMV_PRE") ? atoi(getenv("MI_GEMV_PRE")) : 8;
     a.order = order;
     a.pre = pre;

@@ -156,6 +156,11 @@ struct GemmParams {
     int kv_dim;
     int need_q8k, need_q80;
     int grid;                  // set by launch_gemm
+    // mmq32 grouped launch (MoE prompt batches): expert e's MFMA-order copy is A.sw + e*grp_stride,
+    // its activation rows [grp[e], grp[e] + grp[grp_n + 1 + e]) (launch_moe_group's layout)
+    const int* grp;
+    long long grp_stride;
+    int grp_n;
 };
 void launch_gemm(const GemmParams& p, hipStream_t s);
 
@@ -247,6 +252,14 @@ void launch_router_multi(const RouterParams& p, int ntok, hipStream_t s);
 // build_moe_ffn's aggregation over a physical batch: x[t] = (y[pos[t][0]]*w[t][0] + y[pos[t][1]]*w[t][1])
 // + x[t] (ggml_mul by the weights, ggml_add of the slots in slot order, then the residual add);
 // y holds the experts' down outputs in compact rows (grouped by expert)
+// Groups the n (token, slot) picks of a physical batch (sel[t*U + k] = expert) by expert on the
+// device: expert e's rows are [grp[e], grp[e] + cnt_e) with grp[e] a multiple of 32 (whole MFMA
+// token tiles), tokens ascending within an expert; grp = {off[0..E], cnt[0..E-1]}.  rows[r] = the
+// source token of row r (-1 for padding, up to rows_cap), rowsel[r] = r or -1, pos[t*U + k] = row.
+constexpr int MOE_GROUP_MAXE = 16;
+inline int moe_rows_cap(int n, int E) { return (n + E * 31 + 31) / 32 * 32; }
+void launch_moe_group(const int* sel, int n, int U, int E, int* grp, int* rows, int* rowsel, int* pos, int rows_cap,
+                      hipStream_t s);
 void launch_moe_combine(const float* y, const int* pos, const float* w, float* x, int ntok, int n_embd,
                         hipStream_t s);
 

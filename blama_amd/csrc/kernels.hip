@@ -1295,6 +1295,64 @@ void launch_router_multi(const RouterParams& p, int ntok, hipStream_t s) {
     MI_HIP(hipGetLastError());
 }
 
+// One workgroup: 256 threads, each over a contiguous range of the picks (so that the rows of an
+// expert come in pick order = token ascending), per-thread counts per expert in LDS, then an
+// exclusive scan over the threads per expert, padded expert offsets, and the row assignment.
+__global__ __launch_bounds__(256) void moe_group_kernel(const int* sel, int n, int U, int E, int* grp, int* rows,
+                                                        int* rowsel, int* pos, int rows_cap) {
+    __shared__ int cnt[256][MOE_GROUP_MAXE];
+    __shared__ int off[MOE_GROUP_MAXE + 1];
+    const int t = threadIdx.x;
+    const int per = (n + 255) / 256;
+    const int i0 = min(n, t * per), i1 = min(n, i0 + per);
+    for (int e = 0; e < E; ++e) cnt[t][e] = 0;
+    for (int i = i0; i < i1; ++i) {
+        const int e = sel[i];
+        if (e >= 0 && e < E) cnt[t][e] += 1;
+    }
+    __syncthreads();
+    if (t < E) {   // exclusive scan over the threads: this expert's rows before thread th's
+        int run = 0;
+        for (int th = 0; th < 256; ++th) {
+            const int c = cnt[th][t];
+            cnt[th][t] = run;
+            run += c;
+        }
+        grp[E + 1 + t] = run;
+    }
+    __syncthreads();
+    if (t == 0) {
+        off[0] = 0;
+        for (int e = 0; e < E; ++e) off[e + 1] = off[e] + (grp[E + 1 + e] + 31) / 32 * 32;
+        for (int e = 0; e <= E; ++e) grp[e] = off[e];
+    }
+    __syncthreads();
+    // padding rows (and every row past the last expert's) first, then the picks' rows
+    for (int r = t; r < rows_cap; r += 256) {
+        rows[r] = -1;
+        rowsel[r] = -1;
+    }
+    __syncthreads();
+    int used[MOE_GROUP_MAXE];
+    for (int e = 0; e < E; ++e) used[e] = 0;
+    for (int i = i0; i < i1; ++i) {
+        const int e = sel[i];
+        if (e < 0 || e >= E) continue;   // the router never picks one (checked on the decode path)
+        const int r = off[e] + cnt[t][e] + used[e]++;
+        rows[r] = i / U;
+        rowsel[r] = r;
+        pos[i] = r;
+    }
+}
+
+void launch_moe_group(const int* sel, int n, int U, int E, int* grp, int* rows, int* rowsel, int* pos, int rows_cap,
+                      hipStream_t s) {
+    if (E < 1 || E > MOE_GROUP_MAXE) throw Error("moe_group: 1..16 experts");
+    if (rows_cap < moe_rows_cap(n, E)) throw Error("moe_group: row capacity too small");
+    hipLaunchKernelGGL(moe_group_kernel, dim3(1), dim3(256), 0, s, sel, n, U, E, grp, rows, rowsel, pos, rows_cap);
+    MI_HIP(hipGetLastError());
+}
+
 __global__ void moe_combine_kernel(const float* y, const int* pos, const float* w, float* x, int n_embd) {
     const int t = blockIdx.y;
     const float* y0 = y + (long long)pos[2 * t] * n_embd;

@@ -88,7 +88,7 @@ __global__ __launch_bounds__(256) void quant_act_kernel(const float* x, int x_st
     const int fj = lane >> 3, fh = (lane >> 2) & 1, fw = lane & 3;   // this lane's 4 elements
     int8_t* q = a.q + (long long)tile * nb * 8192 + fj * 1024 + (fh * 32 + tr) * 16 + 4 * fw;
     int8_t* bsb = a.q80 ? nullptr : a.bsb + ((long long)tile * nb * 32 + tr) * 16;
-    if (t >= a.ntok) {
+    if (t >= a.ntok || (rows && rows[t] < 0)) {   // padding rows (and MoE group padding) are zero
         for (int blk = wave; blk < nb; blk += 4) {
             *reinterpret_cast<int*>(q + blk * 8192) = 0;
             if (!a.q80 && lane < 4) reinterpret_cast<int*>(bsb + blk * 512)[lane] = 0;
@@ -289,7 +289,7 @@ __global__ void swizzle_kernel(const QMat A, const QMat B, int pair, uint8_t* ds
 }
 
 template <bool AB>
-__device__ __forceinline__ void mmq_epilogue(const GemmParams& P, const ActQ8& act, const float2* rope, int ttok0,
+__device__ __forceinline__ void mmq_epilogue(const GemmParams& P, int tend, const float2* rope, int ttok0,
                                              int lane, int row, const float v[16]);
 
 // KSPLIT 4: the 4 waves split the superblocks of all 4 token tiles (partials meet in LDS);
@@ -302,17 +302,38 @@ __global__ __launch_bounds__(256, OCC) void mmq32_t(const GemmParams P, const Ac
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int col = lane & 31, h = lane >> 5;
     const int nb = P.K >> 8;
-    const int ntg = (act.npad + 32 * TT - 1) / (32 * TT);
     const int nrt = AB ? (P.A.rows + 15) / 16 : (P.A.rows + 31) / 32;
-    // blockIdx -> (row tile, token group): the token groups of a row tile on one XCD
-    const int b = blockIdx.x, xcd = b & 7, slot = b >> 3;
-    const int rt = (slot / ntg) * 8 + xcd, tg = slot % ntg;
-    if (rt >= nrt) return;
+    int rt, tg_b, tg_e, base, tend;
+    const uint8_t* swA = P.A.sw;
+    if (KSPLIT == 1 && P.grp) {
+        // grouped (MoE): blockIdx -> (expert, row tile); the expert's token groups in turn
+        const int nrt8 = (nrt + 7) / 8 * 8;
+        const int e = (int)blockIdx.x / nrt8;
+        rt = (int)blockIdx.x % nrt8;
+        if (rt >= nrt) return;
+        base = P.grp[e];
+        const int cnt = P.grp[P.grp_n + 1 + e];
+        tend = base + cnt;
+        tg_b = 0;
+        tg_e = (cnt + 32 * TT - 1) / (32 * TT);
+        swA += (long long)e * P.grp_stride;
+    } else {
+        // blockIdx -> (row tile, token group): the token groups of a row tile on one XCD
+        const int ntg = (act.npad + 32 * TT - 1) / (32 * TT);
+        const int b = blockIdx.x, xcd = b & 7, slot = b >> 3;
+        rt = (slot / ntg) * 8 + xcd;
+        tg_b = slot % ntg;
+        tg_e = tg_b + 1;
+        base = 0;
+        tend = act.ntok;
+        if (rt >= nrt) return;
+    }
     // this lane's weight row
     const int row = AB ? rt * 16 + (col & 15) : rt * 32 + col;
     const int sb0 = KSPLIT > 1 ? nb * w / KS : 0, sb1 = KSPLIT > 1 ? nb * (w + 1) / KS : nb;
-    const int tok0 = tg * 32 * TT;
-    int ntt = (act.npad - tok0) / 32;
+  for (int tg = tg_b; tg < tg_e; ++tg) {
+    const int tok0 = base + tg * 32 * TT;
+    int ntt = P.grp ? (tend - tok0 + 31) / 32 : (act.npad - tok0) / 32;
     ntt = ntt > TT ? TT : ntt;
     const int t_begin = KSPLIT > 1 ? 0 : w, t_end = KSPLIT > 1 ? ntt : (w < ntt ? w + 1 : w);
 
@@ -328,7 +349,7 @@ __global__ __launch_bounds__(256, OCC) void mmq32_t(const GemmParams P, const Ac
             int S[16];
 #pragma unroll
             for (int r = 0; r < 16; ++r) S[r] = 0;
-            const uint8_t* wt = P.A.sw + ((long long)rt * nb + sb) * mmq32_tile_bytes_d(T);
+            const uint8_t* wt = swA + ((long long)rt * nb + sb) * mmq32_tile_bytes_d(T);
             if (T == T_Q8_0) {   // vec_dot_q8_0_q8_0: per 32-block sumi * (d_x * d_y)
                 const u32x4 dwv = *gp(reinterpret_cast<const u32x4*>(wt + 8192 + col * 16));
                 const unsigned dw[4] = {dwv.x, dwv.y, dwv.z, dwv.w};
@@ -426,10 +447,10 @@ __global__ __launch_bounds__(256, OCC) void mmq32_t(const GemmParams P, const Ac
 #pragma unroll
             for (int r = 0; r < 16; ++r) red[w][t][r][lane] = y[r];
         } else {
-            mmq_epilogue<AB>(P, act, rope, tok0 + 32 * t, lane, row, y);
+            mmq_epilogue<AB>(P, tend, rope, tok0 + 32 * t, lane, row, y);
         }
     }
-    if (KSPLIT == 1) return;
+    if (KSPLIT == 1) continue;
     // ---- the superblock splits meet in LDS, in wave order
     __syncthreads();
     const int t = w;   // this wave's epilogue: token tile w
@@ -437,12 +458,13 @@ __global__ __launch_bounds__(256, OCC) void mmq32_t(const GemmParams P, const Ac
     float v[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) v[r] = ((red[0][t][r][lane] + red[1][t][r][lane]) + red[2][t][r][lane]) + red[3][t][r][lane];
-    mmq_epilogue<AB>(P, act, rope, tok0 + 32 * t, lane, row, v);
+    mmq_epilogue<AB>(P, tend, rope, tok0 + 32 * t, lane, row, v);
+  }
 }
 
 // The epilogue of one 32-token x 32-row D tile (v: this lane's 16 results).
 template <bool AB>
-__device__ __forceinline__ void mmq_epilogue(const GemmParams& P, const ActQ8& act, const float2* rope, int ttok0,
+__device__ __forceinline__ void mmq_epilogue(const GemmParams& P, int tend, const float2* rope, int ttok0,
                                              int lane, int row, const float v[16]) {
     const int col = lane & 31, h = lane >> 5;
     const int epi = P.epi;
@@ -451,7 +473,7 @@ __device__ __forceinline__ void mmq_epilogue(const GemmParams& P, const ActQ8& a
     for (int r = 0; r < 16; ++r) {
         const int tok = ttok0 + (r & 3) + 8 * (r >> 2) + 4 * h;
         const float pv = __shfl_xor(v[r], AB ? 16 : 1, 64);   // SwiGLU partner / RoPE partner
-        if (tok >= act.ntok) continue;
+        if (tok >= tend) continue;
         if (AB) {
             if (col >= 16 || row >= P.A.rows) continue;
             P.out[(long long)tok * P.out_stride + row] = silu(v[r]) * pv;   // silu(gate) * up
@@ -487,12 +509,243 @@ __device__ __forceinline__ void mmq_epilogue(const GemmParams& P, const ActQ8& a
     }
 }
 
+// =============================================================================================
+// mmq2: the same arithmetic on a 128-token x 32*RT-column block per workgroup, its operands
+// staged in LDS by LDS-DMA (global_load_lds_dwordx4) two superblocks deep.
+//   * the weight tiles of the block's RT row tiles and the activation tiles of its 4 token tiles
+//     for superblock sb land in stage sb % 2 while stage (sb - 1) % 2 is computed: the whole
+//     workgroup issues one superblock's copy (~55 KiB for Q4_K) per step, so a step's L2/HBM
+//     latency hides behind the previous step's MFMAs, which the register-direct mmq32 could not
+//     do (its loads of a superblock were waited for before the superblock's MFMAs);
+//   * 4 waves as 2 (token halves) x 2 (row halves): a wave computes 2 token tiles x RT/2 row
+//     tiles (the B fragment of a row tile read from LDS once for both token tiles, the A
+//     fragments of both token tiles kept in registers across the row tiles);
+//   * per 32x32 tile the integer sums and their float update are mmq32's (exact int32 sub-block
+//     sums; the per-superblock fp32 update in the same order), so results are bit-identical
+//     to mmq32's.
+// LDS stage: [RT weight slots of SLOT bytes][4 x 8 KiB activations][2 KiB bsb][dT: 1 KiB, Q8_0 4 KiB]
+// =============================================================================================
+template <int T> struct M2 {
+    static constexpr int RT = 2;                                        // row tiles per block
+    static constexpr int NW = 4 * RT;                                    // waves: one 32x32 tile each
+    static constexpr int SLOT = (mmq32_tile_bytes_d(T) + 1023) / 1024 * 1024;
+    static constexpr int A_OFF = RT * SLOT;
+    static constexpr int BSB_OFF = A_OFF + 4 * 8192;
+    static constexpr int DT_OFF = BSB_OFF + 2048;
+    static constexpr int DT_KB = T == T_Q8_0 ? 4 : 1;
+    static constexpr int STAGE = DT_OFF + DT_KB * 1024;
+    static constexpr int NI = STAGE / 1024;                             // 1 KiB LDS-DMA pieces
+    static constexpr int NIW = (NI + NW - 1) / NW;                      // per wave (some repeat)
+};
+
+typedef __attribute__((address_space(3))) char lchar;
+template <typename V>
+__device__ __forceinline__ V lds_ld(const lchar* p) { return *reinterpret_cast<const __attribute__((address_space(3))) V*>(p); }
+
+template <int T, bool AB>
+__global__ __launch_bounds__(64 * M2<T>::NW) void mmq2_t(const GemmParams P, const ActQ8 act, const float2* rope) {
+    using C = M2<T>;
+    constexpr int RT = C::RT;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int w = wv & 3;                             // this wave's token tile
+    const int wr = wv >> 2;                           // this wave's row tile (of the block's RT)
+    const int col = lane & 31, h = lane >> 5;
+    const int nb = P.K >> 8;
+    const int nrt = AB ? (P.A.rows + 15) / 16 : (P.A.rows + 31) / 32;
+    const int nrb = (nrt + RT - 1) / RT;              // row blocks
+    const int ntb = (act.npad + 127) / 128;           // token blocks
+    // blockIdx -> (row block, token block): the token blocks of a row block on one XCD
+    const int b = blockIdx.x, xcd = b & 7, slot = b >> 3;
+    const int rb = (slot / ntb) * 8 + xcd, tb = slot % ntb;
+    if (rb >= nrb) return;
+    const int tok0 = tb * 128;
+    const int ntt = min(4, (act.npad - tok0) / 32);   // token tiles of this block (npad: whole tiles)
+    const int TB = mmq32_tile_bytes_d(T);
+
+    // ---- the LDS-DMA copy of superblock sb into stage st: piece i (1 KiB) of the stage image.
+    // Every piece is a wave-uniform base (scalar registers) + a per-lane 32-bit offset, so the
+    // copy holds no 64-bit per-lane addresses across the loop.
+    auto ubase = [](const void* p) {
+        const unsigned long long v = reinterpret_cast<unsigned long long>(p);
+        const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v), hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+        return reinterpret_cast<const uint8_t*>(((unsigned long long)hi << 32) | lo);
+    };
+    auto copy_stage = [&](int sb, int st) {
+        char* base = smem + st * C::STAGE;
+#pragma unroll
+        for (int k = 0; k < C::NIW; ++k) {
+            int i = wv + C::NW * k;
+            if (i >= C::NI) i = C::NI - 1;            // a repeated piece: same bytes, same place
+            const int off = i * 1024;                 // byte offset of the piece in the stage
+            const uint8_t* ub;
+            unsigned vo;
+            if (off < C::A_OFF) {                     // weight slot r, bytes o.. within it
+                const int r = off / C::SLOT, o = off % C::SLOT;
+                const int rt = min(rb * RT + r, nrt - 1);
+                ub = ubase(P.A.sw + ((long long)rt * nb + sb) * TB + o);
+                vo = o + lane * 16 < TB ? lane * 16 : 0;   // past the tile: any valid bytes (padding)
+            } else if (off < C::BSB_OFF) {            // activation tile t, 1 KiB piece j
+                const int o = off - C::A_OFF, t = o >> 13, j = (o >> 10) & 7;
+                const int tt = min(tb * 4 + t, act.npad / 32 - 1);
+                ub = ubase(act.q + ((long long)tt * nb + sb) * 8192 + j * 1024);
+                vo = lane * 16;
+            } else if (off < C::DT_OFF) {             // bsb of tiles 2q, 2q+1 (512 B each)
+                const int q = (off - C::BSB_OFF) >> 10;
+                const int tt = min(tb * 4 + 2 * q, act.npad / 32 - 2);
+                ub = ubase(act.q80 ? reinterpret_cast<const int8_t*>(act.q) : act.bsb + ((long long)tt * nb + sb) * 512);
+                vo = act.q80 ? 0u : (unsigned)((lane >> 5) * nb * 512 + (lane & 31) * 16);
+            } else {                                  // dT: 128 tokens x 4 B per row of dT
+                const int q = (off - C::DT_OFF) >> 10;    // Q8_0: rows 8sb + 2q, 8sb + 2q + 1
+                const int dtrow = act.q80 ? 8 * sb + 2 * q : sb;
+                ub = ubase(act.dT + (long long)dtrow * act.npad + tok0);
+                const int tk = min(4 * (lane & 31), act.npad - 4 - tok0);
+                vo = (unsigned)(tk * 4 + (act.q80 ? (lane >> 5) * act.npad * 4 : 0));
+            }
+            __builtin_amdgcn_global_load_lds(gp(ub + vo), (__attribute__((address_space(3))) void*)(base + off), 16, 0, 0);
+        }
+    };
+
+    float y[1][16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) y[0][e] = 0.0f;
+
+    copy_stage(0, 0);
+    if (nb > 1) copy_stage(1, 1);
+#pragma unroll 1
+    for (int sb = 0; sb < nb; ++sb) {
+        // this wave's copy of superblock sb landed (the next one's stays in flight), then the
+        // workgroup's (barrier); LDS-DMA is a pending LDS write on the VM counter
+        if (sb + 1 < nb) __builtin_amdgcn_s_waitcnt((C::NIW & 15) | ((C::NIW >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+        else __builtin_amdgcn_s_waitcnt((0x7 << 4) | (0xF << 8));
+        __builtin_amdgcn_s_barrier();
+        const lchar* stg = (const lchar*)(smem + (sb & 1) * C::STAGE);
+        const lchar* A0 = stg + C::A_OFF + w * 8192 + lane * 16;       // this wave's token tile
+        const lchar* dTw = stg + C::DT_OFF + (w * 32 + 4 * h) * 4;
+        if (T == T_Q8_0) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const v4i a = lds_ld<v4i>(A0 + j * 1024);
+                {
+                    constexpr int r = 0;
+                    const lchar* wt = stg + wr * C::SLOT;
+                    const v4i wq = lds_ld<v4i>(wt + j * 1024 + lane * 16);
+                    const unsigned dwp = lds_ld<unsigned>(wt + 8192 + col * 16 + (j >> 1) * 4);
+                    const float dwj = h2f(dwp >> (16 * (j & 1)));
+                    const v16i dj = mfma(a, wq);
+                    const lchar* dT8 = dTw + (j >> 1) * 1024 + (j & 1) * 512;
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {
+                        const f32x4 dx4 = lds_ld<f32x4>(dT8 + 32 * g);
+                        const float dx[4] = {dx4.x, dx4.y, dx4.z, dx4.w};
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) y[r][4 * g + i] = fmaf((float)dj[4 * g + i], dwj * dx[i], y[r][4 * g + i]);
+                    }
+                    asm volatile("" ::: "memory");   // no LDS load hoisted across sub-blocks
+                }
+            }
+        } else if (T == T_Q4_K || T == T_Q5_K) {
+            {
+                constexpr int r = 0;
+                const lchar* wt = stg + wr * C::SLOT;
+                const u32x4 hd = lds_ld<u32x4>(wt + (T == T_Q5_K ? 5120 : 4096) + col * 16);
+                const u32x4 qh = T == T_Q5_K ? lds_ld<u32x4>(wt + 4096 + lane * 16) : u32x4{0u, 0u, 0u, 0u};
+                int sc[8], mn[8];
+                q4k_scales(hd, sc, mn);
+                int S[16];
+#pragma unroll
+                for (int e = 0; e < 16; ++e) S[e] = 0;
+#pragma unroll
+                for (int p = 0; p < 4; ++p) {
+                    const u32x4 wq = lds_ld<u32x4>(wt + p * 1024 + lane * 16);
+                    const unsigned sl = 2 * p, sh = 2 * p + 1;
+                    const v4i blo = v4i{(int)((wq.x & 0x0F0F0F0Fu) | (((qh.x >> sl) & 0x01010101u) << 4)),
+                                        (int)((wq.y & 0x0F0F0F0Fu) | (((qh.y >> sl) & 0x01010101u) << 4)),
+                                        (int)((wq.z & 0x0F0F0F0Fu) | (((qh.z >> sl) & 0x01010101u) << 4)),
+                                        (int)((wq.w & 0x0F0F0F0Fu) | (((qh.w >> sl) & 0x01010101u) << 4))};
+                    const v4i bhi = v4i{(int)(((wq.x >> 4) & 0x0F0F0F0Fu) | (((qh.x >> sh) & 0x01010101u) << 4)),
+                                        (int)(((wq.y >> 4) & 0x0F0F0F0Fu) | (((qh.y >> sh) & 0x01010101u) << 4)),
+                                        (int)(((wq.z >> 4) & 0x0F0F0F0Fu) | (((qh.z >> sh) & 0x01010101u) << 4)),
+                                        (int)(((wq.w >> 4) & 0x0F0F0F0Fu) | (((qh.w >> sh) & 0x01010101u) << 4))};
+                    const v16i d0 = mfma(lds_ld<v4i>(A0 + (2 * p) * 1024), blo);
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) S[e] = __mul24(sc[2 * p], d0[e]) + S[e];
+                    const v16i d1 = mfma(lds_ld<v4i>(A0 + (2 * p + 1) * 1024), bhi);
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) S[e] = __mul24(sc[2 * p + 1], d1[e]) + S[e];
+                    // keep the scheduler from hoisting every sub-block's MFMA ahead of its
+                    // scaling (16 accumulator registers each: the registers run out)
+                    asm volatile("" ::: "memory");   // no LDS load hoisted across sub-blocks
+                }
+                // sum_j m_j*bsum_j: mins as int8 B operands, k 0-7 (against hi) / k 8-15 (against lo)
+                const int m03 = mn[0] | (mn[1] << 8) | (mn[2] << 16) | (mn[3] << 24);
+                const int m47 = mn[4] | (mn[5] << 8) | (mn[6] << 16) | (mn[7] << 24);
+                const v4i bm1 = h == 0 ? v4i{m03, m47, 0, 0} : v4i{0, 0, 0, 0};
+                const v4i bm2 = h == 0 ? v4i{0, 0, m03, m47} : v4i{0, 0, 0, 0};
+                const v4i ab = h == 0 ? lds_ld<v4i>(stg + C::BSB_OFF + w * 512 + col * 16) : v4i{0, 0, 0, 0};
+                const v16i x1 = mfma(ab, bm1);
+                const v16i x2 = mfma(ab, bm2);
+                const float dr = h2f(hd.x), dmr = h2f(hd.x >> 16);
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const f32x4 dx4 = lds_ld<f32x4>(dTw + 32 * g);
+                    const float dx[4] = {dx4.x, dx4.y, dx4.z, dx4.w};
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int e = 4 * g + i;
+                        const float d = dr * dx[i], dm = dmr * dx[i];
+                        y[r][e] = fmaf(-dm, (float)(64 * x1[e] + x2[e]), fmaf(d, (float)S[e], y[r][e]));
+                    }
+                }
+            }
+        } else {   // Q6_K: the 8 spans of w = 64*hi + lo, each operand accumulated by the MFMA
+            {
+                constexpr int r = 0;
+                const lchar* wt = stg + wr * C::SLOT;
+                v16i ah = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, al = ah;
+#pragma unroll
+                for (int sp = 0; sp < 8; ++sp) {
+                    const v4i a = lds_ld<v4i>(A0 + sp * 1024);
+                    const v4i bh = lds_ld<v4i>(wt + sp * 1024 + lane * 16);
+                    const v4i bl = lds_ld<v4i>(wt + 8192 + sp * 1024 + lane * 16);
+                    ah = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bh, ah, 0, 0, 0);
+                    al = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bl, al, 0, 0, 0);
+                }
+                const float dr = h2f(lds_ld<unsigned short>(wt + 16384 + col * 2));
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const f32x4 dx4 = lds_ld<f32x4>(dTw + 32 * g);
+                    const float dx[4] = {dx4.x, dx4.y, dx4.z, dx4.w};
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int e = 4 * g + i;
+                        y[r][e] = fmaf(dr * dx[i], (float)(ah[e] * 64 + al[e]), y[r][e]);
+                    }
+                }
+            }
+        }
+        // every wave is done with stage sb % 2: refill it with superblock sb + 2
+        __builtin_amdgcn_s_waitcnt((0xF) | (0x3 << 14) | (0x7 << 4));   // lgkmcnt(0): this wave's LDS reads done
+        __builtin_amdgcn_s_barrier();
+        if (sb + 2 < nb) copy_stage(sb + 2, sb & 1);
+    }
+    // ---- epilogue: token tile w, row tile rb*RT + wr
+    const int rt = rb * RT + wr;
+    if (w >= ntt || rt >= nrt) return;
+    const int row = AB ? rt * 16 + (col & 15) : rt * 32 + col;
+    mmq_epilogue<AB>(P, act.ntok, rope, tok0 + 32 * w, lane, row, y[0]);
+}
+
+template <int T> constexpr int m2_lds() { return 2 * M2<T>::STAGE; }
+
 }  // namespace mmq
 
 void launch_quant_act(const float* x, int x_stride, const float* norm_w, float eps, const ActQ8& a, hipStream_t s,
                       const int* rows) {
     if (a.K % 256) throw Error("quant_act: K must be a multiple of 256");
-    if (a.npad % 32 || a.ntok > a.npad || a.npad > UB_MAX) throw Error("quant_act: bad token count");
+    // (more than UB_MAX rows only for the MoE rows of a batch: one per (token, slot), padded)
+    if (a.npad % 32 || a.ntok > a.npad || a.npad > 4 * UB_MAX) throw Error("quant_act: bad token count");
     hipLaunchKernelGGL(mmq::quant_act_kernel, dim3(a.npad), dim3(256), 0, s, x, x_stride, norm_w, eps, a, rows);
     MI_HIP(hipGetLastError());
 }
@@ -532,15 +785,19 @@ void launch_mmq32(const GemmParams& p, const ActQ8& act, const float2* rope, hip
     if (!ab && p.epi == EPI_SWIGLU) throw Error("mmq32: SwiGLU needs a pair");
     if ((p.epi == EPI_ROPE_Q || p.epi == EPI_ROPE_K) && (!rope || p.head_dim % 2 || p.n_rot > p.head_dim))
         throw Error("mmq32: RoPE epilogue needs the rope table");
-    if (act.ntok < 1 || act.npad % 32 || act.npad > UB_MAX) throw Error("mmq32: bad token count");
+    if (act.ntok < 1 || act.npad % 32 || act.npad > (p.grp ? 4 * UB_MAX : UB_MAX)) throw Error("mmq32: bad token count");
     if (!p.A.sw) throw Error("mmq32: the matrix has no MFMA-order copy");
     const int ntg = (act.npad + 32 * mmq::TT - 1) / (32 * mmq::TT);
     const int nrt = ab ? (p.A.rows + 15) / 16 : (p.A.rows + 31) / 32;
-    const int grid = (nrt + 7) / 8 * 8 * ntg;
+    // grouped (MoE): a workgroup per (expert, row tile), each over its expert's token groups
+    const int grid = p.grp ? p.grp_n * ((nrt + 7) / 8 * 8) : (nrt + 7) / 8 * 8 * ntg;
+    if (p.grp && (p.grp_n < 1 || (p.epi != EPI_SWIGLU && p.epi != EPI_STORE)))
+        throw Error("mmq32: a grouped launch is an expert gate/up or down");
     // MI_MMQ=<v>: 0 = K split over the waves (2 waves/SIMD), 1 (default) = a token tile per wave over
     // all superblocks at 2 waves/SIMD, 2 = the same at 3 waves/SIMD.  Measured on the 7B 512-token
     // prefill: 21.97 / 21.19 / 22.69 ms (profiles/r02_prefill_*).
-    static const int var = getenv("MI_MMQ") ? atoi(getenv("MI_MMQ")) : 1;
+    static const int var_env = getenv("MI_MMQ") ? atoi(getenv("MI_MMQ")) : 1;
+    const int var = p.grp && var_env == 0 ? 1 : var_env;   // grouped launches: a token tile per wave
     decltype(&mmq::mmq32_t<T_Q4_K, false, 4, 2>) fn;
 #define MMQ_PICK(KS_, OCC_)                                                                              \
     fn = p.A.type == T_Q4_K ? (ab ? mmq::mmq32_t<T_Q4_K, true, KS_, OCC_> : mmq::mmq32_t<T_Q4_K, false, KS_, OCC_>) \
@@ -551,6 +808,32 @@ void launch_mmq32(const GemmParams& p, const ActQ8& act, const float2* rope, hip
     else if (var == 2) MMQ_PICK(1, 3);
     else MMQ_PICK(4, 2);
 #undef MMQ_PICK
+    if (!p.grp && var == 1 && getenv("MI_MMQ_OLD") == nullptr) {
+        // mmq2: 128-token x 32*RT-column blocks, LDS-DMA staged two superblocks deep
+        const int T = p.A.type;
+        const int RT = mmq::M2<T_Q4_K>::RT;
+        const int NWv = 4 * RT;
+        const int nrb = (nrt + RT - 1) / RT;
+        const int ntb = (act.npad + 127) / 128;
+        const int g2 = (nrb + 7) / 8 * 8 * ntb;
+        decltype(&mmq::mmq2_t<T_Q4_K, false>) f2;
+        int lds;
+        switch (T) {
+        case T_Q4_K: f2 = ab ? mmq::mmq2_t<T_Q4_K, true> : mmq::mmq2_t<T_Q4_K, false>; lds = mmq::m2_lds<T_Q4_K>(); break;
+        case T_Q5_K: f2 = ab ? mmq::mmq2_t<T_Q5_K, true> : mmq::mmq2_t<T_Q5_K, false>; lds = mmq::m2_lds<T_Q5_K>(); break;
+        case T_Q6_K: f2 = ab ? mmq::mmq2_t<T_Q6_K, true> : mmq::mmq2_t<T_Q6_K, false>; lds = mmq::m2_lds<T_Q6_K>(); break;
+        default: f2 = ab ? mmq::mmq2_t<T_Q8_0, true> : mmq::mmq2_t<T_Q8_0, false>; lds = mmq::m2_lds<T_Q8_0>(); break;
+        }
+        static bool attr_done[4][2] = {};
+        const int ti = T == T_Q4_K ? 0 : T == T_Q5_K ? 1 : T == T_Q6_K ? 2 : 3;
+        if (!attr_done[ti][ab]) {
+            MI_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(f2), hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+            attr_done[ti][ab] = true;
+        }
+        hipLaunchKernelGGL(f2, dim3(g2), dim3(64 * NWv), (size_t)lds, s, p, act, rope);
+        MI_HIP(hipGetLastError());
+        return;
+    }
     hipLaunchKernelGGL(fn, dim3(grid), dim3(256), 0, s, p, act, rope);
     MI_HIP(hipGetLastError());
 }

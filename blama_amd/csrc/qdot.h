@@ -128,25 +128,23 @@ __device__ __forceinline__ float wave_max(float v) {
 // ties), iscale = -127/max, q = min(127, nearest_int(iscale*x)), d = 1/iscale.
 __device__ __forceinline__ void quant_q8k_block(const float v[4], int lane, int8_t* q8, int* bsum,
                                                 float* dk) {
+    // branch-free (selects only), so that the blocks a wave quantises back to back form one
+    // basic block whose dependent chains (DPP max, division) the scheduler can interleave
     const float a0 = fabsf(v[0]), a1 = fabsf(v[1]), a2 = fabsf(v[2]), a3 = fabsf(v[3]);
     const float amax = wave_max_pos(fmaxf(fmaxf(a0, a1), fmaxf(a2, a3)));
+    // the signed value at the FIRST index whose |x| is the maximum (amax == 0: every lane's
+    // first element, unused)
+    const int e = a0 == amax ? 0 : a1 == amax ? 1 : a2 == amax ? 2 : a3 == amax ? 3 : 4;
+    const float mine = e == 0 ? v[0] : e == 1 ? v[1] : e == 2 ? v[2] : v[3];
+    const unsigned long long m = __ballot(e < 4);
+    const int src = __builtin_ctzll(m | (1ull << 63));
+    const float mx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mine), src));
+    const bool zero = amax == 0.0f;
+    const float iscale = -127.0f / mx;
     int q[4];
-    float d;
-    if (amax == 0.0f) {
-        q[0] = q[1] = q[2] = q[3] = 0;
-        d = 0.0f;
-    } else {
-        // the signed value at the FIRST index whose |x| is the maximum
-        const int e = a0 == amax ? 0 : a1 == amax ? 1 : a2 == amax ? 2 : a3 == amax ? 3 : 4;
-        const float mine = e == 0 ? v[0] : e == 1 ? v[1] : e == 2 ? v[2] : v[3];
-        const unsigned long long m = __ballot(e < 4);
-        const int src = __builtin_ctzll(m);
-        const float mx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mine), src));
-        const float iscale = -127.0f / mx;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) q[k] = min(127, (int)rintf(iscale * v[k]));
-        d = 1.0f / iscale;
-    }
+    for (int k = 0; k < 4; ++k) q[k] = zero ? 0 : min(127, (int)rintf(iscale * v[k]));
+    const float d = zero ? 0.0f : 1.0f / iscale;
     const int packed = (q[0] & 0xFF) | ((q[1] & 0xFF) << 8) | ((q[2] & 0xFF) << 16) | ((q[3] & 0xFF) << 24);
     reinterpret_cast<int*>(q8)[lane] = packed;
     int sm = q[0] + q[1] + q[2] + q[3];
