@@ -236,13 +236,11 @@ __device__ __forceinline__ void gv_body(const GvArgs& a, char* lds, Wait&& wait 
 #define GV_STAMP(k) \
     if (a.stamps && threadIdx.x == 0) a.stamps[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime();
     // order 4: the stamps of the last wave (a streaming wave) instead of wave 0's
-#define GV_STAMPL(k)
-#define GV_STAMPP(k) \
-    if (a.stamps && threadIdx.x == 0) a.stamps[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime();
+#define GV_STAMPL(k) \
+    if (a.stamps && threadIdx.x == 64 * (GV_NW - 1)) a.stamps[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime();
 #else
 #define GV_STAMP(k)
 #define GV_STAMPL(k)
-#define GV_STAMPP(k)
 #endif
     GV_STAMP(0)
 #ifdef MI_STAMPS   // 6: the workgroup's last wave to start
@@ -525,7 +523,6 @@ __device__ __forceinline__ void gv_body(const GvArgs& a, char* lds, Wait&& wait 
             GV_STAMPL(1)
         } else {
             wait_vm<0>();   // this wave's staged blocks landed
-            GV_STAMPP(1)
             float scale = 1.0f;
             if (pro == PRO_RMSNORM) {
                 // ggml_compute_forward_rms_norm_f32: sum of float squares in double
@@ -542,7 +539,6 @@ __device__ __forceinline__ void gv_body(const GvArgs& a, char* lds, Wait&& wait 
                 __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the partial is written
                 if (lane == 63) flg[wave] = 1;
                 wait_flags(0, pmask);
-                GV_STAMPP(3)
                 double tot = 0.0;
                 for (int w = 0; w < npro; ++w) tot += red[w];
                 scale = 1.0f / sqrtf((float)(tot / (double)a.K) + a.eps);
@@ -576,14 +572,12 @@ __device__ __forceinline__ void gv_body(const GvArgs& a, char* lds, Wait&& wait 
                 }
             }
             __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this wave's blocks are written
-            GV_STAMPP(2)
             if (lane == 0) flg[GV_NW + wave] = 1;
 #ifdef MI_STAMPS   // 7 (order 4): the workgroup's last prologue wave done
             if (a.stamps && lane == 0) atomicMax(a.stamps + blockIdx.x * 8 + 7, (unsigned long long)__builtin_amdgcn_s_memrealtime());
 #endif
 #pragma unroll
             for (int k = 0; k < D - 1; ++k) issue(ring[k], false);
-            // (diag) no stamp
         }
         wait_flags(1, pmask | (rope_wave || (qkv && a.n_rot > 0) ? (1u << (GV_NW - 1)) : 0u));
         GV_STAMPL(2)
@@ -879,6 +873,7 @@ __device__ __forceinline__ void gv_body(const GvArgs& a, char* lds, Wait&& wait 
     if (a.stamps && lane == 0) atomicMax(a.stamps + blockIdx.x * 8 + 5, (unsigned long long)__builtin_amdgcn_s_memrealtime());
 #endif
 #undef GV_STAMP
+#undef GV_STAMPL
 }
 
 // T1: -1 one segment; -2 two segments of type T0; else the type of segment 1.

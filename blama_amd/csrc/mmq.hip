@@ -510,20 +510,24 @@ __device__ __forceinline__ void mmq_epilogue(const GemmParams& P, int tend, cons
 }
 
 // =============================================================================================
-// mmq2: the same arithmetic on a 128-token x 32*RT-column block per workgroup, its operands
-// staged in LDS by LDS-DMA (global_load_lds_dwordx4) two superblocks deep.
+// mmq2: the same arithmetic on a 128-token x 32*RT-column block per workgroup (8 waves: wave wv
+// computes token tile wv & 3 x row tile wv >> 2, one 32x32 tile), its operands staged in LDS by
+// LDS-DMA (global_load_lds_dwordx4):
 //   * the weight tiles of the block's RT row tiles and the activation tiles of its 4 token tiles
-//     for superblock sb land in stage sb % 2 while stage (sb - 1) % 2 is computed: the whole
-//     workgroup issues one superblock's copy (~55 KiB for Q4_K) per step, so a step's L2/HBM
-//     latency hides behind the previous step's MFMAs, which the register-direct mmq32 could not
-//     do (its loads of a superblock were waited for before the superblock's MFMAs);
-//   * 4 waves as 2 (token halves) x 2 (row halves): a wave computes 2 token tiles x RT/2 row
-//     tiles (the B fragment of a row tile read from LDS once for both token tiles, the A
-//     fragments of both token tiles kept in registers across the row tiles);
-//   * per 32x32 tile the integer sums and their float update are mmq32's (exact int32 sub-block
-//     sums; the per-superblock fp32 update in the same order), so results are bit-identical
-//     to mmq32's.
-// LDS stage: [RT weight slots of SLOT bytes][4 x 8 KiB activations][2 KiB bsb][dT: 1 KiB, Q8_0 4 KiB]
+//     for superblock sb + 1 land in one stage while superblock sb is computed from the other;
+//     every piece address is a scalar base + a lane offset, computed once per token block;
+//   * Q4_K / Q5_K: the 4 waves of a row tile first decode its superblock into int8 operand
+//     planes of the SCALED weights sc_j * q (P0 + 8 P1 [+ 16 P2], every plane byte <= 105), so
+//     the MFMAs accumulate sum_j sc_j * dot_j over the 8 sub-blocks themselves: the nibble
+//     split and scale work is done once per row tile instead of once per wave, and the 16
+//     integer multiply-adds per sub-block and result are gone (VALU was the bound: ~310 VALU
+//     against 10 MFMAs per wave and superblock);
+//   * Q6_K: the scaled hi/lo operands of the MFMA-order copy, accumulated by the MFMA; Q8_0:
+//     one MFMA per 32-block and a float update per block (vec_dot_q8_0_q8_0's order);
+//   * per 32x32 tile the integer sums are exact (the same int32 values as mmq32's) and the
+//     per-superblock fp32 update is mmq32's.
+// LDS: 2 stages of [RT weight slots of SLOT bytes][4 x 8 KiB activations][2 KiB bsb][dT: 1 KiB,
+// Q8_0 4 KiB], then (Q4_K / Q5_K) the operand planes [RT][NPL][8 sub-blocks][64 lanes x 16 B].
 // =============================================================================================
 template <int T> struct M2 {
     static constexpr int RT = 2;                                        // row tiles per block
@@ -536,9 +540,22 @@ template <int T> struct M2 {
     static constexpr int STAGE = DT_OFF + DT_KB * 1024;
     static constexpr int NI = STAGE / 1024;                             // 1 KiB LDS-DMA pieces
     static constexpr int NIW = (NI + NW - 1) / NW;                      // per wave (some repeat)
+    static constexpr int NPL = T == T_Q5_K ? 3 : 2;                     // K-quant operand planes
+    static constexpr int PLANES = (T == T_Q4_K || T == T_Q5_K) ? RT * NPL * 8 * 1024 : 0;
+    static constexpr int LDS = 2 * STAGE + PLANES;
 };
 
 typedef __attribute__((address_space(3))) char lchar;
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+// the bytes of x times s, every byte product < 256 (no carry between bytes): v_pk_mul_lo_u16
+__device__ __forceinline__ unsigned bmul(unsigned x, unsigned s) {
+    u16x2 a;
+    __builtin_memcpy(&a, &x, 4);
+    const u16x2 r = a * u16x2{(unsigned short)s, (unsigned short)s};
+    unsigned o;
+    __builtin_memcpy(&o, &r, 4);
+    return o;
+}
 template <typename V>
 __device__ __forceinline__ V lds_ld(const lchar* p) { return *reinterpret_cast<const __attribute__((address_space(3))) V*>(p); }
 
@@ -546,6 +563,7 @@ template <int T, bool AB>
 __global__ __launch_bounds__(64 * M2<T>::NW) void mmq2_t(const GemmParams P, const ActQ8 act, const float2* rope) {
     using C = M2<T>;
     constexpr int RT = C::RT;
+    constexpr int NPL = C::NPL;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -556,54 +574,90 @@ __global__ __launch_bounds__(64 * M2<T>::NW) void mmq2_t(const GemmParams P, con
     const int nrt = AB ? (P.A.rows + 15) / 16 : (P.A.rows + 31) / 32;
     const int nrb = (nrt + RT - 1) / RT;              // row blocks
     const int ntb = (act.npad + 127) / 128;           // token blocks
-    // blockIdx -> (row block, token block): the token blocks of a row block on one XCD
-    const int b = blockIdx.x, xcd = b & 7, slot = b >> 3;
-    const int rb = (slot / ntb) * 8 + xcd, tb = slot % ntb;
-    if (rb >= nrb) return;
-    const int tok0 = tb * 128;
-    const int ntt = min(4, (act.npad - tok0) / 32);   // token tiles of this block (npad: whole tiles)
     const int TB = mmq32_tile_bytes_d(T);
+    int rb, tb_b, tb_e, base, tend;
+    const uint8_t* swA = P.A.sw;
+    if (P.grp) {
+        // grouped (MoE): blockIdx -> (expert, row block); the expert's 128-token blocks in turn
+        const int nrb8 = (nrb + 7) / 8 * 8;
+        const int e = (int)blockIdx.x / nrb8;
+        rb = (int)blockIdx.x % nrb8;
+        if (rb >= nrb) return;
+        base = P.grp[e];
+        tend = base + P.grp[P.grp_n + 1 + e];
+        tb_b = 0;
+        tb_e = (tend - base + 127) / 128;
+        swA += (long long)e * P.grp_stride;
+    } else {
+        // blockIdx -> (row block, token block): the token blocks of a row block on one XCD
+        const int b = blockIdx.x, xcd = b & 7, slot = b >> 3;
+        rb = (slot / ntb) * 8 + xcd;
+        tb_b = slot % ntb;
+        tb_e = tb_b + 1;
+        base = 0;
+        tend = act.ntok;
+        if (rb >= nrb) return;
+    }
+    const int tile_end = (tend + 31) / 32;            // tiles past the batch's (group's) last: clamped
+  for (int tb = tb_b; tb < tb_e; ++tb) {
+    // (grouped: the previous token block's last stage may still be read by other waves)
+    if (tb != tb_b) __builtin_amdgcn_s_barrier();
+    const int tok0 = base + tb * 128;
+    const int tile0 = tok0 / 32;
+    const int ntt = min(4, tile_end - tile0);         // token tiles of this block
 
     // ---- the LDS-DMA copy of superblock sb into stage st: piece i (1 KiB) of the stage image.
-    // Every piece is a wave-uniform base (scalar registers) + a per-lane 32-bit offset, so the
-    // copy holds no 64-bit per-lane addresses across the loop.
+    // Every piece is a wave-uniform base (scalar registers) + a per-lane 32-bit offset; the bases
+    // of superblock 0 and their per-superblock steps are computed once per token block.
     auto ubase = [](const void* p) {
         const unsigned long long v = reinterpret_cast<unsigned long long>(p);
         const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v), hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
         return reinterpret_cast<const uint8_t*>(((unsigned long long)hi << 32) | lo);
     };
+    const uint8_t* pbase[C::NIW];
+    unsigned pstep[C::NIW], pvo[C::NIW];
+#pragma unroll
+    for (int k = 0; k < C::NIW; ++k) {
+        int i = wv + C::NW * k;
+        if (i >= C::NI) i = C::NI - 1;                // a repeated piece: same bytes, same place
+        const int off = i * 1024;                     // byte offset of the piece in the stage
+        if (off < C::A_OFF) {                         // weight slot r, bytes o.. within it
+            const int r = off / C::SLOT, o = off % C::SLOT;
+            const int rt = min(rb * RT + r, nrt - 1);
+            pbase[k] = ubase(swA + (long long)rt * nb * TB + o);
+            pstep[k] = TB;
+            pvo[k] = o + lane * 16 < TB ? lane * 16 : 0;   // past the tile: any valid bytes (padding)
+        } else if (off < C::BSB_OFF) {                // activation tile t, 1 KiB piece j
+            const int o = off - C::A_OFF, t = o >> 13, j = (o >> 10) & 7;
+            const int tt = min(tile0 + t, tile_end - 1);
+            pbase[k] = ubase(act.q + (long long)tt * nb * 8192 + j * 1024);
+            pstep[k] = 8192;
+            pvo[k] = lane * 16;
+        } else if (off < C::DT_OFF) {                 // bsb of tiles 2q, 2q+1 (512 B each)
+            // (tiles past the batch's last are clamped to it: their slots are never read, and
+            // a batch of one or three tiles has no tile pair to read)
+            const int q = (off - C::BSB_OFF) >> 10;
+            const int tt = min(tile0 + 2 * q, tile_end - 1), t2 = min(tile0 + 2 * q + (lane >> 5), tile_end - 1);
+            pbase[k] = ubase(act.q80 ? reinterpret_cast<const int8_t*>(act.q) : act.bsb + (long long)tt * nb * 512);
+            pstep[k] = act.q80 ? 0u : 512u;
+            pvo[k] = act.q80 ? 0u : (unsigned)((t2 - tt) * nb * 512 + (lane & 31) * 16);
+        } else {                                      // dT: 128 tokens x 4 B per row of dT
+            const int q = (off - C::DT_OFF) >> 10;    // Q8_0: rows 8sb + 2q, 8sb + 2q + 1
+            pbase[k] = ubase(act.dT + (long long)(act.q80 ? 2 * q : 0) * act.npad + tok0);
+            pstep[k] = (unsigned)(act.q80 ? 8 : 1) * act.npad * 4u;
+            const int tk = min(4 * (lane & 31), act.npad - 4 - tok0);
+            pvo[k] = (unsigned)(tk * 4 + (act.q80 ? (lane >> 5) * act.npad * 4 : 0));
+        }
+    }
     auto copy_stage = [&](int sb, int st) {
         char* base = smem + st * C::STAGE;
 #pragma unroll
         for (int k = 0; k < C::NIW; ++k) {
             int i = wv + C::NW * k;
-            if (i >= C::NI) i = C::NI - 1;            // a repeated piece: same bytes, same place
-            const int off = i * 1024;                 // byte offset of the piece in the stage
-            const uint8_t* ub;
-            unsigned vo;
-            if (off < C::A_OFF) {                     // weight slot r, bytes o.. within it
-                const int r = off / C::SLOT, o = off % C::SLOT;
-                const int rt = min(rb * RT + r, nrt - 1);
-                ub = ubase(P.A.sw + ((long long)rt * nb + sb) * TB + o);
-                vo = o + lane * 16 < TB ? lane * 16 : 0;   // past the tile: any valid bytes (padding)
-            } else if (off < C::BSB_OFF) {            // activation tile t, 1 KiB piece j
-                const int o = off - C::A_OFF, t = o >> 13, j = (o >> 10) & 7;
-                const int tt = min(tb * 4 + t, act.npad / 32 - 1);
-                ub = ubase(act.q + ((long long)tt * nb + sb) * 8192 + j * 1024);
-                vo = lane * 16;
-            } else if (off < C::DT_OFF) {             // bsb of tiles 2q, 2q+1 (512 B each)
-                const int q = (off - C::BSB_OFF) >> 10;
-                const int tt = min(tb * 4 + 2 * q, act.npad / 32 - 2);
-                ub = ubase(act.q80 ? reinterpret_cast<const int8_t*>(act.q) : act.bsb + ((long long)tt * nb + sb) * 512);
-                vo = act.q80 ? 0u : (unsigned)((lane >> 5) * nb * 512 + (lane & 31) * 16);
-            } else {                                  // dT: 128 tokens x 4 B per row of dT
-                const int q = (off - C::DT_OFF) >> 10;    // Q8_0: rows 8sb + 2q, 8sb + 2q + 1
-                const int dtrow = act.q80 ? 8 * sb + 2 * q : sb;
-                ub = ubase(act.dT + (long long)dtrow * act.npad + tok0);
-                const int tk = min(4 * (lane & 31), act.npad - 4 - tok0);
-                vo = (unsigned)(tk * 4 + (act.q80 ? (lane >> 5) * act.npad * 4 : 0));
-            }
-            __builtin_amdgcn_global_load_lds(gp(ub + vo), (__attribute__((address_space(3))) void*)(base + off), 16, 0, 0);
+            if (i >= C::NI) i = C::NI - 1;
+            // (written as one offset: `ub + pvo[k]` here drops the kernel's host stub, hipcc 7.2)
+            const uint8_t* ub = pbase[k] + (size_t)((unsigned long long)sb * pstep[k] + pvo[k]);
+            __builtin_amdgcn_global_load_lds(gp(ub), (__attribute__((address_space(3))) void*)(base + i * 1024), 16, 0, 0);
         }
     };
 
@@ -612,19 +666,20 @@ __global__ __launch_bounds__(64 * M2<T>::NW) void mmq2_t(const GemmParams P, con
     for (int e = 0; e < 16; ++e) y[0][e] = 0.0f;
 
     copy_stage(0, 0);
-    if (nb > 1) copy_stage(1, 1);
 #pragma unroll 1
     for (int sb = 0; sb < nb; ++sb) {
-        // this wave's copy of superblock sb landed (the next one's stays in flight), then the
-        // workgroup's (barrier); LDS-DMA is a pending LDS write on the VM counter
-        if (sb + 1 < nb) __builtin_amdgcn_s_waitcnt((C::NIW & 15) | ((C::NIW >> 4) << 14) | (0x7 << 4) | (0xF << 8));
-        else __builtin_amdgcn_s_waitcnt((0x7 << 4) | (0xF << 8));
+        // this wave's copy of superblock sb landed, then the workgroup's (barrier; LDS-DMA is a
+        // pending LDS write on the VM counter).  Past the barrier every wave is done with
+        // superblock sb - 1, whose stage takes the copy of sb + 1 (in flight during this step)
+        // and whose operand planes take this step's decode.
+        __builtin_amdgcn_s_waitcnt((0x7 << 4) | (0xF << 8));   // vmcnt(0)
         __builtin_amdgcn_s_barrier();
+        if (sb + 1 < nb) copy_stage(sb + 1, (sb + 1) & 1);
         const lchar* stg = (const lchar*)(smem + (sb & 1) * C::STAGE);
         const lchar* A0 = stg + C::A_OFF + w * 8192 + lane * 16;       // this wave's token tile
         const lchar* dTw = stg + C::DT_OFF + (w * 32 + 4 * h) * 4;
         if (T == T_Q8_0) {
-#pragma unroll
+#pragma unroll 2
             for (int j = 0; j < 8; ++j) {
                 const v4i a = lds_ld<v4i>(A0 + j * 1024);
                 {
@@ -646,41 +701,82 @@ __global__ __launch_bounds__(64 * M2<T>::NW) void mmq2_t(const GemmParams P, con
                 }
             }
         } else if (T == T_Q4_K || T == T_Q5_K) {
+            // (1) decode: the 4 waves of row tile wr turn its superblock into the int8 operand
+            //     planes of the scaled weights sc_j * q (sc = 8*sh + sl; Q5_K q = lo4 + 16*hb):
+            //       P0 = lo4 * sl, P1 = lo4 * sh (<= 105), Q5_K P2 = hb * sc (<= 63),
+            //     so  sc_j * q = P0 + 8 P1 + 16 P2  and the MFMAs accumulate the scaled sub-block
+            //     sums over all 8 sub-blocks exactly (no per-sub-block integer multiply per result);
+            //     wave w decodes piece w (sub-blocks 2w, 2w + 1) for every lane's row.
+            const lchar* wt = stg + wr * C::SLOT;
+            lchar* pl = (lchar*)(smem + 2 * C::STAGE) + wr * (NPL * 8 * 1024) + lane * 16;
+            {
+                const u32x4 hd = lds_ld<u32x4>(wt + (T == T_Q5_K ? 5120 : 4096) + col * 16);
+                const unsigned Y = hd.y, W = hd.w;
+                // get_scale_min_k4 for j = 2w, 2w + 1 (w is wave-uniform: a scalar branch)
+                int s0, s1;
+                if (w < 2) {
+                    s0 = (Y >> (16 * w)) & 63;
+                    s1 = (Y >> (16 * w + 8)) & 63;
+                } else {
+                    const int k = 2 * w - 4;
+                    s0 = ((W >> (8 * k)) & 0xF) | (((Y >> (8 * k + 6)) & 3) << 4);
+                    s1 = ((W >> (8 * k + 8)) & 0xF) | (((Y >> (8 * k + 14)) & 3) << 4);
+                }
+                const u32x4 wq = lds_ld<u32x4>(wt + w * 1024 + lane * 16);
+                const unsigned q[4] = {wq.x, wq.y, wq.z, wq.w};
+                u32x4 o0, o1, o2, o3;   // P0/P1 of sub-block 2w, P0/P1 of sub-block 2w + 1
+                unsigned* p0 = reinterpret_cast<unsigned*>(&o0);
+                unsigned* p1 = reinterpret_cast<unsigned*>(&o1);
+                unsigned* p2 = reinterpret_cast<unsigned*>(&o2);
+                unsigned* p3 = reinterpret_cast<unsigned*>(&o3);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const unsigned lo = q[i] & 0x0F0F0F0Fu, hi = (q[i] >> 4) & 0x0F0F0F0Fu;
+                    p0[i] = bmul(lo, s0 & 7);
+                    p1[i] = bmul(lo, s0 >> 3);
+                    p2[i] = bmul(hi, s1 & 7);
+                    p3[i] = bmul(hi, s1 >> 3);
+                }
+                *reinterpret_cast<__attribute__((address_space(3))) u32x4*>(pl + (0 * 8 + 2 * w) * 1024) = o0;
+                *reinterpret_cast<__attribute__((address_space(3))) u32x4*>(pl + (1 * 8 + 2 * w) * 1024) = o1;
+                *reinterpret_cast<__attribute__((address_space(3))) u32x4*>(pl + (0 * 8 + 2 * w + 1) * 1024) = o2;
+                *reinterpret_cast<__attribute__((address_space(3))) u32x4*>(pl + (1 * 8 + 2 * w + 1) * 1024) = o3;
+                if (T == T_Q5_K) {
+                    const u32x4 qh = lds_ld<u32x4>(wt + 4096 + lane * 16);
+                    const unsigned b[4] = {qh.x, qh.y, qh.z, qh.w};
+                    u32x4 h0, h1;
+                    unsigned* q0 = reinterpret_cast<unsigned*>(&h0);
+                    unsigned* q1 = reinterpret_cast<unsigned*>(&h1);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        q0[i] = bmul((b[i] >> (2 * w)) & 0x01010101u, s0);
+                        q1[i] = bmul((b[i] >> (2 * w + 1)) & 0x01010101u, s1);
+                    }
+                    *reinterpret_cast<__attribute__((address_space(3))) u32x4*>(pl + (2 * 8 + 2 * w) * 1024) = h0;
+                    *reinterpret_cast<__attribute__((address_space(3))) u32x4*>(pl + (2 * 8 + 2 * w + 1) * 1024) = h1;
+                }
+            }
+            __builtin_amdgcn_s_waitcnt((0xF) | (0x3 << 14) | (0x7 << 4));   // lgkmcnt(0): planes written
+            __builtin_amdgcn_s_barrier();
+            // (2) the MFMAs: token tile w x row tile wr, the planes accumulated over the sub-blocks
             {
                 constexpr int r = 0;
-                const lchar* wt = stg + wr * C::SLOT;
                 const u32x4 hd = lds_ld<u32x4>(wt + (T == T_Q5_K ? 5120 : 4096) + col * 16);
-                const u32x4 qh = T == T_Q5_K ? lds_ld<u32x4>(wt + 4096 + lane * 16) : u32x4{0u, 0u, 0u, 0u};
-                int sc[8], mn[8];
-                q4k_scales(hd, sc, mn);
-                int S[16];
+                v16i acc0 = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, acc1 = acc0, acc2 = acc0;
+                const lchar* plr = (const lchar*)pl;
 #pragma unroll
-                for (int e = 0; e < 16; ++e) S[e] = 0;
-#pragma unroll
-                for (int p = 0; p < 4; ++p) {
-                    const u32x4 wq = lds_ld<u32x4>(wt + p * 1024 + lane * 16);
-                    const unsigned sl = 2 * p, sh = 2 * p + 1;
-                    const v4i blo = v4i{(int)((wq.x & 0x0F0F0F0Fu) | (((qh.x >> sl) & 0x01010101u) << 4)),
-                                        (int)((wq.y & 0x0F0F0F0Fu) | (((qh.y >> sl) & 0x01010101u) << 4)),
-                                        (int)((wq.z & 0x0F0F0F0Fu) | (((qh.z >> sl) & 0x01010101u) << 4)),
-                                        (int)((wq.w & 0x0F0F0F0Fu) | (((qh.w >> sl) & 0x01010101u) << 4))};
-                    const v4i bhi = v4i{(int)(((wq.x >> 4) & 0x0F0F0F0Fu) | (((qh.x >> sh) & 0x01010101u) << 4)),
-                                        (int)(((wq.y >> 4) & 0x0F0F0F0Fu) | (((qh.y >> sh) & 0x01010101u) << 4)),
-                                        (int)(((wq.z >> 4) & 0x0F0F0F0Fu) | (((qh.z >> sh) & 0x01010101u) << 4)),
-                                        (int)(((wq.w >> 4) & 0x0F0F0F0Fu) | (((qh.w >> sh) & 0x01010101u) << 4))};
-                    const v16i d0 = mfma(lds_ld<v4i>(A0 + (2 * p) * 1024), blo);
-#pragma unroll
-                    for (int e = 0; e < 16; ++e) S[e] = __mul24(sc[2 * p], d0[e]) + S[e];
-                    const v16i d1 = mfma(lds_ld<v4i>(A0 + (2 * p + 1) * 1024), bhi);
-#pragma unroll
-                    for (int e = 0; e < 16; ++e) S[e] = __mul24(sc[2 * p + 1], d1[e]) + S[e];
-                    // keep the scheduler from hoisting every sub-block's MFMA ahead of its
-                    // scaling (16 accumulator registers each: the registers run out)
-                    asm volatile("" ::: "memory");   // no LDS load hoisted across sub-blocks
+                for (int j = 0; j < 8; ++j) {
+                    const v4i a = lds_ld<v4i>(A0 + j * 1024);
+                    acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, lds_ld<v4i>(plr + (0 * 8 + j) * 1024), acc0, 0, 0, 0);
+                    acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, lds_ld<v4i>(plr + (1 * 8 + j) * 1024), acc1, 0, 0, 0);
+                    if (T == T_Q5_K)
+                        acc2 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, lds_ld<v4i>(plr + (2 * 8 + j) * 1024), acc2, 0, 0, 0);
                 }
                 // sum_j m_j*bsum_j: mins as int8 B operands, k 0-7 (against hi) / k 8-15 (against lo)
-                const int m03 = mn[0] | (mn[1] << 8) | (mn[2] << 16) | (mn[3] << 24);
-                const int m47 = mn[4] | (mn[5] << 8) | (mn[6] << 16) | (mn[7] << 24);
+                const unsigned Y = hd.y, Z = hd.z, W = hd.w;
+                const int m03 = (int)(Z & 0x3F3F3F3Fu);
+                const int m47 = (int)(((W >> 4) & 0x0F0F0F0Fu) | ((Z >> 2) & 0x30303030u));
+                (void)Y;
                 const v4i bm1 = h == 0 ? v4i{m03, m47, 0, 0} : v4i{0, 0, 0, 0};
                 const v4i bm2 = h == 0 ? v4i{0, 0, m03, m47} : v4i{0, 0, 0, 0};
                 const v4i ab = h == 0 ? lds_ld<v4i>(stg + C::BSB_OFF + w * 512 + col * 16) : v4i{0, 0, 0, 0};
@@ -694,8 +790,9 @@ __global__ __launch_bounds__(64 * M2<T>::NW) void mmq2_t(const GemmParams P, con
 #pragma unroll
                     for (int i = 0; i < 4; ++i) {
                         const int e = 4 * g + i;
+                        const int S = acc0[e] + 8 * acc1[e] + (T == T_Q5_K ? 16 * acc2[e] : 0);
                         const float d = dr * dx[i], dm = dmr * dx[i];
-                        y[r][e] = fmaf(-dm, (float)(64 * x1[e] + x2[e]), fmaf(d, (float)S[e], y[r][e]));
+                        y[r][e] = fmaf(-dm, (float)(64 * x1[e] + x2[e]), fmaf(d, (float)S, y[r][e]));
                     }
                 }
             }
@@ -725,19 +822,18 @@ __global__ __launch_bounds__(64 * M2<T>::NW) void mmq2_t(const GemmParams P, con
                 }
             }
         }
-        // every wave is done with stage sb % 2: refill it with superblock sb + 2
         __builtin_amdgcn_s_waitcnt((0xF) | (0x3 << 14) | (0x7 << 4));   // lgkmcnt(0): this wave's LDS reads done
-        __builtin_amdgcn_s_barrier();
-        if (sb + 2 < nb) copy_stage(sb + 2, sb & 1);
     }
-    // ---- epilogue: token tile w, row tile rb*RT + wr
+    // ---- epilogue: token tile w, row tile rb*RT + wr (no LDS: the next block's copy may start)
     const int rt = rb * RT + wr;
-    if (w >= ntt || rt >= nrt) return;
-    const int row = AB ? rt * 16 + (col & 15) : rt * 32 + col;
-    mmq_epilogue<AB>(P, act.ntok, rope, tok0 + 32 * w, lane, row, y[0]);
+    if (w < ntt && rt < nrt) {
+        const int row = AB ? rt * 16 + (col & 15) : rt * 32 + col;
+        mmq_epilogue<AB>(P, tend, rope, tok0 + 32 * w, lane, row, y[0]);
+    }
+  }
 }
 
-template <int T> constexpr int m2_lds() { return 2 * M2<T>::STAGE; }
+template <int T> constexpr int m2_lds() { return M2<T>::LDS; }
 
 }  // namespace mmq
 
@@ -808,14 +904,16 @@ void launch_mmq32(const GemmParams& p, const ActQ8& act, const float2* rope, hip
     else if (var == 2) MMQ_PICK(1, 3);
     else MMQ_PICK(4, 2);
 #undef MMQ_PICK
-    if (!p.grp && var == 1 && getenv("MI_MMQ_OLD") == nullptr) {
+    static const bool old_env = getenv("MI_MMQ_OLD") != nullptr;
+    if (var == 1 && !old_env) {
         // mmq2: 128-token x 32*RT-column blocks, LDS-DMA staged two superblocks deep
         const int T = p.A.type;
         const int RT = mmq::M2<T_Q4_K>::RT;
         const int NWv = 4 * RT;
         const int nrb = (nrt + RT - 1) / RT;
         const int ntb = (act.npad + 127) / 128;
-        const int g2 = (nrb + 7) / 8 * 8 * ntb;
+        // grouped (MoE): a workgroup per (expert, row block), each over its expert's token blocks
+        const int g2 = (nrb + 7) / 8 * 8 * (p.grp ? p.grp_n : ntb);
         decltype(&mmq::mmq2_t<T_Q4_K, false>) f2;
         int lds;
         switch (T) {

@@ -13,7 +13,7 @@ ok() {  # continue only on 0 (pass) or 1 (pytest test failures)
   if [ "$rc" -ne 0 ] && [ "$rc" -ne 1 ]; then echo "stopping after $what"; exit "$rc"; fi
 }
 if [ -z "$SKIP_TESTS" ]; then
-  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+  timeout -k 10 ${PYTEST_LIMIT:-900} python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
       > $OUT/pytest_gpu.log 2>&1
   ok $? pytest
   tail -3 $OUT/pytest_gpu.log

@@ -137,6 +137,9 @@ def test_mmq32_rows_not_multiple_of_tile(gpu_lib):
     """Row counts that leave a partial 32-row (pair: 16-row) tile."""
     _check_gemm(R.Q4_K, 1000, 2048, 40, False, seed=7)
     _check_gemm(R.Q4_K, 1000, 2048, 40, True, seed=8)
+    _check_gemm(R.Q4_K, 1000, 2048, 5, True, seed=11)       # one token tile
+    _check_gemm(R.Q4_K, 1000, 2048, 70, False, seed=12)     # three token tiles (no tile pair for the last)
+    _check_gemm(R.Q5_K, 77, 1024, 200, True, seed=13)       # a second 128-token block of two tiles
     _check_gemm(R.Q6_K, 77, 1024, 5, False, seed=9)
     _check_gemm(R.Q5_K, 77, 1024, 5, True, seed=10)
 

@@ -19,7 +19,7 @@ import ggml_cpu
 import ggml_ref as R
 from blama_amd import engine, synthetic
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.timeout(600)]   # the 32-layer oracle: ~1 min per model
 
 MODELS = ["llama2-7b-q4_k_m", "llama3-8b-q6_k"]
 
