@@ -72,11 +72,36 @@ __global__ __launch_bounds__(64 * NW) void attn_mfma_kernel(const AttnParams P, 
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int col = lane & 31, h = lane >> 5;
-    const int t0 = blockIdx.y * 32;                 // the token tile
+    // the token tile: the last (longest causal extent) first, so that the short tiles fill in
+    // behind the long ones (one workgroup per CU at 8 waves x ~250 VGPRs)
+    const int t0 = (gridDim.y - 1 - blockIdx.y) * 32;
     const int tok = t0 + col;                       // this lane's query token (D column)
     const bool tv = tok < ntok;
     const int qcell = tv ? P.tokpos[tok * 4 + 2] : -1;
     const int qpos = tv ? P.tokpos[tok * 4 + 1] : 0;
+    const __half* kbase = P.kcache + (long long)g * HD;
+    const __half* vbase = P.vcache + (long long)g * HD;
+    auto kload = [&](int c, u32x4 (&kf)[KS], i32x4 (&cp)[4]) {
+        const int c0 = c * CH;
+        const int cr = min(c0 + col, P.n_ctx - 1);  // the A operand row this lane supplies
+#pragma unroll
+        for (int s = 0; s < KS; ++s) kf[s] = *reinterpret_cast<const u32x4*>(kbase + (long long)cr * P.kv_dim + 16 * s + 8 * h);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int cb = c0 + 8 * q + 4 * h;
+            if (cb + 3 < P.n_ctx) {
+                cp[q] = *reinterpret_cast<const i32x4*>(P.cell_pos + cb);
+            } else {   // the cache's last cells (cells past n_ctx are masked by cell <= qcell)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) cp[q][e] = P.cell_pos[min(cb + e, P.n_ctx - 1)];
+            }
+        }
+    };
+    // the wave's first chunk (w) is loaded at entry, before the tile's extent is known: a chunk
+    // past it is unused
+    u32x4 kf0[KS];
+    i32x4 cp0[4];
+    kload(w, kf0, cp0);
     // the tile's last cell (its last valid token's): the causal end of every token in it
     const int wlast = __builtin_amdgcn_readfirstlane(P.tokpos[(min(ntok, t0 + 32) - 1) * 4 + 2]);
     const int nch = wlast / CH + 1;                 // chunks of the tile
@@ -96,26 +121,10 @@ __global__ __launch_bounds__(64 * NW) void attn_mfma_kernel(const AttnParams P, 
                        : u32x4{0u, 0u, 0u, 0u};
         }
     }
-    const __half* kbase = P.kcache + (long long)g * HD;
-    const __half* vbase = P.vcache + (long long)g * HD;
-    // scores of chunk c into st: masked, scaled w (lane = token, register r = cell (r&3)+8(r>>2)+4h)
-    auto scores = [&](int c, f16x16& st) {
+    // scores of chunk c into st: masked, scaled w (lane = token, register r = cell (r&3)+8(r>>2)+4h);
+    // kload (above) issues the chunk's K rows and cell positions, kcompute runs the MFMAs and the mask
+    auto kcompute = [&](int c, const u32x4 (&kf)[KS], const i32x4 (&cp)[4], f16x16& st) {
         const int c0 = c * CH;
-        const int cr = min(c0 + col, P.n_ctx - 1);  // the A operand row this lane supplies
-        u32x4 kf[KS];
-#pragma unroll
-        for (int s = 0; s < KS; ++s) kf[s] = *reinterpret_cast<const u32x4*>(kbase + (long long)cr * P.kv_dim + 16 * s + 8 * h);
-        i32x4 cp[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int cb = c0 + 8 * q + 4 * h;
-            if (cb + 3 < P.n_ctx) {
-                cp[q] = *reinterpret_cast<const i32x4*>(P.cell_pos + cb);
-            } else {   // the cache's last cells (cells past n_ctx are masked by cell <= qcell)
-#pragma unroll
-                for (int e = 0; e < 4; ++e) cp[q][e] = P.cell_pos[min(cb + e, P.n_ctx - 1)];
-            }
-        }
 #pragma unroll
         for (int r = 0; r < 16; ++r) st[r] = 0.0f;
 #pragma unroll
@@ -128,6 +137,12 @@ __global__ __launch_bounds__(64 * NW) void attn_mfma_kernel(const AttnParams P, 
             st[r] = ok ? st[r] * P.scale : -INFINITY;
         }
     };
+    auto scores = [&](int c, f16x16& st) {
+        u32x4 kf[KS];
+        i32x4 cp[4];
+        kload(c, kf, cp);
+        kcompute(c, kf, cp, st);
+    };
 
     // ---- pass 1: the token's max over every cell ------------------------------------------------
     f16x16 st[CPR];
@@ -137,7 +152,8 @@ __global__ __launch_bounds__(64 * NW) void attn_mfma_kernel(const AttnParams P, 
         for (int i = 0; i < CPR; ++i) {
             const int k = rd * CPR + i;
             if (k < myn) {
-                scores(w + NW * k, st[i]);
+                if (k == 0) kcompute(w, kf0, cp0, st[i]);   // (loaded at entry)
+                else scores(w + NW * k, st[i]);
 #pragma unroll
                 for (int r = 0; r < 16; ++r) mx = fmaxf(mx, st[i][r]);
             }
@@ -150,6 +166,21 @@ __global__ __launch_bounds__(64 * NW) void attn_mfma_kernel(const AttnParams P, 
 #pragma unroll
     for (int k = 1; k < NW; ++k) M = fmaxf(M, xmax[k][col]);
 
+    // V chunk c: piece i of this lane = row (lane + 64 i) / (HD/8), chunk (lane + 64 i) % (HD/8);
+    // rows past the tile's last cell are zero (p = 0 there, and 0 * stale bits could be NaN)
+    u32x4 vr[VPL];
+    auto vload = [&](int c) {
+#pragma unroll
+        for (int i = 0; i < VPL; ++i) {
+            const int pc = lane + 64 * i;
+            const int row = pc / (HD / 8), ch = pc % (HD / 8);
+            const int cell = c * CH + row;
+            const u32x4 z = {0u, 0u, 0u, 0u};
+            vr[i] = cell <= wlast ? *reinterpret_cast<const u32x4*>(vbase + (long long)min(cell, P.n_ctx - 1) * P.kv_dim + 8 * ch) : z;
+        }
+    };
+    if (myn > 0) vload(w);   // the first chunk's V in flight during pass 2
+
     // ---- pass 2: the sum of expf(w - M) in double, waves added in order ------------------------
     double sum = 0.0;
     for (int rd = 0; rd < nround; ++rd) {
@@ -159,7 +190,11 @@ __global__ __launch_bounds__(64 * NW) void attn_mfma_kernel(const AttnParams P, 
             if (k < myn) {
                 if (!keep) scores(w + NW * k, st[i]);
 #pragma unroll
-                for (int r = 0; r < 16; ++r) sum += (double)expf(st[i][r] - M);
+                for (int r = 0; r < 16; ++r) {
+                    const float e = expf(st[i][r] - M);
+                    sum += (double)e;
+                    if (keep) st[i][r] = e;   // kept for pass 3: one expf per score
+                }
             }
         }
     }
@@ -183,20 +218,6 @@ __global__ __launch_bounds__(64 * NW) void attn_mfma_kernel(const AttnParams P, 
 #pragma unroll
         for (int r = 0; r < 16; ++r) o[b][r] = 0.0f;
     char* const vw = vimg + w * VIMG;
-    // V chunk c: piece i of this lane = row (lane + 64 i) / (HD/8), chunk (lane + 64 i) % (HD/8);
-    // rows past the tile's last cell are zero (p = 0 there, and 0 * stale bits could be NaN)
-    u32x4 vr[VPL];
-    auto vload = [&](int c) {
-#pragma unroll
-        for (int i = 0; i < VPL; ++i) {
-            const int pc = lane + 64 * i;
-            const int row = pc / (HD / 8), ch = pc % (HD / 8);
-            const int cell = c * CH + row;
-            const u32x4 z = {0u, 0u, 0u, 0u};
-            vr[i] = cell <= wlast ? *reinterpret_cast<const u32x4*>(vbase + (long long)min(cell, P.n_ctx - 1) * P.kv_dim + 8 * ch) : z;
-        }
-    };
-    if (myn > 0) vload(w);
     for (int rd = 0; rd < nround; ++rd) {
 #pragma unroll
         for (int i = 0; i < CPR; ++i) {
@@ -218,7 +239,8 @@ __global__ __launch_bounds__(64 * NW) void attn_mfma_kernel(const AttnParams P, 
                 for (int s = 0; s < 2; ++s) {
                     float p[8];
 #pragma unroll
-                    for (int j = 0; j < 8; ++j) p[j] = tv ? expf(st[i][8 * s + j] - M) * inv : 0.0f;
+                    for (int j = 0; j < 8; ++j)
+                        p[j] = tv ? (keep ? st[i][8 * s + j] : expf(st[i][8 * s + j] - M)) * inv : 0.0f;
                     pf[s] = u32x4{pack2(p[0], p[1]), pack2(p[2], p[3]), pack2(p[4], p[5]), pack2(p[6], p[7])};
                 }
                 __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the V image is written
