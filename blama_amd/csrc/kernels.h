@@ -161,6 +161,7 @@ struct GemmParams {
     const int* grp;
     long long grp_stride;
     int grp_n;
+    int diag;   // mmq2 timing experiments only (MI_MMQ2_DIAG): 1 = no compute, 2 = no copies past the first
 };
 void launch_gemm(const GemmParams& p, hipStream_t s);
 

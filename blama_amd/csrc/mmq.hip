@@ -546,6 +546,10 @@ template <int T> struct M2 {
 };
 
 typedef __attribute__((address_space(3))) char lchar;
+// register pins: the value is materialised at this point of the (volatile) instruction stream,
+// so LDS reads issued before it stay in flight together instead of being sunk to their uses
+__device__ __forceinline__ void pin(v4i& x) { asm volatile("" : "+v"(x)); }
+__device__ __forceinline__ void pin_all() { asm volatile("" ::: "memory"); }
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 // the bytes of x times s, every byte product < 256 (no carry between bytes): v_pk_mul_lo_u16
 __device__ __forceinline__ unsigned bmul(unsigned x, unsigned s) {
@@ -674,7 +678,8 @@ __global__ __launch_bounds__(64 * M2<T>::NW) void mmq2_t(const GemmParams P, con
         // and whose operand planes take this step's decode.
         __builtin_amdgcn_s_waitcnt((0x7 << 4) | (0xF << 8));   // vmcnt(0)
         __builtin_amdgcn_s_barrier();
-        if (sb + 1 < nb) copy_stage(sb + 1, (sb + 1) & 1);
+        if (sb + 1 < nb && (P.diag != 2 || sb == 0)) copy_stage(sb + 1, (sb + 1) & 1);
+        if (P.diag == 1) continue;
         const lchar* stg = (const lchar*)(smem + (sb & 1) * C::STAGE);
         const lchar* A0 = stg + C::A_OFF + w * 8192 + lane * 16;       // this wave's token tile
         const lchar* dTw = stg + C::DT_OFF + (w * 32 + 4 * h) * 4;
@@ -764,14 +769,34 @@ __global__ __launch_bounds__(64 * M2<T>::NW) void mmq2_t(const GemmParams P, con
                 const u32x4 hd = lds_ld<u32x4>(wt + (T == T_Q5_K ? 5120 : 4096) + col * 16);
                 v16i acc0 = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, acc1 = acc0, acc2 = acc0;
                 const lchar* plr = (const lchar*)pl;
+                // every operand of the superblock read first (at 2 waves per SIMD the LDS latency
+                // is hidden only by reads in flight: counted waits, not lgkmcnt(0) per MFMA pair)
+                v4i av[8], b0[8], b1[8], b2[8];
+                auto ld = [&](int j) {
+                    av[j] = lds_ld<v4i>(A0 + j * 1024);
+                    b0[j] = lds_ld<v4i>(plr + (0 * 8 + j) * 1024);
+                    b1[j] = lds_ld<v4i>(plr + (1 * 8 + j) * 1024);
+                    if (T == T_Q5_K) b2[j] = lds_ld<v4i>(plr + (2 * 8 + j) * 1024);
+                };
+                auto mm = [&](int j) {
+                    pin(av[j]);
+                    pin(b0[j]);
+                    pin(b1[j]);
+                    acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(av[j], b0[j], acc0, 0, 0, 0);
+                    acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(av[j], b1[j], acc1, 0, 0, 0);
+                    if (T == T_Q5_K) {
+                        pin(b2[j]);
+                        acc2 = __builtin_amdgcn_mfma_i32_32x32x32_i8(av[j], b2[j], acc2, 0, 0, 0);
+                    }
+                };
+                // sub-blocks 0-3 read, then 4-7 read while 0-3 run
 #pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const v4i a = lds_ld<v4i>(A0 + j * 1024);
-                    acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, lds_ld<v4i>(plr + (0 * 8 + j) * 1024), acc0, 0, 0, 0);
-                    acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, lds_ld<v4i>(plr + (1 * 8 + j) * 1024), acc1, 0, 0, 0);
-                    if (T == T_Q5_K)
-                        acc2 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, lds_ld<v4i>(plr + (2 * 8 + j) * 1024), acc2, 0, 0, 0);
-                }
+                for (int j = 0; j < 4; ++j) ld(j);
+                pin_all();
+#pragma unroll
+                for (int j = 4; j < 8; ++j) ld(j);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) mm(j);
                 // sum_j m_j*bsum_j: mins as int8 B operands, k 0-7 (against hi) / k 8-15 (against lo)
                 const unsigned Y = hd.y, Z = hd.z, W = hd.w;
                 const int m03 = (int)(Z & 0x3F3F3F3Fu);
@@ -801,13 +826,20 @@ __global__ __launch_bounds__(64 * M2<T>::NW) void mmq2_t(const GemmParams P, con
                 constexpr int r = 0;
                 const lchar* wt = stg + wr * C::SLOT;
                 v16i ah = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, al = ah;
+                v4i av[8], bh[8], bl[8];   // operands read first (counted LDS waits)
 #pragma unroll
                 for (int sp = 0; sp < 8; ++sp) {
-                    const v4i a = lds_ld<v4i>(A0 + sp * 1024);
-                    const v4i bh = lds_ld<v4i>(wt + sp * 1024 + lane * 16);
-                    const v4i bl = lds_ld<v4i>(wt + 8192 + sp * 1024 + lane * 16);
-                    ah = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bh, ah, 0, 0, 0);
-                    al = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bl, al, 0, 0, 0);
+                    av[sp] = lds_ld<v4i>(A0 + sp * 1024);
+                    bh[sp] = lds_ld<v4i>(wt + sp * 1024 + lane * 16);
+                    bl[sp] = lds_ld<v4i>(wt + 8192 + sp * 1024 + lane * 16);
+                }
+#pragma unroll
+                for (int sp = 0; sp < 8; ++sp) {
+                    pin(av[sp]);
+                    pin(bh[sp]);
+                    pin(bl[sp]);
+                    ah = __builtin_amdgcn_mfma_i32_32x32x32_i8(av[sp], bh[sp], ah, 0, 0, 0);
+                    al = __builtin_amdgcn_mfma_i32_32x32x32_i8(av[sp], bl[sp], al, 0, 0, 0);
                 }
                 const float dr = h2f(lds_ld<unsigned short>(wt + 16384 + col * 2));
 #pragma unroll
@@ -928,7 +960,10 @@ void launch_mmq32(const GemmParams& p, const ActQ8& act, const float2* rope, hip
             MI_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(f2), hipFuncAttributeMaxDynamicSharedMemorySize, lds));
             attr_done[ti][ab] = true;
         }
-        hipLaunchKernelGGL(f2, dim3(g2), dim3(64 * NWv), (size_t)lds, s, p, act, rope);
+        static const int diag = getenv("MI_MMQ2_DIAG") ? atoi(getenv("MI_MMQ2_DIAG")) : 0;
+        GemmParams p2 = p;
+        p2.diag = diag;
+        hipLaunchKernelGGL(f2, dim3(g2), dim3(64 * NWv), (size_t)lds, s, p2, act, rope);
         MI_HIP(hipGetLastError());
         return;
     }
