@@ -11,3 +11,4 @@ for cfg in llama2-7b-q4_k_m llama3-8b-q6_k; do
   timeout -k 10 300 python -u bench.py --no-cpu --prefill 0 --verify 0 --steps 64 --warmup 4 --config $cfg --prompt 3968 > $OUT/lc_$cfg.json 2> $OUT/lc_$cfg.err || { tail $OUT/lc_$cfg.err; exit 1; }
   python3 -c "import json;d=json.load(open('$OUT/lc_$cfg.json'));print('$cfg','3968 cells decode',d['value'])" | tee -a $OUT/summary.txt
 done
+# (the 3968-token prompt's kernel trace: scripts/lc_trace.sh, eager launches)
