@@ -542,7 +542,7 @@ template <int T> struct M2 {
     static constexpr int NIW = (NI + NW - 1) / NW;                      // per wave (some repeat)
     static constexpr int NPL = T == T_Q5_K ? 3 : 2;                     // K-quant operand planes
     static constexpr int PLANES = (T == T_Q4_K || T == T_Q5_K) ? RT * NPL * 8 * 1024 : 0;
-    static constexpr int LDS = 2 * STAGE + PLANES;
+    static constexpr int lds(int nst) { return nst * STAGE + PLANES; }
 };
 
 typedef __attribute__((address_space(3))) char lchar;
@@ -563,8 +563,11 @@ __device__ __forceinline__ unsigned bmul(unsigned x, unsigned s) {
 template <typename V>
 __device__ __forceinline__ V lds_ld(const lchar* p) { return *reinterpret_cast<const __attribute__((address_space(3))) V*>(p); }
 
-template <int T, bool AB>
-__global__ __launch_bounds__(64 * M2<T>::NW) void mmq2_t(const GemmParams P, const ActQ8 act, const float2* rope) {
+// NST 2: two stages (copy of sb + 1 during sb), one workgroup per CU.  NST 1: one stage, copy and
+// compute in turn, sized (LDS, <= 128 VGPRs) for two workgroups per CU that overlap each other.
+template <int T, bool AB, int NST>
+__global__ __launch_bounds__(64 * M2<T>::NW) __attribute__((amdgpu_waves_per_eu(NST == 1 ? 4 : 2)))
+void mmq2_t(const GemmParams P, const ActQ8 act, const float2* rope) {
     using C = M2<T>;
     constexpr int RT = C::RT;
     constexpr int NPL = C::NPL;
@@ -678,9 +681,9 @@ __global__ __launch_bounds__(64 * M2<T>::NW) void mmq2_t(const GemmParams P, con
         // and whose operand planes take this step's decode.
         __builtin_amdgcn_s_waitcnt((0x7 << 4) | (0xF << 8));   // vmcnt(0)
         __builtin_amdgcn_s_barrier();
-        if (sb + 1 < nb && (P.diag != 2 || sb == 0)) copy_stage(sb + 1, (sb + 1) & 1);
+        if (NST == 2 && sb + 1 < nb && (P.diag != 2 || sb == 0)) copy_stage(sb + 1, (sb + 1) & 1);
         if (P.diag == 1) continue;
-        const lchar* stg = (const lchar*)(smem + (sb & 1) * C::STAGE);
+        const lchar* stg = (const lchar*)(smem + (NST == 2 ? (sb & 1) : 0) * C::STAGE);
         const lchar* A0 = stg + C::A_OFF + w * 8192 + lane * 16;       // this wave's token tile
         const lchar* dTw = stg + C::DT_OFF + (w * 32 + 4 * h) * 4;
         if (T == T_Q8_0) {
@@ -713,7 +716,7 @@ __global__ __launch_bounds__(64 * M2<T>::NW) void mmq2_t(const GemmParams P, con
             //     sums over all 8 sub-blocks exactly (no per-sub-block integer multiply per result);
             //     wave w decodes piece w (sub-blocks 2w, 2w + 1) for every lane's row.
             const lchar* wt = stg + wr * C::SLOT;
-            lchar* pl = (lchar*)(smem + 2 * C::STAGE) + wr * (NPL * 8 * 1024) + lane * 16;
+            lchar* pl = (lchar*)(smem + NST * C::STAGE) + wr * (NPL * 8 * 1024) + lane * 16;
             {
                 const u32x4 hd = lds_ld<u32x4>(wt + (T == T_Q5_K ? 5120 : 4096) + col * 16);
                 const unsigned Y = hd.y, W = hd.w;
@@ -779,20 +782,22 @@ __global__ __launch_bounds__(64 * M2<T>::NW) void mmq2_t(const GemmParams P, con
                     if (T == T_Q5_K) b2[j] = lds_ld<v4i>(plr + (2 * 8 + j) * 1024);
                 };
                 auto mm = [&](int j) {
-                    pin(av[j]);
-                    pin(b0[j]);
-                    pin(b1[j]);
+                    if (NST == 2) {
+                        pin(av[j]);
+                        pin(b0[j]);
+                        pin(b1[j]);
+                    }
                     acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(av[j], b0[j], acc0, 0, 0, 0);
                     acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(av[j], b1[j], acc1, 0, 0, 0);
                     if (T == T_Q5_K) {
-                        pin(b2[j]);
+                        if (NST == 2) pin(b2[j]);
                         acc2 = __builtin_amdgcn_mfma_i32_32x32x32_i8(av[j], b2[j], acc2, 0, 0, 0);
                     }
                 };
                 // sub-blocks 0-3 read, then 4-7 read while 0-3 run
 #pragma unroll
                 for (int j = 0; j < 4; ++j) ld(j);
-                pin_all();
+                if (NST == 2) pin_all();
 #pragma unroll
                 for (int j = 4; j < 8; ++j) ld(j);
 #pragma unroll
@@ -835,9 +840,11 @@ __global__ __launch_bounds__(64 * M2<T>::NW) void mmq2_t(const GemmParams P, con
                 }
 #pragma unroll
                 for (int sp = 0; sp < 8; ++sp) {
-                    pin(av[sp]);
-                    pin(bh[sp]);
-                    pin(bl[sp]);
+                    if (NST == 2) {
+                        pin(av[sp]);
+                        pin(bh[sp]);
+                        pin(bl[sp]);
+                    }
                     ah = __builtin_amdgcn_mfma_i32_32x32x32_i8(av[sp], bh[sp], ah, 0, 0, 0);
                     al = __builtin_amdgcn_mfma_i32_32x32x32_i8(av[sp], bl[sp], al, 0, 0, 0);
                 }
@@ -855,6 +862,10 @@ __global__ __launch_bounds__(64 * M2<T>::NW) void mmq2_t(const GemmParams P, con
             }
         }
         __builtin_amdgcn_s_waitcnt((0xF) | (0x3 << 14) | (0x7 << 4));   // lgkmcnt(0): this wave's LDS reads done
+        if (NST == 1 && sb + 1 < nb) {   // the one stage is free once every wave is past it
+            __builtin_amdgcn_s_barrier();
+            copy_stage(sb + 1, 0);
+        }
     }
     // ---- epilogue: token tile w, row tile rb*RT + wr (no LDS: the next block's copy may start)
     const int rt = rb * RT + wr;
@@ -865,7 +876,7 @@ __global__ __launch_bounds__(64 * M2<T>::NW) void mmq2_t(const GemmParams P, con
   }
 }
 
-template <int T> constexpr int m2_lds() { return M2<T>::LDS; }
+template <int T, int NST> constexpr int m2_lds() { return M2<T>::lds(NST); }
 
 }  // namespace mmq
 
@@ -946,19 +957,35 @@ void launch_mmq32(const GemmParams& p, const ActQ8& act, const float2* rope, hip
         const int ntb = (act.npad + 127) / 128;
         // grouped (MoE): a workgroup per (expert, row block), each over its expert's token blocks
         const int g2 = (nrb + 7) / 8 * 8 * (p.grp ? p.grp_n : ntb);
-        decltype(&mmq::mmq2_t<T_Q4_K, false>) f2;
-        int lds;
-        switch (T) {
-        case T_Q4_K: f2 = ab ? mmq::mmq2_t<T_Q4_K, true> : mmq::mmq2_t<T_Q4_K, false>; lds = mmq::m2_lds<T_Q4_K>(); break;
-        case T_Q5_K: f2 = ab ? mmq::mmq2_t<T_Q5_K, true> : mmq::mmq2_t<T_Q5_K, false>; lds = mmq::m2_lds<T_Q5_K>(); break;
-        case T_Q6_K: f2 = ab ? mmq::mmq2_t<T_Q6_K, true> : mmq::mmq2_t<T_Q6_K, false>; lds = mmq::m2_lds<T_Q6_K>(); break;
-        default: f2 = ab ? mmq::mmq2_t<T_Q8_0, true> : mmq::mmq2_t<T_Q8_0, false>; lds = mmq::m2_lds<T_Q8_0>(); break;
+        // MI_MMQ2_NST: 1 = one stage, two workgroups per CU; 2 = two stages, one workgroup per CU;
+        // 0 (default) = one stage when the grid fills two workgroups per CU, else two.  7B 512-token
+        // prefill, NST 1 vs 2: 15.5 vs 16.8 ms (same box, scripts/ab_prefill.sh)
+        static const int nst_req = getenv("MI_MMQ2_NST") ? atoi(getenv("MI_MMQ2_NST")) : 0;
+        static int n_cu = 0;
+        if (!n_cu) {
+            int dev = 0;
+            MI_HIP(hipGetDevice(&dev));
+            MI_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
         }
-        static bool attr_done[4][2] = {};
+        const int nst_env = nst_req ? nst_req : (g2 >= 2 * n_cu ? 1 : 2);
+        decltype(&mmq::mmq2_t<T_Q4_K, false, 2>) f2;
+        int lds;
+#define M2_PICK(NST_)                                                                                           \
+        switch (T) {                                                                                            \
+        case T_Q4_K: f2 = ab ? mmq::mmq2_t<T_Q4_K, true, NST_> : mmq::mmq2_t<T_Q4_K, false, NST_>; lds = mmq::m2_lds<T_Q4_K, NST_>(); break; \
+        case T_Q5_K: f2 = ab ? mmq::mmq2_t<T_Q5_K, true, NST_> : mmq::mmq2_t<T_Q5_K, false, NST_>; lds = mmq::m2_lds<T_Q5_K, NST_>(); break; \
+        case T_Q6_K: f2 = ab ? mmq::mmq2_t<T_Q6_K, true, NST_> : mmq::mmq2_t<T_Q6_K, false, NST_>; lds = mmq::m2_lds<T_Q6_K, NST_>(); break; \
+        default: f2 = ab ? mmq::mmq2_t<T_Q8_0, true, NST_> : mmq::mmq2_t<T_Q8_0, false, NST_>; lds = mmq::m2_lds<T_Q8_0, NST_>(); break; \
+        }
+        const int nst = T == T_Q5_K ? 2 : nst_env;   // (Q5_K: 3 planes do not fit two workgroups per CU)
+        if (nst == 1) { M2_PICK(1) } else { M2_PICK(2) }
+#undef M2_PICK
+        static bool attr_done[2][4][2] = {};
         const int ti = T == T_Q4_K ? 0 : T == T_Q5_K ? 1 : T == T_Q6_K ? 2 : 3;
-        if (!attr_done[ti][ab]) {
+        const int ni = nst == 1 ? 0 : 1;
+        if (!attr_done[ni][ti][ab]) {
             MI_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(f2), hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-            attr_done[ti][ab] = true;
+            attr_done[ni][ti][ab] = true;
         }
         static const int diag = getenv("MI_MMQ2_DIAG") ? atoi(getenv("MI_MMQ2_DIAG")) : 0;
         GemmParams p2 = p;
