@@ -20,11 +20,8 @@
 //   B operand of k-step s, k-permuted), V^T comes from the wave's V chunk staged row-major in
 //   LDS (XOR-swizzled 256-B rows) and read with ds_read_b64_tr_b16.  The 8 waves' O^T
 //   partials are added in a fixed tree order through LDS.
-// Up to 8 * CPR chunks (CPR per wave; 512 cells) the scores are computed once and kept in
-// registers over the three softmax passes.  Past that they are computed twice (pass 1: the max;
-// pass 2: the double sum and O^T = sum f16(e) v, e = expf(w - max), then O^T * (1/sum)): the
-// only departure from the CPU's rounding is that p is rounded to f16 before the 1/sum scale
-// instead of after it (one f16 rounding of a value in (0, 1] either way).
+// Up to 8 * CPR chunks (CPR per wave) the scores are computed once and kept in registers over
+// the three softmax passes; past that the passes recompute them, CPR chunks at a time.
 #include "kernels.h"
 #include <hip/hip_runtime.h>
 
@@ -110,10 +107,7 @@ __global__ __launch_bounds__(64 * NW) void attn_mfma_kernel(const AttnParams P, 
     const int nch = wlast / CH + 1;                 // chunks of the tile
     const int myn = nch > w ? (nch - w + NW - 1) / NW : 0;   // this wave's chunks: w, w+8, ...
     const int nround = (myn + CPR - 1) / CPR;
-    // the tile's chunks fit the waves' registers (<= CPR each): scores computed once and kept, the
-    // exact three passes; otherwise (workgroup-uniform) two passes: the max, then the sum and
-    // O^T = sum f16(e) v with e = expf(w - M), scaled by 1/sum at the end
-    const bool keep = nch <= NW * CPR;
+    const bool keep = nround <= 1;                  // scores computed once, kept in registers
 
     // Q^T fragments (B operand): lane (token col, half h), k-step s: q[tok][16s + 8h .. +7] as f16
     u32x4 qf[KS];
@@ -189,33 +183,33 @@ __global__ __launch_bounds__(64 * NW) void attn_mfma_kernel(const AttnParams P, 
 
     // ---- pass 2: the sum of expf(w - M) in double, waves added in order ------------------------
     double sum = 0.0;
-    auto finish_sum = [&]() {
-        const long long b = __double_as_longlong(sum);
-        const int lo = __shfl_xor((int)b, 32, 64), hi = __shfl_xor((int)(b >> 32), 32, 64);
-        const double other = __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-        const double both = h == 0 ? sum + other : other + sum;   // same order in both halves
-        if (h == 0) xsum[w][col] = both;
-        __syncthreads();
-        double tot = 0.0;
-#pragma unroll
-        for (int k = 0; k < NW; ++k) tot += xsum[k][col];
-        return (float)(1.0 / tot);
-    };
-    float inv = 0.0f;
-    if (keep) {
+    for (int rd = 0; rd < nround; ++rd) {
 #pragma unroll
         for (int i = 0; i < CPR; ++i) {
-            if (i < myn) {
+            const int k = rd * CPR + i;
+            if (k < myn) {
+                if (!keep) scores(w + NW * k, st[i]);
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     const float e = expf(st[i][r] - M);
                     sum += (double)e;
-                    st[i][r] = e;   // kept for pass 3: one expf per score
+                    if (keep) st[i][r] = e;   // kept for pass 3: one expf per score
                 }
             }
         }
-        inv = finish_sum();
     }
+    {
+        const long long b = __double_as_longlong(sum);
+        const int lo = __shfl_xor((int)b, 32, 64), hi = __shfl_xor((int)(b >> 32), 32, 64);
+        const double other = __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+        sum = h == 0 ? sum + other : other + sum;   // same order in both halves
+    }
+    if (h == 0) xsum[w][col] = sum;
+    __syncthreads();
+    double tot = 0.0;
+#pragma unroll
+    for (int k = 0; k < NW; ++k) tot += xsum[k][col];
+    const float inv = (float)(1.0 / tot);
 
     // ---- pass 3: O^T += V^T P^T over the wave's chunks --------------------------------------------
     f16x16 o[HB];
@@ -239,21 +233,14 @@ __global__ __launch_bounds__(64 * NW) void attn_mfma_kernel(const AttnParams P, 
                     *reinterpret_cast<u32x4*>(vw + vimg_off<HD>(pc / (HD / 8), pc % (HD / 8))) = vr[j];
                 }
                 if (k + 1 < myn) vload(c + NW);     // the next chunk's V in flight during this one
-                // p = f16(expf(w - M) * inv) (kept scores) or f16(expf(w - M)) with the sum taken
-                // here: the B operand of k-steps 0 (registers 0-7), 1 (8-15)
+                // p = f16(expf(w - M) * inv): the B operand of k-steps 0 (registers 0-7), 1 (8-15)
                 u32x4 pf[2];
 #pragma unroll
                 for (int s = 0; s < 2; ++s) {
                     float p[8];
 #pragma unroll
-                    for (int j = 0; j < 8; ++j) {
-                        float e = st[i][8 * s + j];
-                        if (!keep) {
-                            e = expf(e - M);
-                            sum += (double)e;
-                        }
-                        p[j] = tv ? (keep ? e * inv : e) : 0.0f;
-                    }
+                    for (int j = 0; j < 8; ++j)
+                        p[j] = tv ? (keep ? st[i][8 * s + j] : expf(st[i][8 * s + j] - M)) * inv : 0.0f;
                     pf[s] = u32x4{pack2(p[0], p[1]), pack2(p[2], p[3]), pack2(p[4], p[5]), pack2(p[6], p[7])};
                 }
                 __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the V image is written
@@ -279,14 +266,6 @@ __global__ __launch_bounds__(64 * NW) void attn_mfma_kernel(const AttnParams P, 
                 }
             }
         }
-    }
-
-    if (!keep) {   // the sum is complete: O^T = (sum f16(e) v) / sum
-        inv = finish_sum();
-#pragma unroll
-        for (int b = 0; b < HB; ++b)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) o[b][r] *= inv;
     }
 
     // ---- the waves' partials, added in a fixed tree: ((0+4)+(2+6)) + ((1+5)+(3+7)) ----------------
