@@ -21,7 +21,10 @@
 //   LDS (XOR-swizzled 256-B rows) and read with ds_read_b64_tr_b16.  The 8 waves' O^T
 //   partials are added in a fixed tree order through LDS.
 // Up to 8 * CPR chunks (CPR per wave) the scores are computed once and kept in registers over
-// the three softmax passes; past that the passes recompute them, CPR chunks at a time.
+// the three softmax passes.  Past that a wave computes them twice, CPR chunks at a time: pass 1
+// takes the max and, against its running max, the double sum (rescaled to the global max at the
+// end: the terms' float rounding is the only difference from the direct sum); pass 3 recomputes
+// them for p = f16(expf(w - max) * (1/sum)), exactly as the CPU rounds p.
 #include "kernels.h"
 #include <hip/hip_runtime.h>
 
@@ -145,8 +148,13 @@ __global__ __launch_bounds__(64 * NW) void attn_mfma_kernel(const AttnParams P, 
     };
 
     // ---- pass 1: the token's max over every cell ------------------------------------------------
+    // (a wave that cannot keep its scores also sums expf(w - m) against its running max m, in
+    // double, rescaling by exp(m_old - m_new) when m grows; at the end the sum is rescaled to the
+    // global max: the scores are computed twice instead of three times, and the sum differs from
+    // the direct one by float rounding of its terms only)
     f16x16 st[CPR];
     float mx = -INFINITY;
+    double srun = 0.0;
     for (int rd = 0; rd < nround; ++rd) {
 #pragma unroll
         for (int i = 0; i < CPR; ++i) {
@@ -154,11 +162,22 @@ __global__ __launch_bounds__(64 * NW) void attn_mfma_kernel(const AttnParams P, 
             if (k < myn) {
                 if (k == 0) kcompute(w, kf0, cp0, st[i]);   // (loaded at entry)
                 else scores(w + NW * k, st[i]);
+                float cm = -INFINITY;
 #pragma unroll
-                for (int r = 0; r < 16; ++r) mx = fmaxf(mx, st[i][r]);
+                for (int r = 0; r < 16; ++r) cm = fmaxf(cm, st[i][r]);
+                if (!keep && cm > mx) {
+                    if (mx != -INFINITY) srun *= exp((double)mx - (double)cm);
+                    mx = cm;
+                }
+                if (!keep && mx != -INFINITY) {
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) srun += (double)expf(st[i][r] - mx);
+                }
+                mx = fmaxf(mx, cm);
             }
         }
     }
+    const float mlane = mx;   // this lane's own max (the running max of srun)
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));         // the token's other half of the cells
     if (h == 0) xmax[w][col] = mx;
     __syncthreads();
@@ -183,20 +202,20 @@ __global__ __launch_bounds__(64 * NW) void attn_mfma_kernel(const AttnParams P, 
 
     // ---- pass 2: the sum of expf(w - M) in double, waves added in order ------------------------
     double sum = 0.0;
-    for (int rd = 0; rd < nround; ++rd) {
+    if (keep) {
 #pragma unroll
         for (int i = 0; i < CPR; ++i) {
-            const int k = rd * CPR + i;
-            if (k < myn) {
-                if (!keep) scores(w + NW * k, st[i]);
+            if (i < myn) {
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     const float e = expf(st[i][r] - M);
                     sum += (double)e;
-                    if (keep) st[i][r] = e;   // kept for pass 3: one expf per score
+                    st[i][r] = e;   // kept for pass 3: one expf per score
                 }
             }
         }
+    } else if (mlane != -INFINITY) {
+        sum = srun * exp((double)mlane - (double)M);
     }
     {
         const long long b = __double_as_longlong(sum);
