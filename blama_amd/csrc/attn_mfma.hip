@@ -155,26 +155,41 @@ __global__ __launch_bounds__(64 * NW) void attn_mfma_kernel(const AttnParams P, 
     f16x16 st[CPR];
     float mx = -INFINITY;
     double srun = 0.0;
-    for (int rd = 0; rd < nround; ++rd) {
+    if (keep) {
 #pragma unroll
         for (int i = 0; i < CPR; ++i) {
-            const int k = rd * CPR + i;
-            if (k < myn) {
-                if (k == 0) kcompute(w, kf0, cp0, st[i]);   // (loaded at entry)
-                else scores(w + NW * k, st[i]);
-                float cm = -INFINITY;
+            if (i < myn) {
+                if (i == 0) kcompute(w, kf0, cp0, st[i]);   // (loaded at entry)
+                else scores(w + NW * i, st[i]);
 #pragma unroll
-                for (int r = 0; r < 16; ++r) cm = fmaxf(cm, st[i][r]);
-                if (!keep && cm > mx) {
-                    if (mx != -INFINITY) srun *= exp((double)mx - (double)cm);
-                    mx = cm;
-                }
-                if (!keep && mx != -INFINITY) {
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) srun += (double)expf(st[i][r] - mx);
-                }
-                mx = fmaxf(mx, cm);
+                for (int r = 0; r < 16; ++r) mx = fmaxf(mx, st[i][r]);
             }
+        }
+    } else {
+        // chunk by chunk, the next chunk's K rows in flight during this one's MFMAs
+        auto step = [&](int k, const u32x4 (&kf)[KS], const i32x4 (&cp)[4]) {
+            f16x16 sc;
+            kcompute(w + NW * k, kf, cp, sc);
+            float cm = -INFINITY;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) cm = fmaxf(cm, sc[r]);
+            if (cm > mx) {
+                if (mx != -INFINITY) srun *= exp((double)mx - (double)cm);
+                mx = cm;
+            }
+            if (mx != -INFINITY) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) srun += (double)expf(sc[r] - mx);
+            }
+        };
+        u32x4 kf1[KS];
+        i32x4 cp1[4];
+        for (int k = 0; k < myn; k += 2) {
+            if (k + 1 < myn) kload(w + NW * (k + 1), kf1, cp1);
+            step(k, kf0, cp0);
+            if (k + 1 >= myn) break;
+            if (k + 2 < myn) kload(w + NW * (k + 2), kf0, cp0);
+            step(k + 1, kf1, cp1);
         }
     }
     const float mlane = mx;   // this lane's own max (the running max of srun)
@@ -237,13 +252,20 @@ __global__ __launch_bounds__(64 * NW) void attn_mfma_kernel(const AttnParams P, 
 #pragma unroll
         for (int r = 0; r < 16; ++r) o[b][r] = 0.0f;
     char* const vw = vimg + w * VIMG;
+    // (recomputed scores: the next chunk's K rows in flight during this chunk's PV)
+    u32x4 kfp[KS];
+    i32x4 cpp[4];
+    if (!keep && myn > 0) kload(w, kfp, cpp);
     for (int rd = 0; rd < nround; ++rd) {
 #pragma unroll
         for (int i = 0; i < CPR; ++i) {
             const int k = rd * CPR + i;
             if (k < myn) {
                 const int c = w + NW * k;
-                if (!keep) scores(c, st[i]);
+                if (!keep) {
+                    kcompute(c, kfp, cpp, st[i]);
+                    if (k + 1 < myn) kload(c + NW, kfp, cpp);
+                }
                 // stage this chunk's V (wave-private image; the previous chunk's reads are done:
                 // ds ops of one wave complete in order)
 #pragma unroll
