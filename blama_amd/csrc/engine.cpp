@@ -1278,6 +1278,7 @@ void Ctx::moe_ffn_batch(int l, int nt) {
     p.tokpos = tokpos_b;
     p.grp = moe_grp;
     p.grp_n = E;
+    p.grp_max = nt;
     // gate/up + SwiGLU: rms_norm(x) * ffn_norm of each row's token
     const ActQ8 act = act_of(hp.n_embd, L.gate.type);
     launch_quant_act(xb, hp.n_embd, L.ffn_norm, hp.eps, act, stream, moe_rows);
@@ -1372,13 +1373,23 @@ void Ctx::decode_ubatch(const int32_t* tokens, int n, bool all) {
                 for (const QMat* q : mats) need = need || (q->type == T_Q8_0) == (f == 1);
                 if (need) launch_quant_act(xb, hp.n_embd, L.attn_norm, hp.eps, ub_act(hp.n_embd, nt, f ? T_Q8_0 : T_Q4_K), stream);
             }
+            // the matrices of one type in one launch (7B: Q/K/V, or Q/K plus a Q6_K V)
             for (int i = 0; i < 3; ++i) {
-                GemmParams p = b;
-                p.A = *mats[i];
-                p.pair = PAIR_ADJ;
-                p.epi = epis[i];
-                p.out = qb;
-                launch_mmq32(p, ub_act(hp.n_embd, nt, mats[i]->type), ub_rope, stream);
+                bool first = true;
+                for (int j = 0; j < i; ++j) first = first && mats[j]->type != mats[i]->type;
+                if (!first) continue;
+                GemmParams ps[3];
+                int n = 0;
+                for (int j = i; j < 3; ++j) {
+                    if (mats[j]->type != mats[i]->type) continue;
+                    ps[n] = b;
+                    ps[n].A = *mats[j];
+                    ps[n].pair = PAIR_ADJ;
+                    ps[n].epi = epis[j];
+                    ps[n].out = qb;
+                    ++n;
+                }
+                launch_mmq32_multi(ps, n, ub_act(hp.n_embd, nt, mats[i]->type), ub_rope, stream);
             }
             AttnParams a{qb, kl, vl, tokpos_b, cell_pos, attn_scores, attn_smax, attnb, hp.n_head, hp.n_head_kv,
                          hp.head_dim, kv_dim, (int)n_ctx, kq_scale};

@@ -161,6 +161,7 @@ struct GemmParams {
     const int* grp;
     long long grp_stride;
     int grp_n;
+    int grp_max;   // mmq2 grouped: the most rows one expert can have (the batch's tokens)
     int diag;   // mmq2 timing experiments only (MI_MMQ2_DIAG): 1 = no compute, 2 = no copies past the first
 };
 void launch_gemm(const GemmParams& p, hipStream_t s);
@@ -325,5 +326,8 @@ void launch_mmq32_swizzle(const QMat& A, const QMat* B, uint8_t* dst, hipStream_
 // GemmParams: A (B = up for PAIR_AB / EPI_SWIGLU), epi, K, out/out_stride, resid, tokpos [ntok][4],
 // RoPE fields (rope table from launch_rope_table), caches; the tokens are act's.
 void launch_mmq32(const GemmParams& p, const ActQ8& act, const float2* rope, hipStream_t s);
+// several matrices of one type over the same activation (Q / K / V) as ONE mmq2 launch when they
+// qualify (no pairs, no grouping, a shared output buffer), else one launch each
+void launch_mmq32_multi(const GemmParams* ps, int n, const ActQ8& act, const float2* rope, hipStream_t s);
 
 }  // namespace mi

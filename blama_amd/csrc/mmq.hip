@@ -290,7 +290,7 @@ __global__ void swizzle_kernel(const QMat A, const QMat B, int pair, uint8_t* ds
 
 template <bool AB>
 __device__ __forceinline__ void mmq_epilogue(const GemmParams& P, int tend, const float2* rope, int ttok0,
-                                             int lane, int row, const float v[16]);
+                                             int lane, int row, const float v[16], int epi, int nrows);
 
 // KSPLIT 4: the 4 waves split the superblocks of all 4 token tiles (partials meet in LDS);
 // KSPLIT 1: wave w owns token tile w over all superblocks (no LDS; the 4 waves read the same
@@ -447,7 +447,7 @@ __global__ __launch_bounds__(256, OCC) void mmq32_t(const GemmParams P, const Ac
 #pragma unroll
             for (int r = 0; r < 16; ++r) red[w][t][r][lane] = y[r];
         } else {
-            mmq_epilogue<AB>(P, tend, rope, tok0 + 32 * t, lane, row, y);
+            mmq_epilogue<AB>(P, tend, rope, tok0 + 32 * t, lane, row, y, P.epi, P.A.rows);
         }
     }
     if (KSPLIT == 1) continue;
@@ -458,16 +458,15 @@ __global__ __launch_bounds__(256, OCC) void mmq32_t(const GemmParams P, const Ac
     float v[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) v[r] = ((red[0][t][r][lane] + red[1][t][r][lane]) + red[2][t][r][lane]) + red[3][t][r][lane];
-    mmq_epilogue<AB>(P, tend, rope, tok0 + 32 * t, lane, row, v);
+    mmq_epilogue<AB>(P, tend, rope, tok0 + 32 * t, lane, row, v, P.epi, P.A.rows);
   }
 }
 
 // The epilogue of one 32-token x 32-row D tile (v: this lane's 16 results).
 template <bool AB>
 __device__ __forceinline__ void mmq_epilogue(const GemmParams& P, int tend, const float2* rope, int ttok0,
-                                             int lane, int row, const float v[16]) {
+                                             int lane, int row, const float v[16], int epi, int nrows) {
     const int col = lane & 31, h = lane >> 5;
-    const int epi = P.epi;
     const bool roped = epi == EPI_ROPE_Q || epi == EPI_ROPE_K;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -475,11 +474,11 @@ __device__ __forceinline__ void mmq_epilogue(const GemmParams& P, int tend, cons
         const float pv = __shfl_xor(v[r], AB ? 16 : 1, 64);   // SwiGLU partner / RoPE partner
         if (tok >= tend) continue;
         if (AB) {
-            if (col >= 16 || row >= P.A.rows) continue;
+            if (col >= 16 || row >= nrows) continue;
             P.out[(long long)tok * P.out_stride + row] = silu(v[r]) * pv;   // silu(gate) * up
             continue;
         }
-        if (row >= P.A.rows) continue;
+        if (row >= nrows) continue;
         float o = v[r];
         if (roped) {
             const int i0 = row % P.head_dim;
@@ -529,6 +528,14 @@ __device__ __forceinline__ void mmq_epilogue(const GemmParams& P, int tend, cons
 // LDS: 2 stages of [RT weight slots of SLOT bytes][4 x 8 KiB activations][2 KiB bsb][dT: 1 KiB,
 // Q8_0 4 KiB], then (Q4_K / Q5_K) the operand planes [RT][NPL][8 sub-blocks][64 lanes x 16 B].
 // =============================================================================================
+constexpr int MMQ_SEGS = 3;
+struct MmqSegs {
+    const uint8_t* sw[MMQ_SEGS];
+    int rows[MMQ_SEGS];
+    int epi[MMQ_SEGS];
+    int n;
+};
+
 template <int T> struct M2 {
     static constexpr int RT = 2;                                        // row tiles per block
     static constexpr int NW = 4 * RT;                                    // waves: one 32x32 tile each
@@ -540,7 +547,7 @@ template <int T> struct M2 {
     static constexpr int STAGE = DT_OFF + DT_KB * 1024;
     static constexpr int NI = STAGE / 1024;                             // 1 KiB LDS-DMA pieces
     static constexpr int NIW = (NI + NW - 1) / NW;                      // per wave (some repeat)
-    static constexpr int NPL = T == T_Q5_K ? 3 : 2;                     // K-quant operand planes
+    static constexpr int NPL = 2;                                       // K-quant operand planes
     static constexpr int PLANES = (T == T_Q4_K || T == T_Q5_K) ? RT * NPL * 8 * 1024 : 0;
     static constexpr int lds(int nst) { return nst * STAGE + PLANES; }
 };
@@ -551,6 +558,15 @@ typedef __attribute__((address_space(3))) char lchar;
 __device__ __forceinline__ void pin(v4i& x) { asm volatile("" : "+v"(x)); }
 __device__ __forceinline__ void pin_all() { asm volatile("" ::: "memory"); }
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+// the two 16-bit halves of x times s (v_pk_mul_lo_u16), each product < 65536
+__device__ __forceinline__ unsigned wmul16(unsigned x, unsigned s) {
+    u16x2 a;
+    __builtin_memcpy(&a, &x, 4);
+    const u16x2 r = a * u16x2{(unsigned short)s, (unsigned short)s};
+    unsigned o;
+    __builtin_memcpy(&o, &r, 4);
+    return o;
+}
 // the bytes of x times s, every byte product < 256 (no carry between bytes): v_pk_mul_lo_u16
 __device__ __forceinline__ unsigned bmul(unsigned x, unsigned s) {
     u16x2 a;
@@ -567,7 +583,7 @@ __device__ __forceinline__ V lds_ld(const lchar* p) { return *reinterpret_cast<c
 // compute in turn, sized (LDS, <= 128 VGPRs) for two workgroups per CU that overlap each other.
 template <int T, bool AB, int NST>
 __global__ __launch_bounds__(64 * M2<T>::NW) __attribute__((amdgpu_waves_per_eu(NST == 1 ? 4 : 2)))
-void mmq2_t(const GemmParams P, const ActQ8 act, const float2* rope) {
+void mmq2_t(const GemmParams P, const ActQ8 act, const float2* rope, const MmqSegs S) {
     using C = M2<T>;
     constexpr int RT = C::RT;
     constexpr int NPL = C::NPL;
@@ -578,23 +594,33 @@ void mmq2_t(const GemmParams P, const ActQ8 act, const float2* rope) {
     const int wr = wv >> 2;                           // this wave's row tile (of the block's RT)
     const int col = lane & 31, h = lane >> 5;
     const int nb = P.K >> 8;
-    const int nrt = AB ? (P.A.rows + 15) / 16 : (P.A.rows + 31) / 32;
-    const int nrb = (nrt + RT - 1) / RT;              // row blocks
+    // segments: S.n matrices of this type over the same activation in one grid (Q / K / V),
+    // their row blocks concatenated; segment s: S.rows[s] rows, MFMA-order copy S.sw[s],
+    // epilogue S.epi[s].  A plain or grouped launch is one segment.
+    int nrb = 0;
+#pragma unroll
+    for (int i = 0; i < MMQ_SEGS; ++i)
+        if (i < S.n) nrb += ((AB ? (S.rows[i] + 15) / 16 : (S.rows[i] + 31) / 32) + RT - 1) / RT;
     const int ntb = (act.npad + 127) / 128;           // token blocks
     const int TB = mmq32_tile_bytes_d(T);
-    int rb, tb_b, tb_e, base, tend;
-    const uint8_t* swA = P.A.sw;
+    int rb, tb_b, tb_e, base, tend, grp_e = 0;
     if (P.grp) {
-        // grouped (MoE): blockIdx -> (expert, row block); the expert's 128-token blocks in turn
+        // grouped (MoE): blockIdx -> (token block, expert, row block), token block slowest: the
+        // first blocks of every expert go first, an expert's later blocks (its tokens past 128)
+        // after them, and a block past its expert's tokens exits
         const int nrb8 = (nrb + 7) / 8 * 8;
-        const int e = (int)blockIdx.x / nrb8;
-        rb = (int)blockIdx.x % nrb8;
+        const int per = nrb8 * P.grp_n;
+        const int tbi = (int)blockIdx.x / per, rem = (int)blockIdx.x % per;
+        const int e = rem / nrb8;
+        grp_e = e;
+        rb = rem % nrb8;
         if (rb >= nrb) return;
         base = P.grp[e];
-        tend = base + P.grp[P.grp_n + 1 + e];
-        tb_b = 0;
-        tb_e = (tend - base + 127) / 128;
-        swA += (long long)e * P.grp_stride;
+        const int cnt = P.grp[P.grp_n + 1 + e];
+        if (tbi * 128 >= cnt) return;
+        tend = base + cnt;
+        tb_b = tbi;
+        tb_e = tbi + 1;
     } else {
         // blockIdx -> (row block, token block): the token blocks of a row block on one XCD
         const int b = blockIdx.x, xcd = b & 7, slot = b >> 3;
@@ -605,6 +631,21 @@ void mmq2_t(const GemmParams P, const ActQ8 act, const float2* rope) {
         tend = act.ntok;
         if (rb >= nrb) return;
     }
+    // this row block's segment
+    int seg = 0;
+#pragma unroll
+    for (int i = 0; i < MMQ_SEGS - 1; ++i) {
+        const int nrb_i = ((AB ? (S.rows[i] + 15) / 16 : (S.rows[i] + 31) / 32) + RT - 1) / RT;
+        if (i + 1 < S.n && seg == i && rb >= nrb_i) {
+            rb -= nrb_i;
+            seg = i + 1;
+        }
+    }
+    const int rows_s = seg == 0 ? S.rows[0] : seg == 1 ? S.rows[1] : S.rows[2];
+    const int epi_s = seg == 0 ? S.epi[0] : seg == 1 ? S.epi[1] : S.epi[2];
+    const int nrt = AB ? (rows_s + 15) / 16 : (rows_s + 31) / 32;
+    const uint8_t* swA = seg == 0 ? S.sw[0] : seg == 1 ? S.sw[1] : S.sw[2];
+    if (P.grp) swA += (long long)grp_e * P.grp_stride;
     const int tile_end = (tend + 31) / 32;            // tiles past the batch's (group's) last: clamped
   for (int tb = tb_b; tb < tb_e; ++tb) {
     // (grouped: the previous token block's last stage may still be read by other waves)
@@ -686,7 +727,11 @@ void mmq2_t(const GemmParams P, const ActQ8 act, const float2* rope) {
         const lchar* stg = (const lchar*)(smem + (NST == 2 ? (sb & 1) : 0) * C::STAGE);
         const lchar* A0 = stg + C::A_OFF + w * 8192 + lane * 16;       // this wave's token tile
         const lchar* dTw = stg + C::DT_OFF + (w * 32 + 4 * h) * 4;
+        // a wave whose token tile is past the block's tokens (or row tile past the matrix) skips
+        // its MFMAs (it still copies and decodes for the others): partial blocks, MoE groups
+        const bool busy = w < ntt && rb * RT + wr < nrt;
         if (T == T_Q8_0) {
+          if (busy) {
 #pragma unroll 2
             for (int j = 0; j < 8; ++j) {
                 const v4i a = lds_ld<v4i>(A0 + j * 1024);
@@ -708,13 +753,16 @@ void mmq2_t(const GemmParams P, const ActQ8 act, const float2* rope) {
                     asm volatile("" ::: "memory");   // no LDS load hoisted across sub-blocks
                 }
             }
+          }
         } else if (T == T_Q4_K || T == T_Q5_K) {
-            // (1) decode: the 4 waves of row tile wr turn its superblock into the int8 operand
-            //     planes of the scaled weights sc_j * q (sc = 8*sh + sl; Q5_K q = lo4 + 16*hb):
-            //       P0 = lo4 * sl, P1 = lo4 * sh (<= 105), Q5_K P2 = hb * sc (<= 63),
-            //     so  sc_j * q = P0 + 8 P1 + 16 P2  and the MFMAs accumulate the scaled sub-block
-            //     sums over all 8 sub-blocks exactly (no per-sub-block integer multiply per result);
-            //     wave w decodes piece w (sub-blocks 2w, 2w + 1) for every lane's row.
+            // (1) decode: the 4 waves of row tile wr turn its superblock into two int8 operand
+            //     planes of the scaled weights sc_j * q, every byte <= 127:
+            //       Q4_K (sc = 8 sh + sl, q <= 15):  P0 = q * sl, P1 = q * sh,  sc q = P0 + 8 P1
+            //       Q5_K (q = lo4 + 16 hb <= 31):    p = sc * q <= 1953 (16-bit products),
+            //                                        P0 = p & 127, P1 = p >> 7,  sc q = P0 + 128 P1
+            //     and the MFMAs accumulate the scaled sub-block sums over all 8 sub-blocks exactly
+            //     (no integer multiply per result); wave w decodes piece w (sub-blocks 2w, 2w + 1)
+            //     for every lane's row.
             const lchar* wt = stg + wr * C::SLOT;
             lchar* pl = (lchar*)(smem + NST * C::STAGE) + wr * (NPL * 8 * 1024) + lane * 16;
             {
@@ -737,49 +785,52 @@ void mmq2_t(const GemmParams P, const ActQ8 act, const float2* rope) {
                 unsigned* p1 = reinterpret_cast<unsigned*>(&o1);
                 unsigned* p2 = reinterpret_cast<unsigned*>(&o2);
                 unsigned* p3 = reinterpret_cast<unsigned*>(&o3);
+                if (T == T_Q4_K) {
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const unsigned lo = q[i] & 0x0F0F0F0Fu, hi = (q[i] >> 4) & 0x0F0F0F0Fu;
-                    p0[i] = bmul(lo, s0 & 7);
-                    p1[i] = bmul(lo, s0 >> 3);
-                    p2[i] = bmul(hi, s1 & 7);
-                    p3[i] = bmul(hi, s1 >> 3);
+                    for (int i = 0; i < 4; ++i) {
+                        const unsigned lo = q[i] & 0x0F0F0F0Fu, hi = (q[i] >> 4) & 0x0F0F0F0Fu;
+                        p0[i] = bmul(lo, s0 & 7);
+                        p1[i] = bmul(lo, s0 >> 3);
+                        p2[i] = bmul(hi, s1 & 7);
+                        p3[i] = bmul(hi, s1 >> 3);
+                    }
+                } else {
+                    const u32x4 qh = lds_ld<u32x4>(wt + 4096 + lane * 16);
+                    const unsigned b[4] = {qh.x, qh.y, qh.z, qh.w};
+                    // 4 elements q (bytes) times s as 16-bit products, split into lo7 / hi bytes
+                    auto split = [](unsigned q5, unsigned sc, unsigned& lo, unsigned& hi) {
+                        const unsigned m02 = wmul16(q5 & 0x00FF00FFu, sc), m13 = wmul16((q5 >> 8) & 0x00FF00FFu, sc);
+                        lo = (m02 & 0x007F007Fu) | ((m13 & 0x007F007Fu) << 8);
+                        hi = ((m02 >> 7) & 0x001F001Fu) | (((m13 >> 7) & 0x001F001Fu) << 8);
+                    };
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const unsigned q5a = (q[i] & 0x0F0F0F0Fu) | (((b[i] >> (2 * w)) & 0x01010101u) << 4);
+                        const unsigned q5b = ((q[i] >> 4) & 0x0F0F0F0Fu) | (((b[i] >> (2 * w + 1)) & 0x01010101u) << 4);
+                        split(q5a, s0, p0[i], p1[i]);
+                        split(q5b, s1, p2[i], p3[i]);
+                    }
                 }
                 *reinterpret_cast<__attribute__((address_space(3))) u32x4*>(pl + (0 * 8 + 2 * w) * 1024) = o0;
                 *reinterpret_cast<__attribute__((address_space(3))) u32x4*>(pl + (1 * 8 + 2 * w) * 1024) = o1;
                 *reinterpret_cast<__attribute__((address_space(3))) u32x4*>(pl + (0 * 8 + 2 * w + 1) * 1024) = o2;
                 *reinterpret_cast<__attribute__((address_space(3))) u32x4*>(pl + (1 * 8 + 2 * w + 1) * 1024) = o3;
-                if (T == T_Q5_K) {
-                    const u32x4 qh = lds_ld<u32x4>(wt + 4096 + lane * 16);
-                    const unsigned b[4] = {qh.x, qh.y, qh.z, qh.w};
-                    u32x4 h0, h1;
-                    unsigned* q0 = reinterpret_cast<unsigned*>(&h0);
-                    unsigned* q1 = reinterpret_cast<unsigned*>(&h1);
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        q0[i] = bmul((b[i] >> (2 * w)) & 0x01010101u, s0);
-                        q1[i] = bmul((b[i] >> (2 * w + 1)) & 0x01010101u, s1);
-                    }
-                    *reinterpret_cast<__attribute__((address_space(3))) u32x4*>(pl + (2 * 8 + 2 * w) * 1024) = h0;
-                    *reinterpret_cast<__attribute__((address_space(3))) u32x4*>(pl + (2 * 8 + 2 * w + 1) * 1024) = h1;
-                }
             }
             __builtin_amdgcn_s_waitcnt((0xF) | (0x3 << 14) | (0x7 << 4));   // lgkmcnt(0): planes written
             __builtin_amdgcn_s_barrier();
             // (2) the MFMAs: token tile w x row tile wr, the planes accumulated over the sub-blocks
-            {
+            if (busy) {
                 constexpr int r = 0;
                 const u32x4 hd = lds_ld<u32x4>(wt + (T == T_Q5_K ? 5120 : 4096) + col * 16);
-                v16i acc0 = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, acc1 = acc0, acc2 = acc0;
+                v16i acc0 = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, acc1 = acc0;
                 const lchar* plr = (const lchar*)pl;
                 // every operand of the superblock read first (at 2 waves per SIMD the LDS latency
                 // is hidden only by reads in flight: counted waits, not lgkmcnt(0) per MFMA pair)
-                v4i av[8], b0[8], b1[8], b2[8];
+                v4i av[8], b0[8], b1[8];
                 auto ld = [&](int j) {
                     av[j] = lds_ld<v4i>(A0 + j * 1024);
                     b0[j] = lds_ld<v4i>(plr + (0 * 8 + j) * 1024);
                     b1[j] = lds_ld<v4i>(plr + (1 * 8 + j) * 1024);
-                    if (T == T_Q5_K) b2[j] = lds_ld<v4i>(plr + (2 * 8 + j) * 1024);
                 };
                 auto mm = [&](int j) {
                     if (NST == 2) {
@@ -789,10 +840,6 @@ void mmq2_t(const GemmParams P, const ActQ8 act, const float2* rope) {
                     }
                     acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(av[j], b0[j], acc0, 0, 0, 0);
                     acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(av[j], b1[j], acc1, 0, 0, 0);
-                    if (T == T_Q5_K) {
-                        if (NST == 2) pin(b2[j]);
-                        acc2 = __builtin_amdgcn_mfma_i32_32x32x32_i8(av[j], b2[j], acc2, 0, 0, 0);
-                    }
                 };
                 // sub-blocks 0-3 read, then 4-7 read while 0-3 run
 #pragma unroll
@@ -820,14 +867,14 @@ void mmq2_t(const GemmParams P, const ActQ8 act, const float2* rope) {
 #pragma unroll
                     for (int i = 0; i < 4; ++i) {
                         const int e = 4 * g + i;
-                        const int S = acc0[e] + 8 * acc1[e] + (T == T_Q5_K ? 16 * acc2[e] : 0);
+                        const int S = acc0[e] + (T == T_Q5_K ? 128 : 8) * acc1[e];
                         const float d = dr * dx[i], dm = dmr * dx[i];
                         y[r][e] = fmaf(-dm, (float)(64 * x1[e] + x2[e]), fmaf(d, (float)S, y[r][e]));
                     }
                 }
             }
         } else {   // Q6_K: the 8 spans of w = 64*hi + lo, each operand accumulated by the MFMA
-            {
+            if (busy) {
                 constexpr int r = 0;
                 const lchar* wt = stg + wr * C::SLOT;
                 v16i ah = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, al = ah;
@@ -871,7 +918,7 @@ void mmq2_t(const GemmParams P, const ActQ8 act, const float2* rope) {
     const int rt = rb * RT + wr;
     if (w < ntt && rt < nrt) {
         const int row = AB ? rt * 16 + (col & 15) : rt * 32 + col;
-        mmq_epilogue<AB>(P, tend, rope, tok0 + 32 * w, lane, row, y[0]);
+        mmq_epilogue<AB>(P, tend, rope, tok0 + 32 * w, lane, row, y[0], epi_s, rows_s);
     }
   }
 }
@@ -914,6 +961,90 @@ void launch_mmq32_swizzle(const QMat& A, const QMat* B, uint8_t* dst, hipStream_
     MI_HIP(hipGetLastError());
 }
 
+namespace {
+bool mmq2_enabled() {
+    static const int var_env = getenv("MI_MMQ") ? atoi(getenv("MI_MMQ")) : 1;
+    static const bool old_env = getenv("MI_MMQ_OLD") != nullptr;
+    return var_env == 1 && !old_env;
+}
+// one mmq2 launch over the segments S (all of p.A's type; one segment unless launch_mmq32_multi)
+void launch_mmq2(const GemmParams& p, const mmq::MmqSegs& S, const ActQ8& act, const float2* rope, hipStream_t s) {
+    const bool ab = p.pair == PAIR_AB;
+    const int T = p.A.type;
+    const int RT = mmq::M2<T_Q4_K>::RT;
+    const int NWv = 4 * RT;
+    int nrb = 0;
+    for (int i = 0; i < S.n; ++i) nrb += ((ab ? (S.rows[i] + 15) / 16 : (S.rows[i] + 31) / 32) + RT - 1) / RT;
+    const int ntb = (act.npad + 127) / 128;
+    // grouped (MoE): a workgroup per (token block, expert, row block)
+    const int g2 = (nrb + 7) / 8 * 8 * (p.grp ? p.grp_n * ((max(p.grp_max, 1) + 127) / 128) : ntb);
+    // MI_MMQ2_NST: 1 = one stage, two workgroups per CU; 2 = two stages, one workgroup per CU;
+    // 0 (default) = one stage when the grid fills two workgroups per CU, else two.  7B 512-token
+    // prefill, NST 1 vs 2: 15.5 vs 16.8 ms (same box, scripts/ab_prefill.sh)
+    static const int nst_req = getenv("MI_MMQ2_NST") ? atoi(getenv("MI_MMQ2_NST")) : 0;
+    static int n_cu = 0;
+    if (!n_cu) {
+        int dev = 0;
+        MI_HIP(hipGetDevice(&dev));
+        MI_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
+    }
+    const int nst = nst_req ? nst_req : (g2 >= 2 * n_cu ? 1 : 2);
+    decltype(&mmq::mmq2_t<T_Q4_K, false, 2>) f2;
+    int lds;
+#define M2_PICK(NST_)                                                                                           \
+    switch (T) {                                                                                                \
+    case T_Q4_K: f2 = ab ? mmq::mmq2_t<T_Q4_K, true, NST_> : mmq::mmq2_t<T_Q4_K, false, NST_>; lds = mmq::m2_lds<T_Q4_K, NST_>(); break; \
+    case T_Q5_K: f2 = ab ? mmq::mmq2_t<T_Q5_K, true, NST_> : mmq::mmq2_t<T_Q5_K, false, NST_>; lds = mmq::m2_lds<T_Q5_K, NST_>(); break; \
+    case T_Q6_K: f2 = ab ? mmq::mmq2_t<T_Q6_K, true, NST_> : mmq::mmq2_t<T_Q6_K, false, NST_>; lds = mmq::m2_lds<T_Q6_K, NST_>(); break; \
+    default: f2 = ab ? mmq::mmq2_t<T_Q8_0, true, NST_> : mmq::mmq2_t<T_Q8_0, false, NST_>; lds = mmq::m2_lds<T_Q8_0, NST_>(); break; \
+    }
+    if (nst == 1) { M2_PICK(1) } else { M2_PICK(2) }
+#undef M2_PICK
+    static bool attr_done[2][4][2] = {};
+    const int ti = T == T_Q4_K ? 0 : T == T_Q5_K ? 1 : T == T_Q6_K ? 2 : 3;
+    const int ni = nst == 1 ? 0 : 1;
+    if (!attr_done[ni][ti][ab]) {
+        MI_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(f2), hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+        attr_done[ni][ti][ab] = true;
+    }
+    static const int diag = getenv("MI_MMQ2_DIAG") ? atoi(getenv("MI_MMQ2_DIAG")) : 0;
+    GemmParams p2 = p;
+    p2.diag = diag;
+    hipLaunchKernelGGL(f2, dim3(g2), dim3(64 * NWv), (size_t)lds, s, p2, act, rope, S);
+    MI_HIP(hipGetLastError());
+}
+}  // namespace
+
+void launch_mmq32_multi(const GemmParams* ps, int n, const ActQ8& act, const float2* rope, hipStream_t s) {
+    bool one = n >= 2 && n <= mmq::MMQ_SEGS && mmq2_enabled();
+    for (int i = 0; i < n && one; ++i)
+        one = ps[i].A.type == ps[0].A.type && ps[i].pair != PAIR_AB && !ps[i].grp && ps[i].K == ps[0].K &&
+              ps[i].A.sw && ps[i].A.K == ps[0].K && ps[i].epi != EPI_SWIGLU;
+    if (!one) {
+        for (int i = 0; i < n; ++i) launch_mmq32(ps[i], act, rope, s);
+        return;
+    }
+    for (int i = 0; i < n; ++i) {   // the same checks as one launch each (the shared fields are ps[0]'s)
+        const GemmParams& p = ps[i];
+        if ((p.epi == EPI_ROPE_Q || p.epi == EPI_ROPE_K) && (!rope || p.head_dim % 2 || p.n_rot > p.head_dim))
+            throw Error("mmq32: RoPE epilogue needs the rope table");
+        if (p.out != ps[0].out || p.out_stride != ps[0].out_stride || p.resid != ps[0].resid)
+            throw Error("mmq32 multi: the segments share one output buffer");
+    }
+    if (!mmq32_supported(ps[0].A.type)) throw Error("mmq32: Q4_K / Q5_K / Q6_K / Q8_0 only");
+    if ((ps[0].A.type == T_Q8_0) != (act.q80 != 0)) throw Error("mmq32: Q8_0 weights take Q8_0 activations, k-quants Q8_K");
+    if (act.K != ps[0].K) throw Error("mmq32: activation length differs from K");
+    if (act.ntok < 1 || act.npad % 32 || act.npad > UB_MAX) throw Error("mmq32: bad token count");
+    mmq::MmqSegs S{};
+    S.n = n;
+    for (int i = 0; i < n; ++i) {
+        S.sw[i] = ps[i].A.sw;
+        S.rows[i] = ps[i].A.rows;
+        S.epi[i] = ps[i].epi;
+    }
+    launch_mmq2(ps[0], S, act, rope, s);
+}
+
 void launch_mmq32(const GemmParams& p, const ActQ8& act, const float2* rope, hipStream_t s) {
     if (!mmq32_supported(p.A.type)) throw Error("mmq32: Q4_K / Q5_K / Q6_K / Q8_0 only");
     if ((p.A.type == T_Q8_0) != (act.q80 != 0)) throw Error("mmq32: Q8_0 weights take Q8_0 activations, k-quants Q8_K");
@@ -947,51 +1078,13 @@ void launch_mmq32(const GemmParams& p, const ActQ8& act, const float2* rope, hip
     else if (var == 2) MMQ_PICK(1, 3);
     else MMQ_PICK(4, 2);
 #undef MMQ_PICK
-    static const bool old_env = getenv("MI_MMQ_OLD") != nullptr;
-    if (var == 1 && !old_env) {
-        // mmq2: 128-token x 32*RT-column blocks, LDS-DMA staged two superblocks deep
-        const int T = p.A.type;
-        const int RT = mmq::M2<T_Q4_K>::RT;
-        const int NWv = 4 * RT;
-        const int nrb = (nrt + RT - 1) / RT;
-        const int ntb = (act.npad + 127) / 128;
-        // grouped (MoE): a workgroup per (expert, row block), each over its expert's token blocks
-        const int g2 = (nrb + 7) / 8 * 8 * (p.grp ? p.grp_n : ntb);
-        // MI_MMQ2_NST: 1 = one stage, two workgroups per CU; 2 = two stages, one workgroup per CU;
-        // 0 (default) = one stage when the grid fills two workgroups per CU, else two.  7B 512-token
-        // prefill, NST 1 vs 2: 15.5 vs 16.8 ms (same box, scripts/ab_prefill.sh)
-        static const int nst_req = getenv("MI_MMQ2_NST") ? atoi(getenv("MI_MMQ2_NST")) : 0;
-        static int n_cu = 0;
-        if (!n_cu) {
-            int dev = 0;
-            MI_HIP(hipGetDevice(&dev));
-            MI_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
-        }
-        const int nst_env = nst_req ? nst_req : (g2 >= 2 * n_cu ? 1 : 2);
-        decltype(&mmq::mmq2_t<T_Q4_K, false, 2>) f2;
-        int lds;
-#define M2_PICK(NST_)                                                                                           \
-        switch (T) {                                                                                            \
-        case T_Q4_K: f2 = ab ? mmq::mmq2_t<T_Q4_K, true, NST_> : mmq::mmq2_t<T_Q4_K, false, NST_>; lds = mmq::m2_lds<T_Q4_K, NST_>(); break; \
-        case T_Q5_K: f2 = ab ? mmq::mmq2_t<T_Q5_K, true, NST_> : mmq::mmq2_t<T_Q5_K, false, NST_>; lds = mmq::m2_lds<T_Q5_K, NST_>(); break; \
-        case T_Q6_K: f2 = ab ? mmq::mmq2_t<T_Q6_K, true, NST_> : mmq::mmq2_t<T_Q6_K, false, NST_>; lds = mmq::m2_lds<T_Q6_K, NST_>(); break; \
-        default: f2 = ab ? mmq::mmq2_t<T_Q8_0, true, NST_> : mmq::mmq2_t<T_Q8_0, false, NST_>; lds = mmq::m2_lds<T_Q8_0, NST_>(); break; \
-        }
-        const int nst = T == T_Q5_K ? 2 : nst_env;   // (Q5_K: 3 planes do not fit two workgroups per CU)
-        if (nst == 1) { M2_PICK(1) } else { M2_PICK(2) }
-#undef M2_PICK
-        static bool attr_done[2][4][2] = {};
-        const int ti = T == T_Q4_K ? 0 : T == T_Q5_K ? 1 : T == T_Q6_K ? 2 : 3;
-        const int ni = nst == 1 ? 0 : 1;
-        if (!attr_done[ni][ti][ab]) {
-            MI_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(f2), hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-            attr_done[ni][ti][ab] = true;
-        }
-        static const int diag = getenv("MI_MMQ2_DIAG") ? atoi(getenv("MI_MMQ2_DIAG")) : 0;
-        GemmParams p2 = p;
-        p2.diag = diag;
-        hipLaunchKernelGGL(f2, dim3(g2), dim3(64 * NWv), (size_t)lds, s, p2, act, rope);
-        MI_HIP(hipGetLastError());
+    if (var == 1 && mmq2_enabled()) {   // mmq2: 128-token x 64-row blocks, LDS-DMA staged
+        mmq::MmqSegs S{};
+        S.n = 1;
+        S.sw[0] = p.A.sw;
+        S.rows[0] = p.A.rows;
+        S.epi[0] = p.epi;
+        launch_mmq2(p, S, act, rope, s);
         return;
     }
     hipLaunchKernelGGL(fn, dim3(grid), dim3(256), 0, s, p, act, rope);
