@@ -76,12 +76,14 @@ __device__ __forceinline__ float wave_max_pos(float v) {
 // lo in 0..63): bytes 0-7 hi_j, 8-15 lo_j -- the int8 A operand of the MFMA that forms
 // sum_j m_j*bsum_j = 64*sum m_j hi_j + sum m_j lo_j exactly.  Rows ntok..npad-1 are zero.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void quant_act_kernel(const float* x, int x_stride, const float* norm_w,
+// QA_W waves per token row (16: one 256-element block each at K = 4096)
+template <int QA_W>
+__global__ __launch_bounds__(64 * QA_W) void quant_act_kernel(const float* x, int x_stride, const float* norm_w,
                                                         float eps, ActQ8 a, const int* rows) {
     const int t = blockIdx.x;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int nb = a.K >> 8;
-    __shared__ double red[4];
+    __shared__ double red[QA_W];
     // MFMA-fragment order (one wave load = 1 KiB contiguous): q [tile][sb][j][h*32 + t%32][16 B],
     // element 32j + 16h + e of superblock sb of token t at byte e; bsb [tile][sb][t%32][16 B]
     const int tile = t >> 5, tr = t & 31;
@@ -89,7 +91,7 @@ __global__ __launch_bounds__(256) void quant_act_kernel(const float* x, int x_st
     int8_t* q = a.q + (long long)tile * nb * 8192 + fj * 1024 + (fh * 32 + tr) * 16 + 4 * fw;
     int8_t* bsb = a.q80 ? nullptr : a.bsb + ((long long)tile * nb * 32 + tr) * 16;
     if (t >= a.ntok || (rows && rows[t] < 0)) {   // padding rows (and MoE group padding) are zero
-        for (int blk = wave; blk < nb; blk += 4) {
+        for (int blk = wave; blk < nb; blk += QA_W) {
             *reinterpret_cast<int*>(q + blk * 8192) = 0;
             if (!a.q80 && lane < 4) reinterpret_cast<int*>(bsb + blk * 512)[lane] = 0;
             if (a.q80 && lane < 8) a.dT[(long long)(blk * 8 + lane) * a.npad + t] = 0.0f;
@@ -98,25 +100,39 @@ __global__ __launch_bounds__(256) void quant_act_kernel(const float* x, int x_st
         return;
     }
     const f32x4* x4 = reinterpret_cast<const f32x4*>(x + (long long)(rows ? rows[t] : t) * x_stride);
+    // this wave's blocks (wave, wave + QA_W, ...) read once, kept for the quantisation
+    constexpr int XR = 16;   // K <= QA_W * 16 * 256
+    f32x4 xr[XR];
+#pragma unroll
+    for (int i = 0; i < XR; ++i)
+        if (wave + QA_W * i < nb) xr[i] = x4[(wave + QA_W * i) * 64 + lane];
     float scale = 1.0f;
     if (norm_w) {   // ggml_compute_forward_rms_norm_f32: sum of squares in double
         double sacc = 0.0;
-        for (int blk = wave; blk < nb; blk += 4) {
-            const f32x4 v = x4[blk * 64 + lane];
-            sacc += (double)(v.x * v.x);
-            sacc += (double)(v.y * v.y);
-            sacc += (double)(v.z * v.z);
-            sacc += (double)(v.w * v.w);
+#pragma unroll
+        for (int i = 0; i < XR; ++i) {
+            if (wave + QA_W * i < nb) {
+                const f32x4 v = xr[i];
+                sacc += (double)(v.x * v.x);
+                sacc += (double)(v.y * v.y);
+                sacc += (double)(v.z * v.z);
+                sacc += (double)(v.w * v.w);
+            }
         }
         sacc = wave_sum63_d(sacc);
         if (lane == 63) red[wave] = sacc;
         __syncthreads();
-        const double tot = ((red[0] + red[1]) + red[2]) + red[3];
+        double tot = 0.0;
+#pragma unroll
+        for (int k = 0; k < QA_W; ++k) tot += red[k];
         scale = 1.0f / sqrtf((float)(tot / (double)a.K) + eps);
     }
     const f32x4* w4 = reinterpret_cast<const f32x4*>(norm_w);
-    for (int blk = wave; blk < nb; blk += 4) {
-        const f32x4 xv = x4[blk * 64 + lane];
+#pragma unroll
+    for (int i = 0; i < XR; ++i) {
+        const int blk = wave + QA_W * i;
+        if (blk >= nb) break;
+        const f32x4 xv = xr[i];
         float v[4] = {xv.x, xv.y, xv.z, xv.w};
         if (norm_w) {
             const f32x4 w = w4[blk * 64 + lane];
@@ -932,7 +948,13 @@ void launch_quant_act(const float* x, int x_stride, const float* norm_w, float e
     if (a.K % 256) throw Error("quant_act: K must be a multiple of 256");
     // (more than UB_MAX rows only for the MoE rows of a batch: one per (token, slot), padded)
     if (a.npad % 32 || a.ntok > a.npad || a.npad > 4 * UB_MAX) throw Error("quant_act: bad token count");
-    hipLaunchKernelGGL(mmq::quant_act_kernel, dim3(a.npad), dim3(256), 0, s, x, x_stride, norm_w, eps, a, rows);
+    if (a.K > 65536) throw Error("quant_act: K past 65536");
+    // MI_QA_W: waves per token row, 16 (default) or 4
+    static const int qaw = getenv("MI_QA_W") ? atoi(getenv("MI_QA_W")) : 16;
+    if (qaw == 4 && a.K <= 4 * 16 * 256)
+        hipLaunchKernelGGL(mmq::quant_act_kernel<4>, dim3(a.npad), dim3(256), 0, s, x, x_stride, norm_w, eps, a, rows);
+    else
+        hipLaunchKernelGGL(mmq::quant_act_kernel<16>, dim3(a.npad), dim3(1024), 0, s, x, x_stride, norm_w, eps, a, rows);
     MI_HIP(hipGetLastError());
 }
 
