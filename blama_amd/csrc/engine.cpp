@@ -663,6 +663,10 @@ Ctx::Ctx(Model* model, uint32_t nctx, uint32_t nbatch, uint32_t nubatch) : m(mod
                 MI_HIP(hipMalloc(&moe_bsb, (size_t)cap * (kmax / 256) * 16));
             }
             MI_HIP(hipMalloc(&ub_rope, (size_t)UB_MAX * std::max(1, hp.n_rot / 2) * sizeof(float2)));
+            // split-K partials of the residual GEMMs (WO, FFN down) of dense models
+            static const bool ksplit_env = getenv("MI_MMQ_KSPLIT") == nullptr || atoi(getenv("MI_MMQ_KSPLIT")) != 0;
+            if (ksplit_env && hp.n_expert == 0 && mmq2_active())
+                MI_HIP(hipMalloc(&ub_part, (size_t)2 * UB_MAX * hp.n_embd * sizeof(float)));
         }
         // MoE prompts need the MFMA path (the v_dot4 GEMM has no routed-expert form)
         if (hp.n_expert > 0 && !mmq_ok) batch_ok = false;
@@ -716,7 +720,7 @@ Ctx::~Ctx() {
                     (void*)topk_vals, (void*)sel, (void*)selw, (void*)gather_ids, (void*)gather_out,
                     (void*)cell_delta, (void*)move_src, (void*)part_o, (void*)attn_smax, (void*)attn_scores, (void*)stamps,
                     (void*)attn_xflags, (void*)attn_xmax, (void*)attn_xsum, (void*)step_ctr,
-                    (void*)xb, (void*)qb, (void*)attnb, (void*)hb, (void*)tokpos_b, (void*)ub_q, (void*)ub_dT, (void*)ub_bsb, (void*)ub_rope,
+                    (void*)xb, (void*)qb, (void*)attnb, (void*)hb, (void*)tokpos_b, (void*)ub_q, (void*)ub_dT, (void*)ub_bsb, (void*)ub_rope, (void*)ub_part,
                     (void*)ub_q0, (void*)ub_dT0, (void*)yb, (void*)sel_b, (void*)selw_b, (void*)moe_rows, (void*)moe_pos,
                     (void*)moe_rowsel, (void*)moe_grp, (void*)moe_q, (void*)moe_dT, (void*)moe_bsb,
                     (void*)logits_all, (void*)grows_ids, (void*)grows_out})
@@ -1348,6 +1352,7 @@ void Ctx::decode_ubatch(const int32_t* tokens, int n, bool all) {
         EmbedParams ep{m->tok_embd, tokpos_b, xb, hp.n_embd};
         launch_embed_multi(ep, nt, stream);
         launch_rope_table(tokpos_b, nt, hp.n_rot, theta_scale, hp.freq_scale, m->rope_freqs, ub_rope, stream);
+        const float* pend = nullptr;   // split-K partials not yet added into xb (the next quant_act does)
         for (int l = 0; l < hp.n_layer; ++l) {
             const Layer& L = m->layers[l];
             __half* kl = kcache + (size_t)l * n_ctx * kv_dim;
@@ -1371,7 +1376,11 @@ void Ctx::decode_ubatch(const int32_t* tokens, int n, bool all) {
             for (int f = 0; f < 2; ++f) {
                 bool need = false;
                 for (const QMat* q : mats) need = need || (q->type == T_Q8_0) == (f == 1);
-                if (need) launch_quant_act(xb, hp.n_embd, L.attn_norm, hp.eps, ub_act(hp.n_embd, nt, f ? T_Q8_0 : T_Q4_K), stream);
+                if (need) {
+                    launch_quant_act(xb, hp.n_embd, L.attn_norm, hp.eps, ub_act(hp.n_embd, nt, f ? T_Q8_0 : T_Q4_K), stream,
+                                     nullptr, pend);
+                    pend = nullptr;
+                }
             }
             // the matrices of one type in one launch (7B: Q/K/V, or Q/K plus a Q6_K V)
             for (int i = 0; i < 3; ++i) {
@@ -1404,6 +1413,11 @@ void Ctx::decode_ubatch(const int32_t* tokens, int n, bool all) {
                 p.epi = EPI_ADD;
                 p.out = xb;
                 p.resid = xb;
+                if (ub_part && L.wo.nb >= 2) {   // halves of K; the FFN's quant_act adds them
+                    p.ksplit = 2;
+                    p.part = ub_part;
+                    pend = ub_part;
+                }
                 launch_mmq32(p, act, ub_rope, stream);
             }
             if (hp.n_expert > 0) {   // routed experts (build_moe_ffn) + residual
@@ -1412,7 +1426,8 @@ void Ctx::decode_ubatch(const int32_t* tokens, int n, bool all) {
             }
             {   // FFN gate/up + SwiGLU
                 const ActQ8 act = ub_act(hp.n_embd, nt, L.gate.type);
-                launch_quant_act(xb, hp.n_embd, L.ffn_norm, hp.eps, act, stream);
+                launch_quant_act(xb, hp.n_embd, L.ffn_norm, hp.eps, act, stream, nullptr, pend);
+                pend = nullptr;
                 GemmParams p = b;
                 p.A = L.gate;
                 p.B = L.up;
@@ -1432,6 +1447,11 @@ void Ctx::decode_ubatch(const int32_t* tokens, int n, bool all) {
                 p.K = hp.n_ff;
                 p.out = xb;
                 p.resid = xb;
+                if (ub_part && L.down.nb >= 2 && l + 1 < hp.n_layer) {   // the next layer's quant_act adds them
+                    p.ksplit = 2;
+                    p.part = ub_part;
+                    pend = ub_part;
+                }
                 launch_mmq32(p, act, ub_rope, stream);
             }
         }

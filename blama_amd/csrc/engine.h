@@ -169,6 +169,7 @@ struct Ctx {
     float* ub_dT = nullptr;             // [kmax/256][UB_MAX]
     int8_t* ub_bsb = nullptr;           // [UB_MAX][kmax/256][16]
     float2* ub_rope = nullptr;          // [UB_MAX][n_rot/2]
+    float* ub_part = nullptr;           // [2][UB_MAX][n_embd] split-K partials (dense models; MI_MMQ_KSPLIT=0: off)
     bool out_mmq = false;               // the output head is mmq32-capable (batched logits of every token)
     bool ub_q80 = false;                // the layer matrices are Q8_0: Q8_0 batch activations
     bool attn_mfma = false;             // batch attention on f16 MFMA (attn_mfma.hip); MI_ATTN_VALU=1: VALU kernel

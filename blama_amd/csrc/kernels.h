@@ -162,6 +162,11 @@ struct GemmParams {
     long long grp_stride;
     int grp_n;
     int grp_max;   // mmq2 grouped: the most rows one expert can have (the batch's tokens)
+    // mmq2 split over K (EPI_ADD of a dense prompt batch): ksplit 2 halves of the superblocks write
+    // their partial sums to part[2][ntok][out_stride] (no residual); the next launch_quant_act
+    // over the same buffer adds them, x = (p0 + p1) + x, writes x back and quantises it
+    int ksplit;
+    float* part;
     int diag;   // mmq2 timing experiments only (MI_MMQ2_DIAG): 1 = no compute, 2 = no copies past the first
 };
 void launch_gemm(const GemmParams& p, hipStream_t s);
@@ -311,8 +316,12 @@ struct ActQ8 {
     int q80;                   // 1: Q8_0 activations (for Q8_0 weights): dT is [K/32][npad] f16-rounded d, no bsb
 };
 // rows (optional): token t of the batch reads row rows[t] of x (the tokens routed to one expert)
+// part (optional): the split-K partial sums of the GEMM that produced x (see GemmParams::ksplit):
+// x += p0 + p1 first, written back
 void launch_quant_act(const float* x, int x_stride, const float* norm_w, float eps, const ActQ8& a, hipStream_t s,
-                      const int* rows = nullptr);
+                      const int* rows = nullptr, const float* part = nullptr);
+// whether prompt-batch GEMMs take the mmq2 path (the only one with ksplit)
+bool mmq2_active();
 // ggml_rope_cache_init per token of the batch: out [ntok][n_rot/2] (cos, sin)
 void launch_rope_table(const int* tokpos, int ntok, int n_rot, float theta_scale, float freq_scale,
                        const float* freq_factors, float2* out, hipStream_t s);

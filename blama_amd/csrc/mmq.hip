@@ -79,7 +79,7 @@ __device__ __forceinline__ float wave_max_pos(float v) {
 // QA_W waves per token row (16: one 256-element block each at K = 4096)
 template <int QA_W>
 __global__ __launch_bounds__(64 * QA_W) void quant_act_kernel(const float* x, int x_stride, const float* norm_w,
-                                                        float eps, ActQ8 a, const int* rows) {
+                                                        float eps, ActQ8 a, const int* rows, const float* part) {
     const int t = blockIdx.x;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int nb = a.K >> 8;
@@ -106,6 +106,21 @@ __global__ __launch_bounds__(64 * QA_W) void quant_act_kernel(const float* x, in
 #pragma unroll
     for (int i = 0; i < XR; ++i)
         if (wave + QA_W * i < nb) xr[i] = x4[(wave + QA_W * i) * 64 + lane];
+    if (part) {   // the split-K GEMM's halves: x = (p0 + p1) + x (EPI_ADD's o + resid), written back
+        const f32x4* p0 = reinterpret_cast<const f32x4*>(part + (long long)t * a.K);
+        const f32x4* p1 = reinterpret_cast<const f32x4*>(part + ((long long)a.ntok + t) * a.K);
+        f32x4* xw = reinterpret_cast<f32x4*>(const_cast<float*>(x) + (long long)t * x_stride);
+#pragma unroll
+        for (int i = 0; i < XR; ++i) {
+            const int blk = wave + QA_W * i;
+            if (blk < nb) {
+                const f32x4 a0 = p0[blk * 64 + lane], a1 = p1[blk * 64 + lane];
+                xr[i] = f32x4{(a0.x + a1.x) + xr[i].x, (a0.y + a1.y) + xr[i].y, (a0.z + a1.z) + xr[i].z,
+                              (a0.w + a1.w) + xr[i].w};
+                xw[blk * 64 + lane] = xr[i];
+            }
+        }
+    }
     float scale = 1.0f;
     if (norm_w) {   // ggml_compute_forward_rms_norm_f32: sum of squares in double
         double sacc = 0.0;
@@ -306,7 +321,8 @@ __global__ void swizzle_kernel(const QMat A, const QMat B, int pair, uint8_t* ds
 
 template <bool AB>
 __device__ __forceinline__ void mmq_epilogue(const GemmParams& P, int tend, const float2* rope, int ttok0,
-                                             int lane, int row, const float v[16], int epi, int nrows);
+                                             int lane, int row, const float v[16], int epi, int nrows,
+                                             float* out);
 
 // KSPLIT 4: the 4 waves split the superblocks of all 4 token tiles (partials meet in LDS);
 // KSPLIT 1: wave w owns token tile w over all superblocks (no LDS; the 4 waves read the same
@@ -463,7 +479,7 @@ __global__ __launch_bounds__(256, OCC) void mmq32_t(const GemmParams P, const Ac
 #pragma unroll
             for (int r = 0; r < 16; ++r) red[w][t][r][lane] = y[r];
         } else {
-            mmq_epilogue<AB>(P, tend, rope, tok0 + 32 * t, lane, row, y, P.epi, P.A.rows);
+            mmq_epilogue<AB>(P, tend, rope, tok0 + 32 * t, lane, row, y, P.epi, P.A.rows, P.out);
         }
     }
     if (KSPLIT == 1) continue;
@@ -474,14 +490,15 @@ __global__ __launch_bounds__(256, OCC) void mmq32_t(const GemmParams P, const Ac
     float v[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) v[r] = ((red[0][t][r][lane] + red[1][t][r][lane]) + red[2][t][r][lane]) + red[3][t][r][lane];
-    mmq_epilogue<AB>(P, tend, rope, tok0 + 32 * t, lane, row, v, P.epi, P.A.rows);
+    mmq_epilogue<AB>(P, tend, rope, tok0 + 32 * t, lane, row, v, P.epi, P.A.rows, P.out);
   }
 }
 
 // The epilogue of one 32-token x 32-row D tile (v: this lane's 16 results).
 template <bool AB>
 __device__ __forceinline__ void mmq_epilogue(const GemmParams& P, int tend, const float2* rope, int ttok0,
-                                             int lane, int row, const float v[16], int epi, int nrows) {
+                                             int lane, int row, const float v[16], int epi, int nrows,
+                                             float* out) {
     const int col = lane & 31, h = lane >> 5;
     const bool roped = epi == EPI_ROPE_Q || epi == EPI_ROPE_K;
 #pragma unroll
@@ -491,7 +508,7 @@ __device__ __forceinline__ void mmq_epilogue(const GemmParams& P, int tend, cons
         if (tok >= tend) continue;
         if (AB) {
             if (col >= 16 || row >= nrows) continue;
-            P.out[(long long)tok * P.out_stride + row] = silu(v[r]) * pv;   // silu(gate) * up
+            out[(long long)tok * P.out_stride + row] = silu(v[r]) * pv;   // silu(gate) * up
             continue;
         }
         if (row >= nrows) continue;
@@ -506,10 +523,10 @@ __device__ __forceinline__ void mmq_epilogue(const GemmParams& P, int tend, cons
         const int* tp = P.tokpos + tok * 4;
         switch (epi) {
         case EPI_STORE:
-        case EPI_ROPE_Q: P.out[(long long)tok * P.out_stride + row] = o; break;
+        case EPI_ROPE_Q: out[(long long)tok * P.out_stride + row] = o; break;
         case EPI_ADD: {
             const long long i = (long long)tok * P.out_stride + row;
-            P.out[i] = o + P.resid[i];
+            out[i] = o + P.resid[i];
             break;
         }
         case EPI_ROPE_K: {
@@ -619,6 +636,11 @@ void mmq2_t(const GemmParams P, const ActQ8 act, const float2* rope, const MmqSe
         if (i < S.n) nrb += ((AB ? (S.rows[i] + 15) / 16 : (S.rows[i] + 31) / 32) + RT - 1) / RT;
     const int ntb = (act.npad + 127) / 128;           // token blocks
     const int TB = mmq32_tile_bytes_d(T);
+    // split-K: the grid's second half takes the upper superblocks (kh 1)
+    const int nbid = P.ksplit == 2 ? (int)gridDim.x / 2 : (int)gridDim.x;
+    const int kh = (int)blockIdx.x / nbid, bid = (int)blockIdx.x % nbid;
+    const int nbh = (nb + 1) / 2;
+    const int sb0 = P.ksplit == 2 && kh ? nbh : 0, sb1 = P.ksplit == 2 && !kh ? nbh : nb;
     int rb, tb_b, tb_e, base, tend, grp_e = 0;
     if (P.grp) {
         // grouped (MoE): blockIdx -> (token block, expert, row block), token block slowest: the
@@ -626,7 +648,7 @@ void mmq2_t(const GemmParams P, const ActQ8 act, const float2* rope, const MmqSe
         // after them, and a block past its expert's tokens exits
         const int nrb8 = (nrb + 7) / 8 * 8;
         const int per = nrb8 * P.grp_n;
-        const int tbi = (int)blockIdx.x / per, rem = (int)blockIdx.x % per;
+        const int tbi = bid / per, rem = bid % per;
         const int e = rem / nrb8;
         grp_e = e;
         rb = rem % nrb8;
@@ -639,7 +661,7 @@ void mmq2_t(const GemmParams P, const ActQ8 act, const float2* rope, const MmqSe
         tb_e = tbi + 1;
     } else {
         // blockIdx -> (row block, token block): the token blocks of a row block on one XCD
-        const int b = blockIdx.x, xcd = b & 7, slot = b >> 3;
+        const int b = bid, xcd = b & 7, slot = b >> 3;
         rb = (slot / ntb) * 8 + xcd;
         tb_b = slot % ntb;
         tb_e = tb_b + 1;
@@ -729,16 +751,16 @@ void mmq2_t(const GemmParams P, const ActQ8 act, const float2* rope, const MmqSe
 #pragma unroll
     for (int e = 0; e < 16; ++e) y[0][e] = 0.0f;
 
-    copy_stage(0, 0);
+    copy_stage(sb0, NST == 2 ? (sb0 & 1) : 0);
 #pragma unroll 1
-    for (int sb = 0; sb < nb; ++sb) {
+    for (int sb = sb0; sb < sb1; ++sb) {
         // this wave's copy of superblock sb landed, then the workgroup's (barrier; LDS-DMA is a
         // pending LDS write on the VM counter).  Past the barrier every wave is done with
         // superblock sb - 1, whose stage takes the copy of sb + 1 (in flight during this step)
         // and whose operand planes take this step's decode.
         __builtin_amdgcn_s_waitcnt((0x7 << 4) | (0xF << 8));   // vmcnt(0)
         __builtin_amdgcn_s_barrier();
-        if (NST == 2 && sb + 1 < nb && (P.diag != 2 || sb == 0)) copy_stage(sb + 1, (sb + 1) & 1);
+        if (NST == 2 && sb + 1 < sb1 && (P.diag != 2 || sb == sb0)) copy_stage(sb + 1, (sb + 1) & 1);
         if (P.diag == 1) continue;
         const lchar* stg = (const lchar*)(smem + (NST == 2 ? (sb & 1) : 0) * C::STAGE);
         const lchar* A0 = stg + C::A_OFF + w * 8192 + lane * 16;       // this wave's token tile
@@ -925,7 +947,7 @@ void mmq2_t(const GemmParams P, const ActQ8 act, const float2* rope, const MmqSe
             }
         }
         __builtin_amdgcn_s_waitcnt((0xF) | (0x3 << 14) | (0x7 << 4));   // lgkmcnt(0): this wave's LDS reads done
-        if (NST == 1 && sb + 1 < nb) {   // the one stage is free once every wave is past it
+        if (NST == 1 && sb + 1 < sb1) {   // the one stage is free once every wave is past it
             __builtin_amdgcn_s_barrier();
             copy_stage(sb + 1, 0);
         }
@@ -934,7 +956,12 @@ void mmq2_t(const GemmParams P, const ActQ8 act, const float2* rope, const MmqSe
     const int rt = rb * RT + wr;
     if (w < ntt && rt < nrt) {
         const int row = AB ? rt * 16 + (col & 15) : rt * 32 + col;
-        mmq_epilogue<AB>(P, tend, rope, tok0 + 32 * w, lane, row, y[0], epi_s, rows_s);
+        // split-K: this half's partial sums, stored plainly; else the segment's epilogue
+        if (P.ksplit == 2)
+            mmq_epilogue<AB>(P, tend, rope, tok0 + 32 * w, lane, row, y[0], EPI_STORE, rows_s,
+                             P.part + (long long)kh * P.ntok * P.out_stride);
+        else
+            mmq_epilogue<AB>(P, tend, rope, tok0 + 32 * w, lane, row, y[0], epi_s, rows_s, P.out);
     }
   }
 }
@@ -944,17 +971,18 @@ template <int T, int NST> constexpr int m2_lds() { return M2<T>::lds(NST); }
 }  // namespace mmq
 
 void launch_quant_act(const float* x, int x_stride, const float* norm_w, float eps, const ActQ8& a, hipStream_t s,
-                      const int* rows) {
+                      const int* rows, const float* part) {
     if (a.K % 256) throw Error("quant_act: K must be a multiple of 256");
+    if (part && (rows || x_stride != a.K)) throw Error("quant_act: split-K partials take a dense [ntok][K] x");
     // (more than UB_MAX rows only for the MoE rows of a batch: one per (token, slot), padded)
     if (a.npad % 32 || a.ntok > a.npad || a.npad > 4 * UB_MAX) throw Error("quant_act: bad token count");
     if (a.K > 65536) throw Error("quant_act: K past 65536");
     // MI_QA_W: waves per token row, 16 (default) or 4
     static const int qaw = getenv("MI_QA_W") ? atoi(getenv("MI_QA_W")) : 16;
     if (qaw == 4 && a.K <= 4 * 16 * 256)
-        hipLaunchKernelGGL(mmq::quant_act_kernel<4>, dim3(a.npad), dim3(256), 0, s, x, x_stride, norm_w, eps, a, rows);
+        hipLaunchKernelGGL(mmq::quant_act_kernel<4>, dim3(a.npad), dim3(256), 0, s, x, x_stride, norm_w, eps, a, rows, part);
     else
-        hipLaunchKernelGGL(mmq::quant_act_kernel<16>, dim3(a.npad), dim3(1024), 0, s, x, x_stride, norm_w, eps, a, rows);
+        hipLaunchKernelGGL(mmq::quant_act_kernel<16>, dim3(a.npad), dim3(1024), 0, s, x, x_stride, norm_w, eps, a, rows, part);
     MI_HIP(hipGetLastError());
 }
 
@@ -999,7 +1027,10 @@ void launch_mmq2(const GemmParams& p, const mmq::MmqSegs& S, const ActQ8& act, c
     for (int i = 0; i < S.n; ++i) nrb += ((ab ? (S.rows[i] + 15) / 16 : (S.rows[i] + 31) / 32) + RT - 1) / RT;
     const int ntb = (act.npad + 127) / 128;
     // grouped (MoE): a workgroup per (token block, expert, row block)
-    const int g2 = (nrb + 7) / 8 * 8 * (p.grp ? p.grp_n * ((max(p.grp_max, 1) + 127) / 128) : ntb);
+    const int g1 = (nrb + 7) / 8 * 8 * (p.grp ? p.grp_n * ((max(p.grp_max, 1) + 127) / 128) : ntb);
+    if (p.ksplit == 2 && (p.grp || p.pair == PAIR_AB || p.epi != EPI_ADD || !p.part || S.n != 1 || p.A.nb < 2))
+        throw Error("mmq2: split-K is for a single EPI_ADD matrix with a partials buffer");
+    const int g2 = g1 * (p.ksplit == 2 ? 2 : 1);
     // MI_MMQ2_NST: 1 = one stage, two workgroups per CU; 2 = two stages, one workgroup per CU;
     // 0 (default) = one stage when the grid fills two workgroups per CU, else two.  7B 512-token
     // prefill, NST 1 vs 2: 15.5 vs 16.8 ms (same box, scripts/ab_prefill.sh)
@@ -1067,7 +1098,10 @@ void launch_mmq32_multi(const GemmParams* ps, int n, const ActQ8& act, const flo
     launch_mmq2(ps[0], S, act, rope, s);
 }
 
+bool mmq2_active() { return mmq2_enabled(); }
+
 void launch_mmq32(const GemmParams& p, const ActQ8& act, const float2* rope, hipStream_t s) {
+    if (p.ksplit == 2 && !mmq2_enabled()) throw Error("mmq32: split-K needs the mmq2 path");
     if (!mmq32_supported(p.A.type)) throw Error("mmq32: Q4_K / Q5_K / Q6_K / Q8_0 only");
     if ((p.A.type == T_Q8_0) != (act.q80 != 0)) throw Error("mmq32: Q8_0 weights take Q8_0 activations, k-quants Q8_K");
     if (act.K != p.K || p.A.K != p.K) throw Error("mmq32: activation length differs from K");
