@@ -665,7 +665,7 @@ Ctx::Ctx(Model* model, uint32_t nctx, uint32_t nbatch, uint32_t nubatch) : m(mod
             MI_HIP(hipMalloc(&ub_rope, (size_t)UB_MAX * std::max(1, hp.n_rot / 2) * sizeof(float2)));
             // split-K partials of the residual GEMMs (WO, FFN down) of dense models
             static const bool ksplit_env = getenv("MI_MMQ_KSPLIT") == nullptr || atoi(getenv("MI_MMQ_KSPLIT")) != 0;
-            if (ksplit_env && hp.n_expert == 0 && mmq2_active())
+            if (ksplit_env && mmq2_active())
                 MI_HIP(hipMalloc(&ub_part, (size_t)2 * UB_MAX * hp.n_embd * sizeof(float)));
         }
         // MoE prompts need the MFMA path (the v_dot4 GEMM has no routed-expert form)
@@ -1257,11 +1257,11 @@ void Ctx::decode_batch(const int32_t* tokens, int n) {
 // launch for the experts' gate/up + SwiGLU and one for their down projections (a workgroup per
 // (expert, row tile) over that expert's token tiles), then every token's x += w0*y0 + w1*y1 in
 // slot order (launch_moe_combine, the decode GEMV's EPI_MOE_DOWN arithmetic).  No host round trip.
-void Ctx::moe_ffn_batch(int l, int nt) {
+void Ctx::moe_ffn_batch(int l, int nt, const float* pend) {
     const HParams& hp = m->hp;
     const Layer& L = m->layers[l];
     const int U = hp.n_expert_used, E = hp.n_expert;
-    RouterParams rp{xb, L.ffn_norm, hp.eps, L.router, hp.n_embd, E, U, sel_b, selw_b, hp.n_embd};
+    RouterParams rp{xb, L.ffn_norm, hp.eps, L.router, hp.n_embd, E, U, sel_b, selw_b, hp.n_embd, pend, nt};
     launch_router_multi(rp, nt, stream);
     const int cap = moe_rows_cap(nt * U, E);
     launch_moe_group(sel_b, nt * U, U, E, moe_grp, moe_rows, moe_rowsel, moe_pos, cap, stream);
@@ -1421,7 +1421,8 @@ void Ctx::decode_ubatch(const int32_t* tokens, int n, bool all) {
                 launch_mmq32(p, act, ub_rope, stream);
             }
             if (hp.n_expert > 0) {   // routed experts (build_moe_ffn) + residual
-                moe_ffn_batch(l, nt);
+                moe_ffn_batch(l, nt, pend);
+                pend = nullptr;
                 continue;
             }
             {   // FFN gate/up + SwiGLU

@@ -264,7 +264,7 @@ struct Ctx {
     int8_t* moe_q = nullptr;            // the rows' Q8_K / Q8_0 activations (moe_rows_cap rows)
     float* moe_dT = nullptr;
     int8_t* moe_bsb = nullptr;
-    void moe_ffn_batch(int l, int nt);
+    void moe_ffn_batch(int l, int nt, const float* pend = nullptr);
     const float* out_row(int row) const;   // device logits of output row `row` (-1: the last)
     hipGraphExec_t build_graph(bool with_logits, int seg);
     void invalidate_graphs();

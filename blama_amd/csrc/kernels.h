@@ -252,6 +252,10 @@ struct RouterParams {
     int* sel;                  // [token][n_used]
     float* selw;
     long long x_stride;        // elements between token rows (launch_router_multi)
+    // (batch, optional) split-K partials of the WO GEMM that produced x, [2][ntok][n_embd]:
+    // x = (p0 + p1) + x first, written back (GemmParams::ksplit)
+    const float* part;
+    int part_ntok;
 };
 void launch_router(const RouterParams& p, hipStream_t s);
 // the router of ntok token rows x[t * x_stride] -> sel/selw [t][n_used] (one workgroup each)

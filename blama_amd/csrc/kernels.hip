@@ -1249,6 +1249,13 @@ __global__ __launch_bounds__(256) void router_kernel(const RouterParams P0) {
     P.sel += blockIdx.x * P.n_used;
     P.selw += blockIdx.x * P.n_used;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (P.part) {   // the split WO's halves: x = (p0 + p1) + x, written back for the experts
+        const float* p0 = P.part + (long long)blockIdx.x * P.n_embd;
+        const float* p1 = P.part + ((long long)P.part_ntok + blockIdx.x) * P.n_embd;
+        float* xw = const_cast<float*>(P.x);
+        for (int i = tid; i < P.n_embd; i += 256) xw[i] = (p0[i] + p1[i]) + xw[i];
+        __syncthreads();
+    }
     double s = 0.0;
     for (int i = tid; i < P.n_embd; i += 256) s += (double)(P.x[i] * P.x[i]);
     s = wave_sum_d(s);
