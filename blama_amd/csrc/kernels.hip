@@ -1243,6 +1243,8 @@ void launch_gather(const float* logits, const int* ids, int n, float* out, hipSt
 __global__ __launch_bounds__(256) void router_kernel(const RouterParams P0) {
     __shared__ double redd[4];
     __shared__ float logit[64];
+    __shared__ float prs[64], topp[64];
+    __shared__ int topi[64];
     // token blockIdx.x of a batch (launch_router_multi); one token for the decode step
     RouterParams P = P0;
     P.x += (long long)blockIdx.x * P.x_stride;
@@ -1273,23 +1275,40 @@ __global__ __launch_bounds__(256) void router_kernel(const RouterParams P0) {
         if (lane == 0) logit[e] = acc;
     }
     __syncthreads();
-    if (tid == 0) {
-        float mx = -INFINITY;
-        for (int e = 0; e < P.n_expert; ++e) mx = fmaxf(mx, logit[e]);
-        float pr[64];
+    // softmax over the experts and the top n_used, in wave 0 with one lane per expert (per-thread
+    // arrays here would live in scratch memory: ~45 us per call, measured)
+    if (wave == 0) {
+        const int E = P.n_expert;
+        const float lg = lane < E ? logit[lane] : -INFINITY;
+        float mx = lg;   // the max is order-free
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));
+        const float pe = lane < E ? expf(lg - mx) : 0.0f;
+        prs[lane] = pe;
+        __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+        __builtin_amdgcn_wave_barrier();
+        // soft_max's double sum in expert order, then p = e * (1/sum)
         double sum = 0.0;
-        for (int e = 0; e < P.n_expert; ++e) { pr[e] = expf(logit[e] - mx); sum += (double)pr[e]; }
+        for (int e = 0; e < E; ++e) sum += (double)prs[e];
         const float inv = (float)(1.0 / sum);
-        for (int e = 0; e < P.n_expert; ++e) pr[e] = pr[e] * inv;
-        // ggml_argsort (desc) selection order, then ggml_top_k's first n_used
-        int idx[64];
-        for (int e = 0; e < P.n_expert; ++e) idx[e] = e;
-        for (int a = 0; a < P.n_expert; ++a)
-            for (int b = a + 1; b < P.n_expert; ++b)
-                if (pr[idx[a]] < pr[idx[b]]) { int t = idx[a]; idx[a] = idx[b]; idx[b] = t; }
-        float wsum = 0.0f;
-        for (int k = 0; k < P.n_used; ++k) wsum += pr[idx[k]];
-        for (int k = 0; k < P.n_used; ++k) { P.sel[k] = idx[k]; P.selw[k] = pr[idx[k]] / wsum; }
+        const float pr = pe * inv;
+        // ggml_argsort (desc; the selection sort above kept ties in index order) as a rank
+        int rank = 0;
+        for (int e = 0; e < E; ++e) {
+            const float pq = __shfl(pr, e, 64);
+            rank += (pq > pr || (pq == pr && e < lane)) ? 1 : 0;
+        }
+        if (lane < E && rank < P.n_used) {
+            topi[rank] = lane;
+            topp[rank] = pr;
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_wave_barrier();
+        if (lane == 0) {
+            float wsum = 0.0f;
+            for (int k = 0; k < P.n_used; ++k) wsum += topp[k];
+            for (int k = 0; k < P.n_used; ++k) { P.sel[k] = topi[k]; P.selw[k] = topp[k] / wsum; }
+        }
     }
 }
 
