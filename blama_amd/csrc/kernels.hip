@@ -1258,19 +1258,56 @@ __global__ __launch_bounds__(256) void router_kernel(const RouterParams P0) {
         for (int i = tid; i < P.n_embd; i += 256) xw[i] = (p0[i] + p1[i]) + xw[i];
         __syncthreads();
     }
+    // every load of a phase issued before its arithmetic (a serial loop of dependent loads took
+    // ~40 us per token, measured): the row as float4 per lane, kept in registers (n_embd <= 4096)
+    constexpr int RK = 16;
+    const f32x4* x4 = reinterpret_cast<const f32x4*>(P.x);
+    const f32x4* n4 = reinterpret_cast<const f32x4*>(P.norm_w);
+    const int nk = P.n_embd / 256;   // float4 per lane
+    f32x4 xv[RK];
+#pragma unroll
+    for (int k = 0; k < RK; ++k)
+        if (k < nk) xv[k] = x4[k * 64 + lane];
     double s = 0.0;
-    for (int i = tid; i < P.n_embd; i += 256) s += (double)(P.x[i] * P.x[i]);
-    s = wave_sum_d(s);
-    if (lane == 0) redd[wave] = s;
-    __syncthreads();
-    const double tot = ((redd[0] + redd[1]) + redd[2]) + redd[3];
-    const float mean = (float)(tot / (double)P.n_embd);
+#pragma unroll
+    for (int k = 0; k < RK; ++k)
+        if (k < nk) {
+            s += (double)(xv[k].x * xv[k].x);
+            s += (double)(xv[k].y * xv[k].y);
+            s += (double)(xv[k].z * xv[k].z);
+            s += (double)(xv[k].w * xv[k].w);
+        }
+    s = wave_sum_d(s);   // (every wave holds the whole row: each computes the same sum)
+    const float mean = (float)(__shfl(s, 0, 64) / (double)P.n_embd);
     const float scale = 1.0f / sqrtf(mean + P.eps);
+    (void)redd;
+    {   // x * scale * norm_w, in place
+        f32x4 nv[RK];
+#pragma unroll
+        for (int k = 0; k < RK; ++k)
+            if (k < nk) nv[k] = n4[k * 64 + lane];
+#pragma unroll
+        for (int k = 0; k < RK; ++k)
+            if (k < nk)
+                xv[k] = f32x4{(xv[k].x * scale) * nv[k].x, (xv[k].y * scale) * nv[k].y, (xv[k].z * scale) * nv[k].z,
+                              (xv[k].w * scale) * nv[k].w};
+    }
     // expert e handled by wave e%4: logits = W_e . (x*scale*w)
     for (int e = wave; e < P.n_expert; e += 4) {
-        const float* we = P.w + (long long)e * P.n_embd;
+        const f32x4* we = reinterpret_cast<const f32x4*>(P.w + (long long)e * P.n_embd);
+        f32x4 wv[RK];
+#pragma unroll
+        for (int k = 0; k < RK; ++k)
+            if (k < nk) wv[k] = we[k * 64 + lane];
         float acc = 0.0f;
-        for (int i = lane; i < P.n_embd; i += 64) acc = fmaf(we[i], (P.x[i] * scale) * P.norm_w[i], acc);
+#pragma unroll
+        for (int k = 0; k < RK; ++k)
+            if (k < nk) {
+                acc = fmaf(wv[k].x, xv[k].x, acc);
+                acc = fmaf(wv[k].y, xv[k].y, acc);
+                acc = fmaf(wv[k].z, xv[k].z, acc);
+                acc = fmaf(wv[k].w, xv[k].w, acc);
+            }
         acc = wave_sum(acc);
         if (lane == 0) logit[e] = acc;
     }
@@ -1316,6 +1353,7 @@ void launch_router(const RouterParams& p, hipStream_t s) { launch_router_multi(p
 
 void launch_router_multi(const RouterParams& p, int ntok, hipStream_t s) {
     if (p.n_expert > 64) throw Error("router: too many experts");
+    if (p.n_embd % 256 || p.n_embd > 4096) throw Error("router: n_embd must be a multiple of 256, at most 4096");
     if (ntok < 1) return;
     hipLaunchKernelGGL(router_kernel, dim3(ntok), dim3(256), 0, s, p);
     MI_HIP(hipGetLastError());
