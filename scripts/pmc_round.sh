@@ -15,6 +15,6 @@ cp $CSV $OUT/counter_collection.csv
 python3 scripts/pmc_traffic.py $CSV "gemv_kernel<12, -1, 2, 1, 3, 1>" profiles/${RND}_pmc_ffn.json
 python3 scripts/pmc_traffic.py $CSV "gemv_kernel<12, -1, 1, 1, 4, 0>" profiles/${RND}_pmc_wo.json
 python3 scripts/pmc_traffic.py $CSV "attn_mfma_kernel<128>" profiles/${RND}_pmc_attn_mfma.json
-python3 scripts/pmc_traffic.py $CSV "mmq2_t<12, true>" profiles/${RND}_pmc_mmq_gateup.json
-python3 scripts/pmc_traffic.py $CSV "mmq2_t<14, false>" profiles/${RND}_pmc_mmq_down_q6k.json
+python3 scripts/pmc_traffic.py $CSV "mmq2_t<12, true," profiles/${RND}_pmc_mmq_gateup.json
+python3 scripts/pmc_traffic.py $CSV "mmq2_t<14, false," profiles/${RND}_pmc_mmq_down_q6k.json
 true
