@@ -1132,9 +1132,9 @@ static void gv_prepare(const GemvParams& p, int cap, GvArgs& a, int& grid_out, G
     {
         static const int npro_env = getenv("MI_GEMV_NPRO") ? atoi(getenv("MI_GEMV_NPRO")) : 0;
         const int nb = p.K / 256;
-        // (default 8: 555 vs 548 tok/s against ceil(nb/4) = 4 for the K = 4096 launches, same box;
-        // 2 prologue waves: 455)
-        a.npro = npro_env > 0 ? npro_env : 8;
+        // (default 8 from K = 4096 up: 556 vs 548 tok/s against ceil(nb/4) = 4 on the 7B, same box;
+        // 2 prologue waves: 455.  Narrower K keeps ceil(nb/4), the r04 rule it was measured with)
+        a.npro = npro_env > 0 ? npro_env : (nb >= 16 ? 8 : (nb + 3) / 4);
         a.npro = std::max(1, std::min(a.npro, std::min(GV_NW - 2, nb)));
         static const int touch_env = getenv("MI_GEMV_TOUCH") ? atoi(getenv("MI_GEMV_TOUCH")) : 0;
         a.touch = touch_env;
