@@ -3,7 +3,9 @@
 #include "engine.h"
 
 #include <dlfcn.h>
+#include <execinfo.h>
 #include <fcntl.h>
+#include <signal.h>
 #include <rccl/rccl.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
@@ -36,22 +38,102 @@ struct Rccl {
     decltype(&ncclGroupEnd) gend = nullptr;
     decltype(&ncclCommDestroy) destroy = nullptr;
     decltype(&ncclGetErrorString) err = nullptr;
+    std::string load_error;     // why the library or a symbol is missing (dlerror() read once, here)
 };
 const Rccl& rccl() {
     static const Rccl r = [] {
         Rccl x;
         void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
         if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_LOCAL);
-        if (!h) return x;
+        if (!h) {
+            const char* e = dlerror();
+            x.load_error = e ? e : "dlopen(librccl.so) failed";
+            return x;
+        }
         x.init = reinterpret_cast<decltype(x.init)>(dlsym(h, "ncclCommInitAll"));
         x.bcast = reinterpret_cast<decltype(x.bcast)>(dlsym(h, "ncclBroadcast"));
         x.gstart = reinterpret_cast<decltype(x.gstart)>(dlsym(h, "ncclGroupStart"));
         x.gend = reinterpret_cast<decltype(x.gend)>(dlsym(h, "ncclGroupEnd"));
         x.destroy = reinterpret_cast<decltype(x.destroy)>(dlsym(h, "ncclCommDestroy"));
         x.err = reinterpret_cast<decltype(x.err)>(dlsym(h, "ncclGetErrorString"));
+        if (!x.init || !x.bcast || !x.gstart || !x.gend || !x.destroy) x.load_error = "missing symbols";
         return x;
     }();
     return r;
+}
+// Diagnostic (MI_SEGV_MAPS=1): on SIGSEGV / SIGBUS print the fault address, the faulting PC and
+// every backtrace frame with the mapping that holds it (path + offset, from /proc/self/maps), so
+// the frames of a crash inside the ROCm libraries can be symbolised offline (llvm-symbolizer
+// --obj=<path> <offset>); then the default action.  Installed when a context is created, i.e.
+// after any profiler's own handler.
+char g_maps[1 << 20];
+void segv_out(const char* s) { ssize_t r = write(2, s, strlen(s)); (void)r; }
+void segv_where(const char* tag, unsigned long long a, int nmaps) {
+    char line[512];
+    const char* p = g_maps;
+    const char* end = g_maps + nmaps;
+    const char* prev = nullptr;
+    while (p < end) {
+        const char* nl = (const char*)memchr(p, '\n', end - p);
+        if (!nl) nl = end;
+        unsigned long long lo = 0, hi = 0, off = 0;
+        if (sscanf(p, "%llx-%llx %*s %llx", &lo, &hi, &off) == 3 && a >= lo && a < hi) {
+            const char* path = (const char*)memchr(p, '/', nl - p);
+            const int pl = path ? (int)(nl - path) : 0;
+            snprintf(line, sizeof line, "mi_segv %s 0x%llx = %.*s +0x%llx (mapping %.*s)\n", tag, a, pl, path ? path : "",
+                     a - lo + off, (int)(nl - p), p);
+            segv_out(line);
+            return;
+        }
+        if (lo > a && prev) {   // unmapped: the mappings on either side
+            const char* pn = (const char*)memchr(prev, '\n', end - prev);
+            snprintf(line, sizeof line, "mi_segv %s 0x%llx unmapped, between\n  %.*s\n  %.*s\n", tag, a,
+                     (int)((pn ? pn : end) - prev), prev, (int)(nl - p), p);
+            segv_out(line);
+            return;
+        }
+        prev = p;
+        p = nl + 1;
+    }
+    snprintf(line, sizeof line, "mi_segv %s 0x%llx not found in maps\n", tag, a);
+    segv_out(line);
+}
+void segv_handler(int sig, siginfo_t* si, void* ucv) {
+    int fd = open("/proc/self/maps", O_RDONLY);
+    int n = 0;
+    if (fd >= 0) {
+        for (ssize_t r; n < (int)sizeof(g_maps) - 1 && (r = read(fd, g_maps + n, sizeof(g_maps) - 1 - n)) > 0;) n += (int)r;
+        close(fd);
+    }
+    char line[128];
+    snprintf(line, sizeof line, "mi_segv signal %d fault address %p\n", sig, si ? si->si_addr : nullptr);
+    segv_out(line);
+    segv_where("fault", (unsigned long long)(si ? si->si_addr : nullptr), n);
+    const ucontext_t* uc = reinterpret_cast<const ucontext_t*>(ucv);
+    if (uc) segv_where("pc", (unsigned long long)uc->uc_mcontext.gregs[REG_RIP], n);
+    void* fr[64];
+    const int nf = backtrace(fr, 64);
+    for (int i = 0; i < nf; ++i) {
+        char tag[16];
+        snprintf(tag, sizeof tag, "frame%02d", i);
+        segv_where(tag, (unsigned long long)fr[i], n);
+    }
+    signal(sig, SIG_DFL);
+    raise(sig);
+}
+void segv_maps_install() {
+    static bool done = false;
+    if (done || !getenv("MI_SEGV_MAPS")) return;
+    done = true;
+    void* warm[2];
+    backtrace(warm, 2);   // loads the unwinder before any signal
+    struct sigaction sa;
+    memset(&sa, 0, sizeof sa);
+    sa.sa_sigaction = segv_handler;
+    sa.sa_flags = SA_SIGINFO;
+    sigaction(SIGSEGV, &sa, nullptr);
+    sigaction(SIGBUS, &sa, nullptr);
+    segv_out("mi_segv: handler installed\n");
 }
 void nccl_ck(ncclResult_t r, const char* what) {
     if (r != ncclSuccess) throw Error(std::string("RCCL ") + what + ": " + (rccl().err ? rccl().err(r) : "error"));
@@ -248,7 +330,7 @@ int32_t mi_model_replicate(mi_model* const* models, int32_t n) {
         if (devs.size() > 1 || self_recv > 0) {
             const Rccl& R = rccl();
             if (!R.init || !R.bcast || !R.gstart || !R.gend || !R.destroy)
-                throw Error(std::string("replicate: librccl not usable: ") + (dlerror() ? dlerror() : "missing symbols"));
+                throw Error("replicate: librccl not usable: " + R.load_error);
             const int nd = (int)devs.size();
             guard.comms.assign(nd, nullptr);
             replicate_log("ncclCommInitAll over " + std::to_string(nd) + " device(s)");
@@ -313,6 +395,7 @@ int32_t mi_model_type_histogram(const mi_model* m, int64_t* out, int32_t n) {
 mi_ctx* mi_ctx_create(mi_model* model, uint32_t n_ctx, uint32_t n_batch, uint32_t n_ubatch) {
     try {
         if (!model) throw Error("null model");
+        segv_maps_install();
         auto* c = new mi_ctx();
         try {
             c->impl.reset(new Ctx(&model->impl, n_ctx, n_batch, n_ubatch));

@@ -13,6 +13,7 @@ tensor data.  This mirrors what ``llama_model_load_from_file``
 from __future__ import annotations
 
 import io
+import os
 import struct
 from dataclasses import dataclass
 
@@ -137,6 +138,7 @@ class GGUFWriter:
         buf = np.empty(total, np.uint8)
         buf[: len(hdr)] = np.frombuffer(hdr, np.uint8)
         prev_end = len(hdr)
+        jobs = []
         for (name, gt, shape, data), off in zip(self.tensors, offs):
             a = len(hdr) + off
             n = tensor_nbytes(gt, shape)
@@ -145,8 +147,19 @@ class GGUFWriter:
             if data is not None:
                 view[:] = data
             else:
-                fill(name, gt, shape, view)
+                jobs.append((name, gt, shape, view))
             prev_end = a + n
+        # each declared tensor is filled from its own generator (synthetic._rng keys it by name),
+        # so the bytes do not depend on the order or the thread that fills them
+        workers = min(16, os.cpu_count() or 1)
+        if workers > 1 and len(jobs) > 1:
+            from concurrent.futures import ThreadPoolExecutor
+            with ThreadPoolExecutor(workers) as ex:
+                for f in [ex.submit(fill, *j) for j in jobs]:
+                    f.result()
+        else:
+            for j in jobs:
+                fill(*j)
         return buf
 
     def write(self, path: str):

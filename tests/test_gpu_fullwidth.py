@@ -31,6 +31,8 @@ and the run must pass the reference's acceptance gate (t-LogitComparer.cpp:76-78
 score >= 0.95, mean logitSimilarity >= 0.98, top-1 match on every step).  The kernels' own
 arithmetic is checked without this chaos at op level (test_gpu_ops.py: GEMV at these shapes,
 attention at these head shapes)."""
+import warnings
+
 import numpy as np
 import pytest
 
@@ -203,8 +205,10 @@ def test_fullwidth_batched_verification_matches_oracle(gpu_lib, name):
             # ggml order: util.c_alt_floor), i.e. the CPU algorithm itself ranks them either way.
             _, floor = c_alt_floor(buf, 64, prompt, claimed)
             for i, gid, cid, margin in ties:
-                print(f"{name} row {i}: GPU top-1 {gid}, CPU {cid}, CPU margin {margin:.3e}, "
-                      f"CPU reorder floor {floor[i + 1]:.3e}")
+                msg = (f"live-floor waiver: {name} row {i}: GPU top-1 {gid}, CPU {cid}, CPU margin {margin:.3e}, "
+                       f"CPU reorder floor {floor[i + 1]:.3e}")
+                print(msg)
+                warnings.warn(msg)   # listed in pytest's warnings summary, also under -q
                 assert margin <= floor[i + 1], (name, i, gid, cid, margin, floor[i + 1])
                 top1[i] = 1.0
         assert score >= 0.95 and float(np.mean(sims)) >= 0.98 and min(top1) == 1.0, (score, np.mean(sims))
