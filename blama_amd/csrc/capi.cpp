@@ -503,19 +503,6 @@ int32_t mi_prof_read(mi_ctx* c, float* us, int32_t n) {
 }
 int64_t mi_prof_ffn_bytes(const mi_ctx* c) { return c ? c->impl->ffn_bytes() : -1; }
 int64_t mi_prof_bytes(const mi_ctx* c) { return c ? c->impl->prof_bytes : -1; }
-int64_t mi_debug_persist_stamps(mi_ctx* c, uint64_t* out, int64_t n) {
-    try {
-        if (!c || !out) throw Error("null argument");
-        mi::Ctx* x = c->impl.get();
-        return (int64_t)mi::persist_read_stamps(x->pst[1], reinterpret_cast<unsigned long long*>(out), (size_t)n);
-    }
-    MI_TRY(-1)
-}
-int32_t mi_persist_stages(const mi_ctx* c) {
-    if (!c) return -1;
-    const mi::Ctx* x = c->impl.get();
-    return x->persist_ok ? mi::persist_stages(x->pst[1]) : 0;
-}
 int32_t mi_debug_stamps(mi_ctx* c, uint64_t* out, int32_t n_launch) {
     try {
         if (!c || !out) throw Error("null argument");

@@ -539,7 +539,6 @@ std::vector<int> g_attr_done(64, 0);
 namespace {
 struct DevChain {
     std::mutex mu;
-    hipEvent_t ev = nullptr;   // the last persistent step enqueued on the device
     std::atomic<int> nctx{0};  // live contexts on the device (attention co-residency budget)
 };
 DevChain& dev_chain(int device) {
@@ -604,9 +603,6 @@ Ctx::Ctx(Model* model, uint32_t nctx, uint32_t nbatch, uint32_t nubatch) : m(mod
     // GPT-2 prompts run token by token (one decode graph each): its batch kernels (LayerNorm,
     // biases, GELU) are not built
     batch_ok = hp.arch == ARCH_LLAMA && getenv("MI_NO_BATCH") == nullptr;
-    // the persistent step is opt-in (MI_PERSIST=1): measured slower than the graph
-    persist_ok = hp.n_expert == 0 && hp.arch == ARCH_LLAMA && use_graphs && getenv("MI_PERSIST") != nullptr &&
-                 getenv("MI_NO_PERSIST") == nullptr;
     if (batch_ok) {
         // MFMA batch path (decode_ubatch / mmq32) when every layer matrix is mmq32-capable (each
         // matrix reads the activation format of its type: Q8_0 activations for Q8_0 weights, Q8_K
@@ -701,6 +697,7 @@ Ctx::Ctx(Model* model, uint32_t nctx, uint32_t nbatch, uint32_t nubatch) : m(mod
     MI_HIP(hipHostMalloc(&h_logits, (size_t)hp.n_vocab * sizeof(float)));
     MI_HIP(hipHostMalloc(&h_gather, 4096 * sizeof(float)));
     h_cell_pos.assign(n_ctx, 0);
+    sp_ok = sp_setup();
     dev_chain(device).nctx++;
 }
 
@@ -709,11 +706,6 @@ Ctx::~Ctx() {
     hipSetDevice(device);
     if (stream) hipStreamSynchronize(stream);
     invalidate_graphs();
-    for (PersistStep*& p : pst) {
-        persist_free(p);
-        p = nullptr;
-    }
-    if (pbuf) hipFree(pbuf);
     for (auto e : prof_ev) if (e) hipEventDestroy(e);
     for (void* p : {(void*)kcache, (void*)vcache, (void*)kv_scratch, (void*)cell_pos, (void*)tokpos, (void*)x,
                     (void*)q, (void*)attn, (void*)h, (void*)h2, (void*)logits, (void*)cand, (void*)topk_ids,
@@ -723,7 +715,7 @@ Ctx::~Ctx() {
                     (void*)xb, (void*)qb, (void*)attnb, (void*)hb, (void*)tokpos_b, (void*)ub_q, (void*)ub_dT, (void*)ub_bsb, (void*)ub_rope, (void*)ub_part,
                     (void*)ub_q0, (void*)ub_dT0, (void*)yb, (void*)sel_b, (void*)selw_b, (void*)moe_rows, (void*)moe_pos,
                     (void*)moe_rowsel, (void*)moe_grp, (void*)moe_q, (void*)moe_dT, (void*)moe_bsb,
-                    (void*)logits_all, (void*)grows_ids, (void*)grows_out})
+                    (void*)logits_all, (void*)grows_ids, (void*)grows_out, (void*)sp_mem})
         if (p) hipFree(p);
     for (void* p : {(void*)h_tokpos, (void*)h_topk_ids, (void*)h_topk_vals, (void*)h_logits, (void*)h_gather, (void*)h_grows,
                     (void*)h_tokpos_b, (void*)h_attn_xerr})
@@ -745,14 +737,15 @@ long long Ctx::ffn_bytes() const {
     auto mb = [](const QMat& q) { return (long long)q.rows * q.nb * ((long long)block_bytes(q.type) * 256 / block_elems(q.type)); };
     const HParams& hp = m->hp;
     const long long w = hp.n_expert > 0 ? 2 * (mb(L.gate) + mb(L.up)) : mb(L.gate) + mb(L.up);
+    if (sp_ok)   // streaming path: the quantised input read, h written
+        return w + (long long)dv_act_bytes(hp.n_embd, sp[0].fC & 1, sp[0].fC >> 1) + (long long)hp.n_ff * 4;
     const long long act = (long long)hp.n_embd * 4 * 2 + (long long)hp.n_ff * 4 * (hp.n_expert > 0 ? 2 : 1);
     return w + act;   // weights + x and norm weight read + h written
 }
 
 // The ops of one llm_build_llama layer for the token in tokpos, as launch parameters handed to
-// `gemv` (role: 0 QKV, 1 WO, 2 FFN gate/up, 3 FFN down), `attn` and `router`.  The buffers are
-// the graph path's (the residual updated in place) or the persistent step's (every output a
-// buffer of its own, written once per step).
+// `gemv` (role: 0 QKV, 1 WO, 2 FFN gate/up, 3 FFN down), `attn` and `router` (the residual
+// updated in place).
 void Ctx::layer_ops(int l, const LayerBufs& B, const std::function<void(const GemvParams&, int)>& gemv,
                     const std::function<void(const AttnParams&)>& attn,
                     const std::function<void(const RouterParams&)>& router) {
@@ -871,13 +864,254 @@ void Ctx::layer_ops(int l, const LayerBufs& B, const std::function<void(const Ge
     }
 }
 
+namespace {
+// activation formats a set of matrices reads: bit 0 Q8_K (k-quants), bit 1 Q8_0
+int act_fmt(std::initializer_list<int> types) {
+    int f = 0;
+    for (int t : types) f |= t == T_Q8_0 ? 2 : 1;
+    return f;
+}
+}  // namespace
+
+// The streaming decode step's buffers (dense LLaMA; DESIGN.md §4 "dgemv"), and whether every
+// launch of the step has a compiled variant.  MI_DECODE_OLD=1 keeps the gemv_kernel graph.
+bool Ctx::sp_setup() {
+    const HParams& hp = m->hp;
+    if (hp.arch != ARCH_LLAMA || hp.n_expert > 0 || getenv("MI_DECODE_OLD")) return false;
+    if (hp.n_embd % 256 || hp.n_ff % 256 || hp.n_embd > 16384 || hp.n_ff > 16384) return false;
+    if (hp.n_head * hp.head_dim != hp.n_embd) return false;
+    const int nl = hp.n_layer;
+    sp.assign(nl, SpLayer{});
+    sp_fH = act_fmt({m->output.type});
+    size_t off = 0;
+    auto take = [&](size_t bytes) { const size_t o = off; off += (bytes + 255) / 256 * 256; return o; };
+    std::vector<size_t> o(nl * 8);
+    for (int l = 0; l < nl; ++l) {
+        const Layer& L = m->layers[l];
+        SpLayer& b = sp[l];
+        b.fA = 0;
+        for (int g = 0; g < L.n_qkv; ++g) b.fA |= act_fmt({L.qkv[g].type});
+        b.fB = act_fmt({L.wo.type});
+        b.fC = act_fmt({L.gate.type, L.up.type});
+        b.fD = act_fmt({L.down.type});
+        o[l * 8 + 0] = take((size_t)hp.n_embd * 4);
+        o[l * 8 + 1] = take((size_t)hp.n_embd * 4);
+        o[l * 8 + 2] = take((size_t)hp.n_embd * 4);
+        o[l * 8 + 3] = take((size_t)hp.n_ff * 4);
+        o[l * 8 + 4] = take(dv_act_bytes(hp.n_embd, b.fA & 1, b.fA >> 1));
+        o[l * 8 + 5] = take(dv_act_bytes(hp.n_embd, b.fB & 1, b.fB >> 1));
+        o[l * 8 + 6] = take(dv_act_bytes(hp.n_embd, b.fC & 1, b.fC >> 1));
+        o[l * 8 + 7] = take(dv_act_bytes(hp.n_ff, b.fD & 1, b.fD >> 1));
+    }
+    const size_t oH = take(dv_act_bytes(hp.n_embd, sp_fH & 1, sp_fH >> 1));
+    MI_HIP(hipSetDevice(device));
+    MI_HIP(hipMalloc(&sp_mem, off));
+    MI_HIP(hipMemset(sp_mem, 0, off));
+    for (int l = 0; l < nl; ++l) {
+        SpLayer& b = sp[l];
+        b.xw = reinterpret_cast<float*>(sp_mem + o[l * 8 + 0]);
+        b.xd = reinterpret_cast<float*>(sp_mem + o[l * 8 + 1]);
+        b.att = reinterpret_cast<float*>(sp_mem + o[l * 8 + 2]);
+        b.h = reinterpret_cast<float*>(sp_mem + o[l * 8 + 3]);
+        b.aA = sp_mem + o[l * 8 + 4];
+        b.aB = sp_mem + o[l * 8 + 5];
+        b.aC = sp_mem + o[l * 8 + 6];
+        b.aD = sp_mem + o[l * 8 + 7];
+    }
+    sp_aH = sp_mem + oH;
+    // every launch must have a variant: dry-run the step's parameter checks
+    bool ok = true;
+    for (int l = 0; l < nl && ok; ++l) {
+        const Layer& L = m->layers[l];
+        GemvParams p;
+        std::memset(&p, 0, sizeof(p));
+        p.K = hp.n_embd;
+        p.act_in = sp[l].aA;
+        p.act_q8k = sp[l].fA & 1;
+        p.act_q80 = sp[l].fA >> 1;
+        for (int g = 0; g < L.n_qkv && ok;) {
+            p.nseg = 0;
+            for (; g < L.n_qkv && p.nseg < GEMV_MAX_SEG; ++g) {
+                if (p.nseg == 1 && !gemv_pair_supported(p.seg[0].A.type, L.qkv[g].type)) break;
+                p.seg[p.nseg++] = seg_of(L.qkv[g], PAIR_ADJ, EPI_QKV, q);
+            }
+            ok = dgemv_supported(p);
+        }
+        GemvParams w = p;
+        w.nseg = 1;
+        w.seg[0] = seg_of(L.wo, PAIR_ADJ, EPI_ADD, x);
+        w.act_q8k = sp[l].fB & 1;
+        w.act_q80 = sp[l].fB >> 1;
+        ok = ok && dgemv_supported(w);
+        GemvParams gu = w;
+        gu.seg[0] = seg_of(L.gate, PAIR_AB, EPI_SWIGLU, x);
+        gu.seg[0].B = L.up;
+        gu.act_q8k = sp[l].fC & 1;
+        gu.act_q80 = sp[l].fC >> 1;
+        ok = ok && L.gate.type == L.up.type && dgemv_supported(gu);
+        GemvParams d = w;
+        d.K = hp.n_ff;
+        d.seg[0] = seg_of(L.down, PAIR_ADJ, EPI_ADD, x);
+        d.act_q8k = sp[l].fD & 1;
+        d.act_q80 = sp[l].fD >> 1;
+        ok = ok && dgemv_supported(d);
+    }
+    GemvParams hd;
+    std::memset(&hd, 0, sizeof(hd));
+    hd.K = hp.n_embd;
+    hd.nseg = 1;
+    hd.seg[0] = seg_of(m->output, PAIR_ADJ, EPI_STORE, logits);
+    hd.act_in = sp_aH;
+    hd.act_q8k = sp_fH & 1;
+    hd.act_q80 = sp_fH >> 1;
+    ok = ok && dgemv_supported(hd) && attn_quant_supported(hp.n_head, hp.n_head_kv, hp.head_dim);
+    if (!ok) {
+        MI_HIP(hipFree(sp_mem));
+        sp_mem = nullptr;
+        sp.clear();
+    }
+    return ok;
+}
+
+// One batch-1 decode step on the streaming kernels: the embedding (+ layer 0's quantised input),
+// per layer QKV -> attention (+ the WO input quantised) -> WO -> dv_quant(rms_norm * ffn_norm) ->
+// gate/up -> dv_quant(h) -> down -> dv_quant(the next layer's, or the output head's, input), the
+// output head, the top-k.  Profiling segments as enqueue_step's (the gate/up launch of prof_layer
+// carries the event pair).
+void Ctx::enqueue_step_sp(bool with_logits) {
+    const HParams& hp = m->hp;
+    int seg = 0;
+    auto on = [&]() { return seg_filter < 0 || seg_filter == seg; };
+    const float theta_scale = std::pow(hp.rope_base, -2.0f / (float)hp.n_rot);
+    const float kq_scale = 1.0f / std::sqrt((float)hp.head_dim);
+    auto act_out = [&](char* act, int fmt, int K, const float* norm_w) {
+        ActOut t;
+        std::memset(&t, 0, sizeof(t));
+        t.K = K;
+        t.q8k = fmt & 1;
+        t.q80 = fmt >> 1;
+        t.act = act;
+        t.norm_w = norm_w;
+        t.eps = hp.eps;
+        return t;
+    };
+    if (on()) {
+        EmbedParams ep{m->tok_embd, tokpos, x, hp.n_embd, QMat{}, 0, step_ctr};
+        launch_embed_act(ep, act_out(sp[0].aA, sp[0].fA, hp.n_embd, m->layers[0].attn_norm), stream);
+    }
+    const float* x_in = x;
+    for (int l = 0; l < hp.n_layer; ++l) {
+        const Layer& L = m->layers[l];
+        const SpLayer& b = sp[l];
+        __half* kl = kcache + (size_t)l * n_ctx * kv_dim;
+        __half* vl = vcache + (size_t)l * n_ctx * kv_dim;
+        GemvParams base;
+        std::memset(&base, 0, sizeof(base));
+        base.tokpos = tokpos;
+        base.cell_pos = cell_pos;
+        base.head_dim = hp.head_dim;
+        base.kv_dim = kv_dim;
+        base.nslots = 1;
+        base.K = hp.n_embd;
+        {   // Q/K/V + RoPE + KV append
+            GemvParams p = base;
+            p.act_in = b.aA;
+            p.act_q8k = b.fA & 1;
+            p.act_q80 = b.fA >> 1;
+            p.theta_scale = theta_scale;
+            p.freq_scale = hp.freq_scale;
+            p.n_rot = hp.n_rot;
+            p.freq_factors = m->rope_freqs;
+            p.kcache = kl;
+            p.vcache = vl;
+            for (int g = 0; g < L.n_qkv;) {
+                p.nseg = 0;
+                for (; g < L.n_qkv && p.nseg < GEMV_MAX_SEG; ++g) {
+                    if (p.nseg == 1 && !gemv_pair_supported(p.seg[0].A.type, L.qkv[g].type)) break;
+                    GemvSeg& sg = p.seg[p.nseg++];
+                    sg = seg_of(L.qkv[g], PAIR_ADJ, EPI_QKV, q);
+                    sg.nq = L.qkv_nq[g];
+                    sg.nk = L.qkv_nk[g];
+                }
+                if (on()) launch_dgemv(p, stream);
+            }
+        }
+        {   // attention (fused, <= ATTN_SHORT cells); its output quantised for WO
+            AttnParams a{q, kl, vl, tokpos, cell_pos, attn_scores, attn_smax, b.att, hp.n_head, hp.n_head_kv,
+                         hp.head_dim, kv_dim, (int)n_ctx, kq_scale};
+            a.fused = 1;
+            a.act_out = act_out(b.aB, b.fB, hp.n_embd, nullptr);
+            if (on()) launch_attn(a, stream);
+        }
+        {   // output projection + residual, then rms_norm(x) * ffn_norm quantised
+            GemvParams p = base;
+            p.act_in = b.aB;
+            p.act_q8k = b.fB & 1;
+            p.act_q80 = b.fB >> 1;
+            p.nseg = 1;
+            p.seg[0] = seg_of(L.wo, PAIR_ADJ, EPI_ADD, b.xw);
+            p.seg[0].resid = x_in;
+            if (on()) {
+                launch_dgemv(p, stream);
+                launch_dv_quant(b.xw, act_out(b.aC, b.fC, hp.n_embd, L.ffn_norm), stream);
+            }
+        }
+        {   // FFN gate/up + SwiGLU, then h quantised
+            GemvParams p = base;
+            p.act_in = b.aC;
+            p.act_q8k = b.fC & 1;
+            p.act_q80 = b.fC >> 1;
+            p.nseg = 1;
+            p.seg[0] = seg_of(L.gate, PAIR_AB, EPI_SWIGLU, b.h);
+            p.seg[0].B = L.up;
+            if (l == prof_layer) seg = 1;
+            const bool timed = l == prof_layer && seg_filter == 1;
+            if (on()) launch_dgemv(p, stream, timed ? prof_ev[0] : nullptr, timed ? prof_ev[1] : nullptr);
+            if (l == prof_layer) seg = 2;
+            if (on()) launch_dv_quant(b.h, act_out(b.aD, b.fD, hp.n_ff, nullptr), stream);
+        }
+        {   // FFN down + residual, then the next layer's (or the output head's) input quantised
+            GemvParams p = base;
+            p.K = hp.n_ff;
+            p.act_in = b.aD;
+            p.act_q8k = b.fD & 1;
+            p.act_q80 = b.fD >> 1;
+            p.nseg = 1;
+            p.seg[0] = seg_of(L.down, PAIR_ADJ, EPI_ADD, b.xd);
+            p.seg[0].resid = b.xw;
+            if (on()) {
+                launch_dgemv(p, stream);
+                if (l + 1 < hp.n_layer)
+                    launch_dv_quant(b.xd, act_out(sp[l + 1].aA, sp[l + 1].fA, hp.n_embd, m->layers[l + 1].attn_norm),
+                                    stream);
+                else if (with_logits)
+                    launch_dv_quant(b.xd, act_out(sp_aH, sp_fH, hp.n_embd, m->output_norm), stream);
+            }
+        }
+        x_in = b.xd;
+    }
+    if (with_logits && on()) {
+        GemvParams p;
+        std::memset(&p, 0, sizeof(p));
+        p.K = hp.n_embd;
+        p.nseg = 1;
+        p.seg[0] = seg_of(m->output, PAIR_ADJ, EPI_STORE, logits);
+        p.act_in = sp_aH;
+        p.act_q8k = sp_fH & 1;
+        p.act_q80 = sp_fH >> 1;
+        launch_dgemv(p, stream);
+        TopkParams tp{logits, hp.n_vocab, cand, topk_ids, topk_vals, d_h_topk_ids, d_h_topk_vals};
+        launch_topk(tp, stream);
+    }
+}
+
 // One decode step for the token in tokpos (batch 1): the llm_build_llama graph.
 // With seg_filter >= 0 only the ops of that profiling segment are enqueued
 // (0: up to layer prof_layer's FFN gate/up, 1: that launch, 2: the rest).
 void Ctx::enqueue_step(bool with_logits) {
     const HParams& hp = m->hp;
-    if (attn_fused && persist_step(with_logits)) {
-        enqueue_step_persist(with_logits);
+    if (attn_fused && sp_ok) {
+        enqueue_step_sp(with_logits);
         return;
     }
     int seg = 0;
@@ -931,94 +1165,6 @@ void Ctx::enqueue_step(bool with_logits) {
             });
     }
     if (with_logits && on()) enqueue_output(x, stamp());
-}
-
-// The persistent form of a step (contexts within ATTN_SHORT cells): the embedding, ONE launch of
-// the layers and the output head (gemv.hip decode_step_kernel), the top-k.  Profiling segments:
-// 0 the embedding, 1 the persistent launch (eager, with the event pair), 2 the top-k.
-void Ctx::enqueue_step_persist(bool with_logits) {
-    const HParams& hp = m->hp;
-    auto on = [&](int seg) { return seg_filter < 0 || seg_filter == seg; };
-    EmbedParams ep{m->tok_embd, tokpos, x, hp.n_embd, m->pos_embd, 0, step_ctr};
-    if (on(0)) launch_embed(ep, stream);
-    const bool timed = seg_filter == 1 && prof_layer >= 0;
-    if (on(1)) persist_launch(pst[with_logits], stream, timed ? prof_ev[0] : nullptr, timed ? prof_ev[1] : nullptr);
-    if (with_logits && on(2)) {
-        TopkParams tp{logits, hp.n_vocab, cand, topk_ids, topk_vals, d_h_topk_ids, d_h_topk_vals};
-        launch_topk(tp, stream);
-    }
-}
-
-// Builds the persistent stage table of a step on first use; false when the step has no
-// persistent form (not opted in, MoE, GPT-2, a quant type mix outside the compiled classes).
-bool Ctx::persist_step(bool with_logits) {
-    if (!persist_ok) return false;
-    if (pst[with_logits]) return true;
-    const HParams& hp = m->hp;
-    const size_t hq = (size_t)hp.n_head * hp.head_dim;
-    const size_t per_layer = 2 * hq + 2 * (size_t)hp.n_embd + (size_t)hp.n_ff;
-    if (!pbuf) {
-        MI_HIP(hipSetDevice(device));
-        MI_HIP(hipMalloc(&pbuf, per_layer * hp.n_layer * sizeof(float)));
-    }
-    PersistStep* p = persist_new(device);
-    bool ok = p != nullptr;
-    try {
-        const float* xin = x;
-        for (int l = 0; ok && l < hp.n_layer; ++l) {
-            float* b = pbuf + per_layer * l;
-            const LayerBufs B{xin, b, b + hq, b + 2 * hq, b + 2 * hq + 2 * hp.n_embd, nullptr, b + 2 * hq + hp.n_embd};
-            const int saved = attn_fused;
-            attn_fused = 1;
-            layer_ops(
-                l, B, [&](const GemvParams& g, int) { ok = ok && persist_add_gemv(p, g); },
-                [&](const AttnParams& a) { ok = ok && persist_add_attn(p, a, B.po); },
-                [&](const RouterParams&) { ok = false; });
-            attn_fused = saved;
-            xin = B.xf;
-        }
-        if (ok && with_logits) {
-            GemvParams g;
-            std::memset(&g, 0, sizeof(g));
-            g.pro = PRO_RMSNORM;
-            g.nslots = 1;
-            g.x[0] = xin;
-            g.norm_w = m->output_norm;
-            g.eps = hp.eps;
-            g.K = hp.n_embd;
-            g.tokpos = tokpos;
-            g.nseg = 1;
-            g.seg[0] = seg_of(m->output, PAIR_ADJ, EPI_STORE, logits);
-            ok = persist_add_gemv(p, g);
-        }
-        ok = ok && persist_finalize(p);
-    } catch (const std::exception&) {
-        ok = false;
-    }
-    if (!ok) {
-        persist_free(p);
-        persist_ok = false;
-        return false;
-    }
-    pst[with_logits] = p;
-    return true;
-}
-
-// A persistent step whose grid barrier timed out (its grid was not co-resident: another
-// process's persistent kernel on the same GPU) left garbage behind: reject it and stop using
-// the persistent form in this context.
-void Ctx::check_persist() {
-    for (PersistStep* p : pst)
-        if (persist_aborted(p)) {
-            for (PersistStep* r : pst)
-                if (r) persist_reset(r, stream);
-            persist_ok = false;
-            invalidate_graphs();
-            logits_valid = false;
-            throw Error("persistent decode step aborted (its grid was not co-resident; another process's "
-                        "persistent kernel on this GPU?): the step's results are invalid; persistent steps are "
-                        "off for this context (MI_NO_PERSIST=1 disables them everywhere)");
-        }
 }
 
 // One GPT-2 block (llm_build_gpt2, src/llama-model.cpp b5187) of the decode step:
@@ -1120,7 +1266,6 @@ void Ctx::enqueue_output(const float* xrow, unsigned long long* stamps_slab) {
 
 hipGraphExec_t Ctx::build_graph(bool with_logits, int seg) {
     hipGraph_t g = nullptr;
-    if (attn_fused) persist_step(with_logits);   // allocations and uploads cannot be captured
     seg_filter = seg;
     MI_HIP(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
     try {
@@ -1547,29 +1692,13 @@ int Ctx::decode(const int32_t* tokens, int n, bool all) {
                 }
             }
             prof_pending = true;
-            if (attn_fused && pst[1]) {   // the persistent launch: every weight, the KV rows read
-                const HParams& hp = m->hp;
-                prof_bytes = m->weight_bytes + 2LL * hp.n_layer * (cell + 1) * kv_dim * 2;
-            } else {
-                prof_bytes = ffn_bytes();
-            }
+            prof_bytes = ffn_bytes();
         } else if (!use_graphs) {
             enqueue_step(last);
         } else {
             hipGraphExec_t& g = last ? g_full[attn_fused] : g_nolog[attn_fused];
             if (!g) g = build_graph(last, -1);
-            if (attn_fused && pst[last]) {
-                // persistent steps of the contexts on one device run one at a time (two grids of
-                // one workgroup per CU at once would not be co-resident)
-                DevChain& dc = dev_chain(device);
-                std::lock_guard<std::mutex> lk(dc.mu);
-                if (dc.ev) MI_HIP(hipStreamWaitEvent(stream, dc.ev, 0));
-                else MI_HIP(hipEventCreateWithFlags(&dc.ev, hipEventDisableTiming));
-                MI_HIP(hipGraphLaunch(g, stream));
-                MI_HIP(hipEventRecord(dc.ev, stream));
-            } else {
-                MI_HIP(hipGraphLaunch(g, stream));
-            }
+            MI_HIP(hipGraphLaunch(g, stream));
         }
         if (all)   // this token's logits -> row i
             MI_HIP(hipMemcpyAsync(logits_all + (size_t)i * m->hp.n_vocab, logits, (size_t)m->hp.n_vocab * sizeof(float),
@@ -1586,7 +1715,6 @@ int Ctx::decode(const int32_t* tokens, int n, bool all) {
 void Ctx::sync() {
     MI_HIP(hipSetDevice(device));
     MI_HIP(hipStreamSynchronize(stream));
-    check_persist();
     const bool was_unsynced = unsynced;
     unsynced = false;
     if (h_attn_xerr && *h_attn_xerr) {   // an attention exchange gave up: the step's logits are invalid

@@ -224,12 +224,21 @@ struct Ctx {
     // persistent decode step (gemv.hip decode_step_kernel) for contexts within ATTN_SHORT cells:
     // stage tables without / with the output head, built on first use; per-layer activation
     // buffers (q, attention, residual after WO, FFN, residual after down) written once per step
-    PersistStep* pst[2] = {nullptr, nullptr};
-    bool persist_ok = false;            // opt-in (MI_PERSIST=1): dense LLaMA graph with graphs on
-    float* pbuf = nullptr;
-    bool persist_step(bool with_logits);
-    void enqueue_step_persist(bool with_logits);
-    void check_persist();
+    // streaming decode step (dgemv.hip) for dense LLaMA contexts within ATTN_SHORT cells: every
+    // activation arrives quantised, published by the launch before it (the attention kernel, the
+    // embedding, or a one-workgroup dv_quant launch).  Per-layer buffers.
+    struct SpLayer {
+        float *xw, *xd, *att, *h;       // residual after WO / after down, attention output, SwiGLU h
+        char *aA, *aB, *aC, *aD;        // quantised inputs of QKV, WO, gate/up, down
+        int fA, fB, fC, fD;             // their formats: bit 0 Q8_K, bit 1 Q8_0
+    };
+    bool sp_ok = false;                 // MI_DECODE_OLD=1: the gemv_kernel graph instead
+    std::vector<SpLayer> sp;
+    char* sp_mem = nullptr;
+    char* sp_aH = nullptr;              // the output head's input (rms_norm(x) * output_norm)
+    int sp_fH = 0;
+    bool sp_setup();
+    void enqueue_step_sp(bool with_logits);
     struct LayerBufs {
         const float* x_in;              // residual stream into the layer
         float *q, *po, *xa, *h, *h2, *xf;   // q, attention output, residual after WO, FFN (2nd expert), after down

@@ -1164,481 +1164,4 @@ void launch_gemv(const GemvParams& p, hipStream_t s, hipEvent_t ev_start, hipEve
     MI_HIP(hipGetLastError());
 }
 
-// =============================================================================================
-// Persistent decode step: the layers and the output head of one batch-1 llama_decode in ONE
-// launch of one 16-wave workgroup per CU.  The launch walks a table of stages (the same GEMV
-// launches the hipGraph path enqueues, plus attention); between dependent stages every workgroup
-// publishes its completed-stage count in its own 128-byte flag line and waits until all of them
-// reach the stage.  A workgroup issues the next stage's weight ring BEFORE that wait, so the HBM
-// stream continues through the barrier: the latency chain of ~165 kernel launches per token
-// (~7 us each beyond streaming) becomes ~175 barriers overlapped with the weights.
-//
-// Memory model (measured, scripts/exp_gridbar.cpp, 1e9 words, 0 stale): outputs a later stage
-// reads are stored agent-scope (write-through, gst<true>), each into a buffer written once per
-// step (per-layer q / attention / residual / FFN buffers), so no L2 holds a stale line of it;
-// a workgroup publishes only after its stores completed (vmcnt counts in issue order: the
-// prefill's loads are issued after them and excluded from the wait).
-// Co-residency: grid = CUs, one workgroup per CU (checked by occupancy); every wait is bounded
-// (2 s of s_memrealtime): a grid that is not co-resident (another process's persistent kernel on
-// the same GPU) sets a host-mapped abort flag and every workgroup returns; the host then rejects
-// the step and falls back to the launch graph.
-// =============================================================================================
-namespace {
-
-struct PAttn {
-    const float* q;             // this layer's q [n_head][hd]
-    const __half* kcache;       // this layer's caches [n_ctx][kv_dim]
-    const __half* vcache;
-    const int* tokpos;
-    const int* cell_pos;
-    float* out;                 // [n_head][hd]: the single split the WO prologue reads
-    int n_head, n_head_kv, head_dim, kv_dim;
-    float scale;
-};
-
-enum { PS_GEMV = 0, PS_ATTN = 1 };
-struct PStage {
-    int kind, var, nwg, pad;
-    GvArgs g;
-    PAttn at;
-};
-struct PBar {
-    unsigned* flags;            // [grid][32]: completed stages of each workgroup (one line each)
-    unsigned* epoch;            // stage count before this launch (advanced by workgroup 0 at its end)
-    unsigned* abort;            // host-mapped: a wait timed out (written once, read by the host)
-    unsigned* abort_dev;        // the same in device memory (polled with the flags)
-    unsigned long long* stamps; // diagnostics (MI_PERSIST_STAMPS=1): [stage][grid][4] s_memrealtime
-                                // at stage entry, barrier start, barrier end, stage end
-};
-constexpr unsigned long long PBAR_LIMIT = 200000000ull;   // 2 s of the 100 MHz s_memrealtime
-
-__device__ __forceinline__ unsigned ld_agent(const unsigned* p) {
-    return __hip_atomic_load(const_cast<unsigned*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Publish `target` completed stages, then wait until every workgroup has.  Every wave has waited
-// for its own stores (wait_vm) before; returns false after a timeout or another workgroup's abort.
-__device__ __forceinline__ bool pbar_wait(const PBar& b, unsigned target, int* sflag) {
-    __syncthreads();
-    if (threadIdx.x < 64) {
-        if (threadIdx.x == 0) __hip_atomic_store(b.flags + blockIdx.x * 32, target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-        bool ok = true;
-        for (;;) {
-            // the flag loads of a round are issued together (one round trip), then compared
-            unsigned f[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int w = threadIdx.x + 64 * k;
-                f[k] = w < (int)gridDim.x ? ld_agent(b.flags + w * 32) : target;
-            }
-            bool all = true;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) all &= (int)(f[k] - target) >= 0;
-            if (__all(all)) break;
-            const bool ab = ld_agent(b.abort_dev) != 0u;   // another workgroup gave up
-            if (__any(ab) || __builtin_amdgcn_s_memrealtime() - t0 > PBAR_LIMIT) {
-                if (threadIdx.x == 0) {
-                    __hip_atomic_store(b.abort_dev, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(b.abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                }
-                ok = false;
-                break;
-            }
-        }
-        if (threadIdx.x == 0) *sflag = ok ? 1 : 0;
-    }
-    __syncthreads();
-    return *sflag != 0;
-}
-
-// Attention of one q head over <= ATTN_SHORT cells on a 16-wave workgroup: the arithmetic of
-// attn_fused_kernel (kernels.hip: f16(q).k, exact softmax with the global max and the double sum,
-// f16(p) . v), its cells spread over 16 waves instead of 4.
-template <int HD>
-__device__ __forceinline__ void pattn_body(const PAttn& P, char* lds) {
-    constexpr int LPC = HD / 8, CPW = 64 / LPC, NW = GV_NW, U = 4;
-    float* sw = reinterpret_cast<float*>(lds);                   // [ATTN_SHORT] scaled scores
-    float* redm = sw + ATTN_SHORT;                               // [NW]
-    double* dred = reinterpret_cast<double*>(redm + NW);         // [NW]
-    float* red_o = reinterpret_cast<float*>(dred + NW);          // [NW][HD]
-    const int h = blockIdx.x;
-    const int g = h / (P.n_head / P.n_head_kv);
-    int tid = threadIdx.x;
-    asm volatile("" : "+v"(tid));   // opaque per stage (see gv_body)
-    const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int L = lane % LPC, G = lane / LPC;
-    const long long row_off = (long long)g * HD + L * 8;
-    const i32x4 tp = *gptr(reinterpret_cast<const i32x4*>(P.tokpos));
-    const int ncell = min(tp.z + 1, ATTN_SHORT), qpos = tp.y;
-    float q[8];
-    {
-        const auto qp = gptr(reinterpret_cast<const f32x4*>(P.q + (long long)h * HD + L * 8));
-        const f32x4 a = qp[0], b = qp[1];
-        const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-#pragma unroll
-        for (int e = 0; e < 8; ++e) q[e] = __half2float(__float2half_rn(v[e]));
-    }
-    // 1. scaled KQ of every cell into LDS, and the max
-    float mx = -INFINITY;
-    for (int cb = wave * CPW; cb < ncell; cb += NW * CPW * U) {
-        u32x4 kk[U];
-        int cpos[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int c = min(cb + u * NW * CPW + G, ncell - 1);
-            kk[u] = *gptr(reinterpret_cast<const u32x4*>(P.kcache + (long long)c * P.kv_dim + row_off));
-            cpos[u] = gptr(P.cell_pos)[c];
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int c = cb + u * NW * CPW + G;
-            const bool valid = c < ncell && cpos[u] <= qpos;
-            const unsigned kw[4] = {kk[u].x, kk[u].y, kk[u].z, kk[u].w};
-            float d = 0.0f;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                d = fmaf(q[2 * e], h2f(kw[e]), d);
-                d = fmaf(q[2 * e + 1], h2f(kw[e] >> 16), d);
-            }
-#pragma unroll
-            for (int off = LPC / 2; off > 0; off >>= 1) d += __shfl_xor(d, off, 64);
-            const float w = valid ? d * P.scale : -INFINITY;
-            mx = fmaxf(mx, w);
-            if (L == 0 && c < ncell) sw[c] = w;
-        }
-    }
-    mx = wave_max(mx);
-    if (lane == 0) redm[wave] = mx;
-    __syncthreads();
-    float M = redm[0];
-#pragma unroll
-    for (int w = 1; w < NW; ++w) M = fmaxf(M, redm[w]);
-    // 2. sum over all cells of expf(w - max), in double, fixed order
-    double acc = 0.0;
-    for (int c = tid; c < ncell; c += NW * 64) acc += (double)expf(sw[c] - M);
-    acc = wave_sum_d(acc);
-    if (lane == 0) dred[wave] = acc;
-    __syncthreads();
-    double tot = dred[0];
-#pragma unroll
-    for (int w = 1; w < NW; ++w) tot += dred[w];
-    const float inv = (float)(1.0 / tot);
-    // 3. sum_c f16(p_c) v_c
-    float o[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) o[e] = 0.0f;
-    for (int cb = wave * CPW; cb < ncell; cb += NW * CPW * U) {
-        u32x4 vv[U];
-        float pw[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int c0 = cb + u * NW * CPW + G;
-            const bool in = c0 < ncell;
-            const int c = in ? c0 : ncell - 1;
-            vv[u] = *gptr(reinterpret_cast<const u32x4*>(P.vcache + (long long)c * P.kv_dim + row_off));
-            const float p = expf(sw[c] - M) * inv;   // ggml_vec_soft_max_f32, then the f16 vec_dot_type
-            pw[u] = in ? __half2float(__float2half_rn(p)) : 0.0f;
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const unsigned vw[4] = {vv[u].x, vv[u].y, vv[u].z, vv[u].w};
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                o[2 * e] = fmaf(pw[u], h2f(vw[e]), o[2 * e]);
-                o[2 * e + 1] = fmaf(pw[u], h2f(vw[e] >> 16), o[2 * e + 1]);
-            }
-        }
-    }
-#pragma unroll
-    for (int off = LPC; off < 64; off <<= 1)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] += __shfl_xor(o[e], off, 64);
-    if (G == 0) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) red_o[wave * HD + L * 8 + e] = o[e];
-    }
-    __syncthreads();
-    for (int i = tid; i < HD; i += NW * 64) {
-        float a = red_o[i];
-#pragma unroll
-        for (int w = 1; w < NW; ++w) a += red_o[w * HD + i];
-        gst<true>(P.out + (long long)h * HD + i, a);
-    }
-}
-
-__host__ __device__ inline size_t pattn_lds_bytes(int hd) {
-    return (ATTN_SHORT + GV_NW) * 4 + GV_NW * 8 + (size_t)GV_NW * hd * 4;
-}
-
-// GEMV variants of a class (CA, CB): var = ti*6 + (rw-1)*3 + kbi for one segment of type
-// (ti ? CB : CA); 12 + kbi for the two-segment (CA, CB) launch (RW 2); kbi: KB 1, 2, 4.
-constexpr int PV_PAIR = 12, PV_N = 15;
-__host__ __device__ constexpr int pv_kbi(int kb) { return kb == 1 ? 0 : kb == 2 ? 1 : 2; }
-
-template <int T, int RW, int KB, typename W>
-__device__ __forceinline__ void pv_one(const GvArgs& g, char* lds, W& wait) {
-    gv_body<T, 0, RW, KB, GvD<T, RW>::D, false, true>(g, lds, wait);
-}
-template <int TA, int TB, int KB, typename W>
-__device__ __forceinline__ void pv_pair(const GvArgs& g, char* lds, W& wait) {
-    constexpr int D = GvD<TA, 2>::D < GvD<TB, 2>::D ? GvD<TA, 2>::D : GvD<TB, 2>::D;
-    if ((int)blockIdx.x < g.seg[1].blk0) gv_body<TA, 0, 2, KB, D, false, true>(g, lds, wait);
-    else gv_body<TB, 1, 2, KB, D, false, true>(g, lds, wait);
-}
-template <int CA, int CB, typename W>
-__device__ __forceinline__ void pv_run(int var, const GvArgs& g, char* lds, W& wait) {
-    switch (var) {
-    case 0: pv_one<CA, 1, 1>(g, lds, wait); break;
-    case 1: pv_one<CA, 1, 2>(g, lds, wait); break;
-    case 2: pv_one<CA, 1, 4>(g, lds, wait); break;
-    case 3: pv_one<CA, 2, 1>(g, lds, wait); break;
-    case 4: pv_one<CA, 2, 2>(g, lds, wait); break;
-    default:
-        if constexpr (CB >= 0) {
-            switch (var) {
-            case 6: pv_one<CB, 1, 1>(g, lds, wait); break;
-            case 7: pv_one<CB, 1, 2>(g, lds, wait); break;
-            case 8: pv_one<CB, 1, 4>(g, lds, wait); break;
-            case 9: pv_one<CB, 2, 1>(g, lds, wait); break;
-            case 10: pv_one<CB, 2, 2>(g, lds, wait); break;
-            case PV_PAIR + 0: pv_pair<CA, CB, 1>(g, lds, wait); break;
-            case PV_PAIR + 1: pv_pair<CA, CB, 2>(g, lds, wait); break;
-            default: break;
-            }
-        }
-        break;
-    }
-}
-// whether pv_run compiles variant `var` for class (CA, CB)
-__host__ inline bool pv_compiled(int cb, int var) {
-    if (var == 5 || var == 11 || var == PV_PAIR + 2) return false;   // RW 2 with KB 4: K > 8192
-    return var < 6 || (cb >= 0 && var < PV_N);
-}
-
-// The grid barrier of stage s as gv_body's wait hook, with the diagnostic stamps: stage entry,
-// barrier start, barrier end, prologue done.
-struct PWait {
-    const PBar* bar;
-    unsigned target;
-    int s;
-    int* sflag;
-    bool* ok;
-    __device__ void stamp(int k) const {
-        if (bar->stamps && threadIdx.x == 64)   // wave 1: streams (wave 0 polls first)
-            bar->stamps[((size_t)s * gridDim.x + blockIdx.x) * 4 + k] = __builtin_amdgcn_s_memrealtime();
-    }
-    __device__ bool operator()() {
-        stamp(1);
-        if (s > 0) *ok = pbar_wait(*bar, target, sflag);   // stage 0 reads the previous launch's output
-        stamp(2);
-        return *ok;
-    }
-    __device__ void mark() const { stamp(3); }
-};
-
-template <int CA, int CB>
-__global__ __launch_bounds__(GV_NW * 64) void decode_step_kernel(const PStage* __restrict__ st, int n_stages, PBar bar) {
-    extern __shared__ __attribute__((aligned(16))) char lds[];
-    __shared__ int sflag;
-    const unsigned ep0 = __builtin_amdgcn_readfirstlane(*gptr(bar.epoch));
-    for (int s = 0; s < n_stages; ++s) {
-        const PStage& S = st[s];
-        bool ok = true;
-        PWait wait{&bar, ep0 + (unsigned)s, s, &sflag, &ok};
-        wait.stamp(0);
-        if ((int)blockIdx.x >= S.nwg && blockIdx.x != 0) {
-            // not in this stage: publish having completed the previous one (stores done first)
-            wait_vm<0>();
-            __syncthreads();
-            if (s > 0 && threadIdx.x == 0)
-                __hip_atomic_store(bar.flags + blockIdx.x * 32, ep0 + (unsigned)s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            continue;
-        }
-        if (S.kind == PS_ATTN) {
-            wait_vm<0>();
-            if (wait()) {
-                switch (S.at.head_dim) {
-                case 32: pattn_body<32>(S.at, lds); break;
-                case 64: pattn_body<64>(S.at, lds); break;
-                case 128: pattn_body<128>(S.at, lds); break;
-                default: pattn_body<256>(S.at, lds); break;
-                }
-                wait.mark();
-            }
-        } else {
-            pv_run<CA, CB>(S.var, S.g, lds, wait);
-        }
-        if (!ok) return;
-    }
-    if (blockIdx.x == 0 && threadIdx.x == 0) *gptr_w(bar.epoch) = ep0 + (unsigned)n_stages;
-}
-
-typedef void (*PFn)(const PStage*, int, PBar);
-struct PClass {
-    int ca, cb;
-    PFn fn;
-};
-const PClass kPClasses[] = {
-    {T_Q4_K, T_Q6_K, decode_step_kernel<T_Q4_K, T_Q6_K>},
-    {T_Q5_K, T_Q6_K, decode_step_kernel<T_Q5_K, T_Q6_K>},
-    {T_Q6_K, -1, decode_step_kernel<T_Q6_K, -1>},
-    {T_Q8_0, -1, decode_step_kernel<T_Q8_0, -1>},
-};
-
-}  // namespace
-
-struct PersistStep {
-    int device = 0;
-    int grid = 0;
-    std::vector<PStage> st;
-    std::vector<GvKey> keys;
-    std::vector<int> types;
-    size_t smem = 0;
-    const PClass* cls = nullptr;
-    PStage* d_st = nullptr;
-    unsigned* d_flags = nullptr;
-    unsigned* d_epoch = nullptr;        // [0] epoch, [1] device abort flag
-    unsigned* h_abort = nullptr;        // host-mapped
-    unsigned* d_abort = nullptr;
-    unsigned long long* d_stamps = nullptr;   // MI_PERSIST_STAMPS=1
-};
-
-PersistStep* persist_new(int device) {
-    int cus = 0;
-    MI_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
-    if (cus < 1) return nullptr;
-    auto* p = new PersistStep();
-    p->device = device;
-    p->grid = std::min(std::min(cus, gv_grid_cap()), 256);   // the barrier polls 4 flags per lane
-    return p;
-}
-
-void persist_free(PersistStep* p) {
-    if (!p) return;
-    hipSetDevice(p->device);
-    if (p->d_st) hipFree(p->d_st);
-    if (p->d_flags) hipFree(p->d_flags);
-    if (p->d_epoch) hipFree(p->d_epoch);
-    if (p->h_abort) hipHostFree(p->h_abort);
-    if (p->d_stamps) hipFree(p->d_stamps);
-    delete p;
-}
-
-bool persist_add_gemv(PersistStep* p, const GemvParams& g) {
-    PStage s;
-    std::memset(&s, 0, sizeof(s));
-    GvKey key;
-    int grid = 0;
-    gv_prepare(g, p->grid, s.g, grid, key);
-    if (key.tag == 2) return false;                                  // GPT-2 extensions
-    for (int i = 0; i < g.nseg; ++i)
-        if (g.seg[i].expA >= 0 || g.seg[i].expB >= 0) return false;  // MoE: addresses from the router
-    if (g.nseg == 2 && key.t0 == key.t1) return false;
-    s.kind = PS_GEMV;
-    s.nwg = grid;
-    p->smem = std::max(p->smem, gv_lds_bytes(g.K / 256, s.g.nslots, g.n_rot));
-    p->st.push_back(s);
-    p->keys.push_back(key);
-    return true;
-}
-
-bool persist_add_attn(PersistStep* p, const AttnParams& a, float* out) {
-    if (a.head_dim != 32 && a.head_dim != 64 && a.head_dim != 128 && a.head_dim != 256) return false;
-    if (a.n_head % a.n_head_kv || a.n_head > p->grid) return false;
-    PStage s;
-    std::memset(&s, 0, sizeof(s));
-    s.kind = PS_ATTN;
-    s.nwg = a.n_head;
-    s.at = PAttn{a.q, a.kcache, a.vcache, a.tokpos, a.cell_pos, out, a.n_head, a.n_head_kv, a.head_dim, a.kv_dim, a.scale};
-    p->smem = std::max(p->smem, pattn_lds_bytes(a.head_dim));
-    p->st.push_back(s);
-    p->keys.push_back(GvKey{0, -1, -1, 0, 0, 0});
-    return true;
-}
-
-bool persist_finalize(PersistStep* p) {
-    // the class whose two types cover every GEMV stage
-    std::vector<int> ts;
-    for (size_t i = 0; i < p->st.size(); ++i)
-        if (p->st[i].kind == PS_GEMV)
-            for (int t : {p->keys[i].t0, p->keys[i].t1})
-                if (std::find(ts.begin(), ts.end(), t) == ts.end()) ts.push_back(t);
-    const PClass* cls = nullptr;
-    for (const PClass& c : kPClasses) {
-        bool cover = true;
-        for (int t : ts) cover = cover && (t == c.ca || t == c.cb);
-        if (cover) { cls = &c; break; }
-    }
-    if (!cls) return false;
-    for (size_t i = 0; i < p->st.size(); ++i) {
-        PStage& s = p->st[i];
-        if (s.kind != PS_GEMV) continue;
-        const GvKey& k = p->keys[i];
-        int var;
-        if (k.nseg == 2) {
-            if (k.t0 != cls->ca || k.t1 != cls->cb) return false;
-            var = PV_PAIR + pv_kbi(k.kb);
-        } else {
-            var = (k.t0 == cls->ca ? 0 : 6) + (k.rw - 1) * 3 + pv_kbi(k.kb);
-        }
-        if (!pv_compiled(cls->cb, var)) return false;
-        s.var = var;
-    }
-    int occ = 0;
-    MI_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(cls->fn), hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024));
-    MI_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(cls->fn), GV_NW * 64, p->smem));
-    if (occ < 1 || p->smem > 96 * 1024) return false;
-    p->cls = cls;
-    MI_HIP(hipSetDevice(p->device));
-    MI_HIP(hipMalloc(&p->d_st, p->st.size() * sizeof(PStage)));
-    MI_HIP(hipMemcpy(p->d_st, p->st.data(), p->st.size() * sizeof(PStage), hipMemcpyHostToDevice));
-    MI_HIP(hipMalloc(&p->d_flags, (size_t)p->grid * 128));
-    MI_HIP(hipMemset(p->d_flags, 0, (size_t)p->grid * 128));
-    MI_HIP(hipMalloc(&p->d_epoch, 16));
-    MI_HIP(hipMemset(p->d_epoch, 0, 16));
-    MI_HIP(hipHostMalloc(&p->h_abort, 16, hipHostMallocMapped | hipHostMallocCoherent));
-    std::memset(p->h_abort, 0, 16);
-    MI_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&p->d_abort), p->h_abort, 0));
-    if (getenv("MI_PERSIST_STAMPS")) {
-        const size_t n = p->st.size() * p->grid * 4;
-        MI_HIP(hipMalloc(&p->d_stamps, n * 8));
-        MI_HIP(hipMemset(p->d_stamps, 0, n * 8));
-    }
-    return true;
-}
-
-size_t persist_read_stamps(PersistStep* p, unsigned long long* out, size_t n) {
-    if (!p || !p->d_stamps) return 0;
-    n = std::min(n, p->st.size() * p->grid * 4);
-    MI_HIP(hipDeviceSynchronize());
-    MI_HIP(hipMemcpy(out, p->d_stamps, n * 8, hipMemcpyDeviceToHost));
-    return n;
-}
-
-int persist_stages(const PersistStep* p) { return p ? (int)p->st.size() : 0; }
-
-void persist_launch(PersistStep* p, hipStream_t s, hipEvent_t ev_start, hipEvent_t ev_stop) {
-    if (!p->cls) throw Error("persistent step: not finalized");
-    PBar bar{p->d_flags, p->d_epoch, p->d_abort, p->d_epoch + 1, p->d_stamps};
-    const int n = (int)p->st.size();
-    if (ev_start || ev_stop)
-        hipExtLaunchKernelGGL(p->cls->fn, dim3(p->grid), dim3(GV_NW * 64), p->smem, s, ev_start, ev_stop, 0,
-                              (const PStage*)p->d_st, n, bar);
-    else
-        hipLaunchKernelGGL(p->cls->fn, dim3(p->grid), dim3(GV_NW * 64), p->smem, s, (const PStage*)p->d_st, n, bar);
-    MI_HIP(hipGetLastError());
-}
-
-bool persist_aborted(const PersistStep* p) {
-    return p && p->h_abort && __atomic_load_n(p->h_abort, __ATOMIC_ACQUIRE) != 0u;
-}
-
-void persist_reset(PersistStep* p, hipStream_t s) {
-    MI_HIP(hipStreamSynchronize(s));
-    MI_HIP(hipMemset(p->d_flags, 0, (size_t)p->grid * 128));
-    MI_HIP(hipMemset(p->d_epoch, 0, 16));   // epoch and the device abort flag
-    __atomic_store_n(p->h_abort, 0u, __ATOMIC_RELEASE);
-}
-
 }  // namespace mi

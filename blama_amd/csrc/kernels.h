@@ -67,6 +67,18 @@ struct AttnPartials {
     int n_head, head_dim;
 };
 
+// ---- the quantised activation a decode launch publishes for the next one (dgemv.hip) ----
+// Layout in global memory: act_layout(K, q8k, q80) of qdot.h (the Q8_K blocks, the Q8_0 blocks,
+// the Q8_K sub-block sums and scales, the Q8_0 scales), the same bytes the consumer copies into
+// LDS.  norm_w set: the activation is rms_norm(x) * norm_w (ggml's rms_norm then mul).
+struct ActOut {
+    int K;                    // length (multiple of 256)
+    int q8k, q80;             // formats to write (Q8_K for k-quant consumers, Q8_0 for Q8_0 ones)
+    char* act;                // destination
+    const float* norm_w;      // optional
+    float eps;
+};
+
 constexpr int GEMV_MAX_SEG = 2;
 struct GemvParams {
     GemvSeg seg[GEMV_MAX_SEG];
@@ -94,9 +106,18 @@ struct GemvParams {
     AttnPartials attn;        // PRO_ATTN input
     int attn_nsplit;          // PRO_ATTN: splits to add (0: from the cell count in tokpos)
     unsigned long long* stamps;   // diagnostics (MI_STAMPS builds): per-workgroup stamps [grid][8]
+    // streaming form (dgemv.hip, dense LLaMA decode within ATTN_SHORT cells): the activation arrives
+    // quantised (act_layout(K, act_q8k, act_q80) at act_in; pro / x / norm_w unused).
+    // act_in == nullptr: the gemv_kernel path above.
+    const char* act_in;
+    int act_q8k, act_q80;
 };
 
 void init_kernel_attributes();   // once per device, before any graph capture
+// the streaming form (dgemv.hip): p.act_in set; the events as launch_gemv's
+void launch_dgemv(const GemvParams& p, hipStream_t s, hipEvent_t ev_start = nullptr, hipEvent_t ev_stop = nullptr);
+bool dgemv_supported(const GemvParams& p);            // a compiled variant serves this launch
+size_t dv_act_bytes(int K, int q8k, int q80);         // bytes of a quantised activation
 // ev_start/ev_stop (optional): recorded at the kernel's own start and end (hipExtLaunchKernel)
 // -- the bench's in-kernel timing of one launch.
 void launch_gemv(const GemvParams& p, hipStream_t s, hipEvent_t ev_start = nullptr, hipEvent_t ev_stop = nullptr);
@@ -106,26 +127,7 @@ bool gemv_pair_supported(int t1, int t2);
 int gemv_grid(const GemvParams& p);
 void init_gemm_attributes();     // the batch GEMMs' LDS limits (kernels.hip)
 
-// ---- persistent decode step (gemv.hip): a table of stages -- the GEMV launches above and the
-// short-context attention -- run by ONE launch of one 16-wave workgroup per CU, with a grid
-// barrier between stages that the next stage's weight prefetch overlaps.  Dense LLaMA graphs
-// whose matrices fall in one compiled type class (Q4_K+Q6_K, Q5_K+Q6_K, Q6_K, Q8_0). ----
-struct PersistStep;
 struct AttnParams;
-PersistStep* persist_new(int device);                 // nullptr: no compute units reported
-void persist_free(PersistStep* p);
-// append a stage; false: the launch has no persistent form (the caller keeps the graph path).
-// Outputs a later stage reads must be buffers written once per step.
-bool persist_add_gemv(PersistStep* p, const GemvParams& g);
-bool persist_add_attn(PersistStep* p, const AttnParams& a, float* out);   // <= ATTN_SHORT cells
-bool persist_finalize(PersistStep* p);                // false: no compiled class covers the stages
-int persist_stages(const PersistStep* p);
-void persist_launch(PersistStep* p, hipStream_t s, hipEvent_t ev_start = nullptr, hipEvent_t ev_stop = nullptr);
-bool persist_aborted(const PersistStep* p);           // a grid barrier timed out (not co-resident)
-void persist_reset(PersistStep* p, hipStream_t s);    // zero the barrier state after an abort
-// diagnostics (MI_PERSIST_STAMPS=1 at the first step): the last launch's s_memrealtime stamps,
-// [stage][workgroup][4] = entry, barrier start, barrier end, stage end; returns the count copied
-size_t persist_read_stamps(PersistStep* p, unsigned long long* out, size_t n);
 
 // ---- batched quantised GEMM over up to GEMM_NT tokens (prompt ingestion) ----
 // The GEMV's integer arithmetic per token (Q8_K / Q8_0 activations, per-block integer
@@ -182,6 +184,11 @@ struct EmbedParams {
     unsigned* step;            // optional: incremented once per launch (decode step counter)
 };
 void launch_embed(const EmbedParams& p, hipStream_t s);
+// the embedding row and the first layer's quantised activation rms_norm(x) * a.norm_w (one
+// workgroup; LLaMA): the streaming decode path's first launch
+void launch_embed_act(const EmbedParams& p, const ActOut& a, hipStream_t s);
+// rms_norm(x) * a.norm_w (or x itself) of one row, quantised (one workgroup; dgemv.hip)
+void launch_dv_quant(const float* x, const ActOut& a, hipStream_t s);
 
 // ---- attention over the f16 cache: KQ -> soft_max -> KQV, split over cells ----
 // Two launches, grid (n_head_kv, ATTN_SMAX) each; the WO GEMV's PRO_ATTN
@@ -214,8 +221,12 @@ struct AttnParams {
     // that many grids of n_head * ATTN_SMAX workgroups are co-resident (occupancy x CUs)
     int long_share;
     int long_off;                  // 1: never the single launch (an exchange timed out before)
+    ActOut act_out;                // fused kernel, decode (act_out.act set): the output also quantised
+                                   // (a workgroup serves whole 256-blocks of it: 256 / (R * hd) kv heads)
 };
 void launch_attn(const AttnParams& p, hipStream_t s);
+// a decode attention launch can also quantise its output (AttnParams::act_out) for this geometry
+bool attn_quant_supported(int n_head, int n_head_kv, int head_dim);
 // Combine the partials into out[n_head*hd] (tests / the eager debug path).
 void launch_attn_combine(const AttnPartials& a, const int* tokpos, float* out, hipStream_t s);
 

@@ -362,6 +362,55 @@ void launch_embed_multi(const EmbedParams& p, int ntok, hipStream_t s) {
     MI_HIP(hipGetLastError());
 }
 
+// The streaming decode path's first launch (LLaMA): get_rows(tok_embd, token) into x, then
+// rms_norm(x) * attn_norm of layer 0, quantised into t.act (one workgroup of 16 waves; each wave
+// holds blocks wave, wave + 16, ... of the row; the sum of squares in double, waves in order).
+constexpr int EA_KB = 4;   // 256-blocks per wave: n_embd <= 16384
+__global__ __launch_bounds__(1024) void embed_act_kernel(const EmbedParams P, const ActOut t) {
+    __shared__ double red[16];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const long long tok = P.tokpos[0];
+    if (P.step && threadIdx.x == 0) *P.step += 1u;
+    const int nb = P.n_embd >> 8;
+    float v[EA_KB][4];
+    double sq = 0.0;
+#pragma unroll
+    for (int i = 0; i < EA_KB; ++i) {
+        const int b = wave + 16 * i;
+        if (b < nb) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                v[i][k] = dequant_elem(P.E, tok, b * 256 + lane * 4 + k);
+                sq += (double)(v[i][k] * v[i][k]);
+            }
+            *reinterpret_cast<float4*>(P.out + b * 256 + lane * 4) = make_float4(v[i][0], v[i][1], v[i][2], v[i][3]);
+        }
+    }
+    sq = wave_sum63_d(sq);
+    if (lane == 63) red[wave] = sq;
+    __syncthreads();
+    double tot = 0.0;
+    for (int w = 0; w < 16; ++w) tot += red[w];
+    const float scale = 1.0f / sqrtf((float)(tot / (double)P.n_embd) + t.eps);
+#pragma unroll
+    for (int i = 0; i < EA_KB; ++i) {
+        const int b = wave + 16 * i;
+        if (b < nb) {
+            const float4 wn = reinterpret_cast<const float4*>(t.norm_w)[b * 64 + lane];
+            float q[4] = {(v[i][0] * scale) * wn.x, (v[i][1] * scale) * wn.y, (v[i][2] * scale) * wn.z,
+                          (v[i][3] * scale) * wn.w};
+            dv_quant_block(t, b, q, lane);
+        }
+    }
+}
+
+void launch_embed_act(const EmbedParams& p, const ActOut& t, hipStream_t s) {
+    if (p.has_pos || p.n_embd % 256 || p.n_embd > EA_KB * 16 * 256 || t.K != p.n_embd || !t.act || !t.norm_w)
+        throw Error("embed_act: unsupported shape");
+    hipLaunchKernelGGL(embed_act_kernel, dim3(1), dim3(1024), 0, s, p, t);
+    MI_HIP(hipGetLastError());
+}
+
 void launch_embed(const EmbedParams& p, hipStream_t s) {
     hipLaunchKernelGGL(embed_kernel, dim3((p.n_embd + 255) / 256), dim3(256), 0, s, p);
     MI_HIP(hipGetLastError());
@@ -814,18 +863,23 @@ __global__ __launch_bounds__(256) void attn_long_kernel(const AttnParams P) {
 // Short contexts (<= ATTN_SHORT cells): the same arithmetic as the two kernels above with a
 // single split, in one launch.  One workgroup per kv head keeps its scores in LDS, so no
 // other workgroup's result is needed between the softmax statistics and the PV sum.
-template <int R, int LPC>
-__global__ __launch_bounds__(256) void attn_fused_kernel(const AttnParams P) {
+// HG > 1 (the streaming decode step): HG such groups of 4 waves in one workgroup, one kv head (or,
+// qsplit, one q head) each, so that a workgroup's R * HG q heads cover whole 256-blocks of the
+// output, which it then also quantises into P.act_out (the WO launch's activation).
+template <int R, int LPC, int HG>
+__global__ __launch_bounds__(256 * HG) void attn_fused_kernel(const AttnParams P) {
     constexpr int CPW = 64 / LPC;
     constexpr int HD = LPC * 8;
-    __shared__ float sw[R][ATTN_SHORT];
-    __shared__ float redm[4][R];
-    __shared__ double dred[4][R];
-    __shared__ float gm[R], ginv[R];
-    __shared__ float red_o[4][R][HD];
-    // kv head, and the first of the R q heads this workgroup serves (qsplit: one q head each)
-    const int g = P.qsplit ? (int)blockIdx.x / P.qsplit : (int)blockIdx.x;
-    const int gq = P.qsplit ? (int)blockIdx.x : (int)blockIdx.x * R;
+    __shared__ float sw[HG][R][ATTN_SHORT];
+    __shared__ float redm[HG][4][R];
+    __shared__ double dred[HG][4][R];
+    __shared__ float gm[HG][R], ginv[HG][R];
+    __shared__ float red_o[HG][4][R][HD];
+    const int grp = (int)threadIdx.x >> 8;
+    const int unit = (int)blockIdx.x * HG + grp;   // this group's kv head (qsplit: q head)
+    // kv head, and the first of the R q heads this group serves (qsplit: one q head each)
+    const int g = P.qsplit ? unit / P.qsplit : unit;
+    const int gq = P.qsplit ? unit : unit * R;
     const int tok = blockIdx.y;   // query token (launch_attn_multi); 0 for a decode step
 #ifdef MI_STAMPS
     unsigned long long* const stp = P.stamps && tok == 0 ? P.stamps + blockIdx.x * 8 : nullptr;
@@ -835,7 +889,7 @@ __global__ __launch_bounds__(256) void attn_fused_kernel(const AttnParams P) {
     const int tp2 = tp[2], qpos = tp[1];
     const float* qrow = P.q + (long long)tok * P.n_head * HD;
     float* orow = P.part_o + (long long)tok * P.n_head * HD;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x & 255, lane = tid & 63, wave = tid >> 6;
     const int L = lane % LPC, G = lane / LPC;
     const long long row_off = (long long)g * HD + L * 8;
     constexpr int U = 4;
@@ -903,28 +957,28 @@ __global__ __launch_bounds__(256) void attn_fused_kernel(const AttnParams P) {
                 for (int off = LPC / 2; off > 0; off >>= 1) d += __shfl_xor(d, off, 64);
                 const float w = valid ? d * P.scale : -INFINITY;
                 mx[t] = fmaxf(mx[t], w);
-                if (L == 0 && c < ncell) sw[t][c] = w;
+                if (L == 0 && c < ncell) sw[grp][t][c] = w;
             }
         }
     }
 #pragma unroll
     for (int t = 0; t < R; ++t) {
         const float m = wave_max(mx[t]);
-        if (lane == 0) redm[wave][t] = m;
+        if (lane == 0) redm[grp][wave][t] = m;
     }
     __syncthreads();
     // 2. sum over all cells of expf(w - max), in double, fixed order (as attn_pv_kernel)
 #pragma unroll
     for (int t = 0; t < R; ++t) {
-        const float M = fmaxf(fmaxf(redm[0][t], redm[1][t]), fmaxf(redm[2][t], redm[3][t]));
+        const float M = fmaxf(fmaxf(redm[grp][0][t], redm[grp][1][t]), fmaxf(redm[grp][2][t], redm[grp][3][t]));
         double acc = 0.0;
-        for (int c = tid; c < ncell; c += 256) acc += (double)expf(sw[t][c] - M);
+        for (int c = tid; c < ncell; c += 256) acc += (double)expf(sw[grp][t][c] - M);
         acc = wave_sum_d(acc);
-        if (lane == 0) dred[wave][t] = acc;
-        if (tid == 0) gm[t] = M;
+        if (lane == 0) dred[grp][wave][t] = acc;
+        if (tid == 0) gm[grp][t] = M;
     }
     __syncthreads();
-    if (tid < R) ginv[tid] = (float)(1.0 / (((dred[0][tid] + dred[1][tid]) + dred[2][tid]) + dred[3][tid]));
+    if (tid < R) ginv[grp][tid] = (float)(1.0 / (((dred[grp][0][tid] + dred[grp][1][tid]) + dred[grp][2][tid]) + dred[grp][3][tid]));
     __syncthreads();
     // 3. sum_c f16(p_c) v_c
     float o[R][8];
@@ -949,7 +1003,7 @@ __global__ __launch_bounds__(256) void attn_fused_kernel(const AttnParams P) {
             }
 #pragma unroll
             for (int t = 0; t < R; ++t) {
-                const float p = expf(sw[t][c] - gm[t]) * ginv[t];
+                const float p = expf(sw[grp][t][c] - gm[grp][t]) * ginv[grp][t];
                 pw[u][t] = in ? __half2float(__float2half_rn(p)) : 0.0f;
             }
         }
@@ -978,12 +1032,29 @@ __global__ __launch_bounds__(256) void attn_fused_kernel(const AttnParams P) {
 #pragma unroll
         for (int t = 0; t < R; ++t)
 #pragma unroll
-            for (int e = 0; e < 8; ++e) red_o[wave][t][L * 8 + e] = o[t][e];
+            for (int e = 0; e < 8; ++e) red_o[grp][wave][t][L * 8 + e] = o[t][e];
     }
     __syncthreads();
     for (int i = tid; i < R * HD; i += 256) {
         const int t = i / HD, d = i % HD;
-        orow[(long long)(gq + t) * HD + d] = ((red_o[0][t][d] + red_o[1][t][d]) + red_o[2][t][d]) + red_o[3][t][d];
+        orow[(long long)(gq + t) * HD + d] = ((red_o[grp][0][t][d] + red_o[grp][1][t][d]) + red_o[grp][2][t][d]) + red_o[grp][3][t][d];
+    }
+    if (P.act_out.act && gridDim.y == 1) {
+        // the WO launch's quantised activation: this workgroup's R * HG heads are whole 256-blocks
+        // (launch_attn checks), one wave per block; element e of the workgroup's span lies in
+        // group e / (R * HD), head (e / HD) % R
+        constexpr int NE = HG * R * HD;
+        const int e0 = (int)blockIdx.x * HG * (P.qsplit ? 1 : R) * HD;
+        const int gw = (int)threadIdx.x >> 6;
+        for (int b = gw; b < NE / 256; b += 4 * HG) {
+            float v[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int e = b * 256 + lane * 4 + k, gg = e / (R * HD), t = (e / HD) % R, d = e % HD;
+                v[k] = ((red_o[gg][0][t][d] + red_o[gg][1][t][d]) + red_o[gg][2][t][d]) + red_o[gg][3][t][d];
+            }
+            dv_quant_block(P.act_out, e0 / 256 + b, v, lane);
+        }
     }
 #ifdef MI_STAMPS
     if (stp && threadIdx.x == 0) stp[4] = __builtin_amdgcn_s_memrealtime();
@@ -1014,7 +1085,7 @@ static void attn_fns_l(AttnFn& a, AttnFn& b, AttnFn& f) {
         a = attn_scores_kernel<R, LPC, 4>;
         b = attn_pv_kernel<R, LPC, 4>;
     }
-    f = attn_fused_kernel<R, LPC>;
+    f = attn_fused_kernel<R, LPC, 1>;
 }
 template <int R>
 static void attn_fns_r(int hd, AttnFn& a, AttnFn& b, AttnFn& f) {
@@ -1025,6 +1096,30 @@ static void attn_fns_r(int hd, AttnFn& a, AttnFn& b, AttnFn& f) {
     case 256: attn_fns_l<R, 32>(a, b, f); break;
     default: a = b = f = nullptr; break;
     }
+}
+
+// the R = 1 fused kernel with hg groups of 4 waves (the streaming decode step's quantising form)
+static AttnFn attn_fused_hg1(int hd, int hg) {
+    switch (hd * 8 + hg) {
+    case 128 * 8 + 1: return attn_fused_kernel<1, 16, 1>;
+    case 128 * 8 + 2: return attn_fused_kernel<1, 16, 2>;
+    case 64 * 8 + 1: return attn_fused_kernel<1, 8, 1>;
+    case 64 * 8 + 2: return attn_fused_kernel<1, 8, 2>;
+    case 64 * 8 + 4: return attn_fused_kernel<1, 8, 4>;
+    default: return nullptr;
+    }
+}
+
+bool attn_quant_supported(int n_head, int n_head_kv, int head_dim) {
+    if (n_head_kv <= 0 || n_head % n_head_kv) return false;
+    const int r = n_head / n_head_kv;
+    const bool qs = r > 1 && n_head_kv < 16;
+    const int per = (qs ? 1 : r) * head_dim;
+    const int hg = per >= 256 ? 1 : 256 / per;
+    const int units = qs ? n_head : n_head_kv;
+    if (units % hg || per * hg % 256 || (r != 1 && r != 2 && r != 4 && r != 8)) return false;
+    return (hg == 1 && !qs) ? (head_dim == 32 || head_dim == 64 || head_dim == 128 || head_dim == 256)
+                            : attn_fused_hg1(head_dim, hg) != nullptr;
 }
 
 void launch_attn(const AttnParams& p, hipStream_t s) {
@@ -1039,6 +1134,23 @@ void launch_attn(const AttnParams& p, hipStream_t s) {
     default: break;
     }
     if (!fa) throw Error("attn: unsupported head_dim / GQA ratio (head_dim 32..256, ratio 1/2/4/8)");
+    if (p.fused && p.act_out.act) {
+        // the streaming decode step: the output also quantised, whole 256-blocks per workgroup
+        const bool qs = r > 1 && p.n_head_kv < 16;   // few kv heads: a group per q head
+        const int per = (qs ? 1 : r) * p.head_dim;   // output elements of one group
+        const int hg = per >= 256 ? 1 : 256 / per;
+        const int units = qs ? p.n_head : p.n_head_kv;
+        AttnFn f = nullptr;
+        if (hg == 1 && !qs) f = ff;
+        else if (qs || r == 1) f = attn_fused_hg1(p.head_dim, hg);
+        if (!f || units % hg || per * hg % 256 || p.act_out.K != p.n_head * p.head_dim)
+            throw Error("attn: no quantising decode kernel for this head geometry");
+        AttnParams q = p;
+        q.qsplit = qs ? r : 0;
+        hipLaunchKernelGGL(f, dim3(units / hg), dim3(256 * hg), 0, s, q);
+        MI_HIP(hipGetLastError());
+        return;
+    }
     if (p.fused) {   // the caller guarantees <= ATTN_SHORT cells (the kernel clamps anyway)
         if (r > 1 && p.n_head_kv < 16) {   // few kv heads: one workgroup per q head (R=1 kernel)
             AttnFn f1 = nullptr, a1 = nullptr, b1 = nullptr;

@@ -446,6 +446,19 @@ template <> struct Kq<T_Q8_0> {
 
 __device__ __forceinline__ float silu_f(float x) { return x / (1.0f + expf(-x)); }
 
+// ---------------------------------------------------------------------------
+// Block b of a published activation (ActOut, kernels.h) from one wave's 4 values per lane
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void dv_quant_block(const ActOut& t, int b, const float v[4], int lane) {
+    const ActLayout L = act_layout(t.K, t.q8k, t.q80);
+    if (t.q8k)
+        quant_q8k_block(v, lane, reinterpret_cast<int8_t*>(t.act + L.q8k + b * 256),
+                        reinterpret_cast<int*>(t.act + L.bsum) + b * 16, reinterpret_cast<float*>(t.act + L.dk) + b);
+    if (t.q80)
+        quant_q80_block(v, lane, reinterpret_cast<int8_t*>(t.act + L.q80 + b * 256),
+                        reinterpret_cast<float*>(t.act + L.d0) + b * 8);
+}
+
 __device__ __forceinline__ void unit_range(int total, int W, int gw, int& u0, int& u1) {
     // total * (gw + 1) < 2^32 (total <= 65536 units, W <= 4096 waves)
     u0 = (int)(((unsigned)total * (unsigned)gw) / (unsigned)W);

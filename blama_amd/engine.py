@@ -85,8 +85,6 @@ _SIGS = {
     "mi_prof_read": (C.c_int32, [_P, C.POINTER(C.c_float), C.c_int32]),
     "mi_prof_ffn_bytes": (C.c_int64, [_P]),
     "mi_prof_bytes": (C.c_int64, [_P]),
-    "mi_persist_stages": (C.c_int32, [_P]),
-    "mi_debug_persist_stamps": (C.c_int64, [_P, C.POINTER(C.c_uint64), C.c_int64]),
     "mi_debug_stamps": (C.c_int32, [_P, _P, C.c_int32]),
     "mi_op_gemv": (C.c_int32, [C.c_int32, C.c_int32, _P, C.c_int32, C.c_int32, _P, _P]),
     "mi_op_dequant": (C.c_int32, [C.c_int32, C.c_int32, _P, C.c_int32, C.c_int32, _P]),
@@ -319,22 +317,8 @@ class Context:
 
     @property
     def prof_bytes(self) -> int:
-        """Algorithmic bytes of the launch prof_read last timed (gate/up GEMV, or the persistent step)."""
+        """Algorithmic bytes of the launch prof_read last timed (the FFN gate/up GEMV)."""
         return lib().mi_prof_bytes(self.h)
-
-    def persist_stamps(self, n_stages: int, grid: int) -> np.ndarray:
-        """[stage][workgroup][4] s_memrealtime stamps of the last persistent launch (MI_PERSIST_STAMPS=1)."""
-        a = np.zeros(n_stages * grid * 4, np.uint64)
-        k = lib().mi_debug_persist_stamps(self.h, a.ctypes.data_as(C.POINTER(C.c_uint64)), a.size)
-        if k < 0:
-            raise EngineError(f"persist_stamps: {last_error()}")
-        return a[:k].reshape(-1, grid, 4) if k else a[:0]
-
-    @property
-    def persist_stages(self) -> int:
-        """Stages of the persistent decode step (0: steps run as the per-op hipGraph)."""
-        return lib().mi_persist_stages(self.h)
-
 
 # ---- op-level entry points (parity tests / micro-benchmarks) ----
 

@@ -145,21 +145,8 @@ int32_t mi_prof_enable(mi_ctx* ctx, int32_t layer);
 int32_t mi_prof_read(mi_ctx* ctx, float* us, int32_t n);
 /* Algorithmic HBM bytes of one FFN gate/up launch (weights + activation in/out). */
 int64_t mi_prof_ffn_bytes(const mi_ctx* ctx);
-/* Algorithmic HBM bytes of the launch mi_prof_read last timed: the FFN gate/up launch of the
- * graph path, or, for a persistent step (contexts within 512 cells, dense LLaMA graphs), the
- * whole persistent launch: every layer matrix and the output head once, plus the KV cache rows
- * its attention read.  When the step ran persistently, mi_prof_enable's layer only switches
- * the timing on. */
+/* Algorithmic HBM bytes of the launch mi_prof_read last timed (the FFN gate/up launch). */
 int64_t mi_prof_bytes(const mi_ctx* ctx);
-/* Stages of the context's persistent decode step (its layers and output head as ONE launch with
- * grid barriers between stages, gemv.hip decode_step_kernel); 0 when decode steps run as the
- * per-op hipGraph (the default; MI_PERSIST=1 at context creation opts in for dense LLaMA graphs
- * whose matrices fall in a compiled type class) or no step ran yet. */
-int32_t mi_persist_stages(const mi_ctx* ctx);
-/* Diagnostics: with MI_PERSIST_STAMPS=1 set before the context's first step, copies the last
- * persistent launch's s_memrealtime stamps (100 MHz), [stage][workgroup][4] = stage entry,
- * barrier start, barrier end, stage end, to out; returns the count copied (0 without stamps). */
-int64_t mi_debug_persist_stamps(mi_ctx* ctx, uint64_t* out, int64_t n);
 /* Diagnostics: copies the per-workgroup s_memrealtime stamps (100 MHz) of the
  * first n_launch launches of the last decode step, [launch][512][8] uint64, to
  * out.  Returns the number of launches copied; 0 unless the library is the

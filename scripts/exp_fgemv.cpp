@@ -41,12 +41,6 @@ struct FA {
 };
 
 __device__ __forceinline__ void wait_vm_asm0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-__device__ __forceinline__ float ld_sc1(const float* p) {
-    return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_sc1(float* p, float v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 __device__ __forceinline__ unsigned fold(const Kq<T_Q4_K>::Ld& l) { return l.qs.x ^ l.qs.y ^ l.qs.z ^ l.qs.w ^ l.hdr.x ^ l.hdr.y ^ l.hdr.z ^ l.hdr.w; }
 __device__ __forceinline__ unsigned fold(const Kq<T_Q6_K>::Ld& l) {
@@ -294,6 +288,31 @@ __global__ __launch_bounds__(1024) void quant_kernel(const float* x, const float
     }
 }
 
+// Infinity-Cache prefetch of byte ranges (a side stream): default-policy 16-B loads, folded
+struct PfRanges {
+    const uint8_t* p[8];
+    long long n[8];   // bytes (multiple of 16)
+    int cnt;
+};
+__global__ __launch_bounds__(256) void mall_prefetch(PfRanges r) {
+    unsigned f = 0;
+    for (int k = 0; k < r.cnt; ++k) {
+        const u32x4* p = reinterpret_cast<const u32x4*>(r.p[k]);
+        const long long n16 = r.n[k] / 16;
+        for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n16; i += (long long)gridDim.x * 256 * 4) {
+            u32x4 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const long long ii = i + (long long)u * gridDim.x * 256;
+                v[u] = ii < n16 ? *gptr(p + ii) : u32x4{0u, 0u, 0u, 0u};
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) f ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+        }
+    }
+    if (f == 0x9e3779b9u) reinterpret_cast<unsigned*>(const_cast<uint8_t*>(r.p[0]))[0] = f;
+}
+
 // ---------------------------------------------------------------------------------------------
 struct Mat {
     int type, rows, nb;
@@ -331,14 +350,40 @@ static Mat make_mat(int type, int rows, int K) {
 
 typedef void (*KFn)(FA);
 struct Launch {
-    int kind;          // 0 gemv, 1 quant norm, 2 quant plain
+    int kind;          // 0 gemv, 1 quant norm, 2 quant plain, 3 prefetch fork (side stream), 4 join
+    PfRanges pf;
+    int pf_grid;
     KFn fn;
     int nw, grid, smem;
     FA a;
     const float* qx; const float* qnw; int qK; char* qact;
     size_t bytes;
 };
+static hipStream_t g_side = nullptr;
+static std::vector<hipEvent_t> g_evs;
+static size_t g_ev_i = 0;
+static hipEvent_t next_ev() {
+    if (g_ev_i == g_evs.size()) {
+        hipEvent_t ev;
+        CK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        g_evs.push_back(ev);
+    }
+    return g_evs[g_ev_i++];
+}
 static void run(const Launch& L, hipStream_t s) {
+    if (L.kind == 3) {   // fork: the side stream waits for the main stream's progress, then prefetches
+        hipEvent_t ev = next_ev();
+        CK(hipEventRecord(ev, s));
+        CK(hipStreamWaitEvent(g_side, ev, 0));
+        hipLaunchKernelGGL(mall_prefetch, dim3(L.pf_grid), dim3(256), 0, g_side, L.pf);
+        return;
+    }
+    if (L.kind == 4) {   // join
+        hipEvent_t ev = next_ev();
+        CK(hipEventRecord(ev, g_side));
+        CK(hipStreamWaitEvent(s, ev, 0));
+        return;
+    }
     if (L.kind == 0) hipLaunchKernelGGL(L.fn, dim3(L.grid), dim3(L.nw * 64), L.smem, s, L.a);
     else if (L.kind == 1) hipLaunchKernelGGL(quant_kernel<1>, dim3(1), dim3(1024), 0, s, L.qx, L.qnw, L.qK, L.qact);
     else hipLaunchKernelGGL(quant_kernel<0>, dim3(1), dim3(1024), 0, s, L.qx, L.qnw, L.qK, L.qact);
@@ -461,7 +506,8 @@ int main(int argc, char** argv) {
     if (what & 2) {
         // a 7B Q4_K_M-like step: 32 layers x {QKV, [attention out quant], WO, gate/up, down} + the head
         const int L = 32;
-        std::vector<Launch> floor_, sep, tick, pro;
+        std::vector<Launch> floor_, sep, tick, pro, sep3;
+        std::vector<PfRanges> lay;
         size_t bytes = 0;
         FA bq = b; bq.act = actA;                           // QKV reads act A
         FA bw = b; bw.act = actB;                           // WO reads act B (attention output)
@@ -473,6 +519,19 @@ int main(int argc, char** argv) {
             Mat g = make_mat(T_Q4_K, 11008, 4096), u = make_mat(T_Q4_K, 11008, 4096);
             Mat d = make_mat(more ? T_Q6_K : T_Q4_K, 4096, 11008);
             bytes += qkv.bytes + wo.bytes + g.bytes + u.bytes + d.bytes;
+            {
+                PfRanges r{};
+                const Mat* ms[5] = {&qkv, &wo, &g, &u, &d};
+                const int pb4[4] = {128, 16, 0, 0}, pb6[4] = {128, 64, 16, 2};
+                for (const Mat* m : ms) {   // the planes of each matrix are one allocation from p[0]
+                    const int* pb = m->type == T_Q4_K ? pb4 : pb6;
+                    long long tot = 0;
+                    for (int q = 0; q < 4; ++q) tot += ((long long)m->rows * m->nb * pb[q] + 4096 + 255) & ~255LL;
+                    r.p[r.cnt] = m->p[0];
+                    r.n[r.cnt++] = tot & ~15LL;
+                }
+                lay.push_back(r);
+            }
             floor_.push_back(mk<T_Q4_K, 8, 2, 2, 9, 0>(qkv, nullptr, bq));
             floor_.push_back(mk<T_Q4_K, 8, 1, 2, 9, 0>(wo, nullptr, bw));
             floor_.push_back(mk<T_Q4_K, 8, 2, 2, 9, 1>(g, &u, bg));
@@ -491,6 +550,15 @@ int main(int argc, char** argv) {
             if (more) sep.push_back(mk<T_Q6_K, 8, 1, 6, 0, 0>(d, nullptr, bd2));
             else sep.push_back(mk<T_Q4_K, 8, 1, 6, 0, 0>(d, nullptr, bd2));
             sep.push_back(mk_quant(1, x, nw, 4096, actA));
+            // sep3: sep with the attention output quantised by the attention kernel itself
+            sep3.push_back(mk<T_Q4_K, 8, 2, 2, 0, 0>(qkv, nullptr, bq));
+            sep3.push_back(mk<T_Q4_K, 8, 1, 2, 0, 0>(wo, nullptr, bw2));
+            sep3.push_back(mk_quant(1, x2, nw, 4096, actC));
+            sep3.push_back(mk<T_Q4_K, 8, 2, 2, 0, 3>(g, &u, bgs));
+            sep3.push_back(mk_quant(0, h, nw, 11008, actD));
+            if (more) sep3.push_back(mk<T_Q6_K, 8, 1, 6, 0, 0>(d, nullptr, bd2));
+            else sep3.push_back(mk<T_Q4_K, 8, 1, 6, 0, 0>(d, nullptr, bd2));
+            sep3.push_back(mk_quant(1, x, nw, 4096, actA));
             // ticket: WO and down publish the next activation themselves (gate/up too, per block)
             FA bwt = bw; bwt.out = x2; bwt.resid = x; bwt.act_out = actC; bwt.cnt = cnt + 1024;
             FA bdt = bd; bdt.out = x; bdt.resid = x2; bdt.act_out = actA; bdt.cnt = cnt + 2048;
@@ -517,9 +585,36 @@ int main(int argc, char** argv) {
         sep.push_back(mk<T_Q6_K, 8, 1, 2, 0, 0>(o, nullptr, bo));
         tick.push_back(mk<T_Q6_K, 8, 1, 2, 0, 0>(o, nullptr, bo));
         pro.push_back(mk<T_Q6_K, 8, 1, 2, 0, 0>(o, nullptr, bo));
-        const char* names[4] = {"floor", "sep", "ticket", "pro"};
-        for (int pass = 0; pass < 4; ++pass) {
-            const auto& st = pass == 0 ? floor_ : pass == 1 ? sep : pass == 2 ? tick : pro;
+        // the same chains with the next layer's weights prefetched into the Infinity Cache on a side
+        // stream when a layer starts (every launch of layer l marks its start: kind 3 before it)
+        auto with_pf = [&](const std::vector<Launch>& st, int per_layer, int grid) {
+            std::vector<Launch> o;
+            for (size_t i = 0; i < st.size(); ++i) {
+                const int l = (int)(i / per_layer);
+                if (i % per_layer == 0 && (size_t)i < (size_t)per_layer * L && l + 1 < L) {
+                    Launch f{};
+                    f.kind = 3;
+                    f.pf = lay[l + 1];
+                    f.pf_grid = grid;
+                    o.push_back(f);
+                }
+                o.push_back(st[i]);
+            }
+            Launch j{};
+            j.kind = 4;
+            o.push_back(j);
+            return o;
+        };
+        CK(hipStreamCreateWithFlags(&g_side, hipStreamNonBlocking));
+        const auto floor_pf = with_pf(floor_, 4, 128);
+        const auto sep3_pf64 = with_pf(sep3, 7, 64);
+        const auto sep3_pf128 = with_pf(sep3, 7, 128);
+        const auto sep3_pf256 = with_pf(sep3, 7, 256);
+        const char* names[9] = {"floor", "sep", "ticket", "pro", "sep3", "floor+pf", "sep3+pf64", "sep3+pf128", "sep3+pf256"};
+        for (int pass = 0; pass < 9; ++pass) {
+            g_ev_i = 0;
+            const auto& st = pass == 0 ? floor_ : pass == 1 ? sep : pass == 2 ? tick : pass == 3 ? pro : pass == 4 ? sep3
+                           : pass == 5 ? floor_pf : pass == 6 ? sep3_pf64 : pass == 7 ? sep3_pf128 : sep3_pf256;
             hipGraph_t g; hipGraphExec_t ge;
             CK(hipStreamBeginCapture(s, hipStreamCaptureModeGlobal));
             for (const auto& Lc : st) run(Lc, s);
