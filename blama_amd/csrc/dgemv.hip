@@ -8,16 +8,17 @@
 //    as workgroups retire).  Every weight load of a wave is issued at entry -- no ring, nothing
 //    waits on the activation before the weights are in flight (the streaming floor measured by
 //    scripts/exp_gemv2.cpp / exp_fgemv.cpp).
-//  * The activation arrives QUANTISED (Q8_K and/or Q8_0, act_layout): 4.6 KB for K = 4096, copied
-//    into LDS by each workgroup (L2-served), instead of the RMSNorm + quantisation prologue that
-//    gemv.hip's workgroups each run.
-//  * The activation is published by the launch before the GEMV: the attention kernel quantises its
-//    own output (a workgroup owns whole 256-blocks), and dv_quant_kernel -- one workgroup --
-//    computes rms_norm(x) * norm_w (or takes h as it is) and quantises it between the residual /
-//    SwiGLU launch and its consumer.  (Publishing it inside the producing launch by arrival
-//    tickets measured 6-10 us slower per launch than the separate 3 us quant launch:
-//    profiles/r05_exp_fgemv.txt, r05_exp_fgemv_chain.txt.)  Every sum is taken in a fixed order:
-//    results are bit-reproducible.
+//  * The activation is quantised once per workgroup into LDS (Q8_K and/or Q8_0, act_layout): the
+//    8 waves load the f32 row (and the norm weight) ahead of their weights, wave w takes blocks
+//    w, w + 8, ... -- rms_norm(x) * norm_w for the QKV, gate/up and head inputs (the sum of squares
+//    in double: each wave's blocks, then the waves in order), h as it is for FFN down -- or, for
+//    WO, the attention kernel has already quantised its output (whole 256-blocks per workgroup)
+//    and each workgroup copies those 4.6 KB into LDS.  Measured alternatives (scripts/exp_fgemv.cpp,
+//    profiles/r05_exp_fgemv*.txt, r05_sp_sep_eager_kernel_stats.csv): publishing the activation
+//    inside the producing launch by arrival tickets cost 6-10 us per launch; a separate one-
+//    workgroup quantisation launch 4.7 us plus its launch boundary; an Infinity-Cache prefetch
+//    of the next layer's weights from a side stream slowed the chain 1.7-2.6x.
+//    Every sum is taken in a fixed order: results are bit-reproducible.
 #include "qdot.h"
 #include <hip/hip_ext.h>
 
@@ -33,6 +34,7 @@ constexpr int DV_NW = 8;       // waves per workgroup
 constexpr int DV_ACT_LD = 5;   // 16-B activation loads per lane: act bytes <= 5 x 8 KiB
 
 enum DvRole { DV_QKV = 0, DV_ADD = 1, DV_SWIGLU = 2, DV_STORE = 3 };
+
 
 struct DvSeg {
     const uint8_t* a[4];        // planes of A
@@ -76,13 +78,15 @@ __device__ __forceinline__ void dv_body(const DvArgs& a, char* lds) {
     const int u = wg * DV_NW + wave;
     const bool uv = u < S.units;
     const int uc = uv ? u : S.units - 1;
-
+    const ActLayout L = act_layout(a.K, a.q8k, a.q80);
     // ---- 1. the activation and the epilogue's inputs, requested before any weight (loads retire
     // in order: the compiler's wait for them is then a count that leaves the weights in flight)
-    const __amdgpu_buffer_rsrc_t ar = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(a.act), 0, a.act_bytes, 0x00020000);
     u32x4 av[DV_ACT_LD];
+    {
+        const __amdgpu_buffer_rsrc_t ar = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(a.act), 0, a.act_bytes, 0x00020000);
 #pragma unroll
-    for (int k = 0; k < DV_ACT_LD; ++k) av[k] = __builtin_amdgcn_raw_buffer_load_b128(ar, (k * DV_NW * 64 + tid) * 16, 0, 0);
+        for (int k = 0; k < DV_ACT_LD; ++k) av[k] = __builtin_amdgcn_raw_buffer_load_b128(ar, (k * DV_NW * 64 + tid) * 16, 0, 0);
+    }
     i32x4 tp = {0, 0, 0, 0};
     if (ROLE == DV_QKV) tp = *gptr(reinterpret_cast<const i32x4*>(a.tokpos));
     float res = 0.0f;
@@ -120,7 +124,7 @@ __device__ __forceinline__ void dv_body(const DvArgs& a, char* lds) {
         }
     }
 
-    // ---- 3. the activation into LDS (the wait the compiler puts here leaves the weights in flight)
+    // ---- 3. the activation into LDS (the waits the compiler puts here leave the weights in flight)
 #pragma unroll
     for (int k = 0; k < DV_ACT_LD; ++k) {
         const int o = (k * DV_NW * 64 + tid) * 16;
@@ -129,7 +133,6 @@ __device__ __forceinline__ void dv_body(const DvArgs& a, char* lds) {
     dv_lds_barrier();
 
     // ---- 4. the dot products: lane 63 holds each row's sum
-    const ActLayout L = act_layout(a.K, a.q8k, a.q80);
     const Act act = act_view(lds, L, 0);
     float y[RW];
 #pragma unroll
@@ -216,12 +219,14 @@ template <int T0, int ROLE>
 DvFn dv_fn_t1(int t1, int c) {
     constexpr int RW = (ROLE == DV_QKV || ROLE == DV_SWIGLU) ? 2 : 1;
     if (t1 < 0) return dv_fn_c<T0, -1, RW, ROLE>(c);
-    if (ROLE != DV_QKV) return nullptr;
-    switch (t1) {
-    case T_Q6_K: return dv_fn_c<T0, T_Q6_K, RW, ROLE>(c);
-    case T_Q8_0: return dv_fn_c<T0, T_Q8_0, RW, ROLE>(c);
-    default: return nullptr;
+    if constexpr (ROLE == DV_QKV) {   // mixed-type Q/K/V launches only
+        switch (t1) {
+        case T_Q6_K: return dv_fn_c<T0, T_Q6_K, RW, ROLE>(c);
+        case T_Q8_0: return dv_fn_c<T0, T_Q8_0, RW, ROLE>(c);
+        default: return nullptr;
+        }
     }
+    return nullptr;
 }
 template <int ROLE>
 DvFn dv_fn_role(int t0, int t1, int c) {
@@ -247,83 +252,84 @@ int dv_chunks(int K) {
     return c == 5 ? 6 : c;
 }
 
-// rms_norm(x) * norm_w (norm_w null: x itself) of one K-long row, quantised into act (ActOut's
-// formats): one workgroup of 16 waves, wave w holding blocks w, w + 16, ...; the sum of squares
-// in double, the waves' partials added in wave order (ggml_compute_forward_rms_norm_f32)
-constexpr int DQ_KB = 4;   // K <= 16 x 4 x 256
-__global__ __launch_bounds__(1024) void dv_quant_kernel(const float* x, const ActOut t) {
-    __shared__ double red[16];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int nb = t.K >> 8;
-    f32x4 v[DQ_KB], w[DQ_KB];
-#pragma unroll
-    for (int i = 0; i < DQ_KB; ++i) {
-        const int b = wave + 16 * i;
-        if (b < nb) {
-            v[i] = gptr(reinterpret_cast<const f32x4*>(x))[b * 64 + lane];
-            if (t.norm_w) w[i] = gptr(reinterpret_cast<const f32x4*>(t.norm_w))[b * 64 + lane];
-        }
-    }
+
+// rms_norm(x) * norm_w (norm_w set) or x itself, quantised: one workgroup per 256-block.  With the
+// norm, each 4-wave workgroup reads the whole row and takes its sum of squares in double (every
+// workgroup in the same order: thread-strided 16-B pieces, the wave's DPP tree, the 4 waves in
+// order -- so all blocks see one scale, and the result is bit-reproducible); without it, one wave
+// reads its block.  ggml_compute_forward_rms_norm_f32 + ggml_mul, then quantize_row_q8_K /
+// quantize_row_q8_0 (x86 form).
+constexpr int DQ_NORM_W = 4;   // waves per workgroup with the norm
+__global__ __launch_bounds__(DQ_NORM_W * 64) void dv_quant_kernel(const float* x, const ActOut t) {
+    __shared__ double red[DQ_NORM_W];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int b = blockIdx.x;
+    const f32x4 v = gptr(reinterpret_cast<const f32x4*>(x))[b * 64 + lane];   // (waves > 0: unused)
     float scale = 1.0f;
+    f32x4 wn = {1.0f, 1.0f, 1.0f, 1.0f};
     if (t.norm_w) {
+        wn = gptr(reinterpret_cast<const f32x4*>(t.norm_w))[b * 64 + lane];
         double sq = 0.0;
-#pragma unroll
-        for (int i = 0; i < DQ_KB; ++i)
-            if (wave + 16 * i < nb) {
-                sq += (double)(v[i].x * v[i].x);
-                sq += (double)(v[i].y * v[i].y);
-                sq += (double)(v[i].z * v[i].z);
-                sq += (double)(v[i].w * v[i].w);
-            }
+        const int n4 = t.K >> 2;
+        for (int i = tid; i < n4; i += DQ_NORM_W * 64) {
+            const f32x4 y = gptr(reinterpret_cast<const f32x4*>(x))[i];
+            sq += (double)(y.x * y.x);
+            sq += (double)(y.y * y.y);
+            sq += (double)(y.z * y.z);
+            sq += (double)(y.w * y.w);
+        }
         sq = wave_sum63_d(sq);
         if (lane == 63) red[wave] = sq;
         __syncthreads();
         double tot = 0.0;
-        for (int k = 0; k < 16; ++k) tot += red[k];
+#pragma unroll
+        for (int k = 0; k < DQ_NORM_W; ++k) tot += red[k];
         scale = 1.0f / sqrtf((float)(tot / (double)t.K) + t.eps);
     }
-#pragma unroll
-    for (int i = 0; i < DQ_KB; ++i) {
-        const int b = wave + 16 * i;
-        if (b >= nb) continue;
-        float q[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
-        if (t.norm_w) {   // ggml_vec_scale_f32 then ggml_mul
-            q[0] = (q[0] * scale) * w[i].x;
-            q[1] = (q[1] * scale) * w[i].y;
-            q[2] = (q[2] * scale) * w[i].z;
-            q[3] = (q[3] * scale) * w[i].w;
-        }
-        dv_quant_block(t, b, q, lane);
+    if (wave != 0) return;
+    float q[4] = {v.x, v.y, v.z, v.w};
+    if (t.norm_w) {   // ggml_vec_scale_f32 then ggml_mul
+        q[0] = (q[0] * scale) * wn.x;
+        q[1] = (q[1] * scale) * wn.y;
+        q[2] = (q[2] * scale) * wn.z;
+        q[3] = (q[3] * scale) * wn.w;
     }
+    dv_quant_block(t, b, q, lane);
 }
 
 }  // namespace
 
+size_t dv_act_bytes(int K, int q8k, int q80) { return (size_t)act_layout(K, q8k, q80).slot_bytes; }
+
 void launch_dv_quant(const float* x, const ActOut& t, hipStream_t s) {
-    if (t.K % 256 || t.K > DQ_KB * 16 * 256 || !t.act || (!t.q8k && !t.q80)) throw Error("dv_quant: unsupported shape");
-    hipLaunchKernelGGL(dv_quant_kernel, dim3(1), dim3(1024), 0, s, x, t);
+    if (t.K % 256 || t.K <= 0 || !t.act || (!t.q8k && !t.q80)) throw Error("dv_quant: unsupported shape");
+    hipLaunchKernelGGL(dv_quant_kernel, dim3(t.K / 256), dim3(t.norm_w ? DQ_NORM_W * 64 : 64), 0, s, x, t);
     MI_HIP(hipGetLastError());
 }
 
-size_t dv_act_bytes(int K, int q8k, int q80) { return (size_t)act_layout(K, q8k, q80).slot_bytes; }
+namespace {
+int dv_role(const GemvSeg& g) {
+    return g.epi == EPI_QKV ? DV_QKV : g.epi == EPI_ADD ? DV_ADD : g.epi == EPI_SWIGLU ? DV_SWIGLU
+         : g.epi == EPI_STORE ? DV_STORE : -1;
+}
+}  // namespace
 
 bool dgemv_supported(const GemvParams& p) {
-    if (p.nseg < 1 || p.nseg > 2 || p.K % 256 || dv_act_bytes(p.K, p.act_q8k, p.act_q80) > (size_t)DV_ACT_LD * DV_NW * 64 * 16)
+    if (p.nseg < 1 || p.nseg > 2 || p.K % 256 || (!p.act_q8k && !p.act_q80) ||
+        dv_act_bytes(p.K, p.act_q8k, p.act_q80) > (size_t)DV_ACT_LD * DV_NW * 64 * 16)
         return false;
-    const int c = dv_chunks(p.K);
     const GemvSeg& g = p.seg[0];
-    const int role = g.epi == EPI_QKV ? DV_QKV : g.epi == EPI_ADD ? DV_ADD : g.epi == EPI_SWIGLU ? DV_SWIGLU
-                   : g.epi == EPI_STORE ? DV_STORE : -1;
+    const int role = dv_role(g);
     if (role < 0 || g.bias || g.expA >= 0 || g.expB >= 0) return false;
     if (p.nseg == 2 && (role != DV_QKV || p.seg[1].epi != EPI_QKV)) return false;
-    return dv_fn(role, g.A.type, p.nseg == 2 ? p.seg[1].A.type : -1, c) != nullptr;
+    return dv_fn(role, g.A.type, p.nseg == 2 ? p.seg[1].A.type : -1, dv_chunks(p.K)) != nullptr;
 }
 
 void launch_dgemv(const GemvParams& p, hipStream_t s, hipEvent_t ev_start, hipEvent_t ev_stop) {
     if (!p.act_in) throw Error("dgemv: no quantised activation");
     if (!dgemv_supported(p)) throw Error("dgemv: unsupported launch shape");
     const GemvSeg& g0 = p.seg[0];
-    const int role = g0.epi == EPI_QKV ? DV_QKV : g0.epi == EPI_ADD ? DV_ADD : g0.epi == EPI_SWIGLU ? DV_SWIGLU : DV_STORE;
+    const int role = dv_role(g0);
     const int rw = (role == DV_QKV || role == DV_SWIGLU) ? 2 : 1;
     DvArgs a;
     std::memset(&a, 0, sizeof(a));

@@ -737,8 +737,8 @@ long long Ctx::ffn_bytes() const {
     auto mb = [](const QMat& q) { return (long long)q.rows * q.nb * ((long long)block_bytes(q.type) * 256 / block_elems(q.type)); };
     const HParams& hp = m->hp;
     const long long w = hp.n_expert > 0 ? 2 * (mb(L.gate) + mb(L.up)) : mb(L.gate) + mb(L.up);
-    if (sp_ok)   // streaming path: the quantised input read, h written
-        return w + (long long)dv_act_bytes(hp.n_embd, sp[0].fC & 1, sp[0].fC >> 1) + (long long)hp.n_ff * 4;
+    if (sp_ok)   // streaming path: x and the norm weight read (by every workgroup, L2-served), h written
+        return w + (long long)hp.n_embd * 4 * 2 + (long long)hp.n_ff * 4;
     const long long act = (long long)hp.n_embd * 4 * 2 + (long long)hp.n_ff * 4 * (hp.n_expert > 0 ? 2 : 1);
     return w + act;   // weights + x and norm weight read + h written
 }
@@ -878,14 +878,12 @@ int act_fmt(std::initializer_list<int> types) {
 bool Ctx::sp_setup() {
     const HParams& hp = m->hp;
     if (hp.arch != ARCH_LLAMA || hp.n_expert > 0 || getenv("MI_DECODE_OLD")) return false;
-    if (hp.n_embd % 256 || hp.n_ff % 256 || hp.n_embd > 16384 || hp.n_ff > 16384) return false;
-    if (hp.n_head * hp.head_dim != hp.n_embd) return false;
+    if (hp.n_embd % 256 || hp.n_ff % 256 || hp.n_head * hp.head_dim != hp.n_embd) return false;
+    if (!attn_quant_supported(hp.n_head, hp.n_head_kv, hp.head_dim)) return false;
     const int nl = hp.n_layer;
     sp.assign(nl, SpLayer{});
     sp_fH = act_fmt({m->output.type});
-    size_t off = 0;
-    auto take = [&](size_t bytes) { const size_t o = off; off += (bytes + 255) / 256 * 256; return o; };
-    std::vector<size_t> o(nl * 8);
+    size_t act_max = 0;
     for (int l = 0; l < nl; ++l) {
         const Layer& L = m->layers[l];
         SpLayer& b = sp[l];
@@ -894,39 +892,16 @@ bool Ctx::sp_setup() {
         b.fB = act_fmt({L.wo.type});
         b.fC = act_fmt({L.gate.type, L.up.type});
         b.fD = act_fmt({L.down.type});
-        o[l * 8 + 0] = take((size_t)hp.n_embd * 4);
-        o[l * 8 + 1] = take((size_t)hp.n_embd * 4);
-        o[l * 8 + 2] = take((size_t)hp.n_embd * 4);
-        o[l * 8 + 3] = take((size_t)hp.n_ff * 4);
-        o[l * 8 + 4] = take(dv_act_bytes(hp.n_embd, b.fA & 1, b.fA >> 1));
-        o[l * 8 + 5] = take(dv_act_bytes(hp.n_embd, b.fB & 1, b.fB >> 1));
-        o[l * 8 + 6] = take(dv_act_bytes(hp.n_embd, b.fC & 1, b.fC >> 1));
-        o[l * 8 + 7] = take(dv_act_bytes(hp.n_ff, b.fD & 1, b.fD >> 1));
+        act_max = std::max(act_max, dv_act_bytes(hp.n_embd, b.fB & 1, b.fB >> 1));
     }
-    const size_t oH = take(dv_act_bytes(hp.n_embd, sp_fH & 1, sp_fH >> 1));
-    MI_HIP(hipSetDevice(device));
-    MI_HIP(hipMalloc(&sp_mem, off));
-    MI_HIP(hipMemset(sp_mem, 0, off));
-    for (int l = 0; l < nl; ++l) {
-        SpLayer& b = sp[l];
-        b.xw = reinterpret_cast<float*>(sp_mem + o[l * 8 + 0]);
-        b.xd = reinterpret_cast<float*>(sp_mem + o[l * 8 + 1]);
-        b.att = reinterpret_cast<float*>(sp_mem + o[l * 8 + 2]);
-        b.h = reinterpret_cast<float*>(sp_mem + o[l * 8 + 3]);
-        b.aA = sp_mem + o[l * 8 + 4];
-        b.aB = sp_mem + o[l * 8 + 5];
-        b.aC = sp_mem + o[l * 8 + 6];
-        b.aD = sp_mem + o[l * 8 + 7];
-    }
-    sp_aH = sp_mem + oH;
-    // every launch must have a variant: dry-run the step's parameter checks
+    // every launch must have a variant: the step's parameter checks, dry
     bool ok = true;
     for (int l = 0; l < nl && ok; ++l) {
         const Layer& L = m->layers[l];
         GemvParams p;
         std::memset(&p, 0, sizeof(p));
         p.K = hp.n_embd;
-        p.act_in = sp[l].aA;
+        p.act_in = reinterpret_cast<const char*>(x);   // (any non-null pointer: the checks only)
         p.act_q8k = sp[l].fA & 1;
         p.act_q80 = sp[l].fA >> 1;
         for (int g = 0; g < L.n_qkv && ok;) {
@@ -943,14 +918,16 @@ bool Ctx::sp_setup() {
         w.act_q8k = sp[l].fB & 1;
         w.act_q80 = sp[l].fB >> 1;
         ok = ok && dgemv_supported(w);
-        GemvParams gu = w;
-        gu.seg[0] = seg_of(L.gate, PAIR_AB, EPI_SWIGLU, x);
+        GemvParams gu = p;
+        gu.nseg = 1;
+        gu.seg[0] = seg_of(L.gate, PAIR_AB, EPI_SWIGLU, h);
         gu.seg[0].B = L.up;
         gu.act_q8k = sp[l].fC & 1;
         gu.act_q80 = sp[l].fC >> 1;
         ok = ok && L.gate.type == L.up.type && dgemv_supported(gu);
-        GemvParams d = w;
+        GemvParams d = p;
         d.K = hp.n_ff;
+        d.nseg = 1;
         d.seg[0] = seg_of(L.down, PAIR_ADJ, EPI_ADD, x);
         d.act_q8k = sp[l].fD & 1;
         d.act_q80 = sp[l].fD >> 1;
@@ -959,47 +936,54 @@ bool Ctx::sp_setup() {
     GemvParams hd;
     std::memset(&hd, 0, sizeof(hd));
     hd.K = hp.n_embd;
+    hd.act_in = reinterpret_cast<const char*>(x);
     hd.nseg = 1;
     hd.seg[0] = seg_of(m->output, PAIR_ADJ, EPI_STORE, logits);
-    hd.act_in = sp_aH;
     hd.act_q8k = sp_fH & 1;
     hd.act_q80 = sp_fH >> 1;
-    ok = ok && dgemv_supported(hd) && attn_quant_supported(hp.n_head, hp.n_head_kv, hp.head_dim);
+    ok = ok && dgemv_supported(hd);
     if (!ok) {
-        MI_HIP(hipFree(sp_mem));
-        sp_mem = nullptr;
         sp.clear();
+        return false;
     }
-    return ok;
+    size_t act_n = 0, act_f = 0;
+    for (int l = 0; l < nl; ++l) {
+        const SpLayer& b = sp[l];
+        for (int f : {b.fA, b.fB, b.fC}) act_n = std::max(act_n, dv_act_bytes(hp.n_embd, f & 1, f >> 1));
+        act_f = std::max(act_f, dv_act_bytes(hp.n_ff, b.fD & 1, b.fD >> 1));
+    }
+    act_n = std::max(act_n, dv_act_bytes(hp.n_embd, sp_fH & 1, sp_fH >> 1));
+    act_n = (act_n + 255) / 256 * 256;
+    act_f = (act_f + 255) / 256 * 256;
+    MI_HIP(hipSetDevice(device));
+    MI_HIP(hipMalloc(&sp_mem, 4 * act_n + act_f));
+    MI_HIP(hipMemset(sp_mem, 0, 4 * act_n + act_f));
+    sp_act[0] = sp_mem;
+    sp_act[1] = sp_mem + act_n;
+    sp_act[2] = sp_mem + 2 * act_n;
+    sp_act[4] = sp_mem + 3 * act_n;
+    sp_act[3] = sp_mem + 4 * act_n;
+    return true;
 }
 
-// One batch-1 decode step on the streaming kernels: the embedding (+ layer 0's quantised input),
-// per layer QKV -> attention (+ the WO input quantised) -> WO -> dv_quant(rms_norm * ffn_norm) ->
-// gate/up -> dv_quant(h) -> down -> dv_quant(the next layer's, or the output head's, input), the
-// output head, the top-k.  Profiling segments as enqueue_step's (the gate/up launch of prof_layer
-// carries the event pair).
+// One batch-1 decode step on the streaming kernels: the embedding, per layer dv_quant(rms_norm(x) *
+// attn_norm) -> QKV -> attention (its output also quantised) -> WO + residual -> dv_quant(rms_norm
+// * ffn_norm) -> gate/up -> dv_quant(h) -> down + residual, then the output head and the top-k.
+// Profiling segments as enqueue_step's (the gate/up launch of prof_layer carries the event pair).
 void Ctx::enqueue_step_sp(bool with_logits) {
     const HParams& hp = m->hp;
     int seg = 0;
     auto on = [&]() { return seg_filter < 0 || seg_filter == seg; };
     const float theta_scale = std::pow(hp.rope_base, -2.0f / (float)hp.n_rot);
     const float kq_scale = 1.0f / std::sqrt((float)hp.head_dim);
-    auto act_out = [&](char* act, int fmt, int K, const float* norm_w) {
-        ActOut t;
-        std::memset(&t, 0, sizeof(t));
-        t.K = K;
-        t.q8k = fmt & 1;
-        t.q80 = fmt >> 1;
-        t.act = act;
-        t.norm_w = norm_w;
-        t.eps = hp.eps;
-        return t;
+    auto act = [&](int role, int fmt, int K, const float* norm_w) {
+        return ActOut{K, fmt & 1, fmt >> 1, sp_act[role], norm_w, hp.eps};
     };
     if (on()) {
-        EmbedParams ep{m->tok_embd, tokpos, x, hp.n_embd, QMat{}, 0, step_ctr};
-        launch_embed_act(ep, act_out(sp[0].aA, sp[0].fA, hp.n_embd, m->layers[0].attn_norm), stream);
+        EmbedParams ep{m->tok_embd, tokpos, x, hp.n_embd, m->pos_embd, 0, step_ctr};
+        launch_embed(ep, stream);
+        launch_dv_quant(x, act(0, sp[0].fA, hp.n_embd, m->layers[0].attn_norm), stream);
     }
-    const float* x_in = x;
     for (int l = 0; l < hp.n_layer; ++l) {
         const Layer& L = m->layers[l];
         const SpLayer& b = sp[l];
@@ -1015,7 +999,7 @@ void Ctx::enqueue_step_sp(bool with_logits) {
         base.K = hp.n_embd;
         {   // Q/K/V + RoPE + KV append
             GemvParams p = base;
-            p.act_in = b.aA;
+            p.act_in = sp_act[0];
             p.act_q8k = b.fA & 1;
             p.act_q80 = b.fA >> 1;
             p.theta_scale = theta_scale;
@@ -1036,69 +1020,67 @@ void Ctx::enqueue_step_sp(bool with_logits) {
                 if (on()) launch_dgemv(p, stream);
             }
         }
-        {   // attention (fused, <= ATTN_SHORT cells); its output quantised for WO
-            AttnParams a{q, kl, vl, tokpos, cell_pos, attn_scores, attn_smax, b.att, hp.n_head, hp.n_head_kv,
+        {   // attention (fused, <= ATTN_SHORT cells), its output also quantised for WO
+            AttnParams a{q, kl, vl, tokpos, cell_pos, attn_scores, attn_smax, part_o, hp.n_head, hp.n_head_kv,
                          hp.head_dim, kv_dim, (int)n_ctx, kq_scale};
             a.fused = 1;
-            a.act_out = act_out(b.aB, b.fB, hp.n_embd, nullptr);
+            a.act_out = act(1, b.fB, hp.n_embd, nullptr);
             if (on()) launch_attn(a, stream);
         }
-        {   // output projection + residual, then rms_norm(x) * ffn_norm quantised
+        {   // output projection + residual (in place), then rms_norm(x) * ffn_norm quantised
             GemvParams p = base;
-            p.act_in = b.aB;
+            p.act_in = sp_act[1];
             p.act_q8k = b.fB & 1;
             p.act_q80 = b.fB >> 1;
             p.nseg = 1;
-            p.seg[0] = seg_of(L.wo, PAIR_ADJ, EPI_ADD, b.xw);
-            p.seg[0].resid = x_in;
+            p.seg[0] = seg_of(L.wo, PAIR_ADJ, EPI_ADD, x);
+            p.seg[0].resid = x;
             if (on()) {
                 launch_dgemv(p, stream);
-                launch_dv_quant(b.xw, act_out(b.aC, b.fC, hp.n_embd, L.ffn_norm), stream);
+                launch_dv_quant(x, act(2, b.fC, hp.n_embd, L.ffn_norm), stream);
             }
         }
         {   // FFN gate/up + SwiGLU, then h quantised
             GemvParams p = base;
-            p.act_in = b.aC;
+            p.act_in = sp_act[2];
             p.act_q8k = b.fC & 1;
             p.act_q80 = b.fC >> 1;
             p.nseg = 1;
-            p.seg[0] = seg_of(L.gate, PAIR_AB, EPI_SWIGLU, b.h);
+            p.seg[0] = seg_of(L.gate, PAIR_AB, EPI_SWIGLU, h);
             p.seg[0].B = L.up;
             if (l == prof_layer) seg = 1;
             const bool timed = l == prof_layer && seg_filter == 1;
             if (on()) launch_dgemv(p, stream, timed ? prof_ev[0] : nullptr, timed ? prof_ev[1] : nullptr);
             if (l == prof_layer) seg = 2;
-            if (on()) launch_dv_quant(b.h, act_out(b.aD, b.fD, hp.n_ff, nullptr), stream);
+            if (on()) launch_dv_quant(h, act(3, b.fD, hp.n_ff, nullptr), stream);
         }
-        {   // FFN down + residual, then the next layer's (or the output head's) input quantised
+        {   // FFN down + residual (in place), then the next layer's (or the output head's) input quantised
             GemvParams p = base;
+            p.act_in = sp_act[3];
             p.K = hp.n_ff;
-            p.act_in = b.aD;
             p.act_q8k = b.fD & 1;
             p.act_q80 = b.fD >> 1;
             p.nseg = 1;
-            p.seg[0] = seg_of(L.down, PAIR_ADJ, EPI_ADD, b.xd);
-            p.seg[0].resid = b.xw;
+            p.seg[0] = seg_of(L.down, PAIR_ADJ, EPI_ADD, x);
+            p.seg[0].resid = x;
             if (on()) {
                 launch_dgemv(p, stream);
                 if (l + 1 < hp.n_layer)
-                    launch_dv_quant(b.xd, act_out(sp[l + 1].aA, sp[l + 1].fA, hp.n_embd, m->layers[l + 1].attn_norm),
-                                    stream);
+                    launch_dv_quant(x, act(0, sp[l + 1].fA, hp.n_embd, m->layers[l + 1].attn_norm), stream);
                 else if (with_logits)
-                    launch_dv_quant(b.xd, act_out(sp_aH, sp_fH, hp.n_embd, m->output_norm), stream);
+                    launch_dv_quant(x, act(4, sp_fH, hp.n_embd, m->output_norm), stream);
             }
         }
-        x_in = b.xd;
     }
-    if (with_logits && on()) {
+    if (with_logits && on()) {   // the output head, the top-k
         GemvParams p;
         std::memset(&p, 0, sizeof(p));
         p.K = hp.n_embd;
-        p.nseg = 1;
-        p.seg[0] = seg_of(m->output, PAIR_ADJ, EPI_STORE, logits);
-        p.act_in = sp_aH;
+        p.act_in = sp_act[4];
         p.act_q8k = sp_fH & 1;
         p.act_q80 = sp_fH >> 1;
+        p.nseg = 1;
+        p.seg[0] = seg_of(m->output, PAIR_ADJ, EPI_STORE, logits);
         launch_dgemv(p, stream);
         TopkParams tp{logits, hp.n_vocab, cand, topk_ids, topk_vals, d_h_topk_ids, d_h_topk_vals};
         launch_topk(tp, stream);
@@ -1498,6 +1480,11 @@ void Ctx::decode_ubatch(const int32_t* tokens, int n, bool all) {
         launch_embed_multi(ep, nt, stream);
         launch_rope_table(tokpos_b, nt, hp.n_rot, theta_scale, hp.freq_scale, m->rope_freqs, ub_rope, stream);
         const float* pend = nullptr;   // split-K partials not yet added into xb (the next quant_act does)
+        // split-K parts of the residual GEMMs: 4 for short batches of dense models (verification
+        // of tens of tokens: more workgroups, a quarter of the superblock steps each; 4 x nt rows
+        // fit the 2 x UB_MAX partials buffer), else 2 (the MoE router adds 2)
+        static const int ks_short = getenv("MI_MMQ_KS4") ? atoi(getenv("MI_MMQ_KS4")) : 64;
+        const int ks = hp_dense() && nt <= ks_short ? 4 : 2;
         for (int l = 0; l < hp.n_layer; ++l) {
             const Layer& L = m->layers[l];
             __half* kl = kcache + (size_t)l * n_ctx * kv_dim;
@@ -1523,7 +1510,7 @@ void Ctx::decode_ubatch(const int32_t* tokens, int n, bool all) {
                 for (const QMat* q : mats) need = need || (q->type == T_Q8_0) == (f == 1);
                 if (need) {
                     launch_quant_act(xb, hp.n_embd, L.attn_norm, hp.eps, ub_act(hp.n_embd, nt, f ? T_Q8_0 : T_Q4_K), stream,
-                                     nullptr, pend);
+                                     nullptr, pend, ks);
                     pend = nullptr;
                 }
             }
@@ -1558,8 +1545,8 @@ void Ctx::decode_ubatch(const int32_t* tokens, int n, bool all) {
                 p.epi = EPI_ADD;
                 p.out = xb;
                 p.resid = xb;
-                if (ub_part && L.wo.nb >= 2) {   // halves of K; the FFN's quant_act adds them
-                    p.ksplit = 2;
+                if (ub_part && L.wo.nb >= ks) {   // parts of K; the FFN's quant_act adds them
+                    p.ksplit = ks;
                     p.part = ub_part;
                     pend = ub_part;
                 }
@@ -1572,7 +1559,7 @@ void Ctx::decode_ubatch(const int32_t* tokens, int n, bool all) {
             }
             {   // FFN gate/up + SwiGLU
                 const ActQ8 act = ub_act(hp.n_embd, nt, L.gate.type);
-                launch_quant_act(xb, hp.n_embd, L.ffn_norm, hp.eps, act, stream, nullptr, pend);
+                launch_quant_act(xb, hp.n_embd, L.ffn_norm, hp.eps, act, stream, nullptr, pend, ks);
                 pend = nullptr;
                 GemmParams p = b;
                 p.A = L.gate;
@@ -1593,8 +1580,8 @@ void Ctx::decode_ubatch(const int32_t* tokens, int n, bool all) {
                 p.K = hp.n_ff;
                 p.out = xb;
                 p.resid = xb;
-                if (ub_part && L.down.nb >= 2 && l + 1 < hp.n_layer) {   // the next layer's quant_act adds them
-                    p.ksplit = 2;
+                if (ub_part && L.down.nb >= ks && l + 1 < hp.n_layer) {   // the next layer's quant_act adds them
+                    p.ksplit = ks;
                     p.part = ub_part;
                     pend = ub_part;
                 }

@@ -224,19 +224,17 @@ struct Ctx {
     // persistent decode step (gemv.hip decode_step_kernel) for contexts within ATTN_SHORT cells:
     // stage tables without / with the output head, built on first use; per-layer activation
     // buffers (q, attention, residual after WO, FFN, residual after down) written once per step
-    // streaming decode step (dgemv.hip) for dense LLaMA contexts within ATTN_SHORT cells: every
-    // activation arrives quantised, published by the launch before it (the attention kernel, the
-    // embedding, or a one-workgroup dv_quant launch).  Per-layer buffers.
+    // streaming decode step (dgemv.hip) for dense LLaMA contexts within ATTN_SHORT cells: every GEMV
+    // reads its activation quantised -- WO's from the attention kernel, the others' from a
+    // dv_quant launch (rms_norm'd x, or h) -- from sp_act[role]
     struct SpLayer {
-        float *xw, *xd, *att, *h;       // residual after WO / after down, attention output, SwiGLU h
-        char *aA, *aB, *aC, *aD;        // quantised inputs of QKV, WO, gate/up, down
-        int fA, fB, fC, fD;             // their formats: bit 0 Q8_K, bit 1 Q8_0
+        int fA, fB, fC, fD;             // activation formats of QKV, WO, gate/up, down: bit 0 Q8_K, bit 1 Q8_0
     };
     bool sp_ok = false;                 // MI_DECODE_OLD=1: the gemv_kernel graph instead
     std::vector<SpLayer> sp;
+    int sp_fH = 0;                      // the output head's activation formats
     char* sp_mem = nullptr;
-    char* sp_aH = nullptr;              // the output head's input (rms_norm(x) * output_norm)
-    int sp_fH = 0;
+    char* sp_act[5] = {};               // QKV, WO, gate/up, down, head inputs
     bool sp_setup();
     void enqueue_step_sp(bool with_logits);
     struct LayerBufs {

@@ -67,7 +67,8 @@ struct AttnPartials {
     int n_head, head_dim;
 };
 
-// ---- the quantised activation a decode launch publishes for the next one (dgemv.hip) ----
+// ---- a quantised activation a decode launch publishes for the next one (the attention kernel for
+// the streaming WO launch) ----
 // Layout in global memory: act_layout(K, q8k, q80) of qdot.h (the Q8_K blocks, the Q8_0 blocks,
 // the Q8_K sub-block sums and scales, the Q8_0 scales), the same bytes the consumer copies into
 // LDS.  norm_w set: the activation is rms_norm(x) * norm_w (ggml's rms_norm then mul).
@@ -106,9 +107,8 @@ struct GemvParams {
     AttnPartials attn;        // PRO_ATTN input
     int attn_nsplit;          // PRO_ATTN: splits to add (0: from the cell count in tokpos)
     unsigned long long* stamps;   // diagnostics (MI_STAMPS builds): per-workgroup stamps [grid][8]
-    // streaming form (dgemv.hip, dense LLaMA decode within ATTN_SHORT cells): the activation arrives
-    // quantised (act_layout(K, act_q8k, act_q80) at act_in; pro / x / norm_w unused).
-    // act_in == nullptr: the gemv_kernel path above.
+    // streaming form (launch_dgemv, dense LLaMA decode within ATTN_SHORT cells): the activation
+    // arrives quantised, act_layout(K, act_q8k, act_q80) at act_in (pro / x / norm_w unused)
     const char* act_in;
     int act_q8k, act_q80;
 };
@@ -164,9 +164,10 @@ struct GemmParams {
     long long grp_stride;
     int grp_n;
     int grp_max;   // mmq2 grouped: the most rows one expert can have (the batch's tokens)
-    // mmq2 split over K (EPI_ADD of a dense prompt batch): ksplit 2 halves of the superblocks write
-    // their partial sums to part[2][ntok][out_stride] (no residual); the next launch_quant_act
-    // over the same buffer adds them, x = (p0 + p1) + x, writes x back and quantises it
+    // mmq2 split over K (EPI_ADD of a dense prompt batch): ksplit (2 or 4) parts of the superblocks
+    // write their partial sums to part[ksplit][ntok][out_stride] (no residual); the next
+    // launch_quant_act over the same buffer adds them, x = ((p0 + p1) + ...) + x, writes x back and
+    // quantises it
     int ksplit;
     float* part;
     int diag;   // mmq2 timing experiments only (MI_MMQ2_DIAG): 1 = no compute, 2 = no copies past the first
@@ -184,10 +185,8 @@ struct EmbedParams {
     unsigned* step;            // optional: incremented once per launch (decode step counter)
 };
 void launch_embed(const EmbedParams& p, hipStream_t s);
-// the embedding row and the first layer's quantised activation rms_norm(x) * a.norm_w (one
-// workgroup; LLaMA): the streaming decode path's first launch
-void launch_embed_act(const EmbedParams& p, const ActOut& a, hipStream_t s);
-// rms_norm(x) * a.norm_w (or x itself) of one row, quantised (one workgroup; dgemv.hip)
+// rms_norm(x) * a.norm_w (or x itself) of one row, quantised into a.act (dgemv.hip; one workgroup
+// per 256-block)
 void launch_dv_quant(const float* x, const ActOut& a, hipStream_t s);
 
 // ---- attention over the f16 cache: KQ -> soft_max -> KQV, split over cells ----
@@ -334,7 +333,7 @@ struct ActQ8 {
 // part (optional): the split-K partial sums of the GEMM that produced x (see GemmParams::ksplit):
 // x += p0 + p1 first, written back
 void launch_quant_act(const float* x, int x_stride, const float* norm_w, float eps, const ActQ8& a, hipStream_t s,
-                      const int* rows = nullptr, const float* part = nullptr);
+                      const int* rows = nullptr, const float* part = nullptr, int nks = 2);
 // whether prompt-batch GEMMs take the mmq2 path (the only one with ksplit)
 bool mmq2_active();
 // ggml_rope_cache_init per token of the batch: out [ntok][n_rot/2] (cos, sin)

@@ -362,55 +362,6 @@ void launch_embed_multi(const EmbedParams& p, int ntok, hipStream_t s) {
     MI_HIP(hipGetLastError());
 }
 
-// The streaming decode path's first launch (LLaMA): get_rows(tok_embd, token) into x, then
-// rms_norm(x) * attn_norm of layer 0, quantised into t.act (one workgroup of 16 waves; each wave
-// holds blocks wave, wave + 16, ... of the row; the sum of squares in double, waves in order).
-constexpr int EA_KB = 4;   // 256-blocks per wave: n_embd <= 16384
-__global__ __launch_bounds__(1024) void embed_act_kernel(const EmbedParams P, const ActOut t) {
-    __shared__ double red[16];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const long long tok = P.tokpos[0];
-    if (P.step && threadIdx.x == 0) *P.step += 1u;
-    const int nb = P.n_embd >> 8;
-    float v[EA_KB][4];
-    double sq = 0.0;
-#pragma unroll
-    for (int i = 0; i < EA_KB; ++i) {
-        const int b = wave + 16 * i;
-        if (b < nb) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                v[i][k] = dequant_elem(P.E, tok, b * 256 + lane * 4 + k);
-                sq += (double)(v[i][k] * v[i][k]);
-            }
-            *reinterpret_cast<float4*>(P.out + b * 256 + lane * 4) = make_float4(v[i][0], v[i][1], v[i][2], v[i][3]);
-        }
-    }
-    sq = wave_sum63_d(sq);
-    if (lane == 63) red[wave] = sq;
-    __syncthreads();
-    double tot = 0.0;
-    for (int w = 0; w < 16; ++w) tot += red[w];
-    const float scale = 1.0f / sqrtf((float)(tot / (double)P.n_embd) + t.eps);
-#pragma unroll
-    for (int i = 0; i < EA_KB; ++i) {
-        const int b = wave + 16 * i;
-        if (b < nb) {
-            const float4 wn = reinterpret_cast<const float4*>(t.norm_w)[b * 64 + lane];
-            float q[4] = {(v[i][0] * scale) * wn.x, (v[i][1] * scale) * wn.y, (v[i][2] * scale) * wn.z,
-                          (v[i][3] * scale) * wn.w};
-            dv_quant_block(t, b, q, lane);
-        }
-    }
-}
-
-void launch_embed_act(const EmbedParams& p, const ActOut& t, hipStream_t s) {
-    if (p.has_pos || p.n_embd % 256 || p.n_embd > EA_KB * 16 * 256 || t.K != p.n_embd || !t.act || !t.norm_w)
-        throw Error("embed_act: unsupported shape");
-    hipLaunchKernelGGL(embed_act_kernel, dim3(1), dim3(1024), 0, s, p, t);
-    MI_HIP(hipGetLastError());
-}
-
 void launch_embed(const EmbedParams& p, hipStream_t s) {
     hipLaunchKernelGGL(embed_kernel, dim3((p.n_embd + 255) / 256), dim3(256), 0, s, p);
     MI_HIP(hipGetLastError());

@@ -79,7 +79,7 @@ __device__ __forceinline__ float wave_max_pos(float v) {
 // QA_W waves per token row (16: one 256-element block each at K = 4096)
 template <int QA_W>
 __global__ __launch_bounds__(64 * QA_W) void quant_act_kernel(const float* x, int x_stride, const float* norm_w,
-                                                        float eps, ActQ8 a, const int* rows, const float* part) {
+                                                        float eps, ActQ8 a, const int* rows, const float* part, int nks) {
     const int t = blockIdx.x;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int nb = a.K >> 8;
@@ -106,17 +106,18 @@ __global__ __launch_bounds__(64 * QA_W) void quant_act_kernel(const float* x, in
 #pragma unroll
     for (int i = 0; i < XR; ++i)
         if (wave + QA_W * i < nb) xr[i] = x4[(wave + QA_W * i) * 64 + lane];
-    if (part) {   // the split-K GEMM's halves: x = (p0 + p1) + x (EPI_ADD's o + resid), written back
-        const f32x4* p0 = reinterpret_cast<const f32x4*>(part + (long long)t * a.K);
-        const f32x4* p1 = reinterpret_cast<const f32x4*>(part + ((long long)a.ntok + t) * a.K);
+    if (part) {   // the split-K GEMM's nks partials: x = (((p0 + p1) + p2) + ...) + x (EPI_ADD's o + resid), written back
         f32x4* xw = reinterpret_cast<f32x4*>(const_cast<float*>(x) + (long long)t * x_stride);
 #pragma unroll
         for (int i = 0; i < XR; ++i) {
             const int blk = wave + QA_W * i;
             if (blk < nb) {
-                const f32x4 a0 = p0[blk * 64 + lane], a1 = p1[blk * 64 + lane];
-                xr[i] = f32x4{(a0.x + a1.x) + xr[i].x, (a0.y + a1.y) + xr[i].y, (a0.z + a1.z) + xr[i].z,
-                              (a0.w + a1.w) + xr[i].w};
+                f32x4 acc = reinterpret_cast<const f32x4*>(part + (long long)t * a.K)[blk * 64 + lane];
+                for (int k = 1; k < nks; ++k) {
+                    const f32x4 pk = reinterpret_cast<const f32x4*>(part + ((long long)k * a.ntok + t) * a.K)[blk * 64 + lane];
+                    acc = f32x4{acc.x + pk.x, acc.y + pk.y, acc.z + pk.z, acc.w + pk.w};
+                }
+                xr[i] = f32x4{acc.x + xr[i].x, acc.y + xr[i].y, acc.z + xr[i].z, acc.w + xr[i].w};
                 xw[blk * 64 + lane] = xr[i];
             }
         }
@@ -636,11 +637,11 @@ void mmq2_t(const GemmParams P, const ActQ8 act, const float2* rope, const MmqSe
         if (i < S.n) nrb += ((AB ? (S.rows[i] + 15) / 16 : (S.rows[i] + 31) / 32) + RT - 1) / RT;
     const int ntb = (act.npad + 127) / 128;           // token blocks
     const int TB = mmq32_tile_bytes_d(T);
-    // split-K: the grid's second half takes the upper superblocks (kh 1)
-    const int nbid = P.ksplit == 2 ? (int)gridDim.x / 2 : (int)gridDim.x;
+    // split-K: part kh of the grid's ksplit parts takes superblocks [nb kh / ks, nb (kh + 1) / ks)
+    const int ks = P.ksplit > 1 ? P.ksplit : 1;
+    const int nbid = (int)gridDim.x / ks;
     const int kh = (int)blockIdx.x / nbid, bid = (int)blockIdx.x % nbid;
-    const int nbh = (nb + 1) / 2;
-    const int sb0 = P.ksplit == 2 && kh ? nbh : 0, sb1 = P.ksplit == 2 && !kh ? nbh : nb;
+    const int sb0 = nb * kh / ks, sb1 = nb * (kh + 1) / ks;
     int rb, tb_b, tb_e, base, tend, grp_e = 0;
     if (P.grp) {
         // grouped (MoE): blockIdx -> (token block, expert, row block), token block slowest: the
@@ -956,8 +957,8 @@ void mmq2_t(const GemmParams P, const ActQ8 act, const float2* rope, const MmqSe
     const int rt = rb * RT + wr;
     if (w < ntt && rt < nrt) {
         const int row = AB ? rt * 16 + (col & 15) : rt * 32 + col;
-        // split-K: this half's partial sums, stored plainly; else the segment's epilogue
-        if (P.ksplit == 2)
+        // split-K: this part's partial sums, stored plainly; else the segment's epilogue
+        if (P.ksplit > 1)
             mmq_epilogue<AB>(P, tend, rope, tok0 + 32 * w, lane, row, y[0], EPI_STORE, rows_s,
                              P.part + (long long)kh * P.ntok * P.out_stride);
         else
@@ -971,7 +972,8 @@ template <int T, int NST> constexpr int m2_lds() { return M2<T>::lds(NST); }
 }  // namespace mmq
 
 void launch_quant_act(const float* x, int x_stride, const float* norm_w, float eps, const ActQ8& a, hipStream_t s,
-                      const int* rows, const float* part) {
+                      const int* rows, const float* part, int nks) {
+    if (part && nks != 2 && nks != 4) throw Error("quant_act: 2 or 4 split-K partials");
     if (a.K % 256) throw Error("quant_act: K must be a multiple of 256");
     if (part && (rows || x_stride != a.K)) throw Error("quant_act: split-K partials take a dense [ntok][K] x");
     // (more than UB_MAX rows only for the MoE rows of a batch: one per (token, slot), padded)
@@ -980,9 +982,9 @@ void launch_quant_act(const float* x, int x_stride, const float* norm_w, float e
     // MI_QA_W: waves per token row, 16 (default) or 4
     static const int qaw = getenv("MI_QA_W") ? atoi(getenv("MI_QA_W")) : 16;
     if (qaw == 4 && a.K <= 4 * 16 * 256)
-        hipLaunchKernelGGL(mmq::quant_act_kernel<4>, dim3(a.npad), dim3(256), 0, s, x, x_stride, norm_w, eps, a, rows, part);
+        hipLaunchKernelGGL(mmq::quant_act_kernel<4>, dim3(a.npad), dim3(256), 0, s, x, x_stride, norm_w, eps, a, rows, part, nks);
     else
-        hipLaunchKernelGGL(mmq::quant_act_kernel<16>, dim3(a.npad), dim3(1024), 0, s, x, x_stride, norm_w, eps, a, rows, part);
+        hipLaunchKernelGGL(mmq::quant_act_kernel<16>, dim3(a.npad), dim3(1024), 0, s, x, x_stride, norm_w, eps, a, rows, part, nks);
     MI_HIP(hipGetLastError());
 }
 
@@ -1028,9 +1030,10 @@ void launch_mmq2(const GemmParams& p, const mmq::MmqSegs& S, const ActQ8& act, c
     const int ntb = (act.npad + 127) / 128;
     // grouped (MoE): a workgroup per (token block, expert, row block)
     const int g1 = (nrb + 7) / 8 * 8 * (p.grp ? p.grp_n * ((max(p.grp_max, 1) + 127) / 128) : ntb);
-    if (p.ksplit == 2 && (p.grp || p.pair == PAIR_AB || p.epi != EPI_ADD || !p.part || S.n != 1 || p.A.nb < 2))
-        throw Error("mmq2: split-K is for a single EPI_ADD matrix with a partials buffer");
-    const int g2 = g1 * (p.ksplit == 2 ? 2 : 1);
+    if (p.ksplit > 1 && (p.grp || p.pair == PAIR_AB || p.epi != EPI_ADD || !p.part || S.n != 1 || p.A.nb < p.ksplit ||
+                         (p.ksplit != 2 && p.ksplit != 4)))
+        throw Error("mmq2: split-K (2 or 4 parts) is for a single EPI_ADD matrix with a partials buffer");
+    const int g2 = g1 * (p.ksplit > 1 ? p.ksplit : 1);
     // MI_MMQ2_NST: 1 = one stage, two workgroups per CU; 2 = two stages, one workgroup per CU;
     // 0 (default) = one stage when the grid fills two workgroups per CU, else two.  7B 512-token
     // prefill, NST 1 vs 2: 15.5 vs 16.8 ms (same box, scripts/ab_prefill.sh)

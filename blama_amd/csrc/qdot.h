@@ -446,6 +446,9 @@ template <> struct Kq<T_Q8_0> {
 
 __device__ __forceinline__ float silu_f(float x) { return x / (1.0f + expf(-x)); }
 
+// every storing wave, before its workgroup signals a hand-off (invisible to the compiler's waits)
+__device__ __forceinline__ void drain_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
 // ---------------------------------------------------------------------------
 // Block b of a published activation (ActOut, kernels.h) from one wave's 4 values per lane
 // ---------------------------------------------------------------------------

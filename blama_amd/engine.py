@@ -84,6 +84,7 @@ _SIGS = {
     "mi_prof_enable": (C.c_int32, [_P, C.c_int32]),
     "mi_prof_read": (C.c_int32, [_P, C.POINTER(C.c_float), C.c_int32]),
     "mi_prof_ffn_bytes": (C.c_int64, [_P]),
+    "mi_decode_path": (C.c_int32, [_P]),
     "mi_prof_bytes": (C.c_int64, [_P]),
     "mi_debug_stamps": (C.c_int32, [_P, _P, C.c_int32]),
     "mi_op_gemv": (C.c_int32, [C.c_int32, C.c_int32, _P, C.c_int32, C.c_int32, _P, _P]),
@@ -314,6 +315,10 @@ class Context:
     @property
     def ffn_bytes(self) -> int:
         return lib().mi_prof_ffn_bytes(self.h)
+
+    def decode_path(self) -> int:
+        """1: decode steps within 512 cells run on the streaming GEMV (dgemv.hip); 0: gemv_kernel."""
+        return int(lib().mi_decode_path(self.h))
 
     @property
     def prof_bytes(self) -> int:

@@ -147,6 +147,9 @@ int32_t mi_prof_read(mi_ctx* ctx, float* us, int32_t n);
 int64_t mi_prof_ffn_bytes(const mi_ctx* ctx);
 /* Algorithmic HBM bytes of the launch mi_prof_read last timed (the FFN gate/up launch). */
 int64_t mi_prof_bytes(const mi_ctx* ctx);
+/* Diagnostics: 1 when the context's decode steps (within 512 cells) run on the streaming GEMV
+ * (dgemv.hip), 0 on the gemv_kernel graph; -1 for a null context. */
+int32_t mi_decode_path(const mi_ctx* ctx);
 /* Diagnostics: copies the per-workgroup s_memrealtime stamps (100 MHz) of the
  * first n_launch launches of the last decode step, [launch][512][8] uint64, to
  * out.  Returns the number of launches copied; 0 unless the library is the

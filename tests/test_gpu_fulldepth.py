@@ -64,6 +64,7 @@ def _gate(name, rows, floor_of=None):
 def _floor_by_tokens(buf, n_ctx, seq, n0):
     """c_alt_floor over seq (seq[:n0] as the prompt), indexed by the number of tokens decoded."""
     def f():
+        print(f"computing the CPU reorder floor over {len(seq)} tokens", flush=True)
         _, fl = c_alt_floor(buf, n_ctx, seq[:n0], seq[n0:])
         out = np.full(len(seq) + 1, np.inf)
         out[n0:] = fl
@@ -75,9 +76,11 @@ def _floor_by_tokens(buf, n_ctx, seq, n0):
 def test_fulldepth_decode_and_verify_match_oracle(gpu_lib, name):
     cfg = synthetic.CONFIGS[name]
     buf = synthetic.build_gguf(cfg, seed=21)
+    print(f"{name}: synthetic GGUF built ({len(buf) / 1e9:.1f} GB)", flush=True)
     m = engine.Model(buf)
     ctx = engine.Context(m, n_ctx=128)
     orc = ggml_cpu.Model(buf, n_ctx=128)
+    print(f"{name}: model loaded", flush=True)
     rng = np.random.default_rng(17)
     prompt = [int(t) for t in rng.integers(0, cfg.n_vocab, 16)]
     rows = []
@@ -91,7 +94,8 @@ def test_fulldepth_decode_and_verify_match_oracle(gpu_lib, name):
             ids, vals = ctx.topk(10)
             d = np.abs(got.astype(np.float64) - ref)
             rms = float(np.sqrt(np.mean(ref ** 2)))
-            print(f"{name} decode step {s}: max/rms {d.max() / rms:.2e} l2/rms {np.sqrt(np.mean(d ** 2)) / rms:.2e}")
+            print(f"{name} decode step {s}: max/rms {d.max() / rms:.2e} l2/rms {np.sqrt(np.mean(d ** 2)) / rms:.2e}",
+                  flush=True)
             rows.append(([(int(i), float(v)) for i, v in zip(ids, vals)], ref, len(seq)))
             if s == 16:
                 break
@@ -110,7 +114,8 @@ def test_fulldepth_decode_and_verify_match_oracle(gpu_lib, name):
             d = np.abs(got.astype(np.float64) - ref)
             rms = float(np.sqrt(np.mean(ref ** 2)))
             if i % 16 == 0 or i == len(claimed) - 1:
-                print(f"{name} verify row {i}: max/rms {d.max() / rms:.2e} l2/rms {np.sqrt(np.mean(d ** 2)) / rms:.2e}")
+                print(f"{name} verify row {i}: max/rms {d.max() / rms:.2e} l2/rms {np.sqrt(np.mean(d ** 2)) / rms:.2e}",
+                      flush=True)
             rows.append(([(int(x), float(v)) for x, v in zip(ids, vals)], ref, len(seq)))
         _gate(name, rows, _floor_by_tokens(buf, 128, seq, len(prompt)))
     finally:
@@ -128,6 +133,7 @@ def test_fulldepth_512_token_prefill_matches_oracle(gpu_lib):
     name = "llama2-7b-q4_k_m"
     cfg = synthetic.CONFIGS[name]
     buf = synthetic.build_gguf(cfg, seed=23)
+    print("512-prefill: synthetic GGUF built", flush=True)
     m = engine.Model(buf)
     last_ctx = engine.Context(m, n_ctx=544)
     all_ctx = engine.Context(m, n_ctx=544)
@@ -140,6 +146,8 @@ def test_fulldepth_512_token_prefill_matches_oracle(gpu_lib):
         rows = []
         for i, t in enumerate(prompt):
             ref = orc.decode_one(t)
+            if i % 64 == 0:
+                print(f"512-prefill: oracle at token {i}", flush=True)
             if i not in want:
                 continue
             ref = ref.astype(np.float64)
@@ -150,7 +158,8 @@ def test_fulldepth_512_token_prefill_matches_oracle(gpu_lib):
                 got = ctx.logits(row=row).astype(np.float64)
                 ids, vals = ctx.topk(10, row=row)
                 d = np.abs(got - ref)
-                print(f"512-prefill {tag} row {i}: max/rms {d.max() / rms:.2e} l2/rms {np.sqrt(np.mean(d ** 2)) / rms:.2e}")
+                print(f"512-prefill {tag} row {i}: max/rms {d.max() / rms:.2e} l2/rms {np.sqrt(np.mean(d ** 2)) / rms:.2e}",
+                      flush=True)
                 rows.append(([(int(x), float(v)) for x, v in zip(ids, vals)], ref, i + 1))
         assert len(rows) == len(want) + 1
         _gate(name + " 512-token prefill", rows, _floor_by_tokens(buf, 544, prompt, 1))
