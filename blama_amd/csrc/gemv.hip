@@ -912,14 +912,8 @@ typedef void (*GvFn)(const GvArgs);
 // KB activation blocks per wave (K <= 4096: 1, <= 8192: 2, <= 16384: 4 at 16 waves)
 // (the 128-VGPR budget of a 16-wave workgroup: 4 one-row items, 3 two-row items; 2 for the
 // wider Q5_K / Q6_K / Q8_0 two-row items)
-#ifndef MI_GV_DEEP
-#define MI_GV_DEEP 0   // A/B builds: one more ring item per wave
-#endif
-#ifndef MI_GV_DEEP_Q4
-#define MI_GV_DEEP_Q4 0   // A/B builds: one more item for the two-row Q4_K and one-row rings only
-#endif
 template <int T, int RW> struct GvD {
-    static constexpr int D = (RW == 1 ? 4 + MI_GV_DEEP_Q4 : (T == T_Q4_K ? 3 + MI_GV_DEEP_Q4 : 2)) + MI_GV_DEEP;
+    static constexpr int D = RW == 1 ? 4 : (T == T_Q4_K ? 3 : 2);
 };
 
 template <int T0, int T1, int RW, int TAG>

@@ -170,7 +170,6 @@ struct GemmParams {
     // quantises it
     int ksplit;
     float* part;
-    int diag;   // mmq2 timing experiments only (MI_MMQ2_DIAG): 1 = no compute, 2 = no copies past the first
 };
 void launch_gemm(const GemmParams& p, hipStream_t s);
 

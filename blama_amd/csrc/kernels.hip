@@ -847,14 +847,21 @@ __global__ __launch_bounds__(256 * HG) void attn_fused_kernel(const AttnParams P
     // The first chunk of K, V and cell positions is fetched at entry, before the cell count
     // arrives, so the token-position, K and V round trips overlap instead of chaining.  Cells
     // past the count are clamped to the cache and masked by select below, never by arithmetic.
-    u32x4 k0[U], v0[U];
-    int cp0[U];
+    // (the first TWO chunks of a wave: a decode step within 128 cells makes no dependent cache
+    // round trip after entry)
+    constexpr int STRIDE = 4 * CPW * U;   // cells between a wave's chunks
+    u32x4 k0[U], v0[U], k1[U], v1[U];
+    int cp0[U], cp1[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const int c = min(wave * CPW + u * 4 * CPW + G, P.n_ctx - 1);
+        const int c1 = min(wave * CPW + STRIDE + u * 4 * CPW + G, P.n_ctx - 1);
         k0[u] = *reinterpret_cast<const u32x4*>(P.kcache + (long long)c * P.kv_dim + row_off);
         v0[u] = *reinterpret_cast<const u32x4*>(P.vcache + (long long)c * P.kv_dim + row_off);
         cp0[u] = P.cell_pos[c];
+        k1[u] = *reinterpret_cast<const u32x4*>(P.kcache + (long long)c1 * P.kv_dim + row_off);
+        v1[u] = *reinterpret_cast<const u32x4*>(P.vcache + (long long)c1 * P.kv_dim + row_off);
+        cp1[u] = P.cell_pos[c1];
     }
     const int ncell = min(tp2 + 1, ATTN_SHORT);
     float q[R][8];
@@ -878,6 +885,12 @@ __global__ __launch_bounds__(256 * HG) void attn_fused_kernel(const AttnParams P
             for (int u = 0; u < U; ++u) {
                 kk[u] = k0[u];
                 cpos[u] = cp0[u];
+            }
+        } else if (cb == wave * CPW + STRIDE) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                kk[u] = k1[u];
+                cpos[u] = cp1[u];
             }
         } else {
 #pragma unroll
@@ -940,15 +953,15 @@ __global__ __launch_bounds__(256 * HG) void attn_fused_kernel(const AttnParams P
     for (int cb = wave * CPW; cb < ncell; cb += 4 * CPW * U) {
         u32x4 vv[U];
         float pw[U][R];
-        const bool first = cb == wave * CPW;
+        const bool first = cb == wave * CPW, second = cb == wave * CPW + STRIDE;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             int c = cb + u * 4 * CPW + G;
             const bool in = c < ncell;
             c = in ? c : ncell - 1;
-            if (first) {   // prefetched at entry; a cell past the count may hold non-finite bits
+            if (first || second) {   // prefetched at entry; a cell past the count may hold non-finite bits
                 const u32x4 z = {0u, 0u, 0u, 0u};
-                vv[u] = in ? v0[u] : z;
+                vv[u] = in ? (first ? v0[u] : v1[u]) : z;
             } else {
                 vv[u] = *reinterpret_cast<const u32x4*>(P.vcache + (long long)c * P.kv_dim + row_off);
             }

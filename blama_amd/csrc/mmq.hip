@@ -229,8 +229,6 @@ __device__ __forceinline__ v16i mfma(v4i a, v4i b) {
     return __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b, z, 0, 0, 0);
 }
 
-constexpr int TT = 4;   // token tiles (of 32) per workgroup
-constexpr int KS = 4;   // waves = superblock splits
 
 // get_scale_min_k4 for the 8 sub-blocks of a Q4_K header {d, dmin, scales[12]}
 __device__ __forceinline__ void q4k_scales(const u32x4 hd, int sc[8], int mn[8]) {
@@ -324,176 +322,6 @@ template <bool AB>
 __device__ __forceinline__ void mmq_epilogue(const GemmParams& P, int tend, const float2* rope, int ttok0,
                                              int lane, int row, const float v[16], int epi, int nrows,
                                              float* out);
-
-// KSPLIT 4: the 4 waves split the superblocks of all 4 token tiles (partials meet in LDS);
-// KSPLIT 1: wave w owns token tile w over all superblocks (no LDS; the 4 waves read the same
-// weight bytes, L1/L2 hits).  OCC: waves per SIMD the register budget is sized for.
-template <int T, bool AB, int KSPLIT, int OCC>
-__global__ __launch_bounds__(256, OCC) void mmq32_t(const GemmParams P, const ActQ8 act, const float2* rope) {
-    __shared__ float red[KSPLIT > 1 ? KS : 1][KSPLIT > 1 ? TT : 1][16][64];   // 64 KiB: partial sums
-    const int lane = threadIdx.x & 63;
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int col = lane & 31, h = lane >> 5;
-    const int nb = P.K >> 8;
-    const int nrt = AB ? (P.A.rows + 15) / 16 : (P.A.rows + 31) / 32;
-    int rt, tg_b, tg_e, base, tend;
-    const uint8_t* swA = P.A.sw;
-    if (KSPLIT == 1 && P.grp) {
-        // grouped (MoE): blockIdx -> (expert, row tile); the expert's token groups in turn
-        const int nrt8 = (nrt + 7) / 8 * 8;
-        const int e = (int)blockIdx.x / nrt8;
-        rt = (int)blockIdx.x % nrt8;
-        if (rt >= nrt) return;
-        base = P.grp[e];
-        const int cnt = P.grp[P.grp_n + 1 + e];
-        tend = base + cnt;
-        tg_b = 0;
-        tg_e = (cnt + 32 * TT - 1) / (32 * TT);
-        swA += (long long)e * P.grp_stride;
-    } else {
-        // blockIdx -> (row tile, token group): the token groups of a row tile on one XCD
-        const int ntg = (act.npad + 32 * TT - 1) / (32 * TT);
-        const int b = blockIdx.x, xcd = b & 7, slot = b >> 3;
-        rt = (slot / ntg) * 8 + xcd;
-        tg_b = slot % ntg;
-        tg_e = tg_b + 1;
-        base = 0;
-        tend = act.ntok;
-        if (rt >= nrt) return;
-    }
-    // this lane's weight row
-    const int row = AB ? rt * 16 + (col & 15) : rt * 32 + col;
-    const int sb0 = KSPLIT > 1 ? nb * w / KS : 0, sb1 = KSPLIT > 1 ? nb * (w + 1) / KS : nb;
-  for (int tg = tg_b; tg < tg_e; ++tg) {
-    const int tok0 = base + tg * 32 * TT;
-    int ntt = P.grp ? (tend - tok0 + 31) / 32 : (act.npad - tok0) / 32;
-    ntt = ntt > TT ? TT : ntt;
-    const int t_begin = KSPLIT > 1 ? 0 : w, t_end = KSPLIT > 1 ? ntt : (w < ntt ? w + 1 : w);
-
-    // token tiles outer (one 16-register accumulator live), superblocks inner; the weight
-    // fragments of a superblock are re-read per token tile (L1/L2 hits after the first)
-    for (int t = t_begin; t < t_end; ++t) {
-        float y[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) y[r] = 0.0f;
-        for (int sb = sb0; sb < sb1; ++sb) {
-            const int8_t* aq = act.q + ((long long)(tok0 / 32 + t) * nb + sb) * 8192 + lane * 16;
-            const float* dT = act.dT + (long long)sb * act.npad + tok0 + 32 * t + 4 * h;
-            int S[16];
-#pragma unroll
-            for (int r = 0; r < 16; ++r) S[r] = 0;
-            const uint8_t* wt = swA + ((long long)rt * nb + sb) * mmq32_tile_bytes_d(T);
-            if (T == T_Q8_0) {   // vec_dot_q8_0_q8_0: per 32-block sumi * (d_x * d_y)
-                const u32x4 dwv = *gp(reinterpret_cast<const u32x4*>(wt + 8192 + col * 16));
-                const unsigned dw[4] = {dwv.x, dwv.y, dwv.z, dwv.w};
-                const float* dT8 = act.dT + (long long)sb * 8 * act.npad + tok0 + 32 * t + 4 * h;
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const v4i wq = *gp(reinterpret_cast<const v4i*>(wt + j * 1024 + lane * 16));
-                    const v4i a = *gp(reinterpret_cast<const v4i*>(aq + j * 1024));
-                    const v16i dj = mfma(a, wq);
-                    const float dwj = h2f(dw[j >> 1] >> (16 * (j & 1)));
-#pragma unroll
-                    for (int g = 0; g < 4; ++g) {
-                        const f32x4 dx4 = *gp(reinterpret_cast<const f32x4*>(dT8 + (long long)j * act.npad + 8 * g));
-                        const float dx[4] = {dx4.x, dx4.y, dx4.z, dx4.w};
-#pragma unroll
-                        for (int i = 0; i < 4; ++i) y[4 * g + i] = fmaf((float)dj[4 * g + i], dwj * dx[i], y[4 * g + i]);
-                    }
-                }
-                continue;
-            }
-            if (T == T_Q4_K || T == T_Q5_K) {
-                // qs[32p + l]: low nibble = sub-block 2p element l, high nibble = sub-block 2p+1;
-                // Q5_K: + 16 * bit 2p / 2p+1 of qh[l] (dequantize_row_q5_K)
-                const u32x4 hd = *gp(reinterpret_cast<const u32x4*>(wt + (T == T_Q5_K ? 5120 : 4096) + col * 16));
-                u32x4 qh = {0u, 0u, 0u, 0u};
-                if (T == T_Q5_K) qh = *gp(reinterpret_cast<const u32x4*>(wt + 4096 + lane * 16));
-                int sc[8], mn[8];
-                q4k_scales(hd, sc, mn);
-#pragma unroll
-                for (int p = 0; p < 4; ++p) {
-                    const u32x4 wq = *gp(reinterpret_cast<const u32x4*>(wt + p * 1024 + lane * 16));
-                    const unsigned sl = 2 * p, sh = 2 * p + 1;
-                    const v4i blo = v4i{(int)((wq.x & 0x0F0F0F0Fu) | (((qh.x >> sl) & 0x01010101u) << 4)),
-                                        (int)((wq.y & 0x0F0F0F0Fu) | (((qh.y >> sl) & 0x01010101u) << 4)),
-                                        (int)((wq.z & 0x0F0F0F0Fu) | (((qh.z >> sl) & 0x01010101u) << 4)),
-                                        (int)((wq.w & 0x0F0F0F0Fu) | (((qh.w >> sl) & 0x01010101u) << 4))};
-                    const v4i bhi = v4i{(int)(((wq.x >> 4) & 0x0F0F0F0Fu) | (((qh.x >> sh) & 0x01010101u) << 4)),
-                                        (int)(((wq.y >> 4) & 0x0F0F0F0Fu) | (((qh.y >> sh) & 0x01010101u) << 4)),
-                                        (int)(((wq.z >> 4) & 0x0F0F0F0Fu) | (((qh.z >> sh) & 0x01010101u) << 4)),
-                                        (int)(((wq.w >> 4) & 0x0F0F0F0Fu) | (((qh.w >> sh) & 0x01010101u) << 4))};
-                    const v4i a0 = *gp(reinterpret_cast<const v4i*>(aq + (2 * p) * 1024));
-                    const v4i a1 = *gp(reinterpret_cast<const v4i*>(aq + (2 * p + 1) * 1024));
-                    const v16i d0 = mfma(a0, blo);
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) S[r] = __mul24(sc[2 * p], d0[r]) + S[r];
-                    const v16i d1 = mfma(a1, bhi);
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) S[r] = __mul24(sc[2 * p + 1], d1[r]) + S[r];
-                }
-                // sum_j m_j*bsum_j: mins as int8 B operands, k 0-7 (against hi) / k 8-15 (against lo)
-                const int m03 = mn[0] | (mn[1] << 8) | (mn[2] << 16) | (mn[3] << 24);
-                const int m47 = mn[4] | (mn[5] << 8) | (mn[6] << 16) | (mn[7] << 24);
-                const v4i bm1 = h == 0 ? v4i{m03, m47, 0, 0} : v4i{0, 0, 0, 0};
-                const v4i bm2 = h == 0 ? v4i{0, 0, m03, m47} : v4i{0, 0, 0, 0};
-                const v4i ab = h == 0 ? *gp(reinterpret_cast<const v4i*>(act.bsb + (((long long)(tok0 / 32 + t) * nb + sb) * 32 + col) * 16))
-                                      : v4i{0, 0, 0, 0};
-                const v16i x1 = mfma(ab, bm1);
-                const v16i x2 = mfma(ab, bm2);
-                const float dr = h2f(hd.x), dmr = h2f(hd.x >> 16);
-#pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    const f32x4 dx4 = *gp(reinterpret_cast<const f32x4*>(dT + 8 * g));
-                    const float dx[4] = {dx4.x, dx4.y, dx4.z, dx4.w};
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const int r = 4 * g + i;
-                        const float d = dr * dx[i], dm = dmr * dx[i];
-                        y[r] = fmaf(-dm, (float)(64 * x1[r] + x2[r]), fmaf(d, (float)S[r], y[r]));
-                    }
-                }
-            } else {   // Q6_K: sum of the 8 spans of w = 64*hi + lo, each operand accumulated by the MFMA
-                v16i ah = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, al = ah;
-#pragma unroll
-                for (int sp = 0; sp < 8; ++sp) {
-                    const v4i a = *gp(reinterpret_cast<const v4i*>(aq + sp * 1024));
-                    const v4i bh = *gp(reinterpret_cast<const v4i*>(wt + sp * 1024 + lane * 16));
-                    const v4i bl = *gp(reinterpret_cast<const v4i*>(wt + 8192 + sp * 1024 + lane * 16));
-                    ah = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bh, ah, 0, 0, 0);
-                    al = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bl, al, 0, 0, 0);
-                }
-                const float dr = h2f(*gp(reinterpret_cast<const unsigned short*>(wt + 16384 + col * 2)));
-#pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    const f32x4 dx4 = *gp(reinterpret_cast<const f32x4*>(dT + 8 * g));
-                    const float dx[4] = {dx4.x, dx4.y, dx4.z, dx4.w};
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const int r = 4 * g + i;
-                        y[r] = fmaf(dr * dx[i], (float)(ah[r] * 64 + al[r]), y[r]);   // the exact sumi of the superblock
-                    }
-                }
-            }
-        }
-        if (KSPLIT > 1) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) red[w][t][r][lane] = y[r];
-        } else {
-            mmq_epilogue<AB>(P, tend, rope, tok0 + 32 * t, lane, row, y, P.epi, P.A.rows, P.out);
-        }
-    }
-    if (KSPLIT == 1) continue;
-    // ---- the superblock splits meet in LDS, in wave order
-    __syncthreads();
-    const int t = w;   // this wave's epilogue: token tile w
-    if (t >= ntt) return;
-    float v[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) v[r] = ((red[0][t][r][lane] + red[1][t][r][lane]) + red[2][t][r][lane]) + red[3][t][r][lane];
-    mmq_epilogue<AB>(P, tend, rope, tok0 + 32 * t, lane, row, v, P.epi, P.A.rows, P.out);
-  }
-}
 
 // The epilogue of one 32-token x 32-row D tile (v: this lane's 16 results).
 template <bool AB>
@@ -761,8 +589,7 @@ void mmq2_t(const GemmParams P, const ActQ8 act, const float2* rope, const MmqSe
         // and whose operand planes take this step's decode.
         __builtin_amdgcn_s_waitcnt((0x7 << 4) | (0xF << 8));   // vmcnt(0)
         __builtin_amdgcn_s_barrier();
-        if (NST == 2 && sb + 1 < sb1 && (P.diag != 2 || sb == sb0)) copy_stage(sb + 1, (sb + 1) & 1);
-        if (P.diag == 1) continue;
+        if (NST == 2 && sb + 1 < sb1) copy_stage(sb + 1, (sb + 1) & 1);
         const lchar* stg = (const lchar*)(smem + (NST == 2 ? (sb & 1) : 0) * C::STAGE);
         const lchar* A0 = stg + C::A_OFF + w * 8192 + lane * 16;       // this wave's token tile
         const lchar* dTw = stg + C::DT_OFF + (w * 32 + 4 * h) * 4;
@@ -979,12 +806,7 @@ void launch_quant_act(const float* x, int x_stride, const float* norm_w, float e
     // (more than UB_MAX rows only for the MoE rows of a batch: one per (token, slot), padded)
     if (a.npad % 32 || a.ntok > a.npad || a.npad > 4 * UB_MAX) throw Error("quant_act: bad token count");
     if (a.K > 65536) throw Error("quant_act: K past 65536");
-    // MI_QA_W: waves per token row, 16 (default) or 4
-    static const int qaw = getenv("MI_QA_W") ? atoi(getenv("MI_QA_W")) : 16;
-    if (qaw == 4 && a.K <= 4 * 16 * 256)
-        hipLaunchKernelGGL(mmq::quant_act_kernel<4>, dim3(a.npad), dim3(256), 0, s, x, x_stride, norm_w, eps, a, rows, part, nks);
-    else
-        hipLaunchKernelGGL(mmq::quant_act_kernel<16>, dim3(a.npad), dim3(1024), 0, s, x, x_stride, norm_w, eps, a, rows, part, nks);
+    hipLaunchKernelGGL(mmq::quant_act_kernel<16>, dim3(a.npad), dim3(1024), 0, s, x, x_stride, norm_w, eps, a, rows, part, nks);
     MI_HIP(hipGetLastError());
 }
 
@@ -1014,11 +836,7 @@ void launch_mmq32_swizzle(const QMat& A, const QMat* B, uint8_t* dst, hipStream_
 }
 
 namespace {
-bool mmq2_enabled() {
-    static const int var_env = getenv("MI_MMQ") ? atoi(getenv("MI_MMQ")) : 1;
-    static const bool old_env = getenv("MI_MMQ_OLD") != nullptr;
-    return var_env == 1 && !old_env;
-}
+bool mmq2_enabled() { return true; }
 // one mmq2 launch over the segments S (all of p.A's type; one segment unless launch_mmq32_multi)
 void launch_mmq2(const GemmParams& p, const mmq::MmqSegs& S, const ActQ8& act, const float2* rope, hipStream_t s) {
     const bool ab = p.pair == PAIR_AB;
@@ -1063,10 +881,7 @@ void launch_mmq2(const GemmParams& p, const mmq::MmqSegs& S, const ActQ8& act, c
         MI_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(f2), hipFuncAttributeMaxDynamicSharedMemorySize, lds));
         attr_done[ni][ti][ab] = true;
     }
-    static const int diag = getenv("MI_MMQ2_DIAG") ? atoi(getenv("MI_MMQ2_DIAG")) : 0;
-    GemmParams p2 = p;
-    p2.diag = diag;
-    hipLaunchKernelGGL(f2, dim3(g2), dim3(64 * NWv), (size_t)lds, s, p2, act, rope, S);
+    hipLaunchKernelGGL(f2, dim3(g2), dim3(64 * NWv), (size_t)lds, s, p, act, rope, S);
     MI_HIP(hipGetLastError());
 }
 }  // namespace
@@ -1104,7 +919,6 @@ void launch_mmq32_multi(const GemmParams* ps, int n, const ActQ8& act, const flo
 bool mmq2_active() { return mmq2_enabled(); }
 
 void launch_mmq32(const GemmParams& p, const ActQ8& act, const float2* rope, hipStream_t s) {
-    if (p.ksplit == 2 && !mmq2_enabled()) throw Error("mmq32: split-K needs the mmq2 path");
     if (!mmq32_supported(p.A.type)) throw Error("mmq32: Q4_K / Q5_K / Q6_K / Q8_0 only");
     if ((p.A.type == T_Q8_0) != (act.q80 != 0)) throw Error("mmq32: Q8_0 weights take Q8_0 activations, k-quants Q8_K");
     if (act.K != p.K || p.A.K != p.K) throw Error("mmq32: activation length differs from K");
@@ -1116,38 +930,12 @@ void launch_mmq32(const GemmParams& p, const ActQ8& act, const float2* rope, hip
         throw Error("mmq32: RoPE epilogue needs the rope table");
     if (act.ntok < 1 || act.npad % 32 || act.npad > (p.grp ? 4 * UB_MAX : UB_MAX)) throw Error("mmq32: bad token count");
     if (!p.A.sw) throw Error("mmq32: the matrix has no MFMA-order copy");
-    const int ntg = (act.npad + 32 * mmq::TT - 1) / (32 * mmq::TT);
-    const int nrt = ab ? (p.A.rows + 15) / 16 : (p.A.rows + 31) / 32;
-    // grouped (MoE): a workgroup per (expert, row tile), each over its expert's token groups
-    const int grid = p.grp ? p.grp_n * ((nrt + 7) / 8 * 8) : (nrt + 7) / 8 * 8 * ntg;
-    if (p.grp && (p.grp_n < 1 || (p.epi != EPI_SWIGLU && p.epi != EPI_STORE)))
-        throw Error("mmq32: a grouped launch is an expert gate/up or down");
-    // MI_MMQ=<v>: 0 = K split over the waves (2 waves/SIMD), 1 (default) = a token tile per wave over
-    // all superblocks at 2 waves/SIMD, 2 = the same at 3 waves/SIMD.  Measured on the 7B 512-token
-    // prefill: 21.97 / 21.19 / 22.69 ms (profiles/r02_prefill_*).
-    static const int var_env = getenv("MI_MMQ") ? atoi(getenv("MI_MMQ")) : 1;
-    const int var = p.grp && var_env == 0 ? 1 : var_env;   // grouped launches: a token tile per wave
-    decltype(&mmq::mmq32_t<T_Q4_K, false, 4, 2>) fn;
-#define MMQ_PICK(KS_, OCC_)                                                                              \
-    fn = p.A.type == T_Q4_K ? (ab ? mmq::mmq32_t<T_Q4_K, true, KS_, OCC_> : mmq::mmq32_t<T_Q4_K, false, KS_, OCC_>) \
-       : p.A.type == T_Q5_K ? (ab ? mmq::mmq32_t<T_Q5_K, true, KS_, OCC_> : mmq::mmq32_t<T_Q5_K, false, KS_, OCC_>) \
-       : p.A.type == T_Q6_K ? (ab ? mmq::mmq32_t<T_Q6_K, true, KS_, OCC_> : mmq::mmq32_t<T_Q6_K, false, KS_, OCC_>) \
-                            : (ab ? mmq::mmq32_t<T_Q8_0, true, KS_, OCC_> : mmq::mmq32_t<T_Q8_0, false, KS_, OCC_>)
-    if (var == 1) MMQ_PICK(1, 2);
-    else if (var == 2) MMQ_PICK(1, 3);
-    else MMQ_PICK(4, 2);
-#undef MMQ_PICK
-    if (var == 1 && mmq2_enabled()) {   // mmq2: 128-token x 64-row blocks, LDS-DMA staged
-        mmq::MmqSegs S{};
-        S.n = 1;
-        S.sw[0] = p.A.sw;
-        S.rows[0] = p.A.rows;
-        S.epi[0] = p.epi;
-        launch_mmq2(p, S, act, rope, s);
-        return;
-    }
-    hipLaunchKernelGGL(fn, dim3(grid), dim3(256), 0, s, p, act, rope);
-    MI_HIP(hipGetLastError());
+    mmq::MmqSegs S{};
+    S.n = 1;
+    S.sw[0] = p.A.sw;
+    S.rows[0] = p.A.rows;
+    S.epi[0] = p.epi;
+    launch_mmq2(p, S, act, rope, s);
 }
 
 }  // namespace mi
