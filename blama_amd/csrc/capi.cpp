@@ -761,18 +761,32 @@ int32_t mi_op_gemm(int32_t device, int32_t type, const void* raw, const void* ra
         MI_HIP(hipMemcpy(dx.p, x, (size_t)ntok * K * sizeof(float), hipMemcpyHostToDevice));
         ActQ8 act{dq.as<int8_t>(), ddT.as<float>(), dbs.as<int8_t>(), K, ntok, npad, type == T_Q8_0 ? 1 : 0};
         launch_quant_act(dx.as<float>(), K, nullptr, 0.0f, act, nullptr);
-        GemmParams p;
-        std::memset(&p, 0, sizeof(p));
-        p.A = A;
-        p.B = B;
-        p.pair = pair ? PAIR_AB : PAIR_ADJ;
-        p.epi = pair ? EPI_SWIGLU : EPI_STORE;
-        p.K = K;
-        p.ntok = ntok;
-        p.tokpos = dtp.as<int>();
-        p.out = dy.as<float>();
-        p.out_stride = rows;
-        launch_mmq32(p, act, nullptr, nullptr);
+        // up to MMQS_MAX tokens: the short-batch GEMM (K-part sums, added by part_sum) as the
+        // engine's verification batches take it; MI_MMQS_MAX=0: the tiled GEMM for every count
+        const char* ms = getenv("MI_MMQS_MAX");
+        const bool short_b = ntok <= (ms ? atoi(ms) : MMQS_MAX);
+        if (short_b) {
+            const int pst = pair ? 2 * rows : rows;
+            DevBuf part((size_t)mmqs_parts(K) * ntok * pst * sizeof(float));
+            const QMat* mats[1] = {&A};
+            const int prow[1] = {0};
+            const int kp = launch_mmqs(mats, prow, 1, pair, rows, act, part.as<float>(), pst, nullptr);
+            launch_part_sum(part.as<float>(), kp, ntok, rows, pst, nullptr, 0, dy.as<float>(), rows, nullptr, pair ? rows : 0);
+            MI_HIP(hipDeviceSynchronize());
+        } else {
+            GemmParams p;
+            std::memset(&p, 0, sizeof(p));
+            p.A = A;
+            p.B = B;
+            p.pair = pair ? PAIR_AB : PAIR_ADJ;
+            p.epi = pair ? EPI_SWIGLU : EPI_STORE;
+            p.K = K;
+            p.ntok = ntok;
+            p.tokpos = dtp.as<int>();
+            p.out = dy.as<float>();
+            p.out_stride = rows;
+            launch_mmq32(p, act, nullptr, nullptr);
+        }
         MI_HIP(hipDeviceSynchronize());
         MI_HIP(hipMemcpy(y, dy.p, (size_t)ntok * rows * sizeof(float), hipMemcpyDeviceToHost));
         return 0;

@@ -663,6 +663,16 @@ Ctx::Ctx(Model* model, uint32_t nctx, uint32_t nbatch, uint32_t nubatch) : m(mod
             static const bool ksplit_env = getenv("MI_MMQ_KSPLIT") == nullptr || atoi(getenv("MI_MMQ_KSPLIT")) != 0;
             if (ksplit_env && mmq2_active())
                 MI_HIP(hipMalloc(&ub_part, (size_t)2 * UB_MAX * hp.n_embd * sizeof(float)));
+            mmqs_max = getenv("MI_MMQS_MAX") ? std::min(MMQS_MAX, std::max(0, atoi(getenv("MI_MMQS_MAX")))) : MMQS_MAX;
+            if (mmqs_max > 0 && hp.n_expert == 0) {
+                const size_t qkv = (size_t)hp.n_embd + 2 * (size_t)kv_dim;
+                size_t per = std::max({(size_t)mmqs_parts(hp.n_embd) * std::max({qkv, (size_t)hp.n_embd, 2 * (size_t)hp.n_ff}),
+                                       (size_t)mmqs_parts(hp.n_ff) * hp.n_embd});
+                if (out_mmq) per = std::max(per, (size_t)mmqs_parts(hp.n_embd) * hp.n_vocab);
+                MI_HIP(hipMalloc(&ub_spart, per * MMQS_MAX * sizeof(float)));
+            } else {
+                mmqs_max = 0;
+            }
         }
         // MoE prompts need the MFMA path (the v_dot4 GEMM has no routed-expert form)
         if (hp.n_expert > 0 && !mmq_ok) batch_ok = false;
@@ -712,7 +722,7 @@ Ctx::~Ctx() {
                     (void*)topk_vals, (void*)sel, (void*)selw, (void*)gather_ids, (void*)gather_out,
                     (void*)cell_delta, (void*)move_src, (void*)part_o, (void*)attn_smax, (void*)attn_scores, (void*)stamps,
                     (void*)attn_xflags, (void*)attn_xmax, (void*)attn_xsum, (void*)step_ctr,
-                    (void*)xb, (void*)qb, (void*)attnb, (void*)hb, (void*)tokpos_b, (void*)ub_q, (void*)ub_dT, (void*)ub_bsb, (void*)ub_rope, (void*)ub_part,
+                    (void*)xb, (void*)qb, (void*)attnb, (void*)hb, (void*)tokpos_b, (void*)ub_q, (void*)ub_dT, (void*)ub_bsb, (void*)ub_rope, (void*)ub_part, (void*)ub_spart,
                     (void*)ub_q0, (void*)ub_dT0, (void*)yb, (void*)sel_b, (void*)selw_b, (void*)moe_rows, (void*)moe_pos,
                     (void*)moe_rowsel, (void*)moe_grp, (void*)moe_q, (void*)moe_dT, (void*)moe_bsb,
                     (void*)logits_all, (void*)grows_ids, (void*)grows_out, (void*)sp_mem})
@@ -932,6 +942,10 @@ bool Ctx::sp_setup() {
         d.act_q8k = sp[l].fD & 1;
         d.act_q80 = sp[l].fD >> 1;
         ok = ok && dgemv_supported(d);
+        // FFN down on h as it is (each workgroup quantises it while its weights stream in) in place
+        // of a separate quantisation launch; MI_DOWN_QUANT=1: the separate launch (A/B)
+        d.act_raw = 1;
+        sp[l].rawD = getenv("MI_DOWN_QUANT") == nullptr && dgemv_supported(d);
     }
     GemvParams hd;
     std::memset(&hd, 0, sizeof(hd));
@@ -1052,11 +1066,12 @@ void Ctx::enqueue_step_sp(bool with_logits) {
             const bool timed = l == prof_layer && seg_filter == 1;
             if (on()) launch_dgemv(p, stream, timed ? prof_ev[0] : nullptr, timed ? prof_ev[1] : nullptr);
             if (l == prof_layer) seg = 2;
-            if (on()) launch_dv_quant(h, act(3, b.fD, hp.n_ff, nullptr), stream);
+            if (on() && !b.rawD) launch_dv_quant(h, act(3, b.fD, hp.n_ff, nullptr), stream);
         }
         {   // FFN down + residual (in place), then the next layer's (or the output head's) input quantised
             GemvParams p = base;
-            p.act_in = sp_act[3];
+            p.act_in = b.rawD ? reinterpret_cast<const char*>(h) : sp_act[3];
+            p.act_raw = b.rawD ? 1 : 0;
             p.K = hp.n_ff;
             p.act_q8k = b.fD & 1;
             p.act_q80 = b.fD >> 1;
@@ -1480,12 +1495,18 @@ void Ctx::decode_ubatch(const int32_t* tokens, int n, bool all) {
         launch_embed_multi(ep, nt, stream);
         launch_rope_table(tokpos_b, nt, hp.n_rot, theta_scale, hp.freq_scale, m->rope_freqs, ub_rope, stream);
         const float* pend = nullptr;   // split-K partials not yet added into xb (the next quant_act does)
+        int pend_k = 0;                // (their count)
+        const bool short_b = mmqs_max > 0 && nt <= mmqs_max && hp_dense();
         // split-K parts of the residual GEMMs: 4 for short batches of dense models (verification
         // of tens of tokens: more workgroups, a quarter of the superblock steps each; 4 x nt rows
         // fit the 2 x UB_MAX partials buffer), else 2 (the MoE router adds 2)
         static const int ks_short = getenv("MI_MMQ_KS4") ? atoi(getenv("MI_MMQ_KS4")) : 64;
         const int ks = hp_dense() && nt <= ks_short ? 4 : 2;
-        for (int l = 0; l < hp.n_layer; ++l) {
+        if (short_b) {
+            pend_k = ubatch_layers_short(nt);
+            pend = ub_spart;
+        }
+        for (int l = 0; l < (short_b ? 0 : hp.n_layer); ++l) {
             const Layer& L = m->layers[l];
             __half* kl = kcache + (size_t)l * n_ctx * kv_dim;
             __half* vl = vcache + (size_t)l * n_ctx * kv_dim;
@@ -1588,7 +1609,21 @@ void Ctx::decode_ubatch(const int32_t* tokens, int n, bool all) {
                 launch_mmq32(p, act, ub_rope, stream);
             }
         }
-        if (all) {   // final norm + output head over every token of the batch
+        if (all && short_b) {   // final norm + output head on mmqs, its parts summed into the logits rows
+            const ActQ8 a_out = ub_act(hp.n_embd, nt, m->output.type);
+            launch_quant_act(xb, hp.n_embd, m->output_norm, hp.eps, a_out, stream, nullptr, pend, pend_k);
+            const QMat* mo[1] = {&m->output};
+            const int pr[1] = {0};
+            const int kp = launch_mmqs(mo, pr, 1, false, 0, a_out, ub_spart, hp.n_vocab, stream);
+            launch_part_sum(ub_spart, kp, nt, hp.n_vocab, hp.n_vocab, nullptr, 0, logits_all + (size_t)c0 * hp.n_vocab,
+                            hp.n_vocab, stream);
+            if (c0 + nt == n) {
+                MI_HIP(hipMemcpyAsync(logits, logits_all + (size_t)(n - 1) * hp.n_vocab, (size_t)hp.n_vocab * sizeof(float),
+                                      hipMemcpyDeviceToDevice, stream));
+                TopkParams tp{logits, hp.n_vocab, cand, topk_ids, topk_vals, d_h_topk_ids, d_h_topk_vals};
+                launch_topk(tp, stream);
+            }
+        } else if (all) {   // final norm + output head over every token of the batch
             const ActQ8 a_out = ub_act(hp.n_embd, nt, m->output.type);   // the head's own activation format
             launch_quant_act(xb, hp.n_embd, m->output_norm, hp.eps, a_out, stream);
             GemmParams p;
@@ -1608,11 +1643,83 @@ void Ctx::decode_ubatch(const int32_t* tokens, int n, bool all) {
                 TopkParams tp{logits, hp.n_vocab, cand, topk_ids, topk_vals, d_h_topk_ids, d_h_topk_vals};
                 launch_topk(tp, stream);
             }
-        } else if (c0 + nt == n) {
-            enqueue_output(xb + (size_t)(nt - 1) * hp.n_embd, nullptr);
+        } else {
+            if (short_b)   // the last residual parts into xb (the next chunk, or the output, reads it)
+                launch_part_sum(ub_spart, pend_k, nt, hp.n_embd, hp.n_embd, xb, hp.n_embd, xb, hp.n_embd, stream);
+            if (c0 + nt == n) enqueue_output(xb + (size_t)(nt - 1) * hp.n_embd, nullptr);
         }
     }
     logits_valid = true;
+}
+
+// One short physical batch (<= mmqs_max tokens) through the layers on the split-K streaming GEMM
+// (mmq.hip mmqs): every launch writes K-part sums to ub_spart, and the next kernel adds them --
+// quant_act (the residual, or SwiGLU of the gate/up parts), qkv_finish (RoPE, KV append).
+// Returns the count of the last FFN down's parts, still to be added into xb.
+int Ctx::ubatch_layers_short(int nt) {
+    const HParams& hp = m->hp;
+    const float kq_scale = 1.0f / std::sqrt((float)hp.head_dim);
+    const int qkv_rows = hp.n_embd + 2 * kv_dim;
+    int pend_k = 0;   // residual parts of ub_spart not yet added into xb
+    for (int l = 0; l < hp.n_layer; ++l) {
+        const Layer& L = m->layers[l];
+        __half* kl = kcache + (size_t)l * n_ctx * kv_dim;
+        __half* vl = vcache + (size_t)l * n_ctx * kv_dim;
+        // Q / K / V: one quantisation of rms_norm(x) * attn_norm per activation format (the first
+        // also adds the residual parts), the matrices of one type in one launch, rows [Q | K | V]
+        const QMat* mats[3] = {&L.wq, &L.wk, &L.wv};
+        const int prow[3] = {0, L.wq.rows, L.wq.rows + L.wk.rows};
+        for (int f = 0; f < 2; ++f) {
+            bool need = false;
+            for (const QMat* q : mats) need = need || (q->type == T_Q8_0) == (f == 1);
+            if (need) {
+                launch_quant_act(xb, hp.n_embd, L.attn_norm, hp.eps, ub_act(hp.n_embd, nt, f ? T_Q8_0 : T_Q4_K), stream,
+                                 nullptr, pend_k ? ub_spart : nullptr, pend_k ? pend_k : 2);
+                pend_k = 0;
+            }
+        }
+        int kp = 0;
+        for (int i = 0; i < 3; ++i) {
+            bool first = true;
+            for (int j = 0; j < i; ++j) first = first && mats[j]->type != mats[i]->type;
+            if (!first) continue;
+            const QMat* ms[3];
+            int pr[3], n = 0;
+            for (int j = i; j < 3; ++j)
+                if (mats[j]->type == mats[i]->type) {
+                    ms[n] = mats[j];
+                    pr[n++] = prow[j];
+                }
+            kp = launch_mmqs(ms, pr, n, false, 0, ub_act(hp.n_embd, nt, mats[i]->type), ub_spart, qkv_rows, stream);
+        }
+        QkvFinish F{ub_spart, qkv_rows, kp, nt, L.wq.rows, L.wk.rows, L.wv.rows, qb, hp.n_embd, kl, vl, kv_dim, cell_pos,
+                    tokpos_b, ub_rope, hp.n_rot, hp.head_dim};
+        launch_qkv_finish(F, stream);
+        AttnParams a{qb, kl, vl, tokpos_b, cell_pos, attn_scores, attn_smax, attnb, hp.n_head, hp.n_head_kv,
+                     hp.head_dim, kv_dim, (int)n_ctx, kq_scale};
+        if (attn_mfma) launch_attn_mfma(a, nt, attnb, stream);
+        else launch_attn_multi(a, nt, attnb, stream);
+        {   // output projection: parts of W_o attn, added to x by the FFN's quant_act
+            const ActQ8 act = ub_act(hp.n_embd, nt, L.wo.type);
+            launch_quant_act(attnb, hp.n_embd, nullptr, hp.eps, act, stream);
+            const QMat* mo[1] = {&L.wo};
+            const int pr[1] = {0};
+            pend_k = launch_mmqs(mo, pr, 1, false, 0, act, ub_spart, hp.n_embd, stream);
+        }
+        {   // FFN gate/up: parts of both, SwiGLU'd by the down input's quant_act
+            const ActQ8 act = ub_act(hp.n_embd, nt, L.gate.type);
+            launch_quant_act(xb, hp.n_embd, L.ffn_norm, hp.eps, act, stream, nullptr, ub_spart, pend_k);
+            pend_k = 0;
+            const QMat* mg[1] = {&L.gate};
+            const int pr[1] = {0};
+            const int kg = launch_mmqs(mg, pr, 1, true, hp.n_ff, act, ub_spart, 2 * hp.n_ff, stream);
+            const ActQ8 a2 = ub_act(hp.n_ff, nt, L.down.type);
+            launch_quant_act(nullptr, hp.n_ff, nullptr, hp.eps, a2, stream, nullptr, ub_spart, kg, 1);
+            const QMat* md[1] = {&L.down};
+            pend_k = launch_mmqs(md, pr, 1, false, 0, a2, ub_spart, hp.n_embd, stream);
+        }
+    }
+    return pend_k;
 }
 
 int Ctx::decode(const int32_t* tokens, int n, bool all) {

@@ -170,6 +170,10 @@ struct Ctx {
     int8_t* ub_bsb = nullptr;           // [UB_MAX][kmax/256][16]
     float2* ub_rope = nullptr;          // [UB_MAX][n_rot/2]
     float* ub_part = nullptr;           // [2][UB_MAX][n_embd] split-K partials (dense models; MI_MMQ_KSPLIT=0: off)
+    // short batches (<= mmqs_max tokens, dense models): the split-K streaming GEMM's partial sums
+    // [kp][ntok][rows] of every launch (mmq.hip mmqs; MI_MMQS_MAX=0: off)
+    float* ub_spart = nullptr;
+    int mmqs_max = 0;
     bool out_mmq = false;               // the output head is mmq32-capable (batched logits of every token)
     bool ub_q80 = false;                // the layer matrices are Q8_0: Q8_0 batch activations
     bool attn_mfma = false;             // batch attention on f16 MFMA (attn_mfma.hip); MI_ATTN_VALU=1: VALU kernel
@@ -229,6 +233,7 @@ struct Ctx {
     // dv_quant launch (rms_norm'd x, or h) -- from sp_act[role]
     struct SpLayer {
         int fA, fB, fC, fD;             // activation formats of QKV, WO, gate/up, down: bit 0 Q8_K, bit 1 Q8_0
+        bool rawD;                      // FFN down quantises h itself (dgemv act_raw): no separate launch
     };
     bool sp_ok = false;                 // MI_DECODE_OLD=1: the gemv_kernel graph instead
     std::vector<SpLayer> sp;
@@ -253,6 +258,9 @@ struct Ctx {
                             const std::function<unsigned long long*()>& stamp);
     void decode_batch(const int32_t* tokens, int n);
     void decode_ubatch(const int32_t* tokens, int n, bool all);
+    // the layers of one short physical batch on mmqs; returns the residual parts still to add
+    // into xb (pend_k parts of ub_spart)
+    int ubatch_layers_short(int nt);
     ActQ8 ub_act(int K, int ntok, int type) const;   // the activation format `type`'s matrices read
     bool hp_dense() const { return m->hp.n_expert == 0; }
     // a second activation set (Q8_0) for a model mixing Q8_0 and k-quant matrices

@@ -108,9 +108,12 @@ struct GemvParams {
     int attn_nsplit;          // PRO_ATTN: splits to add (0: from the cell count in tokpos)
     unsigned long long* stamps;   // diagnostics (MI_STAMPS builds): per-workgroup stamps [grid][8]
     // streaming form (launch_dgemv, dense LLaMA decode within ATTN_SHORT cells): the activation
-    // arrives quantised, act_layout(K, act_q8k, act_q80) at act_in (pro / x / norm_w unused)
+    // arrives quantised, act_layout(K, act_q8k, act_q80) at act_in (pro / x / norm_w unused) --
+    // or, act_raw (EPI_ADD, K <= 14336: the FFN down launch), as K floats at act_in that every
+    // workgroup quantises itself (no norm)
     const char* act_in;
     int act_q8k, act_q80;
+    int act_raw;
 };
 
 void init_kernel_attributes();   // once per device, before any graph capture
@@ -330,9 +333,11 @@ struct ActQ8 {
 };
 // rows (optional): token t of the batch reads row rows[t] of x (the tokens routed to one expert)
 // part (optional): the split-K partial sums of the GEMM that produced x (see GemmParams::ksplit):
-// x += p0 + p1 first, written back
+// x = ((p0 + p1) + ...) + x first, written back
+// swiglu: part holds the gate/up parts of a pair launch ([nks][ntok][2 K]: gate rows, then up
+// rows); the row quantised is silu(sum gate) * (sum up) (x unused)
 void launch_quant_act(const float* x, int x_stride, const float* norm_w, float eps, const ActQ8& a, hipStream_t s,
-                      const int* rows = nullptr, const float* part = nullptr, int nks = 2);
+                      const int* rows = nullptr, const float* part = nullptr, int nks = 2, int swiglu = 0);
 // whether prompt-batch GEMMs take the mmq2 path (the only one with ksplit)
 bool mmq2_active();
 // ggml_rope_cache_init per token of the batch: out [ntok][n_rot/2] (cos, sin)
@@ -351,5 +356,37 @@ void launch_mmq32(const GemmParams& p, const ActQ8& act, const float2* rope, hip
 // several matrices of one type over the same activation (Q / K / V) as ONE mmq2 launch when they
 // qualify (no pairs, no grouping, a shared output buffer), else one launch each
 void launch_mmq32_multi(const GemmParams* ps, int n, const ActQ8& act, const float2* rope, hipStream_t s);
+
+// ---- short batches (<= MMQS_MAX tokens, mmq.hip mmqs): a split-K streaming int8-MFMA GEMM ----
+// The matrices (one type; a gate/up pair: one QMat, its pair copy) over act (npad 32 or 64) write
+// the plain partial sums of their K-parts to part[kp][ntok][pstride], matrix i's rows from prow[i]
+// (a pair: gate rows from prow[0], up rows from prow[0] + nff).  Returns kp (mmqs_parts(K)).  The
+// consumer adds the parts in order: launch_quant_act (part / swiglu), launch_qkv_finish,
+// launch_part_sum.
+constexpr int MMQS_MAX = 64;
+int mmqs_parts(int K);
+int launch_mmqs(const QMat* const* mats, const int* prow, int n, bool pair, int nff, const ActQ8& act, float* part,
+                int pstride, hipStream_t s);
+// Q / K / V from the parts of their GEMMs (rows [Q | K | V] of part): RoPE NORM of Q and K (the
+// batch's rope table), Q -> q [ntok][q_stride], K / V -> the f16 caches at the tokens' cells
+struct QkvFinish {
+    const float* part;
+    int pstride, kp, ntok;
+    int nq, nk, nv;
+    float* q;
+    int q_stride;
+    __half* kcache;
+    __half* vcache;
+    int kv_dim;
+    int* cell_pos;
+    const int* tokpos;
+    const float2* rope;
+    int n_rot, head_dim;
+};
+void launch_qkv_finish(const QkvFinish& F, hipStream_t s);
+// out[t][r] = ((p0 + p1) + ...) [+ resid[t][r]] over rows [0, rows) of the parts; swiglu > 0 (a
+// pair launch's parts, up rows from swiglu): silu(sum gate) * (sum up)
+void launch_part_sum(const float* part, int kp, int ntok, int rows, int pstride, const float* resid, int rstride,
+                     float* out, int ostride, hipStream_t s, int swiglu = 0);
 
 }  // namespace mi

@@ -69,6 +69,8 @@ __device__ __forceinline__ float wave_max_pos(float v) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
 }
 
+__device__ __forceinline__ float silu(float x) { return x / (1.0f + expf(-x)); }
+
 // ---------------------------------------------------------------------------
 // Activation rows -> Q8_K (quantize_row_q8_K_ref), one workgroup per token row.
 // Writes q in MFMA-fragment order (below), d transposed [nb][npad] (4 consecutive tokens = one
@@ -79,7 +81,8 @@ __device__ __forceinline__ float wave_max_pos(float v) {
 // QA_W waves per token row (16: one 256-element block each at K = 4096)
 template <int QA_W>
 __global__ __launch_bounds__(64 * QA_W) void quant_act_kernel(const float* x, int x_stride, const float* norm_w,
-                                                        float eps, ActQ8 a, const int* rows, const float* part, int nks) {
+                                                        float eps, ActQ8 a, const int* rows, const float* part, int nks,
+                                                        int swiglu) {
     const int t = blockIdx.x;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int nb = a.K >> 8;
@@ -99,14 +102,32 @@ __global__ __launch_bounds__(64 * QA_W) void quant_act_kernel(const float* x, in
         }
         return;
     }
-    const f32x4* x4 = reinterpret_cast<const f32x4*>(x + (long long)(rows ? rows[t] : t) * x_stride);
+    const f32x4* x4 = x ? reinterpret_cast<const f32x4*>(x + (long long)(rows ? rows[t] : t) * x_stride) : nullptr;
     // this wave's blocks (wave, wave + QA_W, ...) read once, kept for the quantisation
     constexpr int XR = 16;   // K <= QA_W * 16 * 256
     f32x4 xr[XR];
+    if (swiglu) {   // silu(g) * u of the pair launch's parts: g = ((g0 + g1) + ...), u likewise
+        const f32x4* p4 = reinterpret_cast<const f32x4*>(part + (long long)t * 2 * a.K);
+        const long long kst = (long long)a.ntok * 2 * a.K / 4;   // one part, in f32x4
 #pragma unroll
-    for (int i = 0; i < XR; ++i)
-        if (wave + QA_W * i < nb) xr[i] = x4[(wave + QA_W * i) * 64 + lane];
-    if (part) {   // the split-K GEMM's nks partials: x = (((p0 + p1) + p2) + ...) + x (EPI_ADD's o + resid), written back
+        for (int i = 0; i < XR; ++i) {
+            const int blk = wave + QA_W * i;
+            if (blk < nb) {
+                f32x4 g = p4[blk * 64 + lane], u = p4[a.K / 4 + blk * 64 + lane];
+                for (int k = 1; k < nks; ++k) {
+                    const f32x4 gk = p4[k * kst + blk * 64 + lane], uk = p4[k * kst + a.K / 4 + blk * 64 + lane];
+                    g = f32x4{g.x + gk.x, g.y + gk.y, g.z + gk.z, g.w + gk.w};
+                    u = f32x4{u.x + uk.x, u.y + uk.y, u.z + uk.z, u.w + uk.w};
+                }
+                xr[i] = f32x4{silu(g.x) * u.x, silu(g.y) * u.y, silu(g.z) * u.z, silu(g.w) * u.w};
+            }
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < XR; ++i)
+            if (wave + QA_W * i < nb) xr[i] = x4[(wave + QA_W * i) * 64 + lane];
+    }
+    if (part && !swiglu) {   // the split-K GEMM's nks partials: x = (((p0 + p1) + p2) + ...) + x (EPI_ADD's o + resid), written back
         f32x4* xw = reinterpret_cast<f32x4*>(const_cast<float*>(x) + (long long)t * x_stride);
 #pragma unroll
         for (int i = 0; i < XR; ++i) {
@@ -222,7 +243,6 @@ __global__ void rope_table_kernel(const int* tokpos, int ntok, int n_rot, float 
     }
 }
 
-__device__ __forceinline__ float silu(float x) { return x / (1.0f + expf(-x)); }
 
 __device__ __forceinline__ v16i mfma(v4i a, v4i b) {
     const v16i z = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -794,19 +814,373 @@ void mmq2_t(const GemmParams P, const ActQ8 act, const float2* rope, const MmqSe
   }
 }
 
+// =============================================================================================
+// mmqs: short batches (<= MMQS_MAX tokens: the verification sizes, Session.cpp:231-244) on the
+// same int8 MFMAs, streamed like the decode GEMV instead of tiled like a GEMM.  At 20-64 tokens
+// a weight byte feeds at most 2 MFMA token tiles, so the launch is an HBM stream: every weight
+// byte is read once, straight into registers (no LDS staging, no per-superblock barrier), and
+// the grid is spread over K as well as over rows so that enough waves are in flight:
+//   * workgroup = MS_NW waves = MS_NW row tiles (32 rows; a gate/up pair tile: 16 + 16) x one
+//     K-part of sbw superblocks; the part's activation tiles (all NT token tiles, bsums, d) are
+//     LDS-DMA'd once at entry, shared by the waves;
+//   * each wave issues the weight loads of its first D superblocks at entry and refills the ring
+//     as it computes; the arithmetic per superblock is mmq2's (scaled int8 operand planes, the
+//     mins by MFMA, the same fmaf update), so every per-part sum is mmq2's exactly;
+//   * the K-parts write plain partial sums part[kp][ntok][pstride]; the consumer adds them in part
+//     order: launch_quant_act (residual x, or silu(gate) * up for the FFN down input),
+//     launch_qkv_finish (RoPE, KV append), launch_part_sum (output head, the last residual).
+// =============================================================================================
+constexpr int MS_NW = 4;     // waves (row tiles) per workgroup
+constexpr int MS_SBW = 4;    // superblocks per K-part
+struct MsArgs {
+    const uint8_t* sw[MMQ_SEGS];   // MFMA-order copies
+    int nrt[MMQ_SEGS];             // row tiles per segment
+    int rows[MMQ_SEGS];
+    int prow[MMQ_SEGS];            // the segment's first row in the partial row space
+    int n;                         // segments
+    int nrt_tot;
+    int kp;                        // K-parts (grid = row blocks x kp)
+    int nff;                       // pair launches: the up rows' offset in the partial row space
+    float* part;                   // [kp][ntok][pstride]
+    int pstride;
+};
+// 16-B weight loads per superblock of a row tile (NV) and the wave's ring depth (D)
+template <int T> struct MsT;
+template <> struct MsT<T_Q4_K> { static constexpr int NV = 5, D = 4; };    // qs [4] | header
+template <> struct MsT<T_Q5_K> { static constexpr int NV = 6, D = 4; };    // qs [4] | qh | header
+template <> struct MsT<T_Q6_K> { static constexpr int NV = 16, D = 2; };   // hi [8] | lo [8] (+ d)
+template <> struct MsT<T_Q8_0> { static constexpr int NV = 9, D = 2; };    // qs [8] | d [8 x f16]
+template <int T> struct MsW {
+    u32x4 v[MsT<T>::NV];
+    unsigned d6;   // Q6_K: the row's d
+};
+template <int T>
+__device__ __forceinline__ MsW<T> ms_load(const uint8_t* tile, int lane) {
+    const int col = lane & 31;
+    MsW<T> w;
+    auto ld = [&](int off) { return __builtin_nontemporal_load(gp(reinterpret_cast<const u32x4*>(tile + off))); };
+    if (T == T_Q4_K || T == T_Q5_K) {
+#pragma unroll
+        for (int p = 0; p < 4; ++p) w.v[p] = ld(p * 1024 + lane * 16);
+        if (T == T_Q5_K) w.v[4] = ld(4096 + lane * 16);
+        w.v[MsT<T>::NV - 1] = ld((T == T_Q5_K ? 5120 : 4096) + col * 16);
+        w.d6 = 0;
+    } else if (T == T_Q6_K) {
+#pragma unroll
+        for (int sp = 0; sp < 8; ++sp) {
+            w.v[sp] = ld(sp * 1024 + lane * 16);
+            w.v[8 + sp] = ld(8192 + sp * 1024 + lane * 16);
+        }
+        w.d6 = __builtin_nontemporal_load(gp(reinterpret_cast<const unsigned short*>(tile + 16384 + col * 2)));
+    } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) w.v[j] = ld(j * 1024 + lane * 16);
+        w.v[8] = ld(8192 + col * 16);
+        w.d6 = 0;
+    }
+    return w;
+}
+__device__ __forceinline__ v16i mfma_acc(v4i a, v4i b, v16i c) { return __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b, c, 0, 0, 0); }
+__device__ __forceinline__ v4i as_v4i(const unsigned p[4]) { return v4i{(int)p[0], (int)p[1], (int)p[2], (int)p[3]}; }
+
+// one superblock (local index s of the part) of this wave's row tile into y[NT][16]
+template <int T, int NT>
+__device__ __forceinline__ void ms_sb(const MsW<T>& w, int s, const char* lds, int QB, int DB, int lane,
+                                      float y[NT][16]) {
+    typedef __attribute__((address_space(3))) const char lc;
+    const lc* L = (const lc*)lds;
+    const int col = lane & 31, h = lane >> 5;
+    (void)col;
+    auto act = [&](int t, int j) {
+        return *reinterpret_cast<const __attribute__((address_space(3))) v4i*>(L + (s * NT + t) * 8192 + j * 1024 + lane * 16);
+    };
+    auto dx4 = [&](int off) { return *reinterpret_cast<const __attribute__((address_space(3))) f32x4*>(L + off); };
+    if (T == T_Q4_K || T == T_Q5_K) {
+        const u32x4 hd = w.v[MsT<T>::NV - 1];
+        int sc[8], mn[8];
+        q4k_scales(hd, sc, mn);
+        const v16i z = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+        v16i acc0[NT], acc1[NT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc0[t] = acc1[t] = z;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            const unsigned q[4] = {w.v[p].x, w.v[p].y, w.v[p].z, w.v[p].w};
+#pragma unroll
+            for (int hf = 0; hf < 2; ++hf) {
+                const int j = 2 * p + hf;
+                unsigned P0[4], P1[4];
+                if (T == T_Q4_K) {   // sc q = P0 + 8 P1 (P0 = q (sc & 7), P1 = q (sc >> 3), bytes <= 105)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const unsigned nib = hf ? (q[i] >> 4) & 0x0F0F0F0Fu : q[i] & 0x0F0F0F0Fu;
+                        P0[i] = bmul(nib, sc[j] & 7);
+                        P1[i] = bmul(nib, sc[j] >> 3);
+                    }
+                } else {             // sc q = P0 + 128 P1 (q = lo4 + 16 hb <= 31)
+                    const unsigned b[4] = {w.v[4].x, w.v[4].y, w.v[4].z, w.v[4].w};
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const unsigned q5 = ((hf ? q[i] >> 4 : q[i]) & 0x0F0F0F0Fu) | (((b[i] >> j) & 0x01010101u) << 4);
+                        const unsigned m02 = wmul16(q5 & 0x00FF00FFu, sc[j]), m13 = wmul16((q5 >> 8) & 0x00FF00FFu, sc[j]);
+                        P0[i] = (m02 & 0x007F007Fu) | ((m13 & 0x007F007Fu) << 8);
+                        P1[i] = ((m02 >> 7) & 0x001F001Fu) | (((m13 >> 7) & 0x001F001Fu) << 8);
+                    }
+                }
+                const v4i b0 = as_v4i(P0), b1 = as_v4i(P1);
+#pragma unroll
+                for (int t = 0; t < NT; ++t) {
+                    const v4i a = act(t, j);
+                    acc0[t] = mfma_acc(a, b0, acc0[t]);
+                    acc1[t] = mfma_acc(a, b1, acc1[t]);
+                }
+            }
+        }
+        // sum_j m_j*bsum_j by MFMA (mmq2's form): bsums 64 hi + lo as A, the row's mins as B
+        const unsigned Z = hd.z, W = hd.w;
+        const int m03 = (int)(Z & 0x3F3F3F3Fu);
+        const int m47 = (int)(((W >> 4) & 0x0F0F0F0Fu) | ((Z >> 2) & 0x30303030u));
+        const v4i bm1 = h == 0 ? v4i{m03, m47, 0, 0} : v4i{0, 0, 0, 0};
+        const v4i bm2 = h == 0 ? v4i{0, 0, m03, m47} : v4i{0, 0, 0, 0};
+        const float dr = h2f(hd.x), dmr = h2f(hd.x >> 16);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const v4i ab = h == 0 ? *reinterpret_cast<const __attribute__((address_space(3))) v4i*>(L + QB + (s * NT + t) * 1024 + col * 16)
+                                  : v4i{0, 0, 0, 0};
+            const v16i x1 = mfma(ab, bm1);
+            const v16i x2 = mfma(ab, bm2);
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const f32x4 d4 = dx4(DB + s * 256 + (t * 32 + 8 * g + 4 * h) * 4);
+                const float dx[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int e = 4 * g + i;
+                    const int S = acc0[t][e] + (T == T_Q5_K ? 128 : 8) * acc1[t][e];
+                    const float d = dr * dx[i], dm = dmr * dx[i];
+                    y[t][e] = fmaf(-dm, (float)(64 * x1[e] + x2[e]), fmaf(d, (float)S, y[t][e]));
+                }
+            }
+        }
+    } else if (T == T_Q6_K) {
+        const v16i z = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+        v16i ah[NT], al[NT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) ah[t] = al[t] = z;
+#pragma unroll
+        for (int sp = 0; sp < 8; ++sp) {
+            const unsigned ph[4] = {w.v[sp].x, w.v[sp].y, w.v[sp].z, w.v[sp].w};
+            const unsigned pl[4] = {w.v[8 + sp].x, w.v[8 + sp].y, w.v[8 + sp].z, w.v[8 + sp].w};
+            const v4i bh = as_v4i(ph), bl = as_v4i(pl);
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                const v4i a = act(t, sp);
+                ah[t] = mfma_acc(a, bh, ah[t]);
+                al[t] = mfma_acc(a, bl, al[t]);
+            }
+        }
+        const float dr = h2f(w.d6);
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const f32x4 d4 = dx4(DB + s * 256 + (t * 32 + 8 * g + 4 * h) * 4);
+                const float dx[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int e = 4 * g + i;
+                    y[t][e] = fmaf(dr * dx[i], (float)(ah[t][e] * 64 + al[t][e]), y[t][e]);
+                }
+            }
+    } else {   // Q8_0: one MFMA per 32-block, vec_dot_q8_0_q8_0's per-block float update
+        const u32x4 hdr = w.v[8];
+        const unsigned hw[4] = {hdr.x, hdr.y, hdr.z, hdr.w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const unsigned pq[4] = {w.v[j].x, w.v[j].y, w.v[j].z, w.v[j].w};
+            const v4i wq = as_v4i(pq);
+            const float dwj = h2f(hw[j >> 1] >> (16 * (j & 1)));
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                const v16i dj = mfma(act(t, j), wq);
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const f32x4 d4 = dx4(DB + (s * 8 + j) * 256 + (t * 32 + 8 * g + 4 * h) * 4);
+                    const float dx[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) y[t][4 * g + i] = fmaf((float)dj[4 * g + i], dwj * dx[i], y[t][4 * g + i]);
+                }
+            }
+            // block j's updates before block j + 1's operand reads (volatile asm keeps its order, the
+            // memory clobber keeps the LDS reads behind it): one block's MFMA results live at a time
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) asm volatile("" : "+v"(y[t][e]));
+            asm volatile("" ::: "memory");
+        }
+    }
+}
+
+template <int T, bool AB, int NT>
+__global__ __launch_bounds__(64 * MS_NW) void mmqs_t(const MsArgs M, const ActQ8 act) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr bool KQ = T != T_Q8_0;
+    constexpr int D = MsT<T>::D;
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int col = lane & 31, h = lane >> 5;
+    const int nb = act.K >> 8;
+    const int kp = (int)blockIdx.x % M.kp, rb = (int)blockIdx.x / M.kp;
+    const int sb0 = kp * MS_SBW, nsb = min(MS_SBW, nb - sb0);   // (the host sizes kp: nsb >= 1)
+    // LDS: q [s][t] 8 KiB | k-quants: bsb [s][t] 1 KiB, dT [s] 256 B | Q8_0: dT [s][j] 256 B
+    constexpr int QB = MS_SBW * NT * 8192;
+    constexpr int DB = QB + (KQ ? MS_SBW * NT * 1024 : 0);
+    typedef __attribute__((address_space(3))) void lv;
+    // (1) this part's activation pieces (every token tile), LDS-DMA spread over the waves
+    for (int i = wv; i < nsb * NT * 8; i += MS_NW) {
+        const int s = i / (NT * 8), t = (i >> 3) % NT, j = i & 7;
+        const int8_t* src = act.q + ((long long)t * nb + sb0 + s) * 8192 + j * 1024 + lane * 16;
+        __builtin_amdgcn_global_load_lds(gp(src), (lv*)(smem + (s * NT + t) * 8192 + j * 1024), 16, 0, 0);
+    }
+    const int tl = min(lane, act.npad - 1);   // dT: token lane (a 32-token batch: lanes 32.. repeat)
+    if (KQ) {
+        for (int i = wv; i < nsb * NT; i += MS_NW) {   // bsb of (s, t) = i: 32 tokens x 16 B, twice
+            const int s = i / NT, t = i % NT;
+            const int8_t* src = act.bsb + ((long long)t * nb + sb0 + s) * 512 + col * 16;
+            __builtin_amdgcn_global_load_lds(gp(src), (lv*)(smem + QB + i * 1024), 16, 0, 0);
+        }
+        for (int s = wv; s < nsb; s += MS_NW)
+            __builtin_amdgcn_global_load_lds(gp(act.dT + (long long)(sb0 + s) * act.npad + tl), (lv*)(smem + DB + s * 256), 4, 0, 0);
+    } else {
+        for (int i = wv; i < nsb * 8; i += MS_NW)     // rows 8 (sb0 + s) + j of the per-32 d
+            __builtin_amdgcn_global_load_lds(gp(act.dT + (long long)(8 * sb0 + i) * act.npad + tl), (lv*)(smem + DB + i * 256), 4, 0, 0);
+    }
+    // (2) this wave's row tile and the first D superblocks of its weights
+    int g = rb * MS_NW + wv;
+    const bool busy = g < M.nrt_tot;
+    if (!busy) g = M.nrt_tot - 1;
+    int seg = 0, rt = g;
+#pragma unroll
+    for (int i = 0; i < MMQ_SEGS - 1; ++i)
+        if (i + 1 < M.n && seg == i && rt >= M.nrt[i]) {
+            rt -= M.nrt[i];
+            seg = i + 1;
+        }
+    const uint8_t* swA = seg == 0 ? M.sw[0] : seg == 1 ? M.sw[1] : M.sw[2];
+    const int rows_s = seg == 0 ? M.rows[0] : seg == 1 ? M.rows[1] : M.rows[2];
+    const int prow_s = seg == 0 ? M.prow[0] : seg == 1 ? M.prow[1] : M.prow[2];
+    constexpr int TB = mmq32_tile_bytes_d(T);
+    const uint8_t* tile0 = swA + ((long long)rt * nb + sb0) * TB;
+    MsW<T> w[D];
+    if (busy) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) w[d] = ms_load<T>(tile0 + (long long)min(d, nsb - 1) * TB, lane);
+    }
+    __builtin_amdgcn_s_waitcnt((0x7 << 4) | (0xF << 8));   // vmcnt(0): the DMA (and the ring) landed
+    __builtin_amdgcn_s_barrier();
+    if (!busy) return;
+    float y[NT][16];
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) y[t][e] = 0.0f;
+    for (int i = 0; i < nsb; i += D) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            const int s = i + d;
+            if (s < nsb) {
+                const MsW<T> cur = w[d];
+                if (s + D < nsb) w[d] = ms_load<T>(tile0 + (long long)(s + D) * TB, lane);
+                ms_sb<T, NT>(cur, s, smem, QB, DB, lane, y);
+            }
+        }
+    }
+    // (3) the partial sums of this part: lane = weight row, 16 tokens per token tile
+    const int rr = AB ? rt * 16 + (col & 15) : rt * 32 + col;
+    if (rr >= rows_s) return;
+    const int prow = prow_s + (AB && col >= 16 ? M.nff : 0) + rr;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int tok = t * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            if (tok < act.ntok) M.part[((long long)kp * act.ntok + tok) * M.pstride + prow] = y[t][r];
+        }
+}
+
+// the sum of the K-parts in part order, with the consumer's epilogue: Q / K RoPE (ggml NORM, the
+// rope table of the batch), Q to q, K / V to the f16 caches (and the cell positions)
+__global__ __launch_bounds__(256) void qkv_finish_kernel(const QkvFinish F) {
+    const int t = blockIdx.y;
+    const int pr = blockIdx.x * 256 + threadIdx.x;   // row pair
+    const int r = 2 * pr;
+    if (r >= F.nq + F.nk + F.nv) return;
+    const float* p = F.part + (long long)t * F.pstride + r;
+    float v0 = p[0], v1 = p[1];
+    for (int k = 1; k < F.kp; ++k) {
+        const float* pk = p + (long long)k * F.ntok * F.pstride;
+        v0 = v0 + pk[0];
+        v1 = v1 + pk[1];
+    }
+    const int seg = r < F.nq ? 0 : r < F.nq + F.nk ? 1 : 2;
+    const int row = seg == 0 ? r : seg == 1 ? r - F.nq : r - F.nq - F.nk;
+    float o0 = v0, o1 = v1;
+    if (seg < 2) {
+        const int i0 = row % F.head_dim;
+        if (i0 < F.n_rot) {   // mmq_epilogue's expressions: even v cos - pv sin, odd pv sin + v cos
+            const float2 cs = F.rope[(long long)t * (F.n_rot / 2) + i0 / 2];
+            o0 = v0 * cs.x - v1 * cs.y;
+            o1 = v0 * cs.y + v1 * cs.x;
+        }
+    }
+    const int* tp = F.tokpos + t * 4;
+    if (seg == 0) {
+        F.q[(long long)t * F.q_stride + row] = o0;
+        F.q[(long long)t * F.q_stride + row + 1] = o1;
+    } else {
+        __half* c = (seg == 1 ? F.kcache : F.vcache) + (long long)tp[2] * F.kv_dim + row;
+        c[0] = __float2half_rn(o0);
+        c[1] = __float2half_rn(o1);
+        if (seg == 1 && row == 0) F.cell_pos[tp[2]] = tp[1];
+    }
+}
+
+// out[t][r] = ((p0 + p1) + ...) [+ resid[t][r]]; swiglu > 0: silu(sum of row r) * (sum of row
+// swiglu + r) (a pair launch's gate and up rows)
+__global__ __launch_bounds__(256) void part_sum_kernel(const float* part, int kp, int ntok, int rows, int pstride,
+                                                       const float* resid, int rstride, float* out, int ostride,
+                                                       int swiglu) {
+    const int t = blockIdx.y;
+    const int r = blockIdx.x * 256 + threadIdx.x;
+    if (r >= rows) return;
+    float acc = part[(long long)t * pstride + r];
+    for (int k = 1; k < kp; ++k) acc = acc + part[((long long)k * ntok + t) * pstride + r];
+    if (swiglu) {
+        float u = part[(long long)t * pstride + swiglu + r];
+        for (int k = 1; k < kp; ++k) u = u + part[((long long)k * ntok + t) * pstride + swiglu + r];
+        acc = silu(acc) * u;
+    }
+    if (resid) acc = acc + resid[(long long)t * rstride + r];
+    out[(long long)t * ostride + r] = acc;
+}
+
 template <int T, int NST> constexpr int m2_lds() { return M2<T>::lds(NST); }
 
 }  // namespace mmq
 
 void launch_quant_act(const float* x, int x_stride, const float* norm_w, float eps, const ActQ8& a, hipStream_t s,
-                      const int* rows, const float* part, int nks) {
-    if (part && nks != 2 && nks != 4) throw Error("quant_act: 2 or 4 split-K partials");
+                      const int* rows, const float* part, int nks, int swiglu) {
+    if (part && (nks < 1 || nks > 64)) throw Error("quant_act: 1..64 split-K partials");
+    if (swiglu && (!part || rows || norm_w)) throw Error("quant_act: swiglu takes a pair launch's parts, no rows or norm");
+    if (!swiglu && !x) throw Error("quant_act: no input rows");
     if (a.K % 256) throw Error("quant_act: K must be a multiple of 256");
     if (part && (rows || x_stride != a.K)) throw Error("quant_act: split-K partials take a dense [ntok][K] x");
     // (more than UB_MAX rows only for the MoE rows of a batch: one per (token, slot), padded)
     if (a.npad % 32 || a.ntok > a.npad || a.npad > 4 * UB_MAX) throw Error("quant_act: bad token count");
     if (a.K > 65536) throw Error("quant_act: K past 65536");
-    hipLaunchKernelGGL(mmq::quant_act_kernel<16>, dim3(a.npad), dim3(1024), 0, s, x, x_stride, norm_w, eps, a, rows, part, nks);
+    hipLaunchKernelGGL(mmq::quant_act_kernel<16>, dim3(a.npad), dim3(1024), 0, s, x, x_stride, norm_w, eps, a, rows, part, nks,
+                       swiglu);
     MI_HIP(hipGetLastError());
 }
 
@@ -936,6 +1310,76 @@ void launch_mmq32(const GemmParams& p, const ActQ8& act, const float2* rope, hip
     S.rows[0] = p.A.rows;
     S.epi[0] = p.epi;
     launch_mmq2(p, S, act, rope, s);
+}
+
+int mmqs_parts(int K) { return (K / 256 + mmq::MS_SBW - 1) / mmq::MS_SBW; }
+
+int launch_mmqs(const QMat* const* mats, const int* prow, int n, bool pair, int nff, const ActQ8& act, float* part,
+                int pstride, hipStream_t s) {
+    if (n < 1 || n > mmq::MMQ_SEGS || (pair && n != 1)) throw Error("mmqs: 1..3 matrices (a pair: one)");
+    const int T = mats[0]->type;
+    if (!mmq32_supported(T)) throw Error("mmqs: Q4_K / Q5_K / Q6_K / Q8_0 only");
+    if ((T == T_Q8_0) != (act.q80 != 0)) throw Error("mmqs: Q8_0 weights take Q8_0 activations, k-quants Q8_K");
+    if (act.ntok < 1 || act.ntok > MMQS_MAX || (act.npad != 32 && act.npad != 64) || act.npad < act.ntok)
+        throw Error("mmqs: 1..64 tokens");
+    if (act.K % 256 || act.K <= 0) throw Error("mmqs: K must be a multiple of 256");
+    mmq::MsArgs M{};
+    M.n = n;
+    for (int i = 0; i < n; ++i) {
+        const QMat& A = *mats[i];
+        if (A.type != T || A.K != act.K || !A.sw) throw Error("mmqs: the matrices share type and K, with MFMA-order copies");
+        M.sw[i] = A.sw;
+        M.rows[i] = A.rows;
+        M.nrt[i] = pair ? (A.rows + 15) / 16 : (A.rows + 31) / 32;
+        M.prow[i] = prow[i];
+        M.nrt_tot += M.nrt[i];
+        const int top = prow[i] + A.rows + (pair ? nff : 0);
+        if (prow[i] < 0 || top > pstride || (pair && nff < A.rows)) throw Error("mmqs: partial rows past the stride");
+    }
+    M.kp = mmqs_parts(act.K);
+    M.nff = nff;
+    M.part = part;
+    M.pstride = pstride;
+    const int NT = act.npad / 32;
+    const int KQ = T != T_Q8_0;
+    const int lds = mmq::MS_SBW * NT * 8192 + (KQ ? mmq::MS_SBW * NT * 1024 + mmq::MS_SBW * 256 : mmq::MS_SBW * 8 * 256);
+    decltype(&mmq::mmqs_t<T_Q4_K, false, 1>) f = nullptr;
+#define MS_PICK(TT)                                                                                 \
+    f = pair ? (NT == 1 ? mmq::mmqs_t<TT, true, 1> : mmq::mmqs_t<TT, true, 2>)                     \
+             : (NT == 1 ? mmq::mmqs_t<TT, false, 1> : mmq::mmqs_t<TT, false, 2>);
+    switch (T) {
+    case T_Q4_K: MS_PICK(T_Q4_K) break;
+    case T_Q5_K: MS_PICK(T_Q5_K) break;
+    case T_Q6_K: MS_PICK(T_Q6_K) break;
+    default: MS_PICK(T_Q8_0) break;
+    }
+#undef MS_PICK
+    static bool attr_done[4][2][2] = {};
+    const int ti = T == T_Q4_K ? 0 : T == T_Q5_K ? 1 : T == T_Q6_K ? 2 : 3;
+    if (!attr_done[ti][pair][NT - 1]) {
+        MI_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(f), hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+        attr_done[ti][pair][NT - 1] = true;
+    }
+    const int grid = (M.nrt_tot + mmq::MS_NW - 1) / mmq::MS_NW * M.kp;
+    hipLaunchKernelGGL(f, dim3(grid), dim3(64 * mmq::MS_NW), (size_t)lds, s, M, act);
+    MI_HIP(hipGetLastError());
+    return M.kp;
+}
+
+void launch_qkv_finish(const QkvFinish& F, hipStream_t s) {
+    if (F.ntok < 1 || F.kp < 1 || F.nq % 2 || F.nk % 2 || F.nv % 2 || F.head_dim % 2 || F.n_rot > F.head_dim || !F.rope)
+        throw Error("qkv_finish: bad shape");
+    const int npair = (F.nq + F.nk + F.nv) / 2;
+    hipLaunchKernelGGL(mmq::qkv_finish_kernel, dim3((npair + 255) / 256, F.ntok), dim3(256), 0, s, F);
+    MI_HIP(hipGetLastError());
+}
+
+void launch_part_sum(const float* part, int kp, int ntok, int rows, int pstride, const float* resid, int rstride,
+                     float* out, int ostride, hipStream_t s, int swiglu) {
+    if (ntok < 1 || kp < 1 || rows < 1 || rows + swiglu > pstride || (swiglu && swiglu < rows)) throw Error("part_sum: bad shape");
+    hipLaunchKernelGGL(mmq::part_sum_kernel, dim3((rows + 255) / 256, ntok), dim3(256), 0, s, part, kp, ntok, rows, pstride,
+                       resid, rstride, out, ostride, swiglu);
+    MI_HIP(hipGetLastError());
 }
 
 }  // namespace mi

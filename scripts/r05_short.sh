@@ -1,0 +1,23 @@
+#!/bin/bash
+# short-batch GEMM (mmqs): verification parity tests, then the bench's verify_short legs
+OUT=gpurun_out/${1:-r05s}
+mkdir -p $OUT
+export TMPDIR=/tmp
+timeout -k 10 420 python -u -m pytest tests/test_gpu_verify.py tests/test_gpu_fullwidth.py -k "out_all or short or batched or long_prompt" -x -v -s --timeout 300 --timeout-method thread > $OUT/pytest.log 2>&1
+rc=$?; echo "pytest rc $rc"; grep -E "PASS|FAIL|Error|error" $OUT/pytest.log | head -30; tail -3 $OUT/pytest.log
+[ $rc -eq 0 ] || exit 1
+timeout -k 10 200 python -u bench.py --no-cpu --steps 20 --warmup 5 > $OUT/bench.json 2> $OUT/bench.err || { tail -5 $OUT/bench.err; exit 1; }
+python3 -c "import json;d=json.load(open('$OUT/bench.json'));p=d['prefill'];print('decode',d['value'],'prefill',p['ms'],'verify',p['verify']['ms'],'short',p.get('verify_short'))"
+MI_MMQS_MAX=0 timeout -k 10 200 python -u bench.py --no-cpu --steps 20 --warmup 5 > $OUT/bench_tiled.json 2> $OUT/bench_tiled.err || { tail -5 $OUT/bench_tiled.err; exit 1; }
+python3 -c "import json;d=json.load(open('$OUT/bench_tiled.json'));p=d['prefill'];print('tiled: short',p.get('verify_short'))"
+for mode in raw sep raw sep; do
+  if [ $mode = sep ]; then export MI_DOWN_QUANT=1; else unset MI_DOWN_QUANT; fi
+  timeout -k 10 120 python -u bench.py --no-cpu --prefill 0 --verify 0 --steps 128 --warmup 16 > $OUT/dec_$mode.json 2> $OUT/dec_$mode.err || { tail -5 $OUT/dec_$mode.err; exit 1; }
+  python3 -c "import json;d=json.load(open('$OUT/dec_$mode.json'));print('$mode', d['value'], d['roofline']['avg_launch_us'])"
+done
+unset MI_DOWN_QUANT
+MI_NO_GRAPH=1 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python -u bench.py --no-cpu --steps 4 --warmup 2 > $OUT/trace_bench.json 2> $OUT/prof.err || { tail -3 $OUT/prof.err; exit 1; }
+find $OUT/prof -name '*kernel_stats.csv' -exec cp {} $OUT/kernel_stats.csv \;
+find $OUT/prof -name '*kernel_trace.csv' -exec cp {} $OUT/kernel_trace.csv \;
+rm -rf $OUT/prof
+exit 0

@@ -4,8 +4,9 @@ The decode kernels are pinned op by op in test_gpu_ops.py; these are the kernels
 n_ubatch physical batches (Session.cpp:381-392, Instance.hpp:23-24) -- prompt ingestion and
 batched verification:
 
-  mmq32_t (mmq.hip)          v_mfma_i32_32x32x32_i8 GEMM of up to 512 token rows, every weight
-                             row tile and every padded token tile, through mi_op_gemm
+  mmq2_t / mmqs_t (mmq.hip)  v_mfma_i32_32x32x32_i8 GEMMs of up to 512 token rows (mmqs: the
+                             split-K streaming form of <= 64 rows), every weight row tile and
+                             every padded token tile, through mi_op_gemm
   attn_mfma_kernel (attn_mfma.hip)  f16-MFMA causal attention over 512..2048 cells, through
                              mi_op_attention_batch
 
@@ -131,6 +132,30 @@ GEMM_CASES = [
 def test_mmq32_matches_oracle(gpu_lib, t, rows, K, ntoks, pair):
     for ntok in ntoks:
         _check_gemm(t, rows, K, ntok, pair, seed=rows + K + ntok)
+
+
+# the short-batch GEMM (mmqs: <= 64 tokens, split over K; mi_op_gemm sums the K-parts as the
+# engine's consumers do): every type at the widths whose K splits into 4, 11, 14 and 22 parts,
+# one and two token tiles
+MMQS_CASES = [
+    (R.Q4_K, 4096, 4096, (2, 20, 64), False),
+    (R.Q4_K, 11008, 4096, (20, 64), True),
+    (R.Q4_K, 4096, 11008, (20, 64), False),
+    (R.Q5_K, 4096, 14336, (24,), False),
+    (R.Q5_K, 1000, 4096, (40,), True),
+    (R.Q6_K, 4096, 11008, (20, 64), False),
+    (R.Q6_K, 1000, 4096, (33,), True),
+    (R.Q6_K, 32000, 4096, (20,), False),
+    (R.Q8_0, 2048, 5632, (20, 64), False),
+    (R.Q8_0, 5632, 2048, (24,), True),
+]
+
+
+@pytest.mark.parametrize("t,rows,K,ntoks,pair", MMQS_CASES,
+                         ids=[f"{R.TYPE_NAME[c[0]]}-{c[1]}x{c[2]}{'-pair' if c[4] else ''}" for c in MMQS_CASES])
+def test_mmqs_matches_oracle(gpu_lib, t, rows, K, ntoks, pair):
+    for ntok in ntoks:
+        _check_gemm(t, rows, K, ntok, pair, seed=3 * rows + K + ntok)
 
 
 def test_mmq32_rows_not_multiple_of_tile(gpu_lib):

@@ -215,3 +215,35 @@ def test_fullwidth_batched_verification_matches_oracle(gpu_lib, name):
     finally:
         ctx.close()
         orc.close()
+
+
+@pytest.mark.parametrize("name", ["llama2-7b-q4_k_m", "llama3-8b-q6_k", "tinyllama-1.1b-q8_0"])
+def test_fullwidth_short_batches_match_tiled_gemm(gpu_lib, monkeypatch, name):
+    """Short verification batches (20 and 64 claimed tokens) on the split-K streaming GEMM
+    (mmqs: K-parts summed by the consumer kernels) against the same batches on the tiled GEMM
+    (mmq2, MI_MMQS_MAX=0): the same integer sub-block sums and per-superblock fp32 updates, only
+    the order of the K-part sums differs -- every row within 1e-3 x rms, the same top-1, and the
+    KV cache the batch wrote serves the next decode step alike."""
+    cfg, buf, m = full_model(name)
+    rng = np.random.default_rng(21)
+    prompt = [int(t) for t in rng.integers(0, cfg.n_vocab, 12)]
+    for n_claim in (20, 64):
+        claimed = [int(t) for t in rng.integers(0, cfg.n_vocab, n_claim)]
+        outs = []
+        for mode in ("64", "0"):
+            monkeypatch.setenv("MI_MMQS_MAX", mode)
+            ctx = engine.Context(m, n_ctx=128)
+            try:
+                assert ctx.decode(prompt) == 0
+                assert ctx.decode(claimed, all_logits=True) == 0
+                rows = [ctx.logits(row=i).astype(np.float64) for i in range(n_claim)]
+                ctx.decode([7])
+                rows.append(ctx.logits().astype(np.float64))
+                outs.append(rows)
+            finally:
+                ctx.close()
+        for i, (a, b) in enumerate(zip(*outs)):
+            rms = float(np.sqrt(np.mean(b ** 2)))
+            assert float(np.max(np.abs(a - b))) <= 1e-3 * rms, (name, n_claim, i, float(np.max(np.abs(a - b))) / rms)
+            assert int(np.argmax(a)) == int(np.argmax(b)), (name, n_claim, i)
+    monkeypatch.delenv("MI_MMQS_MAX")
