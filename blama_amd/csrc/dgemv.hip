@@ -11,14 +11,13 @@
 //  * The activation arrives quantised (Q8_K and/or Q8_0, act_layout) by its own small launch
 //    (dv_quant_kernel: rms_norm(x) * norm_w for the QKV, gate/up and head inputs) or by the
 //    producer (the attention kernel quantises its output for WO, whole 256-blocks per workgroup);
-//    each workgroup loads those few KB ahead of its weights and copies them into LDS.  The FFN down
-//    launch (DV_ADD_RAW) takes h as it is: its 8 waves load h ahead of the weights and quantise
-//    blocks w, w + 8, ... into LDS while the weights stream in -- the same arithmetic as
-//    dv_quant_kernel, in place of a launch boundary.  Measured alternatives (scripts/exp_fgemv.cpp,
-//    profiles/r05_exp_fgemv*.txt): publishing the activation inside the producing launch by
-//    arrival tickets cost 6-10 us per launch; an rms-norm prologue in every QKV / gate/up
-//    workgroup as much as the separate launch; an Infinity-Cache prefetch of the next layer's
-//    weights from a side stream slowed the chain 1.7-2.6x.
+//    each workgroup loads those few KB ahead of its weights and copies them into LDS.  Measured
+//    alternatives (scripts/exp_fgemv.cpp, profiles/r05_exp_fgemv*.txt): publishing
+//    the activation inside the producing launch by arrival tickets cost 6-10 us per launch; an
+//    rms-norm prologue in every QKV / gate/up workgroup as much as the separate launch; the FFN
+//    down launch quantising h itself in every workgroup (no launch before it) 1-1.5 % slower per
+//    token; an Infinity-Cache prefetch of the next layer's weights from a side stream slowed the
+//    chain 1.7-2.6x.
 //    Every sum is taken in a fixed order: results are bit-reproducible.
 #include "qdot.h"
 #include <hip/hip_ext.h>
@@ -33,10 +32,8 @@ namespace {
 
 constexpr int DV_NW = 8;       // waves per workgroup
 constexpr int DV_ACT_LD = 5;   // 16-B activation loads per lane: act bytes <= 5 x 8 KiB
-constexpr int DV_RAW_LD = 7;   // DV_ADD_RAW: 16-B loads of h per lane, K <= 7 x 2048
 
-// DV_ADD_RAW: DV_ADD whose activation arrives as K floats (h), quantised by each workgroup
-enum DvRole { DV_QKV = 0, DV_ADD = 1, DV_SWIGLU = 2, DV_STORE = 3, DV_ADD_RAW = 4 };
+enum DvRole { DV_QKV = 0, DV_ADD = 1, DV_SWIGLU = 2, DV_STORE = 3 };
 
 
 struct DvSeg {
@@ -81,14 +78,11 @@ __device__ __forceinline__ void dv_body(const DvArgs& a, char* lds) {
     const int u = wg * DV_NW + wave;
     const bool uv = u < S.units;
     const int uc = uv ? u : S.units - 1;
-    constexpr bool RAW = ROLE == DV_ADD_RAW;
-    constexpr bool ADD = ROLE == DV_ADD || RAW;
-    constexpr int NLD = RAW ? DV_RAW_LD : DV_ACT_LD;
+    constexpr bool ADD = ROLE == DV_ADD;
+    constexpr int NLD = DV_ACT_LD;
     const ActLayout L = act_layout(a.K, a.q8k, a.q80);
     // ---- 1. the activation and the epilogue's inputs, requested before any weight (loads retire
-    // in order: the compiler's wait for them is then a count that leaves the weights in flight).
-    // RAW: h itself, 16-B piece k * 512 + tid = elements 4 lane.. of block 8k + wave (the layout
-    // dv_quant_block takes); past K the buffer bound reads zeros
+    // in order: the compiler's wait for them is then a count that leaves the weights in flight)
     u32x4 av[NLD];
     {
         const __amdgpu_buffer_rsrc_t ar = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(a.act), 0, a.act_bytes, 0x00020000);
@@ -132,25 +126,11 @@ __device__ __forceinline__ void dv_body(const DvArgs& a, char* lds) {
         }
     }
 
-    // ---- 3. the activation into LDS (the waits the compiler puts here leave the weights in flight);
-    // RAW: wave w quantises blocks w, w + 8, ... of h there (dv_quant_kernel's arithmetic)
-    if (RAW) {
-        const ActOut t{a.K, a.q8k, a.q80, lds, nullptr, 0.0f};
+    // ---- 3. the activation into LDS (the waits the compiler puts here leave the weights in flight)
 #pragma unroll
-        for (int k = 0; k < NLD; ++k) {
-            const int b = k * DV_NW + wave;
-            if (b < nb) {
-                const float v[4] = {__uint_as_float(av[k].x), __uint_as_float(av[k].y), __uint_as_float(av[k].z),
-                                    __uint_as_float(av[k].w)};
-                dv_quant_block(t, b, v, lane);
-            }
-        }
-    } else {
-#pragma unroll
-        for (int k = 0; k < NLD; ++k) {
-            const int o = (k * DV_NW * 64 + tid) * 16;
-            if (o < a.act_bytes) *reinterpret_cast<u32x4*>(lds + o) = av[k];
-        }
+    for (int k = 0; k < NLD; ++k) {
+        const int o = (k * DV_NW * 64 + tid) * 16;
+        if (o < a.act_bytes) *reinterpret_cast<u32x4*>(lds + o) = av[k];
     }
     dv_lds_barrier();
 
@@ -221,17 +201,13 @@ typedef void (*DvFn)(const DvArgs);
 // input (n_ff) also 3 (5632), 6 (11008), 7 (14336)
 template <int T0, int T1, int RW, int ROLE>
 DvFn dv_fn_c(int c) {
-    if constexpr (ROLE == DV_ADD_RAW) {   // the FFN down input only (n_ff wide)
-        if (c == 4) return dgemv_kernel<T0, T1, RW, 4, ROLE>;
-    } else {
-        switch (c) {
-        case 1: return dgemv_kernel<T0, T1, RW, 1, ROLE>;
-        case 2: return dgemv_kernel<T0, T1, RW, 2, ROLE>;
-        case 4: return dgemv_kernel<T0, T1, RW, 4, ROLE>;
-        default: break;
-        }
+    switch (c) {
+    case 1: return dgemv_kernel<T0, T1, RW, 1, ROLE>;
+    case 2: return dgemv_kernel<T0, T1, RW, 2, ROLE>;
+    case 4: return dgemv_kernel<T0, T1, RW, 4, ROLE>;
+    default: break;
     }
-    if constexpr (ROLE == DV_ADD || ROLE == DV_ADD_RAW) {
+    if constexpr (ROLE == DV_ADD) {
         switch (c) {
         case 3: return dgemv_kernel<T0, T1, RW, 3, ROLE>;
         case 6: return dgemv_kernel<T0, T1, RW, 6, ROLE>;
@@ -268,7 +244,6 @@ DvFn dv_fn(int role, int t0, int t1, int c) {
     switch (role) {
     case DV_QKV: return dv_fn_role<DV_QKV>(t0, t1, c);
     case DV_ADD: return dv_fn_role<DV_ADD>(t0, t1, c);
-    case DV_ADD_RAW: return c >= 3 ? dv_fn_role<DV_ADD_RAW>(t0, t1, c) : nullptr;
     case DV_SWIGLU: return dv_fn_role<DV_SWIGLU>(t0, t1, c);
     case DV_STORE: return dv_fn_role<DV_STORE>(t0, t1, c);
     default: return nullptr;
@@ -337,8 +312,8 @@ void launch_dv_quant(const float* x, const ActOut& t, hipStream_t s) {
 namespace {
 int dv_role(const GemvParams& p) {
     const GemvSeg& g = p.seg[0];
-    return g.epi == EPI_QKV ? DV_QKV : g.epi == EPI_ADD ? (p.act_raw ? DV_ADD_RAW : DV_ADD)
-         : g.epi == EPI_SWIGLU ? DV_SWIGLU : g.epi == EPI_STORE ? DV_STORE : -1;
+    return g.epi == EPI_QKV ? DV_QKV : g.epi == EPI_ADD ? DV_ADD : g.epi == EPI_SWIGLU ? DV_SWIGLU
+         : g.epi == EPI_STORE ? DV_STORE : -1;
 }
 }  // namespace
 
@@ -349,8 +324,6 @@ bool dgemv_supported(const GemvParams& p) {
     const GemvSeg& g = p.seg[0];
     const int role = dv_role(p);
     if (role < 0 || g.bias || g.expA >= 0 || g.expB >= 0) return false;
-    if (p.act_raw && (role != DV_ADD_RAW || p.nseg != 1 || (size_t)p.K * 4 > (size_t)DV_RAW_LD * DV_NW * 64 * 16))
-        return false;
     if (p.nseg == 2 && (role != DV_QKV || p.seg[1].epi != EPI_QKV)) return false;
     return dv_fn(role, g.A.type, p.nseg == 2 ? p.seg[1].A.type : -1, dv_chunks(p.K)) != nullptr;
 }
@@ -389,7 +362,7 @@ void launch_dgemv(const GemvParams& p, hipStream_t s, hipEvent_t ev_start, hipEv
     a.K = p.K;
     a.q8k = p.act_q8k;
     a.q80 = p.act_q80;
-    a.act_bytes = p.act_raw ? p.K * 4 : (int)dv_act_bytes(p.K, p.act_q8k, p.act_q80);
+    a.act_bytes = (int)dv_act_bytes(p.K, p.act_q8k, p.act_q80);
     a.resid = g0.resid;
     a.tokpos = p.tokpos;
     a.cell_pos = p.cell_pos;
@@ -401,7 +374,7 @@ void launch_dgemv(const GemvParams& p, hipStream_t s, hipEvent_t ev_start, hipEv
     a.n_rot = p.n_rot;
     a.head_dim = p.head_dim > 0 ? p.head_dim : 1;
     a.kv_dim = p.kv_dim;
-    if ((role == DV_ADD || role == DV_ADD_RAW) && !g0.resid) throw Error("dgemv: residual epilogue without resid");
+    if (role == DV_ADD && !g0.resid) throw Error("dgemv: residual epilogue without resid");
     if (role == DV_QKV && !p.tokpos) throw Error("dgemv: QKV epilogue needs tokpos");
     const DvFn fn = dv_fn(role, g0.A.type, p.nseg == 2 ? p.seg[1].A.type : -1, dv_chunks(p.K));
     const size_t smem = (dv_act_bytes(p.K, p.act_q8k, p.act_q80) + 15) / 16 * 16;

@@ -942,10 +942,6 @@ bool Ctx::sp_setup() {
         d.act_q8k = sp[l].fD & 1;
         d.act_q80 = sp[l].fD >> 1;
         ok = ok && dgemv_supported(d);
-        // FFN down on h as it is (each workgroup quantises it while its weights stream in) in place
-        // of a separate quantisation launch; MI_DOWN_QUANT=1: the separate launch (A/B)
-        d.act_raw = 1;
-        sp[l].rawD = getenv("MI_DOWN_QUANT") == nullptr && dgemv_supported(d);
     }
     GemvParams hd;
     std::memset(&hd, 0, sizeof(hd));
@@ -1066,12 +1062,11 @@ void Ctx::enqueue_step_sp(bool with_logits) {
             const bool timed = l == prof_layer && seg_filter == 1;
             if (on()) launch_dgemv(p, stream, timed ? prof_ev[0] : nullptr, timed ? prof_ev[1] : nullptr);
             if (l == prof_layer) seg = 2;
-            if (on() && !b.rawD) launch_dv_quant(h, act(3, b.fD, hp.n_ff, nullptr), stream);
+            if (on()) launch_dv_quant(h, act(3, b.fD, hp.n_ff, nullptr), stream);
         }
         {   // FFN down + residual (in place), then the next layer's (or the output head's) input quantised
             GemvParams p = base;
-            p.act_in = b.rawD ? reinterpret_cast<const char*>(h) : sp_act[3];
-            p.act_raw = b.rawD ? 1 : 0;
+            p.act_in = sp_act[3];
             p.K = hp.n_ff;
             p.act_q8k = b.fD & 1;
             p.act_q80 = b.fD >> 1;
@@ -1697,7 +1692,11 @@ int Ctx::ubatch_layers_short(int nt) {
         launch_qkv_finish(F, stream);
         AttnParams a{qb, kl, vl, tokpos_b, cell_pos, attn_scores, attn_smax, attnb, hp.n_head, hp.n_head_kv,
                      hp.head_dim, kv_dim, (int)n_ctx, kq_scale};
-        if (attn_mfma) launch_attn_mfma(a, nt, attnb, stream);
+        // within ATTN_SHORT cells the decode step's fused kernel, one workgroup per (kv head, token)
+        // (20-token verify 3.52 -> 3.30 ms against the MFMA kernel's 32-token tiles; 64 tokens
+        // equal, same box); MI_SHORT_ATTN_MFMA=1: the MFMA kernel
+        static const bool mfma_env = getenv("MI_SHORT_ATTN_MFMA") != nullptr;
+        if (attn_mfma && (mfma_env || n_cells > ATTN_SHORT)) launch_attn_mfma(a, nt, attnb, stream);
         else launch_attn_multi(a, nt, attnb, stream);
         {   // output projection: parts of W_o attn, added to x by the FFN's quant_act
             const ActQ8 act = ub_act(hp.n_embd, nt, L.wo.type);

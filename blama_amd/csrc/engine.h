@@ -233,7 +233,6 @@ struct Ctx {
     // dv_quant launch (rms_norm'd x, or h) -- from sp_act[role]
     struct SpLayer {
         int fA, fB, fC, fD;             // activation formats of QKV, WO, gate/up, down: bit 0 Q8_K, bit 1 Q8_0
-        bool rawD;                      // FFN down quantises h itself (dgemv act_raw): no separate launch
     };
     bool sp_ok = false;                 // MI_DECODE_OLD=1: the gemv_kernel graph instead
     std::vector<SpLayer> sp;

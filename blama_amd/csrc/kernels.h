@@ -108,12 +108,9 @@ struct GemvParams {
     int attn_nsplit;          // PRO_ATTN: splits to add (0: from the cell count in tokpos)
     unsigned long long* stamps;   // diagnostics (MI_STAMPS builds): per-workgroup stamps [grid][8]
     // streaming form (launch_dgemv, dense LLaMA decode within ATTN_SHORT cells): the activation
-    // arrives quantised, act_layout(K, act_q8k, act_q80) at act_in (pro / x / norm_w unused) --
-    // or, act_raw (EPI_ADD, K <= 14336: the FFN down launch), as K floats at act_in that every
-    // workgroup quantises itself (no norm)
+    // arrives quantised, act_layout(K, act_q8k, act_q80) at act_in (pro / x / norm_w unused)
     const char* act_in;
     int act_q8k, act_q80;
-    int act_raw;
 };
 
 void init_kernel_attributes();   // once per device, before any graph capture

@@ -71,6 +71,31 @@ __device__ __forceinline__ float wave_max_pos(float v) {
 
 __device__ __forceinline__ float silu(float x) { return x / (1.0f + expf(-x)); }
 
+// ((p[0] + p[s]) + p[2s]) + ... over n parts, in part order, the loads of up to 8 parts issued
+// together (a runtime-length loop of load-then-add pays one memory round trip per part)
+template <typename V>
+__device__ __forceinline__ V sum_parts(const V* p, long long stride, int n) {
+    V v[7];
+#pragma unroll
+    for (int k = 1; k < 8; ++k)
+        if (k < n) v[k - 1] = p[k * stride];
+    V acc = p[0];
+#pragma unroll
+    for (int k = 1; k < 8; ++k)
+        if (k < n) acc = acc + v[k - 1];
+    for (int k = 8; k < n; k += 4) {   // (past 8 parts: 4 at a time)
+        V w[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (k + q < n) w[q] = p[(k + q) * stride];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (k + q < n) acc = acc + w[q];
+    }
+    return acc;
+}
+
+
 // ---------------------------------------------------------------------------
 // Activation rows -> Q8_K (quantize_row_q8_K_ref), one workgroup per token row.
 // Writes q in MFMA-fragment order (below), d transposed [nb][npad] (4 consecutive tokens = one
@@ -78,8 +103,9 @@ __device__ __forceinline__ float silu(float x) { return x / (1.0f + expf(-x)); }
 // lo in 0..63): bytes 0-7 hi_j, 8-15 lo_j -- the int8 A operand of the MFMA that forms
 // sum_j m_j*bsum_j = 64*sum m_j hi_j + sum m_j lo_j exactly.  Rows ntok..npad-1 are zero.
 // ---------------------------------------------------------------------------
-// QA_W waves per token row (16: one 256-element block each at K = 4096)
-template <int QA_W>
+// QA_W waves per token row (16: one 256-element block each at K = 4096); XR blocks per wave at
+// most (the host picks the smallest that covers K: fewer predicated copies, fewer registers)
+template <int QA_W, int XR>
 __global__ __launch_bounds__(64 * QA_W) void quant_act_kernel(const float* x, int x_stride, const float* norm_w,
                                                         float eps, ActQ8 a, const int* rows, const float* part, int nks,
                                                         int swiglu) {
@@ -104,7 +130,6 @@ __global__ __launch_bounds__(64 * QA_W) void quant_act_kernel(const float* x, in
     }
     const f32x4* x4 = x ? reinterpret_cast<const f32x4*>(x + (long long)(rows ? rows[t] : t) * x_stride) : nullptr;
     // this wave's blocks (wave, wave + QA_W, ...) read once, kept for the quantisation
-    constexpr int XR = 16;   // K <= QA_W * 16 * 256
     f32x4 xr[XR];
     if (swiglu) {   // silu(g) * u of the pair launch's parts: g = ((g0 + g1) + ...), u likewise
         const f32x4* p4 = reinterpret_cast<const f32x4*>(part + (long long)t * 2 * a.K);
@@ -113,14 +138,11 @@ __global__ __launch_bounds__(64 * QA_W) void quant_act_kernel(const float* x, in
         for (int i = 0; i < XR; ++i) {
             const int blk = wave + QA_W * i;
             if (blk < nb) {
-                f32x4 g = p4[blk * 64 + lane], u = p4[a.K / 4 + blk * 64 + lane];
-                for (int k = 1; k < nks; ++k) {
-                    const f32x4 gk = p4[k * kst + blk * 64 + lane], uk = p4[k * kst + a.K / 4 + blk * 64 + lane];
-                    g = f32x4{g.x + gk.x, g.y + gk.y, g.z + gk.z, g.w + gk.w};
-                    u = f32x4{u.x + uk.x, u.y + uk.y, u.z + uk.z, u.w + uk.w};
-                }
+                const f32x4 g = sum_parts(p4 + blk * 64 + lane, kst, nks);
+                const f32x4 u = sum_parts(p4 + a.K / 4 + blk * 64 + lane, kst, nks);
                 xr[i] = f32x4{silu(g.x) * u.x, silu(g.y) * u.y, silu(g.z) * u.z, silu(g.w) * u.w};
             }
+            asm volatile("" ::: "memory");   // one block's part loads in flight at a time (registers)
         }
     } else {
 #pragma unroll
@@ -133,14 +155,12 @@ __global__ __launch_bounds__(64 * QA_W) void quant_act_kernel(const float* x, in
         for (int i = 0; i < XR; ++i) {
             const int blk = wave + QA_W * i;
             if (blk < nb) {
-                f32x4 acc = reinterpret_cast<const f32x4*>(part + (long long)t * a.K)[blk * 64 + lane];
-                for (int k = 1; k < nks; ++k) {
-                    const f32x4 pk = reinterpret_cast<const f32x4*>(part + ((long long)k * a.ntok + t) * a.K)[blk * 64 + lane];
-                    acc = f32x4{acc.x + pk.x, acc.y + pk.y, acc.z + pk.z, acc.w + pk.w};
-                }
+                const f32x4 acc = sum_parts(reinterpret_cast<const f32x4*>(part + (long long)t * a.K) + blk * 64 + lane,
+                                            (long long)a.ntok * a.K / 4, nks);
                 xr[i] = f32x4{acc.x + xr[i].x, acc.y + xr[i].y, acc.z + xr[i].z, acc.w + xr[i].w};
                 xw[blk * 64 + lane] = xr[i];
             }
+            asm volatile("" ::: "memory");   // one block's part loads in flight at a time (registers)
         }
     }
     float scale = 1.0f;
@@ -1073,11 +1093,18 @@ __global__ __launch_bounds__(64 * MS_NW) void mmqs_t(const MsArgs M, const ActQ8
     constexpr int TB = mmq32_tile_bytes_d(T);
     const uint8_t* tile0 = swA + ((long long)rt * nb + sb0) * TB;
     MsW<T> w[D];
+    // a busy wave waits for its DMA only (issued before its NLD weight loads: loads retire in
+    // order), so superblock 0's dots start while the later ones are still arriving
+    constexpr int NLD = D * (MsT<T>::NV + (T == T_Q6_K ? 1 : 0));
+    static_assert(NLD <= 63, "vmcnt range");
     if (busy) {
 #pragma unroll
         for (int d = 0; d < D; ++d) w[d] = ms_load<T>(tile0 + (long long)min(d, nsb - 1) * TB, lane);
+        asm volatile("" ::: "memory");   // every ring load issued before the wait
+        __builtin_amdgcn_s_waitcnt((NLD & 0xF) | ((NLD >> 4) << 14) | (0x7 << 4) | (0xF << 8));   // vmcnt(NLD)
+    } else {
+        __builtin_amdgcn_s_waitcnt((0x7 << 4) | (0xF << 8));   // vmcnt(0)
     }
-    __builtin_amdgcn_s_waitcnt((0x7 << 4) | (0xF << 8));   // vmcnt(0): the DMA (and the ring) landed
     __builtin_amdgcn_s_barrier();
     if (!busy) return;
     float y[NT][16];
@@ -1116,13 +1143,9 @@ __global__ __launch_bounds__(256) void qkv_finish_kernel(const QkvFinish F) {
     const int pr = blockIdx.x * 256 + threadIdx.x;   // row pair
     const int r = 2 * pr;
     if (r >= F.nq + F.nk + F.nv) return;
-    const float* p = F.part + (long long)t * F.pstride + r;
-    float v0 = p[0], v1 = p[1];
-    for (int k = 1; k < F.kp; ++k) {
-        const float* pk = p + (long long)k * F.ntok * F.pstride;
-        v0 = v0 + pk[0];
-        v1 = v1 + pk[1];
-    }
+    const float2* p = reinterpret_cast<const float2*>(F.part + (long long)t * F.pstride + r);
+    const float2 v = sum_parts(p, (long long)F.ntok * F.pstride / 2, F.kp);   // (pstride even: nq, nk, nv are)
+    const float v0 = v.x, v1 = v.y;
     const int seg = r < F.nq ? 0 : r < F.nq + F.nk ? 1 : 2;
     const int row = seg == 0 ? r : seg == 1 ? r - F.nq : r - F.nq - F.nk;
     float o0 = v0, o1 = v1;
@@ -1154,13 +1177,8 @@ __global__ __launch_bounds__(256) void part_sum_kernel(const float* part, int kp
     const int t = blockIdx.y;
     const int r = blockIdx.x * 256 + threadIdx.x;
     if (r >= rows) return;
-    float acc = part[(long long)t * pstride + r];
-    for (int k = 1; k < kp; ++k) acc = acc + part[((long long)k * ntok + t) * pstride + r];
-    if (swiglu) {
-        float u = part[(long long)t * pstride + swiglu + r];
-        for (int k = 1; k < kp; ++k) u = u + part[((long long)k * ntok + t) * pstride + swiglu + r];
-        acc = silu(acc) * u;
-    }
+    float acc = sum_parts(part + (long long)t * pstride + r, (long long)ntok * pstride, kp);
+    if (swiglu) acc = silu(acc) * sum_parts(part + (long long)t * pstride + swiglu + r, (long long)ntok * pstride, kp);
     if (resid) acc = acc + resid[(long long)t * rstride + r];
     out[(long long)t * ostride + r] = acc;
 }
@@ -1179,8 +1197,10 @@ void launch_quant_act(const float* x, int x_stride, const float* norm_w, float e
     // (more than UB_MAX rows only for the MoE rows of a batch: one per (token, slot), padded)
     if (a.npad % 32 || a.ntok > a.npad || a.npad > 4 * UB_MAX) throw Error("quant_act: bad token count");
     if (a.K > 65536) throw Error("quant_act: K past 65536");
-    hipLaunchKernelGGL(mmq::quant_act_kernel<16>, dim3(a.npad), dim3(1024), 0, s, x, x_stride, norm_w, eps, a, rows, part, nks,
-                       swiglu);
+    const int xr = (a.K / 256 + 15) / 16;
+    auto f = xr <= 1 ? mmq::quant_act_kernel<16, 1> : xr <= 2 ? mmq::quant_act_kernel<16, 2>
+           : xr <= 4 ? mmq::quant_act_kernel<16, 4> : mmq::quant_act_kernel<16, 16>;
+    hipLaunchKernelGGL(f, dim3(a.npad), dim3(1024), 0, s, x, x_stride, norm_w, eps, a, rows, part, nks, swiglu);
     MI_HIP(hipGetLastError());
 }
 

@@ -10,12 +10,8 @@ timeout -k 10 200 python -u bench.py --no-cpu --steps 20 --warmup 5 > $OUT/bench
 python3 -c "import json;d=json.load(open('$OUT/bench.json'));p=d['prefill'];print('decode',d['value'],'prefill',p['ms'],'verify',p['verify']['ms'],'short',p.get('verify_short'))"
 MI_MMQS_MAX=0 timeout -k 10 200 python -u bench.py --no-cpu --steps 20 --warmup 5 > $OUT/bench_tiled.json 2> $OUT/bench_tiled.err || { tail -5 $OUT/bench_tiled.err; exit 1; }
 python3 -c "import json;d=json.load(open('$OUT/bench_tiled.json'));p=d['prefill'];print('tiled: short',p.get('verify_short'))"
-for mode in raw sep raw sep; do
-  if [ $mode = sep ]; then export MI_DOWN_QUANT=1; else unset MI_DOWN_QUANT; fi
-  timeout -k 10 120 python -u bench.py --no-cpu --prefill 0 --verify 0 --steps 128 --warmup 16 > $OUT/dec_$mode.json 2> $OUT/dec_$mode.err || { tail -5 $OUT/dec_$mode.err; exit 1; }
-  python3 -c "import json;d=json.load(open('$OUT/dec_$mode.json'));print('$mode', d['value'], d['roofline']['avg_launch_us'])"
-done
-unset MI_DOWN_QUANT
+MI_SHORT_ATTN_FUSED=1 timeout -k 10 200 python -u bench.py --no-cpu --steps 20 --warmup 5 > $OUT/bench_fa.json 2> $OUT/bench_fa.err || { tail -5 $OUT/bench_fa.err; exit 1; }
+python3 -c "import json;d=json.load(open('$OUT/bench_fa.json'));p=d['prefill'];print('fused attn: short',p.get('verify_short'))"
 MI_NO_GRAPH=1 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python -u bench.py --no-cpu --steps 4 --warmup 2 > $OUT/trace_bench.json 2> $OUT/prof.err || { tail -3 $OUT/prof.err; exit 1; }
 find $OUT/prof -name '*kernel_stats.csv' -exec cp {} $OUT/kernel_stats.csv \;
 find $OUT/prof -name '*kernel_trace.csv' -exec cp {} $OUT/kernel_trace.csv \;

