@@ -112,6 +112,9 @@ __global__ __launch_bounds__(64 * QA_W) void quant_act_kernel(const float* x, in
     const int t = blockIdx.x;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int nb = a.K >> 8;
+    // this wave's blocks: w0, w0 + bst, ... (gridDim.y > 1, rows without a norm: the row's blocks
+    // spread over gridDim.y workgroups)
+    const int w0 = (int)blockIdx.y * QA_W + wave, bst = QA_W * (int)gridDim.y;
     __shared__ double red[QA_W];
     // MFMA-fragment order (one wave load = 1 KiB contiguous): q [tile][sb][j][h*32 + t%32][16 B],
     // element 32j + 16h + e of superblock sb of token t at byte e; bsb [tile][sb][t%32][16 B]
@@ -120,7 +123,7 @@ __global__ __launch_bounds__(64 * QA_W) void quant_act_kernel(const float* x, in
     int8_t* q = a.q + (long long)tile * nb * 8192 + fj * 1024 + (fh * 32 + tr) * 16 + 4 * fw;
     int8_t* bsb = a.q80 ? nullptr : a.bsb + ((long long)tile * nb * 32 + tr) * 16;
     if (t >= a.ntok || (rows && rows[t] < 0)) {   // padding rows (and MoE group padding) are zero
-        for (int blk = wave; blk < nb; blk += QA_W) {
+        for (int blk = w0; blk < nb; blk += bst) {
             *reinterpret_cast<int*>(q + blk * 8192) = 0;
             if (!a.q80 && lane < 4) reinterpret_cast<int*>(bsb + blk * 512)[lane] = 0;
             if (a.q80 && lane < 8) a.dT[(long long)(blk * 8 + lane) * a.npad + t] = 0.0f;
@@ -129,14 +132,14 @@ __global__ __launch_bounds__(64 * QA_W) void quant_act_kernel(const float* x, in
         return;
     }
     const f32x4* x4 = x ? reinterpret_cast<const f32x4*>(x + (long long)(rows ? rows[t] : t) * x_stride) : nullptr;
-    // this wave's blocks (wave, wave + QA_W, ...) read once, kept for the quantisation
+    // this wave's blocks read once, kept for the quantisation
     f32x4 xr[XR];
     if (swiglu) {   // silu(g) * u of the pair launch's parts: g = ((g0 + g1) + ...), u likewise
         const f32x4* p4 = reinterpret_cast<const f32x4*>(part + (long long)t * 2 * a.K);
         const long long kst = (long long)a.ntok * 2 * a.K / 4;   // one part, in f32x4
 #pragma unroll
         for (int i = 0; i < XR; ++i) {
-            const int blk = wave + QA_W * i;
+            const int blk = w0 + bst * i;
             if (blk < nb) {
                 const f32x4 g = sum_parts(p4 + blk * 64 + lane, kst, nks);
                 const f32x4 u = sum_parts(p4 + a.K / 4 + blk * 64 + lane, kst, nks);
@@ -147,13 +150,13 @@ __global__ __launch_bounds__(64 * QA_W) void quant_act_kernel(const float* x, in
     } else {
 #pragma unroll
         for (int i = 0; i < XR; ++i)
-            if (wave + QA_W * i < nb) xr[i] = x4[(wave + QA_W * i) * 64 + lane];
+            if (w0 + bst * i < nb) xr[i] = x4[(w0 + bst * i) * 64 + lane];
     }
     if (part && !swiglu) {   // the split-K GEMM's nks partials: x = (((p0 + p1) + p2) + ...) + x (EPI_ADD's o + resid), written back
         f32x4* xw = reinterpret_cast<f32x4*>(const_cast<float*>(x) + (long long)t * x_stride);
 #pragma unroll
         for (int i = 0; i < XR; ++i) {
-            const int blk = wave + QA_W * i;
+            const int blk = w0 + bst * i;
             if (blk < nb) {
                 const f32x4 acc = sum_parts(reinterpret_cast<const f32x4*>(part + (long long)t * a.K) + blk * 64 + lane,
                                             (long long)a.ntok * a.K / 4, nks);
@@ -168,7 +171,7 @@ __global__ __launch_bounds__(64 * QA_W) void quant_act_kernel(const float* x, in
         double sacc = 0.0;
 #pragma unroll
         for (int i = 0; i < XR; ++i) {
-            if (wave + QA_W * i < nb) {
+            if (w0 + bst * i < nb) {
                 const f32x4 v = xr[i];
                 sacc += (double)(v.x * v.x);
                 sacc += (double)(v.y * v.y);
@@ -187,7 +190,7 @@ __global__ __launch_bounds__(64 * QA_W) void quant_act_kernel(const float* x, in
     const f32x4* w4 = reinterpret_cast<const f32x4*>(norm_w);
 #pragma unroll
     for (int i = 0; i < XR; ++i) {
-        const int blk = wave + QA_W * i;
+        const int blk = w0 + bst * i;
         if (blk >= nb) break;
         const f32x4 xv = xr[i];
         float v[4] = {xv.x, xv.y, xv.z, xv.w};
@@ -920,9 +923,11 @@ __device__ __forceinline__ void ms_sb(const MsW<T>& w, int s, const char* lds, i
         int sc[8], mn[8];
         q4k_scales(hd, sc, mn);
         const v16i z = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-        v16i acc0[NT], acc1[NT];
+        // [hf]: even / odd sub-blocks in separate accumulators -- four independent MFMA chains per
+        // token tile instead of two (a dependent MFMA waits out its predecessor's latency)
+        v16i acc0[2][NT], acc1[2][NT];
 #pragma unroll
-        for (int t = 0; t < NT; ++t) acc0[t] = acc1[t] = z;
+        for (int t = 0; t < NT; ++t) acc0[0][t] = acc1[0][t] = acc0[1][t] = acc1[1][t] = z;
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
             const unsigned q[4] = {w.v[p].x, w.v[p].y, w.v[p].z, w.v[p].w};
@@ -951,8 +956,8 @@ __device__ __forceinline__ void ms_sb(const MsW<T>& w, int s, const char* lds, i
 #pragma unroll
                 for (int t = 0; t < NT; ++t) {
                     const v4i a = act(t, j);
-                    acc0[t] = mfma_acc(a, b0, acc0[t]);
-                    acc1[t] = mfma_acc(a, b1, acc1[t]);
+                    acc0[hf][t] = mfma_acc(a, b0, acc0[hf][t]);
+                    acc1[hf][t] = mfma_acc(a, b1, acc1[hf][t]);
                 }
             }
         }
@@ -976,7 +981,7 @@ __device__ __forceinline__ void ms_sb(const MsW<T>& w, int s, const char* lds, i
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     const int e = 4 * g + i;
-                    const int S = acc0[t][e] + (T == T_Q5_K ? 128 : 8) * acc1[t][e];
+                    const int S = (acc0[0][t][e] + acc0[1][t][e]) + (T == T_Q5_K ? 128 : 8) * (acc1[0][t][e] + acc1[1][t][e]);
                     const float d = dr * dx[i], dm = dmr * dx[i];
                     y[t][e] = fmaf(-dm, (float)(64 * x1[e] + x2[e]), fmaf(d, (float)S, y[t][e]));
                 }
@@ -984,9 +989,9 @@ __device__ __forceinline__ void ms_sb(const MsW<T>& w, int s, const char* lds, i
         }
     } else if (T == T_Q6_K) {
         const v16i z = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-        v16i ah[NT], al[NT];
+        v16i ah[2][NT], al[2][NT];   // [sp & 1]: four independent MFMA chains per token tile
 #pragma unroll
-        for (int t = 0; t < NT; ++t) ah[t] = al[t] = z;
+        for (int t = 0; t < NT; ++t) ah[0][t] = al[0][t] = ah[1][t] = al[1][t] = z;
 #pragma unroll
         for (int sp = 0; sp < 8; ++sp) {
             const unsigned ph[4] = {w.v[sp].x, w.v[sp].y, w.v[sp].z, w.v[sp].w};
@@ -995,8 +1000,8 @@ __device__ __forceinline__ void ms_sb(const MsW<T>& w, int s, const char* lds, i
 #pragma unroll
             for (int t = 0; t < NT; ++t) {
                 const v4i a = act(t, sp);
-                ah[t] = mfma_acc(a, bh, ah[t]);
-                al[t] = mfma_acc(a, bl, al[t]);
+                ah[sp & 1][t] = mfma_acc(a, bh, ah[sp & 1][t]);
+                al[sp & 1][t] = mfma_acc(a, bl, al[sp & 1][t]);
             }
         }
         const float dr = h2f(w.d6);
@@ -1009,7 +1014,7 @@ __device__ __forceinline__ void ms_sb(const MsW<T>& w, int s, const char* lds, i
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     const int e = 4 * g + i;
-                    y[t][e] = fmaf(dr * dx[i], (float)(ah[t][e] * 64 + al[t][e]), y[t][e]);
+                    y[t][e] = fmaf(dr * dx[i], (float)((ah[0][t][e] + ah[1][t][e]) * 64 + (al[0][t][e] + al[1][t][e])), y[t][e]);
                 }
             }
     } else {   // Q8_0: one MFMA per 32-block, vec_dot_q8_0_q8_0's per-block float update
@@ -1197,10 +1202,14 @@ void launch_quant_act(const float* x, int x_stride, const float* norm_w, float e
     // (more than UB_MAX rows only for the MoE rows of a batch: one per (token, slot), padded)
     if (a.npad % 32 || a.ntok > a.npad || a.npad > 4 * UB_MAX) throw Error("quant_act: bad token count");
     if (a.K > 65536) throw Error("quant_act: K past 65536");
-    const int xr = (a.K / 256 + 15) / 16;
+    // a row without a norm needs no row-wide sum: its blocks go to ceil(nb / 16) workgroups, one
+    // block per wave (the FFN down input: 3 at n_ff = 11008)
+    const int nb = a.K / 256;
+    const int ny = norm_w ? 1 : (nb + 15) / 16;
+    const int xr = (nb + 16 * ny - 1) / (16 * ny);
     auto f = xr <= 1 ? mmq::quant_act_kernel<16, 1> : xr <= 2 ? mmq::quant_act_kernel<16, 2>
            : xr <= 4 ? mmq::quant_act_kernel<16, 4> : mmq::quant_act_kernel<16, 16>;
-    hipLaunchKernelGGL(f, dim3(a.npad), dim3(1024), 0, s, x, x_stride, norm_w, eps, a, rows, part, nks, swiglu);
+    hipLaunchKernelGGL(f, dim3(a.npad, ny), dim3(1024), 0, s, x, x_stride, norm_w, eps, a, rows, part, nks, swiglu);
     MI_HIP(hipGetLastError());
 }
 
