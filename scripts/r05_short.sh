@@ -3,7 +3,7 @@
 OUT=gpurun_out/${1:-r05s}
 mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -k 10 420 python -u -m pytest tests/test_gpu_verify.py tests/test_gpu_fullwidth.py -k "out_all or short or batched or long_prompt" -x -v -s --timeout 300 --timeout-method thread > $OUT/pytest.log 2>&1
+timeout -k 10 420 python -u -m pytest tests/test_gpu_verify.py tests/test_gpu_fullwidth.py tests/test_gpu_batch_ops.py -k "out_all or short or batched or long_prompt or mmqs" -x -v -s --timeout 300 --timeout-method thread > $OUT/pytest.log 2>&1
 rc=$?; echo "pytest rc $rc"; grep -E "PASS|FAIL|Error|error" $OUT/pytest.log | head -30; tail -3 $OUT/pytest.log
 [ $rc -eq 0 ] || exit 1
 timeout -k 10 200 python -u bench.py --no-cpu --steps 20 --warmup 5 > $OUT/bench.json 2> $OUT/bench.err || { tail -5 $OUT/bench.err; exit 1; }
