@@ -273,12 +273,25 @@ __global__ __launch_bounds__(DQ_NORM_W * 64) void dv_quant_kernel(const float* x
         wn = gptr(reinterpret_cast<const f32x4*>(t.norm_w))[b * 64 + lane];
         double sq = 0.0;
         const int n4 = t.K >> 2;
-        for (int i = tid; i < n4; i += DQ_NORM_W * 64) {
-            const f32x4 y = gptr(reinterpret_cast<const f32x4*>(x))[i];
-            sq += (double)(y.x * y.x);
-            sq += (double)(y.y * y.y);
-            sq += (double)(y.z * y.z);
-            sq += (double)(y.w * y.w);
+        // this thread's pieces tid, tid + 256, ... requested together (DQ_LD at a time: a
+        // load-then-add loop waited out one memory round trip per piece), summed in that order
+        constexpr int DQ_LD = 8;   // K <= 8192 in one round
+        for (int i0 = tid; i0 < n4; i0 += DQ_LD * DQ_NORM_W * 64) {
+            f32x4 y[DQ_LD];
+#pragma unroll
+            for (int k = 0; k < DQ_LD; ++k) {
+                const int i = i0 + k * DQ_NORM_W * 64;
+                if (i < n4) y[k] = gptr(reinterpret_cast<const f32x4*>(x))[i];
+            }
+#pragma unroll
+            for (int k = 0; k < DQ_LD; ++k) {
+                if (i0 + k * DQ_NORM_W * 64 < n4) {
+                    sq += (double)(y[k].x * y[k].x);
+                    sq += (double)(y[k].y * y[k].y);
+                    sq += (double)(y[k].z * y[k].z);
+                    sq += (double)(y[k].w * y[k].w);
+                }
+            }
         }
         sq = wave_sum63_d(sq);
         if (lane == 63) red[wave] = sq;

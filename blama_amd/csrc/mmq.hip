@@ -1142,6 +1142,165 @@ __global__ __launch_bounds__(64 * MS_NW) void mmqs_t(const MsArgs M, const ActQ8
         }
 }
 
+// mmqs1: the one-token-tile (<= 32 tokens) k-quant form with no LDS: a workgroup is ONE wave =
+// one row tile x one K-part (4x the workgroups of mmqs_t, so a launch of few row blocks -- the 7B
+// WO at 128 row tiles -- still covers every CU), and the wave streams its activation pieces
+// (8 A operands, the bsums, the 16 token scales per superblock) through registers next to its
+// weights, both DA / DW superblocks ahead.  No barrier, no LDS-DMA: every wait is the compiler's
+// count of this wave's own loads.  Same arithmetic as ms_sb (sum for sum).
+struct MsAct {
+    v4i a[8];     // A operands of sub-blocks 0..7
+    v4i ab;       // bsums (64 hi + lo) of token col (lanes h = 1: zero)
+    f32x4 dx[4];  // d of tokens 8g + 4h .. + 3
+};
+__device__ __forceinline__ MsAct ms_act_load(const ActQ8& act, int sb, int lane) {
+    const int col = lane & 31, h = lane >> 5;
+    MsAct r;
+    const int8_t* q = act.q + (long long)sb * 8192 + lane * 16;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r.a[j] = __builtin_nontemporal_load(gp(reinterpret_cast<const v4i*>(q + j * 1024)));
+    const v4i b = *gp(reinterpret_cast<const v4i*>(act.bsb + (long long)sb * 512 + col * 16));
+    r.ab = h == 0 ? b : v4i{0, 0, 0, 0};
+#pragma unroll
+    for (int g = 0; g < 4; ++g) r.dx[g] = *gp(reinterpret_cast<const f32x4*>(act.dT + (long long)sb * act.npad + 8 * g + 4 * h));
+    return r;
+}
+template <int T>
+__device__ __forceinline__ void ms1_sb(const MsW<T>& w, const MsAct& A, int lane, float y[16]) {
+    const int h = lane >> 5;
+    const v16i z = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    if (T == T_Q4_K || T == T_Q5_K) {
+        const u32x4 hd = w.v[MsT<T>::NV - 1];
+        int sc[8], mn[8];
+        q4k_scales(hd, sc, mn);
+        v16i acc0 = z, acc1 = z;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            const unsigned q[4] = {w.v[p].x, w.v[p].y, w.v[p].z, w.v[p].w};
+#pragma unroll
+            for (int hf = 0; hf < 2; ++hf) {
+                const int j = 2 * p + hf;
+                unsigned P0[4], P1[4];
+                if (T == T_Q4_K) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const unsigned nib = hf ? (q[i] >> 4) & 0x0F0F0F0Fu : q[i] & 0x0F0F0F0Fu;
+                        P0[i] = bmul(nib, sc[j] & 7);
+                        P1[i] = bmul(nib, sc[j] >> 3);
+                    }
+                } else {
+                    const unsigned b[4] = {w.v[4].x, w.v[4].y, w.v[4].z, w.v[4].w};
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const unsigned q5 = ((hf ? q[i] >> 4 : q[i]) & 0x0F0F0F0Fu) | (((b[i] >> j) & 0x01010101u) << 4);
+                        const unsigned m02 = wmul16(q5 & 0x00FF00FFu, sc[j]), m13 = wmul16((q5 >> 8) & 0x00FF00FFu, sc[j]);
+                        P0[i] = (m02 & 0x007F007Fu) | ((m13 & 0x007F007Fu) << 8);
+                        P1[i] = ((m02 >> 7) & 0x001F001Fu) | (((m13 >> 7) & 0x001F001Fu) << 8);
+                    }
+                }
+                acc0 = mfma_acc(A.a[j], as_v4i(P0), acc0);
+                acc1 = mfma_acc(A.a[j], as_v4i(P1), acc1);
+            }
+        }
+        const unsigned Z = hd.z, W = hd.w;
+        const int m03 = (int)(Z & 0x3F3F3F3Fu);
+        const int m47 = (int)(((W >> 4) & 0x0F0F0F0Fu) | ((Z >> 2) & 0x30303030u));
+        const v4i bm1 = h == 0 ? v4i{m03, m47, 0, 0} : v4i{0, 0, 0, 0};
+        const v4i bm2 = h == 0 ? v4i{0, 0, m03, m47} : v4i{0, 0, 0, 0};
+        const v16i x1 = mfma(A.ab, bm1);
+        const v16i x2 = mfma(A.ab, bm2);
+        const float dr = h2f(hd.x), dmr = h2f(hd.x >> 16);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const float dx[4] = {A.dx[g].x, A.dx[g].y, A.dx[g].z, A.dx[g].w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int e = 4 * g + i;
+                const int S = acc0[e] + (T == T_Q5_K ? 128 : 8) * acc1[e];
+                const float d = dr * dx[i], dm = dmr * dx[i];
+                y[e] = fmaf(-dm, (float)(64 * x1[e] + x2[e]), fmaf(d, (float)S, y[e]));
+            }
+        }
+    } else {   // Q6_K
+        v16i ah = z, al = z;
+#pragma unroll
+        for (int sp = 0; sp < 8; ++sp) {
+            const unsigned ph[4] = {w.v[sp].x, w.v[sp].y, w.v[sp].z, w.v[sp].w};
+            const unsigned pl[4] = {w.v[8 + sp].x, w.v[8 + sp].y, w.v[8 + sp].z, w.v[8 + sp].w};
+            ah = mfma_acc(A.a[sp], as_v4i(ph), ah);
+            al = mfma_acc(A.a[sp], as_v4i(pl), al);
+        }
+        const float dr = h2f(w.d6);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const float dx[4] = {A.dx[g].x, A.dx[g].y, A.dx[g].z, A.dx[g].w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int e = 4 * g + i;
+                y[e] = fmaf(dr * dx[i], (float)(ah[e] * 64 + al[e]), y[e]);
+            }
+        }
+    }
+}
+template <int T> struct Ms1D { static constexpr int DW = 2, DA = 2; };
+template <> struct Ms1D<T_Q6_K> { static constexpr int DW = 1, DA = 2; };
+
+template <int T, bool AB>
+__global__ __launch_bounds__(64) void mmqs1_t(const MsArgs M, const ActQ8 act) {
+    constexpr int DW = Ms1D<T>::DW, DA = Ms1D<T>::DA;
+    const int lane = threadIdx.x & 63;
+    const int col = lane & 31, h = lane >> 5;
+    const int nb = act.K >> 8;
+    const int kp = (int)blockIdx.x % M.kp, g = (int)blockIdx.x / M.kp;
+    const int sb0 = kp * M.sbw, nsb = min(M.sbw, nb - sb0);
+    int seg = 0, rt = g;
+#pragma unroll
+    for (int i = 0; i < MMQ_SEGS - 1; ++i)
+        if (i + 1 < M.n && seg == i && rt >= M.nrt[i]) {
+            rt -= M.nrt[i];
+            seg = i + 1;
+        }
+    const uint8_t* swA = seg == 0 ? M.sw[0] : seg == 1 ? M.sw[1] : M.sw[2];
+    const int rows_s = seg == 0 ? M.rows[0] : seg == 1 ? M.rows[1] : M.rows[2];
+    const int prow_s = seg == 0 ? M.prow[0] : seg == 1 ? M.prow[1] : M.prow[2];
+    constexpr int TB = mmq32_tile_bytes_d(T);
+    const uint8_t* tile0 = swA + ((long long)rt * nb + sb0) * TB;
+    // activation first, then weights (loads retire in order: superblock 0's act is never queued
+    // behind later weights)
+    MsAct a[DA];
+#pragma unroll
+    for (int d = 0; d < DA; ++d) a[d] = ms_act_load(act, sb0 + min(d, nsb - 1), lane);
+    MsW<T> w[DW];
+#pragma unroll
+    for (int d = 0; d < DW; ++d) w[d] = ms_load<T>(tile0 + (long long)min(d, nsb - 1) * TB, lane);
+    float y[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) y[e] = 0.0f;
+    static_assert(DA % DW == 0 || DW % DA == 0, "ring depths");
+    constexpr int DM = DA > DW ? DA : DW;
+    for (int i = 0; i < nsb; i += DM) {
+#pragma unroll
+        for (int d = 0; d < DM; ++d) {
+            const int s = i + d;
+            if (s < nsb) {
+                const MsAct ca = a[d % DA];
+                const MsW<T> cw = w[d % DW];
+                if (s + DA < nsb) a[d % DA] = ms_act_load(act, sb0 + s + DA, lane);
+                if (s + DW < nsb) w[d % DW] = ms_load<T>(tile0 + (long long)(s + DW) * TB, lane);
+                ms1_sb<T>(cw, ca, lane, y);
+            }
+        }
+    }
+    const int rr = AB ? rt * 16 + (col & 15) : rt * 32 + col;
+    if (rr >= rows_s) return;
+    const int prow = prow_s + (AB && col >= 16 ? M.nff : 0) + rr;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int tok = (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (tok < act.ntok) M.part[((long long)kp * act.ntok + tok) * M.pstride + prow] = y[r];
+    }
+}
+
 // the sum of the K-parts in part order, with the consumer's epilogue: Q / K RoPE (ggml NORM, the
 // rope table of the batch), Q to q, K / V to the f16 caches (and the cell positions)
 __global__ __launch_bounds__(256) void qkv_finish_kernel(const QkvFinish F) {
@@ -1376,6 +1535,19 @@ int launch_mmqs(const QMat* const* mats, const int* prow, int n, bool pair, int 
     const int NT = act.npad / 32;
     const int KQ = T != T_Q8_0;
     const int lds = mmq::MS_SBW * NT * 8192 + (KQ ? mmq::MS_SBW * NT * 1024 + mmq::MS_SBW * 256 : mmq::MS_SBW * 8 * 256);
+    // one token tile, k-quants: the one-wave register form (MI_MMQS1=0: the LDS form)
+    static const bool ms1_env = getenv("MI_MMQS1") == nullptr || atoi(getenv("MI_MMQS1")) != 0;
+    if (ms1_env && NT == 1 && T != T_Q8_0) {
+        decltype(&mmq::mmqs1_t<T_Q4_K, false>) f1 = nullptr;
+        switch (T) {
+        case T_Q4_K: f1 = pair ? mmq::mmqs1_t<T_Q4_K, true> : mmq::mmqs1_t<T_Q4_K, false>; break;
+        case T_Q5_K: f1 = pair ? mmq::mmqs1_t<T_Q5_K, true> : mmq::mmqs1_t<T_Q5_K, false>; break;
+        default: f1 = pair ? mmq::mmqs1_t<T_Q6_K, true> : mmq::mmqs1_t<T_Q6_K, false>; break;
+        }
+        hipLaunchKernelGGL(f1, dim3(M.nrt_tot * M.kp), dim3(64), 0, s, M, act);
+        MI_HIP(hipGetLastError());
+        return M.kp;
+    }
     decltype(&mmq::mmqs_t<T_Q4_K, false, 1>) f = nullptr;
 #define MS_PICK(TT)                                                                                 \
     f = pair ? (NT == 1 ? mmq::mmqs_t<TT, true, 1> : mmq::mmqs_t<TT, true, 2>)                     \
