@@ -1486,22 +1486,21 @@ void Ctx::decode_ubatch(const int32_t* tokens, int n, bool all) {
             pos_max = pos;
         }
         MI_HIP(hipMemcpyAsync(tokpos_b, hpos, nt * 4 * sizeof(int), hipMemcpyHostToDevice, stream));
+        if (mmqs_max > 0 && nt <= mmqs_max && hp_dense()) {   // a short batch (its launches captured as a
+            // hipGraph measured no faster: the GPU, not the enqueue, sets the pace)
+            enqueue_ubatch_short(nt, all, c0, c0 + nt == n);
+            continue;
+        }
         EmbedParams ep{m->tok_embd, tokpos_b, xb, hp.n_embd};
         launch_embed_multi(ep, nt, stream);
         launch_rope_table(tokpos_b, nt, hp.n_rot, theta_scale, hp.freq_scale, m->rope_freqs, ub_rope, stream);
         const float* pend = nullptr;   // split-K partials not yet added into xb (the next quant_act does)
-        int pend_k = 0;                // (their count)
-        const bool short_b = mmqs_max > 0 && nt <= mmqs_max && hp_dense();
         // split-K parts of the residual GEMMs: 4 for short batches of dense models (verification
         // of tens of tokens: more workgroups, a quarter of the superblock steps each; 4 x nt rows
         // fit the 2 x UB_MAX partials buffer), else 2 (the MoE router adds 2)
         static const int ks_short = getenv("MI_MMQ_KS4") ? atoi(getenv("MI_MMQ_KS4")) : 64;
         const int ks = hp_dense() && nt <= ks_short ? 4 : 2;
-        if (short_b) {
-            pend_k = ubatch_layers_short(nt);
-            pend = ub_spart;
-        }
-        for (int l = 0; l < (short_b ? 0 : hp.n_layer); ++l) {
+        for (int l = 0; l < hp.n_layer; ++l) {
             const Layer& L = m->layers[l];
             __half* kl = kcache + (size_t)l * n_ctx * kv_dim;
             __half* vl = vcache + (size_t)l * n_ctx * kv_dim;
@@ -1604,21 +1603,7 @@ void Ctx::decode_ubatch(const int32_t* tokens, int n, bool all) {
                 launch_mmq32(p, act, ub_rope, stream);
             }
         }
-        if (all && short_b) {   // final norm + output head on mmqs, its parts summed into the logits rows
-            const ActQ8 a_out = ub_act(hp.n_embd, nt, m->output.type);
-            launch_quant_act(xb, hp.n_embd, m->output_norm, hp.eps, a_out, stream, nullptr, pend, pend_k);
-            const QMat* mo[1] = {&m->output};
-            const int pr[1] = {0};
-            const int kp = launch_mmqs(mo, pr, 1, false, 0, a_out, ub_spart, hp.n_vocab, stream);
-            launch_part_sum(ub_spart, kp, nt, hp.n_vocab, hp.n_vocab, nullptr, 0, logits_all + (size_t)c0 * hp.n_vocab,
-                            hp.n_vocab, stream);
-            if (c0 + nt == n) {
-                MI_HIP(hipMemcpyAsync(logits, logits_all + (size_t)(n - 1) * hp.n_vocab, (size_t)hp.n_vocab * sizeof(float),
-                                      hipMemcpyDeviceToDevice, stream));
-                TopkParams tp{logits, hp.n_vocab, cand, topk_ids, topk_vals, d_h_topk_ids, d_h_topk_vals};
-                launch_topk(tp, stream);
-            }
-        } else if (all) {   // final norm + output head over every token of the batch
+        if (all) {   // final norm + output head over every token of the batch
             const ActQ8 a_out = ub_act(hp.n_embd, nt, m->output.type);   // the head's own activation format
             launch_quant_act(xb, hp.n_embd, m->output_norm, hp.eps, a_out, stream);
             GemmParams p;
@@ -1638,13 +1623,42 @@ void Ctx::decode_ubatch(const int32_t* tokens, int n, bool all) {
                 TopkParams tp{logits, hp.n_vocab, cand, topk_ids, topk_vals, d_h_topk_ids, d_h_topk_vals};
                 launch_topk(tp, stream);
             }
-        } else {
-            if (short_b)   // the last residual parts into xb (the next chunk, or the output, reads it)
-                launch_part_sum(ub_spart, pend_k, nt, hp.n_embd, hp.n_embd, xb, hp.n_embd, xb, hp.n_embd, stream);
-            if (c0 + nt == n) enqueue_output(xb + (size_t)(nt - 1) * hp.n_embd, nullptr);
+        } else if (c0 + nt == n) {
+            enqueue_output(xb + (size_t)(nt - 1) * hp.n_embd, nullptr);
         }
     }
     logits_valid = true;
+}
+
+// One short physical batch (tokens uploaded to tokpos_b): embedding, the rope table, the layers on
+// mmqs, then the output -- every token's logits rows (`all`, rows c0.. of logits_all; the last
+// chunk's last row also feeds `logits` and the top-k) or the last token's through the decode head.
+void Ctx::enqueue_ubatch_short(int nt, bool all, int c0, bool last) {
+    const HParams& hp = m->hp;
+    const float theta_scale = std::pow(hp.rope_base, -2.0f / (float)hp.n_rot);
+    EmbedParams ep{m->tok_embd, tokpos_b, xb, hp.n_embd};
+    launch_embed_multi(ep, nt, stream);
+    launch_rope_table(tokpos_b, nt, hp.n_rot, theta_scale, hp.freq_scale, m->rope_freqs, ub_rope, stream);
+    const int pend_k = ubatch_layers_short(nt);
+    if (all) {   // final norm + output head on mmqs, its parts summed into the logits rows
+        const ActQ8 a_out = ub_act(hp.n_embd, nt, m->output.type);
+        launch_quant_act(xb, hp.n_embd, m->output_norm, hp.eps, a_out, stream, nullptr, ub_spart, pend_k);
+        const QMat* mo[1] = {&m->output};
+        const int pr[1] = {0};
+        const int kp = launch_mmqs(mo, pr, 1, false, 0, a_out, ub_spart, hp.n_vocab, stream);
+        launch_part_sum(ub_spart, kp, nt, hp.n_vocab, hp.n_vocab, nullptr, 0, logits_all + (size_t)c0 * hp.n_vocab,
+                        hp.n_vocab, stream);
+        if (last) {
+            MI_HIP(hipMemcpyAsync(logits, logits_all + (size_t)(c0 + nt - 1) * hp.n_vocab, (size_t)hp.n_vocab * sizeof(float),
+                                  hipMemcpyDeviceToDevice, stream));
+            TopkParams tp{logits, hp.n_vocab, cand, topk_ids, topk_vals, d_h_topk_ids, d_h_topk_vals};
+            launch_topk(tp, stream);
+        }
+    } else {
+        // the last residual parts into xb (the next chunk, or the output, reads it)
+        launch_part_sum(ub_spart, pend_k, nt, hp.n_embd, hp.n_embd, xb, hp.n_embd, xb, hp.n_embd, stream);
+        if (last) enqueue_output(xb + (size_t)(nt - 1) * hp.n_embd, nullptr);
+    }
 }
 
 // One short physical batch (<= mmqs_max tokens) through the layers on the split-K streaming GEMM

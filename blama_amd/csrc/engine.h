@@ -260,6 +260,7 @@ struct Ctx {
     // the layers of one short physical batch on mmqs; returns the residual parts still to add
     // into xb (pend_k parts of ub_spart)
     int ubatch_layers_short(int nt);
+    void enqueue_ubatch_short(int nt, bool all, int c0, bool last);
     ActQ8 ub_act(int K, int ntok, int type) const;   // the activation format `type`'s matrices read
     bool hp_dense() const { return m->hp.n_expert == 0; }
     // a second activation set (Q8_0) for a model mixing Q8_0 and k-quant matrices

@@ -1276,19 +1276,16 @@ __global__ __launch_bounds__(64) void mmqs1_t(const MsArgs M, const ActQ8 act) {
     float y[16];
 #pragma unroll
     for (int e = 0; e < 16; ++e) y[e] = 0.0f;
-    static_assert(DA % DW == 0 || DW % DA == 0, "ring depths");
-    constexpr int DM = DA > DW ? DA : DW;
-    for (int i = 0; i < nsb; i += DM) {
+    // fully unrolled over the part's (at most MS_SBW) superblocks: every ring slot is a value of its
+    // own, so a refill issued before the slot's dots needs no register copy
 #pragma unroll
-        for (int d = 0; d < DM; ++d) {
-            const int s = i + d;
-            if (s < nsb) {
-                const MsAct ca = a[d % DA];
-                const MsW<T> cw = w[d % DW];
-                if (s + DA < nsb) a[d % DA] = ms_act_load(act, sb0 + s + DA, lane);
-                if (s + DW < nsb) w[d % DW] = ms_load<T>(tile0 + (long long)(s + DW) * TB, lane);
-                ms1_sb<T>(cw, ca, lane, y);
-            }
+    for (int s = 0; s < MS_SBW; ++s) {
+        if (s < nsb) {
+            const MsAct ca = a[s % DA];
+            const MsW<T> cw = w[s % DW];
+            if (s + DA < nsb) a[s % DA] = ms_act_load(act, sb0 + s + DA, lane);
+            if (s + DW < nsb) w[s % DW] = ms_load<T>(tile0 + (long long)(s + DW) * TB, lane);
+            ms1_sb<T>(cw, ca, lane, y);
         }
     }
     const int rr = AB ? rt * 16 + (col & 15) : rt * 32 + col;
