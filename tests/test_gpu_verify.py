@@ -170,3 +170,33 @@ def test_long_prompt_batches_match_cpu_oracle(gpu_lib):
         err = float(np.max(np.abs(ctx.logits(row=i) - ref)))
         assert err <= LOGIT_TOL * rms or err <= 2 * floor[i + 1], (i, err / rms, floor[i + 1] / rms)
         assert int(ctx.topk(1, row=i)[0][0]) == int(np.argmax(ref)), i
+
+
+def test_short_tail_chunk_matches_cpu_oracle(gpu_lib):
+    """A call of 512 + k tokens: the 512-token physical batch on the tiled GEMM, the k-token tail
+    on the short-batch path (mmqs, its parts summed by the consumers), with MI_OUT_ALL rows 512..
+    written from the tail's own output head.  A 515-token prompt, then a 520-token verification
+    (rows 500..519 checked) against the C restatement of the CPU path, with
+    test_long_prompt_batches_match_cpu_oracle's bar."""
+    import ggml_cpu
+    cfg = synthetic.CONFIGS["tiny1-q4_k_m"]
+    buf = synthetic.build_gguf(cfg, seed=43)
+    m = engine.Model(buf)
+    rng = np.random.default_rng(14)
+    prompt = [int(t) for t in rng.integers(0, cfg.n_vocab, 515)]
+    claimed = [int(t) for t in rng.integers(0, cfg.n_vocab, 520)]
+    ctx = engine.Context(m, n_ctx=1100)
+    ctx.decode(prompt)
+    orc = ggml_cpu.Model(buf, n_ctx=1100)
+    ref = orc.decode(prompt)
+    orc.close()
+    assert _close(ctx.logits(), ref)
+    ctx.decode(claimed, all_logits=True)
+    base, floor = c_alt_floor(buf, 1100, prompt, claimed)
+    for i in range(500, len(claimed)):
+        ref = base[i + 1]
+        rms = float(np.sqrt(np.mean(ref ** 2)))
+        err = float(np.max(np.abs(ctx.logits(row=i) - ref)))
+        assert err <= LOGIT_TOL * rms or err <= 2 * floor[i + 1], (i, err / rms, floor[i + 1] / rms)
+        assert int(ctx.topk(1, row=i)[0][0]) == int(np.argmax(ref)), i
+    assert np.array_equal(ctx.logits(), ctx.logits(row=len(claimed) - 1))
