@@ -1710,11 +1710,20 @@ int Ctx::ubatch_layers_short(int nt) {
         // (20-token verify 3.52 -> 3.30 ms against the MFMA kernel's 32-token tiles; 64 tokens
         // equal, same box); MI_SHORT_ATTN_MFMA=1: the MFMA kernel
         static const bool mfma_env = getenv("MI_SHORT_ATTN_MFMA") != nullptr;
-        if (attn_mfma && (mfma_env || n_cells > ATTN_SHORT)) launch_attn_mfma(a, nt, attnb, stream);
-        else launch_attn_multi(a, nt, attnb, stream);
+        const ActQ8 act_wo = ub_act(hp.n_embd, nt, L.wo.type);
+        const bool qattn = attn_quant_supported(hp.n_head, hp.n_head_kv, hp.head_dim);
+        if (attn_mfma && (mfma_env || n_cells > ATTN_SHORT)) {
+            launch_attn_mfma(a, nt, attnb, stream);
+            launch_quant_act(attnb, hp.n_embd, nullptr, hp.eps, act_wo, stream);
+        } else if (qattn) {   // the fused kernel also quantises each token's output for W_o
+            a.act_q8 = act_wo;
+            launch_attn_multi(a, nt, attnb, stream);
+        } else {
+            launch_attn_multi(a, nt, attnb, stream);
+            launch_quant_act(attnb, hp.n_embd, nullptr, hp.eps, act_wo, stream);
+        }
         {   // output projection: parts of W_o attn, added to x by the FFN's quant_act
-            const ActQ8 act = ub_act(hp.n_embd, nt, L.wo.type);
-            launch_quant_act(attnb, hp.n_embd, nullptr, hp.eps, act, stream);
+            const ActQ8& act = act_wo;
             const QMat* mo[1] = {&L.wo};
             const int pr[1] = {0};
             pend_k = launch_mmqs(mo, pr, 1, false, 0, act, ub_spart, hp.n_embd, stream);

@@ -67,6 +67,15 @@ struct AttnPartials {
     int n_head, head_dim;
 };
 
+// Q8_K / Q8_0 activations of a physical batch (launch_quant_act; layout below)
+struct ActQ8 {
+    int8_t* q;                 // [npad/32][K/256][8][64][16]: MFMA A fragments (mmq.hip quant_act_kernel)
+    float* dT;                 // [K/256][npad]  (Q8_K d, token-minor)
+    int8_t* bsb;               // [npad/32][K/256][32][16]: sub-block bsums as 64*hi + lo (bytes 0-7 hi, 8-15 lo)
+    int K;
+    int ntok, npad;            // tokens; rows allocated (ntok rounded up to 32, <= UB_MAX)
+    int q80;                   // 1: Q8_0 activations (for Q8_0 weights): dT is [K/32][npad] f16-rounded d, no bsb
+};
 // ---- a quantised activation a decode launch publishes for the next one (the attention kernel for
 // the streaming WO launch) ----
 // Layout in global memory: act_layout(K, q8k, q80) of qdot.h (the Q8_K blocks, the Q8_0 blocks,
@@ -221,6 +230,8 @@ struct AttnParams {
     int long_off;                  // 1: never the single launch (an exchange timed out before)
     ActOut act_out;                // fused kernel, decode (act_out.act set): the output also quantised
                                    // (a workgroup serves whole 256-blocks of it: 256 / (R * hd) kv heads)
+    ActQ8 act_q8;                  // fused kernel, a short batch (act_q8.q set; launch_attn_multi): each
+                                   // token's output quantised in the batch GEMMs' format, same blocks
 };
 void launch_attn(const AttnParams& p, hipStream_t s);
 // a decode attention launch can also quantise its output (AttnParams::act_out) for this geometry
@@ -320,14 +331,6 @@ void launch_attn_mfma(const AttnParams& p, int ntok, float* out, hipStream_t s);
 // Prompt ingestion and batched verification: activations quantised to Q8_K once per matrix
 // input (launch_quant_act), then v_mfma_i32_32x32x32_i8 per sub-block (launch_mmq32).
 constexpr int UB_MAX = 512;    // n_ubatch (reference Instance.hpp:24)
-struct ActQ8 {
-    int8_t* q;                 // [npad/32][K/256][8][64][16]: MFMA A fragments (mmq.hip quant_act_kernel)
-    float* dT;                 // [K/256][npad]  (Q8_K d, token-minor)
-    int8_t* bsb;               // [npad/32][K/256][32][16]: sub-block bsums as 64*hi + lo (bytes 0-7 hi, 8-15 lo)
-    int K;
-    int ntok, npad;            // tokens; rows allocated (ntok rounded up to 32, <= UB_MAX)
-    int q80;                   // 1: Q8_0 activations (for Q8_0 weights): dT is [K/32][npad] f16-rounded d, no bsb
-};
 // rows (optional): token t of the batch reads row rows[t] of x (the tokens routed to one expert)
 // part (optional): the split-K partial sums of the GEMM that produced x (see GemmParams::ksplit):
 // x = ((p0 + p1) + ...) + x first, written back

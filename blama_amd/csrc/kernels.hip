@@ -1003,10 +1003,11 @@ __global__ __launch_bounds__(256 * HG) void attn_fused_kernel(const AttnParams P
         const int t = i / HD, d = i % HD;
         orow[(long long)(gq + t) * HD + d] = ((red_o[grp][0][t][d] + red_o[grp][1][t][d]) + red_o[grp][2][t][d]) + red_o[grp][3][t][d];
     }
-    if (P.act_out.act && gridDim.y == 1) {
+    if ((P.act_out.act && gridDim.y == 1) || P.act_q8.q) {
         // the WO launch's quantised activation: this workgroup's R * HG heads are whole 256-blocks
-        // (launch_attn checks), one wave per block; element e of the workgroup's span lies in
-        // group e / (R * HD), head (e / HD) % R
+        // (launch_attn / launch_attn_multi check), one wave per block; element e of the workgroup's
+        // span lies in group e / (R * HD), head (e / HD) % R.  A decode step writes act_layout
+        // (act_out); a short batch, token blockIdx.y's row of the batch GEMMs' format (act_q8)
         constexpr int NE = HG * R * HD;
         const int e0 = (int)blockIdx.x * HG * (P.qsplit ? 1 : R) * HD;
         const int gw = (int)threadIdx.x >> 6;
@@ -1017,7 +1018,8 @@ __global__ __launch_bounds__(256 * HG) void attn_fused_kernel(const AttnParams P
                 const int e = b * 256 + lane * 4 + k, gg = e / (R * HD), t = (e / HD) % R, d = e % HD;
                 v[k] = ((red_o[gg][0][t][d] + red_o[gg][1][t][d]) + red_o[gg][2][t][d]) + red_o[gg][3][t][d];
             }
-            dv_quant_block(P.act_out, e0 / 256 + b, v, lane);
+            if (P.act_q8.q) quant_actq8_block(P.act_q8, tok, e0 / 256 + b, v, lane);
+            else dv_quant_block(P.act_out, e0 / 256 + b, v, lane);
         }
     }
 #ifdef MI_STAMPS
@@ -1162,6 +1164,33 @@ void launch_attn_multi(const AttnParams& p_in, int ntok, float* out, hipStream_t
     p.fused = 1;
     if (ntok < 1) return;
     const int r = p.n_head / p.n_head_kv;
+    if (p.act_q8.q) {
+        // each token's output also quantised (a short batch's WO input): the decode step's
+        // quantising geometry, whole 256-blocks per workgroup, one grid row per token
+        const bool qs = r > 1 && p.n_head_kv < 16;
+        const int per = (qs ? 1 : r) * p.head_dim;
+        const int hg = per >= 256 ? 1 : 256 / per;
+        const int units = qs ? p.n_head : p.n_head_kv;
+        AttnFn f = nullptr;
+        if (hg == 1 && !qs) {
+            AttnFn fa = nullptr, fb = nullptr;
+            switch (r) {
+            case 1: attn_fns_r<1>(p.head_dim, fa, fb, f); break;
+            case 2: attn_fns_r<2>(p.head_dim, fa, fb, f); break;
+            case 4: attn_fns_r<4>(p.head_dim, fa, fb, f); break;
+            case 8: attn_fns_r<8>(p.head_dim, fa, fb, f); break;
+            default: break;
+            }
+        } else if (qs || r == 1) {
+            f = attn_fused_hg1(p.head_dim, hg);
+        }
+        if (!f || units % hg || per * hg % 256 || p.act_q8.K != p.n_head * p.head_dim || p.act_q8.ntok != ntok)
+            throw Error("attn: no quantising batch kernel for this head geometry");
+        p.qsplit = qs ? r : 0;
+        hipLaunchKernelGGL(f, dim3(units / hg, ntok), dim3(256 * hg), 0, s, p);
+        MI_HIP(hipGetLastError());
+        return;
+    }
     AttnFn fa = nullptr, fb = nullptr, ff = nullptr;
     switch (r) {
     case 1: attn_fns_r<1>(p.head_dim, fa, fb, ff); break;

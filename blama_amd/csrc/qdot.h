@@ -462,6 +462,63 @@ __device__ __forceinline__ void dv_quant_block(const ActOut& t, int b, const flo
                         reinterpret_cast<float*>(t.act + L.d0) + b * 8);
 }
 
+// Block blk (256 elements, 4 per lane: elements 4 lane..) of token row t of a physical batch's
+// activation, quantised as quantize_row_q8_K_ref (a.q80 = 0) or the x86 quantize_row_q8_0 (a.q80
+// = 1) and stored in the batch GEMMs' format (ActQ8: MFMA A fragments, token-minor d, byte-split
+// 32-element bsums) -- the arithmetic and layout of quant_act_kernel, shared with the attention
+// kernel that quantises a short batch's output itself.
+__device__ __forceinline__ void quant_actq8_block(const ActQ8& a, int t, int blk, const float v[4], int lane) {
+    const int nb = a.K >> 8;
+    const int tile = t >> 5, tr = t & 31;
+    const int fj = lane >> 3, fh = (lane >> 2) & 1, fw = lane & 3;
+    int8_t* q = a.q + (long long)tile * nb * 8192 + fj * 1024 + (fh * 32 + tr) * 16 + 4 * fw + (long long)blk * 8192;
+    if (a.q80) {
+        float am = fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3])));
+        am = fmaxf(am, __int_as_float(dpp_i<0xB1, 0xf>(__float_as_int(am))));
+        am = fmaxf(am, __int_as_float(dpp_i<0x4E, 0xf>(__float_as_int(am))));
+        am = fmaxf(am, __int_as_float(dpp_i<0x141, 0xf>(__float_as_int(am))));   // row_half_mirror
+        const float d0 = am / 127.0f;
+        const float id = am != 0.0f ? 127.0f / am : 0.0f;
+        int qz[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) qz[k] = (int)rintf(v[k] * id);
+        *reinterpret_cast<int*>(q) = (qz[0] & 0xFF) | ((qz[1] & 0xFF) << 8) | ((qz[2] & 0xFF) << 16) | ((qz[3] & 0xFF) << 24);
+        if ((lane & 7) == 0) a.dT[(long long)(blk * 8 + (lane >> 3)) * a.npad + t] = __half2float(__float2half_rn(d0));
+        return;
+    }
+    const float a0 = fabsf(v[0]), a1 = fabsf(v[1]), a2 = fabsf(v[2]), a3 = fabsf(v[3]);
+    const float amax = wave_max_pos(fmaxf(fmaxf(a0, a1), fmaxf(a2, a3)));
+    int qv[4];
+    float d;
+    if (amax == 0.0f) {
+        qv[0] = qv[1] = qv[2] = qv[3] = 0;
+        d = 0.0f;
+    } else {   // max = the signed value at the FIRST index whose |x| is the maximum
+        const int e = a0 == amax ? 0 : a1 == amax ? 1 : a2 == amax ? 2 : a3 == amax ? 3 : 4;
+        const float mine = e == 0 ? v[0] : e == 1 ? v[1] : e == 2 ? v[2] : v[3];
+        const unsigned long long m = __ballot(e < 4);
+        const int src = __builtin_ctzll(m);
+        const float mx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mine), src));
+        const float iscale = -127.0f / mx;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) qv[k] = min(127, (int)rintf(iscale * v[k]));
+        d = 1.0f / iscale;
+    }
+    *reinterpret_cast<int*>(q) = (qv[0] & 0xFF) | ((qv[1] & 0xFF) << 8) | ((qv[2] & 0xFF) << 16) | ((qv[3] & 0xFF) << 24);
+    // the 32-element sub-block sums: lanes 8j..8j+7
+    int sm = (qv[0] + qv[1]) + (qv[2] + qv[3]);
+    sm += dpp_i<0xB1, 0xf>(sm);    // quad_perm [1,0,3,2]
+    sm += dpp_i<0x4E, 0xf>(sm);    // quad_perm [2,3,0,1]
+    sm += __shfl_xor(sm, 4, 64);   // the two quads of a sub-block
+    if ((lane & 7) == 0) {
+        int8_t* bsb = a.bsb + ((long long)tile * nb * 32 + tr) * 16 + (long long)blk * 512;
+        const int j = lane >> 3;
+        bsb[j] = (int8_t)(sm >> 6);          // floor(b/64), -64..63
+        bsb[8 + j] = (int8_t)(sm & 63);      // b - 64*floor(b/64), 0..63
+    }
+    if (lane == 0) a.dT[(long long)blk * a.npad + t] = d;
+}
+
 __device__ __forceinline__ void unit_range(int total, int W, int gw, int& u0, int& u1) {
     // total * (gw + 1) < 2^32 (total <= 65536 units, W <= 4096 waves)
     u0 = (int)(((unsigned)total * (unsigned)gw) / (unsigned)W);
