@@ -385,7 +385,8 @@ def op_attention(q: np.ndarray, k16: np.ndarray, v16: np.ndarray, n_head_kv: int
 
 def op_gemm(type_: int, raw: np.ndarray, rows: int, K: int, x: np.ndarray, raw_up=None,
             device: int = 0) -> np.ndarray:
-    """Prompt-batch GEMM (mmq32) of x (ntok, K) f32 -> (ntok, rows); with raw_up the gate/up
+    """Prompt-batch GEMM (mmqs up to MI_MMQS_MAX tokens, mmq32 above) of x (ntok, K) f32 ->
+    (ntok, rows); with raw_up the gate/up
     SwiGLU pair silu(gate . x) * (up . x)."""
     raw = np.ascontiguousarray(raw, np.uint8)
     x = np.ascontiguousarray(x, np.float32)

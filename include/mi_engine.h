@@ -171,7 +171,8 @@ int32_t mi_op_topk(int32_t device, const float* logits, int32_t n, int32_t k, in
 int32_t mi_op_attention(int32_t device, int32_t n_head, int32_t n_head_kv, int32_t head_dim, int32_t n_cells,
                         const float* q, const uint16_t* k_f16, const uint16_t* v_f16, const int32_t* cell_pos,
                         int32_t pos, float* out);
-/* The prompt-batch GEMM (mmq32: int8 MFMA, Session.cpp:381-392's n_ubatch physical batches) of
+/* The prompt-batch GEMM (Session.cpp:381-392's n_ubatch physical batches; ntok <= MI_MMQS_MAX,
+ * default 64: the short-batch GEMM mmqs, otherwise the tiled int8-MFMA GEMM mmq32) of
  * ntok <= 512 token rows x[ntok][K] against a rows x K Q4_K / Q5_K / Q6_K / Q8_0 matrix: each row's
  * activation is quantised to Q8_K (Q8_0 for Q8_0 weights) as the CPU graph does, then
  * y[t][r] = vec_dot(W_r, q(x_t)).  With raw_up non-NULL the launch is the FFN gate/up pair
