@@ -664,13 +664,23 @@ Ctx::Ctx(Model* model, uint32_t nctx, uint32_t nbatch, uint32_t nubatch) : m(mod
             if (ksplit_env && mmq2_active())
                 MI_HIP(hipMalloc(&ub_part, (size_t)2 * UB_MAX * hp.n_embd * sizeof(float)));
             mmqs_max = getenv("MI_MMQS_MAX") ? std::min(MMQS_MAX, std::max(0, atoi(getenv("MI_MMQS_MAX")))) : MMQS_MAX;
-            if (mmqs_max > 0 && hp.n_expert == 0) {
+            // MoE: short batches when every expert matrix has the grouped form (k-quants)
+            moe_short = hp.n_expert > 0 && getenv("MI_MOE_SHORT_OFF") == nullptr;
+            for (const Layer& L : m->layers)
+                moe_short = moe_short && mmqs_grouped_supported(L.gate.type) && L.up.type == L.gate.type &&
+                            mmqs_grouped_supported(L.down.type);
+            if (mmqs_max > 0 && (hp.n_expert == 0 || moe_short)) {
                 const size_t qkv = (size_t)hp.n_embd + 2 * (size_t)kv_dim;
                 size_t per = std::max({(size_t)mmqs_parts(hp.n_embd) * std::max({qkv, (size_t)hp.n_embd, 2 * (size_t)hp.n_ff}),
                                        (size_t)mmqs_parts(hp.n_ff) * hp.n_embd});
                 if (out_mmq) per = std::max(per, (size_t)mmqs_parts(hp.n_embd) * hp.n_vocab);
-                MI_HIP(hipMalloc(&ub_spart, per * MMQS_MAX * sizeof(float)));
+                size_t tot = per * MMQS_MAX;
+                if (moe_short)   // the experts' parts over the MoE rows of MMQS_MAX tokens
+                    tot = std::max(tot, std::max((size_t)mmqs_parts(hp.n_embd) * 2 * hp.n_ff, (size_t)mmqs_parts(hp.n_ff) * hp.n_embd) *
+                                            (size_t)moe_rows_cap(MMQS_MAX * hp.n_expert_used, hp.n_expert));
+                MI_HIP(hipMalloc(&ub_spart, tot * sizeof(float)));
             } else {
+                moe_short = false;
                 mmqs_max = 0;
             }
         }
@@ -1448,6 +1458,41 @@ void Ctx::moe_ffn_batch(int l, int nt, const float* pend) {
     launch_moe_combine(yb, moe_pos, selw_b, xb, nt, hp.n_embd, stream);
 }
 
+// The same build_moe_ffn over a short batch (<= MMQS_MAX tokens; x already holds the residual) on
+// the grouped streaming GEMM: router, grouping, one quantisation of every MoE row, the experts'
+// gate/up pair parts (launch_mmqs_grouped: workgroups per (row tile, K-part, expert, 32-row tile),
+// each expert's matrix streamed once for the rows routed to it), SwiGLU of the parts quantised for
+// down, down's parts, their sum per row, then every token's x += w0*y0 + w1*y1 in slot order.
+void Ctx::moe_ffn_short(int l, int nt) {
+    const HParams& hp = m->hp;
+    const Layer& L = m->layers[l];
+    const int U = hp.n_expert_used, E = hp.n_expert;
+    RouterParams rp{xb, L.ffn_norm, hp.eps, L.router, hp.n_embd, E, U, sel_b, selw_b, hp.n_embd, nullptr, nt};
+    launch_router_multi(rp, nt, stream);
+    const int cap = moe_rows_cap(nt * U, E);
+    launch_moe_group(sel_b, nt * U, U, E, moe_grp, moe_rows, moe_rowsel, moe_pos, cap, stream);
+    auto act_of = [&](int K) {
+        ActQ8 a;
+        a.q = moe_q;
+        a.dT = moe_dT;
+        a.bsb = moe_bsb;
+        a.K = K;
+        a.ntok = cap;
+        a.npad = cap;
+        a.q80 = 0;
+        return a;
+    };
+    const ActQ8 act = act_of(hp.n_embd);
+    launch_quant_act(xb, hp.n_embd, L.ffn_norm, hp.eps, act, stream, moe_rows);
+    // an expert receives each token at most once: at most nt rows
+    const int kg = launch_mmqs_grouped(L.gate, true, hp.n_ff, act, ub_spart, 2 * hp.n_ff, moe_grp, E, nt, stream);
+    const ActQ8 a2 = act_of(hp.n_ff);
+    launch_quant_act(nullptr, hp.n_ff, nullptr, hp.eps, a2, stream, moe_rowsel, ub_spart, kg, 1);
+    const int kd = launch_mmqs_grouped(L.down, false, 0, a2, ub_spart, hp.n_embd, moe_grp, E, nt, stream);
+    launch_part_sum(ub_spart, kd, cap, hp.n_embd, hp.n_embd, nullptr, 0, yb, hp.n_embd, stream);
+    launch_moe_combine(yb, moe_pos, selw_b, xb, nt, hp.n_embd, stream);
+}
+
 ActQ8 Ctx::ub_act(int K, int ntok, int type) const {
     const bool q80 = type == T_Q8_0;
     const bool second = q80 && !ub_q80 && ub_q0;   // the Q8_0 set of a mixed model
@@ -1486,7 +1531,7 @@ void Ctx::decode_ubatch(const int32_t* tokens, int n, bool all) {
             pos_max = pos;
         }
         MI_HIP(hipMemcpyAsync(tokpos_b, hpos, nt * 4 * sizeof(int), hipMemcpyHostToDevice, stream));
-        if (mmqs_max > 0 && nt <= mmqs_max && hp_dense()) {   // a short batch (its launches captured as a
+        if (mmqs_max > 0 && nt <= mmqs_max && short_ok()) {   // a short batch (its launches captured as a
             // hipGraph measured no faster: the GPU, not the enqueue, sets the pace)
             enqueue_ubatch_short(nt, all, c0, c0 + nt == n);
             continue;
@@ -1642,7 +1687,8 @@ void Ctx::enqueue_ubatch_short(int nt, bool all, int c0, bool last) {
     const int pend_k = ubatch_layers_short(nt);
     if (all) {   // final norm + output head on mmqs, its parts summed into the logits rows
         const ActQ8 a_out = ub_act(hp.n_embd, nt, m->output.type);
-        launch_quant_act(xb, hp.n_embd, m->output_norm, hp.eps, a_out, stream, nullptr, ub_spart, pend_k);
+        launch_quant_act(xb, hp.n_embd, m->output_norm, hp.eps, a_out, stream, nullptr, pend_k ? ub_spart : nullptr,
+                         pend_k ? pend_k : 2);
         const QMat* mo[1] = {&m->output};
         const int pr[1] = {0};
         const int kp = launch_mmqs(mo, pr, 1, false, 0, a_out, ub_spart, hp.n_vocab, stream);
@@ -1656,7 +1702,7 @@ void Ctx::enqueue_ubatch_short(int nt, bool all, int c0, bool last) {
         }
     } else {
         // the last residual parts into xb (the next chunk, or the output, reads it)
-        launch_part_sum(ub_spart, pend_k, nt, hp.n_embd, hp.n_embd, xb, hp.n_embd, xb, hp.n_embd, stream);
+        if (pend_k) launch_part_sum(ub_spart, pend_k, nt, hp.n_embd, hp.n_embd, xb, hp.n_embd, xb, hp.n_embd, stream);
         if (last) enqueue_output(xb + (size_t)(nt - 1) * hp.n_embd, nullptr);
     }
 }
@@ -1727,6 +1773,14 @@ int Ctx::ubatch_layers_short(int nt) {
             const QMat* mo[1] = {&L.wo};
             const int pr[1] = {0};
             pend_k = launch_mmqs(mo, pr, 1, false, 0, act, ub_spart, hp.n_embd, stream);
+        }
+        if (hp.n_expert > 0) {   // routed experts: x += W_o parts first (the router reads x)
+            launch_part_sum(ub_spart, pend_k, nt, hp.n_embd, hp.n_embd, xb, hp.n_embd, xb, hp.n_embd, stream);
+            pend_k = 0;
+            static const bool moe_tile_env = getenv("MI_MOE_SHORT_TILE") != nullptr;   // (diagnostic: tiled experts)
+            if (moe_tile_env) moe_ffn_batch(l, nt);
+            else moe_ffn_short(l, nt);
+            continue;
         }
         {   // FFN gate/up: parts of both, SwiGLU'd by the down input's quant_act
             const ActQ8 act = ub_act(hp.n_embd, nt, L.gate.type);

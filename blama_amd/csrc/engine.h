@@ -280,6 +280,10 @@ struct Ctx {
     float* moe_dT = nullptr;
     int8_t* moe_bsb = nullptr;
     void moe_ffn_batch(int l, int nt, const float* pend = nullptr);
+    // a short MoE batch's routed experts on the grouped mmqs (every expert matrix a k-quant)
+    void moe_ffn_short(int l, int nt);
+    bool moe_short = false;
+    bool short_ok() const { return hp_dense() || moe_short; }
     const float* out_row(int row) const;   // device logits of output row `row` (-1: the last)
     hipGraphExec_t build_graph(bool with_logits, int seg);
     void invalidate_graphs();

@@ -367,6 +367,13 @@ constexpr int MMQS_MAX = 64;
 int mmqs_parts(int K);
 int launch_mmqs(const QMat* const* mats, const int* prow, int n, bool pair, int nff, const ActQ8& act, float* part,
                 int pstride, hipStream_t s);
+// The routed experts of a short MoE batch (build_moe_ffn's mul_mat_id): act holds the MoE rows
+// (moe_group_kernel: expert e's at [grp[e], + grp[n_expert + 1 + e]), whole 32-row tiles, at most
+// max_rows each), and expert e's rows multiply its own matrix; the parts go to
+// part[kp][act.ntok][pstride] at the same rows (a pair: up rows from nff).  Returns kp.
+bool mmqs_grouped_supported(int type);
+int launch_mmqs_grouped(const QMat& A, bool pair, int nff, const ActQ8& act, float* part, int pstride, const int* grp,
+                        int n_expert, int max_rows, hipStream_t s);
 // Q / K / V from the parts of their GEMMs (rows [Q | K | V] of part): RoPE NORM of Q and K (the
 // batch's rope table), Q -> q [ntok][q_stride], K / V -> the f16 caches at the tokens' cells
 struct QkvFinish {

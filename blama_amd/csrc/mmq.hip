@@ -865,8 +865,15 @@ struct MsArgs {
     int kp;                        // K-parts (grid = row blocks x kp)
     int sbw;                       // superblocks per K-part (<= MS_SBW)
     int nff;                       // pair launches: the up rows' offset in the partial row space
-    float* part;                   // [kp][ntok][pstride]
+    float* part;                   // [kp][prows][pstride]
     int pstride;
+    int prows;                     // rows of one part: the batch's tokens (grouped: the MoE rows)
+    // grouped (MoE, mmqs1 only): blockIdx.y = expert e, whose rows [grp[e], + grp[grp_n + 1 + e])
+    // of the activation (whole 32-row tiles, moe_group_kernel) read expert e's copy at
+    // sw[0] + e * grp_stride; blockIdx.z = the 32-row tile within the expert
+    const int* grp;
+    int grp_n;
+    long long grp_stride;
 };
 // 16-B weight loads per superblock of a row tile (NV) and the wave's ring depth (D)
 template <int T> struct MsT;
@@ -1245,14 +1252,31 @@ __device__ __forceinline__ void ms1_sb(const MsW<T>& w, const MsAct& A, int lane
 template <int T> struct Ms1D { static constexpr int DW = 2, DA = 2; };
 template <> struct Ms1D<T_Q6_K> { static constexpr int DW = 1, DA = 2; };
 
-template <int T, bool AB>
-__global__ __launch_bounds__(64) void mmqs1_t(const MsArgs M, const ActQ8 act) {
+template <int T, bool AB, bool G>
+__global__ __launch_bounds__(64) void mmqs1_t(const MsArgs M, const ActQ8 act_in) {
     constexpr int DW = Ms1D<T>::DW, DA = Ms1D<T>::DA;
     const int lane = threadIdx.x & 63;
     const int col = lane & 31, h = lane >> 5;
-    const int nb = act.K >> 8;
+    const int nb = act_in.K >> 8;
     const int kp = (int)blockIdx.x % M.kp, g = (int)blockIdx.x / M.kp;
     const int sb0 = kp * M.sbw, nsb = min(M.sbw, nb - sb0);
+    // this workgroup's token rows: [r0, r0 + ntk) of the partial row space, read from the
+    // activation's 32-row tile r0 / 32 (grouped: expert e's tile z; exits past its rows)
+    ActQ8 act = act_in;
+    int r0 = 0, ntk = act_in.ntok;
+    long long eoff = 0;
+    if (G) {
+        const int e = blockIdx.y, z = blockIdx.z;
+        const int cnt = M.grp[M.grp_n + 1 + e];
+        if (z * 32 >= cnt) return;
+        r0 = M.grp[e] + z * 32;
+        ntk = min(32, cnt - z * 32);
+        const int tt = r0 >> 5;
+        act.q += (long long)tt * nb * 8192;
+        act.bsb += (long long)tt * nb * 512;
+        act.dT += tt * 32;
+        eoff = (long long)e * M.grp_stride;
+    }
     int seg = 0, rt = g;
 #pragma unroll
     for (int i = 0; i < MMQ_SEGS - 1; ++i)
@@ -1264,7 +1288,7 @@ __global__ __launch_bounds__(64) void mmqs1_t(const MsArgs M, const ActQ8 act) {
     const int rows_s = seg == 0 ? M.rows[0] : seg == 1 ? M.rows[1] : M.rows[2];
     const int prow_s = seg == 0 ? M.prow[0] : seg == 1 ? M.prow[1] : M.prow[2];
     constexpr int TB = mmq32_tile_bytes_d(T);
-    const uint8_t* tile0 = swA + ((long long)rt * nb + sb0) * TB;
+    const uint8_t* tile0 = swA + eoff + ((long long)rt * nb + sb0) * TB;
     // activation first, then weights (loads retire in order: superblock 0's act is never queued
     // behind later weights)
     MsAct a[DA];
@@ -1294,7 +1318,7 @@ __global__ __launch_bounds__(64) void mmqs1_t(const MsArgs M, const ActQ8 act) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
         const int tok = (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (tok < act.ntok) M.part[((long long)kp * act.ntok + tok) * M.pstride + prow] = y[r];
+        if (tok < ntk) M.part[((long long)kp * M.prows + r0 + tok) * M.pstride + prow] = y[r];
     }
 }
 
@@ -1352,10 +1376,11 @@ template <int T, int NST> constexpr int m2_lds() { return M2<T>::lds(NST); }
 void launch_quant_act(const float* x, int x_stride, const float* norm_w, float eps, const ActQ8& a, hipStream_t s,
                       const int* rows, const float* part, int nks, int swiglu) {
     if (part && (nks < 1 || nks > 64)) throw Error("quant_act: 1..64 split-K partials");
-    if (swiglu && (!part || rows || norm_w)) throw Error("quant_act: swiglu takes a pair launch's parts, no rows or norm");
+    // (swiglu with rows: the MoE rows of a grouped pair launch, rows[t] < 0 marking padding rows)
+    if (swiglu && (!part || norm_w)) throw Error("quant_act: swiglu takes a pair launch's parts, no norm");
     if (!swiglu && !x) throw Error("quant_act: no input rows");
     if (a.K % 256) throw Error("quant_act: K must be a multiple of 256");
-    if (part && (rows || x_stride != a.K)) throw Error("quant_act: split-K partials take a dense [ntok][K] x");
+    if (part && !swiglu && (rows || x_stride != a.K)) throw Error("quant_act: split-K partials take a dense [ntok][K] x");
     // (more than UB_MAX rows only for the MoE rows of a batch: one per (token, slot), padded)
     if (a.npad % 32 || a.ntok > a.npad || a.npad > 4 * UB_MAX) throw Error("quant_act: bad token count");
     if (a.K > 65536) throw Error("quant_act: K past 65536");
@@ -1529,17 +1554,18 @@ int launch_mmqs(const QMat* const* mats, const int* prow, int n, bool pair, int 
     M.nff = nff;
     M.part = part;
     M.pstride = pstride;
+    M.prows = act.ntok;
     const int NT = act.npad / 32;
     const int KQ = T != T_Q8_0;
     const int lds = mmq::MS_SBW * NT * 8192 + (KQ ? mmq::MS_SBW * NT * 1024 + mmq::MS_SBW * 256 : mmq::MS_SBW * 8 * 256);
     // one token tile, k-quants: the one-wave register form (MI_MMQS1=0: the LDS form)
     static const bool ms1_env = getenv("MI_MMQS1") == nullptr || atoi(getenv("MI_MMQS1")) != 0;
     if (ms1_env && NT == 1 && T != T_Q8_0) {
-        decltype(&mmq::mmqs1_t<T_Q4_K, false>) f1 = nullptr;
+        decltype(&mmq::mmqs1_t<T_Q4_K, false, false>) f1 = nullptr;
         switch (T) {
-        case T_Q4_K: f1 = pair ? mmq::mmqs1_t<T_Q4_K, true> : mmq::mmqs1_t<T_Q4_K, false>; break;
-        case T_Q5_K: f1 = pair ? mmq::mmqs1_t<T_Q5_K, true> : mmq::mmqs1_t<T_Q5_K, false>; break;
-        default: f1 = pair ? mmq::mmqs1_t<T_Q6_K, true> : mmq::mmqs1_t<T_Q6_K, false>; break;
+        case T_Q4_K: f1 = pair ? mmq::mmqs1_t<T_Q4_K, true, false> : mmq::mmqs1_t<T_Q4_K, false, false>; break;
+        case T_Q5_K: f1 = pair ? mmq::mmqs1_t<T_Q5_K, true, false> : mmq::mmqs1_t<T_Q5_K, false, false>; break;
+        default: f1 = pair ? mmq::mmqs1_t<T_Q6_K, true, false> : mmq::mmqs1_t<T_Q6_K, false, false>; break;
         }
         hipLaunchKernelGGL(f1, dim3(M.nrt_tot * M.kp), dim3(64), 0, s, M, act);
         MI_HIP(hipGetLastError());
@@ -1564,6 +1590,44 @@ int launch_mmqs(const QMat* const* mats, const int* prow, int n, bool pair, int 
     }
     const int grid = (M.nrt_tot + mmq::MS_NW - 1) / mmq::MS_NW * M.kp;
     hipLaunchKernelGGL(f, dim3(grid), dim3(64 * mmq::MS_NW), (size_t)lds, s, M, act);
+    MI_HIP(hipGetLastError());
+    return M.kp;
+}
+
+bool mmqs_grouped_supported(int type) { return type == T_Q4_K || type == T_Q5_K || type == T_Q6_K; }
+
+int launch_mmqs_grouped(const QMat& A, bool pair, int nff, const ActQ8& act, float* part, int pstride, const int* grp,
+                        int n_expert, int max_rows, hipStream_t s) {
+    const int T = A.type;
+    if (!mmqs_grouped_supported(T)) throw Error("mmqs grouped: Q4_K / Q5_K / Q6_K experts only");
+    if (act.q80) throw Error("mmqs grouped: k-quant experts take Q8_K activations");
+    if (!A.sw || A.K != act.K || act.K % 256 || act.K <= 0) throw Error("mmqs grouped: the experts' MFMA-order copies, K a multiple of 256");
+    if (act.ntok != act.npad || act.npad % 32 || act.npad < 32) throw Error("mmqs grouped: the MoE rows are whole 32-row tiles");
+    if (n_expert < 1 || n_expert > A.n_exp || max_rows < 1 || max_rows > MMQS_MAX) throw Error("mmqs grouped: bad expert / row count");
+    if (A.rows + (pair ? nff : 0) > pstride || (pair && nff < A.rows)) throw Error("mmqs grouped: partial rows past the stride");
+    mmq::MsArgs M{};
+    M.n = 1;
+    M.sw[0] = A.sw;
+    M.rows[0] = A.rows;
+    M.nrt[0] = M.nrt_tot = pair ? (A.rows + 15) / 16 : (A.rows + 31) / 32;
+    M.prow[0] = 0;
+    M.sbw = mmq::MS_SBW;
+    M.kp = mmqs_parts(act.K);
+    M.nff = nff;
+    M.part = part;
+    M.pstride = pstride;
+    M.prows = act.ntok;
+    M.grp = grp;
+    M.grp_n = n_expert;
+    M.grp_stride = A.sw_expert_stride;
+    decltype(&mmq::mmqs1_t<T_Q4_K, false, true>) f1 = nullptr;
+    switch (T) {
+    case T_Q4_K: f1 = pair ? mmq::mmqs1_t<T_Q4_K, true, true> : mmq::mmqs1_t<T_Q4_K, false, true>; break;
+    case T_Q5_K: f1 = pair ? mmq::mmqs1_t<T_Q5_K, true, true> : mmq::mmqs1_t<T_Q5_K, false, true>; break;
+    default: f1 = pair ? mmq::mmqs1_t<T_Q6_K, true, true> : mmq::mmqs1_t<T_Q6_K, false, true>; break;
+    }
+    // an expert holds at most max_rows rows (one per token routed to it): ceil(max_rows / 32) tiles
+    hipLaunchKernelGGL(f1, dim3(M.nrt_tot * M.kp, n_expert, (max_rows + 31) / 32), dim3(64), 0, s, M, act);
     MI_HIP(hipGetLastError());
     return M.kp;
 }

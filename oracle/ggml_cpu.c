@@ -447,7 +447,14 @@ static void trace(const char* what, int l, const float* v, int n) {
 }
 
 /* one llama_decode of `token` at position max(cell_pos)+1; logits -> out[n_vocab] */
+/* Test diagnostics: over the MoE layers of the last orc_decode, the smallest gap between the
+ * router probability of the last expert picked and the best one left out (INFINITY: dense).  A
+ * gap near zero is a routing near-tie, which any other fp32 order may resolve the other way. */
+static float g_moe_margin = INFINITY;
+float orc_last_moe_margin(void) { return g_moe_margin; }
+
 int orc_decode(orc_model* m, int token, float* out) {
+    g_moe_margin = INFINITY;
     const orc_hparams* hp = &m->hp;
     const int d = hp->n_embd, hd = d / hp->n_head, kvd = hp->n_head_kv * hd, ff = hp->n_ff;
     if (m->n_cells >= m->n_ctx) return 1;
@@ -536,6 +543,8 @@ int orc_decode(orc_model* m, int token, float* out) {
             for (int a = 0; a < hp->n_expert; ++a)
                 for (int b = a + 1; b < hp->n_expert; ++b)
                     if (pr[idx[a]] < pr[idx[b]]) { int t = idx[a]; idx[a] = idx[b]; idx[b] = t; }
+            if (hp->n_expert_used < hp->n_expert)   /* the last pick's lead over the first expert left out */
+                g_moe_margin = fminf(g_moe_margin, pr[idx[hp->n_expert_used - 1]] - pr[idx[hp->n_expert_used]]);
             float ws = 0;
             for (int kk = 0; kk < hp->n_expert_used; ++kk) ws += pr[idx[kk]];
             for (int i = 0; i < d; ++i) acc[i] = 0;

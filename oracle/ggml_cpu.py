@@ -38,6 +38,7 @@ def lib():
         L.orc_kv_clear.argtypes = [C.c_void_p]
         L.orc_n_threads.restype = C.c_int
         L.orc_set_alt.argtypes = [C.c_int]
+        L.orc_last_moe_margin.restype = C.c_float
         _lib = L
     return _lib
 
@@ -93,6 +94,8 @@ class Model:
             lib().orc_set_alt(0)
         if rc != 0:
             raise RuntimeError("orc_decode: no KV space")
+        # the smallest router gap (last pick vs first left out) over this token's MoE layers
+        self.last_moe_margin = float(lib().orc_last_moe_margin())
         return out
 
     def reset(self):

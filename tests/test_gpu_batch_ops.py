@@ -142,6 +142,7 @@ MMQS_CASES = [
     (R.Q4_K, 11008, 4096, (20, 64), True),
     (R.Q4_K, 4096, 11008, (20, 64), False),
     (R.Q5_K, 4096, 14336, (24,), False),
+    (R.Q5_K, 4096, 4096, (64,), False),     # Mixtral's Q / W_o at 64 tokens: two token tiles
     (R.Q5_K, 1000, 4096, (40,), True),
     (R.Q6_K, 4096, 11008, (20, 64), False),
     (R.Q6_K, 1000, 4096, (33,), True),

@@ -45,6 +45,9 @@ pytestmark = pytest.mark.gpu
 
 TOL_MAX = 0.12
 TOL_L2 = 0.03
+# MoE: router probabilities of the last expert picked and the first left out closer than this
+# (in the oracle) are a near-tie that another fp32 order of the same arithmetic may swap
+ROUTE_TIE = 0.01
 
 FULL = {
     "llama2-7b-q4_k_m": dict(n_layer=2),
@@ -217,22 +220,39 @@ def test_fullwidth_batched_verification_matches_oracle(gpu_lib, name):
         orc.close()
 
 
-@pytest.mark.parametrize("name", ["llama2-7b-q4_k_m", "llama3-8b-q6_k", "tinyllama-1.1b-q8_0"])
+@pytest.mark.parametrize("name", ["llama2-7b-q4_k_m", "llama3-8b-q6_k", "tinyllama-1.1b-q8_0",
+                                  "mixtral-8x7b-q5_k_m-ff14336"])
 def test_fullwidth_short_batches_match_tiled_gemm(gpu_lib, monkeypatch, name):
     """Short verification batches (20 and 64 claimed tokens) on the split-K streaming GEMM
-    (mmqs: K-parts summed by the consumer kernels) against the same batches on the tiled GEMM
+    (mmqs: K-parts summed by the consumer kernels; Mixtral: the routed experts on the grouped
+    form, each expert's rows over its own matrix) against the same batches on the tiled GEMM
     (mmq2, MI_MMQS_MAX=0).  Per matrix the two agree to the GEMM op bar (test_gpu_batch_ops:
     the same integer sub-block sums, only the fp32 order of the K-parts differs); through the
     layers such differences flip Q8_K roundings of the next activation the way any fp32 order
     does -- on these random-weight models every batch path (and the per-token path) sits 4-7 % of
     rms from the C oracle at its worst element (scripts/diag_short.py) -- so the two paths are
     held to this file's bars against each other, with top-1 equal unless within twice the row's
-    largest difference of a tie; the KV cache each batch wrote serves the next step alike."""
+    largest difference of a tie; the KV cache each batch wrote serves the next step alike.
+    Mixtral: a row may differ beyond the bars only where the oracle's router separates the last
+    expert picked from the first left out by less than ROUTE_TIE (the same noise then picks a
+    different expert: measured on this model at 64 tokens, row 60, last layer, gap 0.0037),
+    at most 2 rows per batch, each printed as a waiver."""
     cfg, buf, m = full_model(name)
     rng = np.random.default_rng(21)
     prompt = [int(t) for t in rng.integers(0, cfg.n_vocab, 12)]
     for n_claim in (20, 64):
         claimed = [int(t) for t in rng.integers(0, cfg.n_vocab, n_claim)]
+        margins = [np.inf] * n_claim
+        if cfg.n_expert:   # the oracle's router gap per claimed token (routing near-ties, below)
+            orc = ggml_cpu.Model(buf, n_ctx=128)
+            try:
+                for t in prompt:
+                    orc.decode_one(t)
+                for i, t in enumerate(claimed):
+                    orc.decode_one(t)
+                    margins[i] = orc.last_moe_margin
+            finally:
+                orc.close()
         outs = []
         for mode in ("64", "0"):
             monkeypatch.setenv("MI_MMQS_MAX", mode)
@@ -246,9 +266,21 @@ def test_fullwidth_short_batches_match_tiled_gemm(gpu_lib, monkeypatch, name):
                 outs.append(rows)
             finally:
                 ctx.close()
+        flips = []
         for i, (a, b) in enumerate(zip(*outs)):
             dmax, rmax, rl2 = _err(a, b)
-            assert rmax <= TOL_MAX and rl2 <= TOL_L2, (name, n_claim, i, rmax, rl2)
+            if i < n_claim and margins[i] < ROUTE_TIE and not (rmax <= TOL_MAX and rl2 <= TOL_L2):
+                # a routing near-tie: the two paths' activations differ by the usual Q8_K
+                # re-quantisation noise, enough to swap two experts whose router probabilities
+                # the oracle separates by less than ROUTE_TIE -- a different expert, a different row
+                flips.append((i, margins[i], rmax))
+                continue
+            assert rmax <= TOL_MAX and rl2 <= TOL_L2, (name, n_claim, i, rmax, rl2, margins[min(i, n_claim - 1)])
             ia, ib = int(np.argmax(a)), int(np.argmax(b))
             assert ia == ib or b[ib] - b[ia] <= 2 * dmax, (name, n_claim, i, ia, ib)
+        if flips:
+            msg = f"routing near-tie waiver: {name} {n_claim} tokens: (row, oracle router gap, max/rms) {flips}"
+            print(msg)
+            warnings.warn(msg)
+        assert len(flips) <= 2, flips
     monkeypatch.delenv("MI_MMQS_MAX")
