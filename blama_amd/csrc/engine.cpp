@@ -1777,9 +1777,7 @@ int Ctx::ubatch_layers_short(int nt) {
         if (hp.n_expert > 0) {   // routed experts: x += W_o parts first (the router reads x)
             launch_part_sum(ub_spart, pend_k, nt, hp.n_embd, hp.n_embd, xb, hp.n_embd, xb, hp.n_embd, stream);
             pend_k = 0;
-            static const bool moe_tile_env = getenv("MI_MOE_SHORT_TILE") != nullptr;   // (diagnostic: tiled experts)
-            if (moe_tile_env) moe_ffn_batch(l, nt);
-            else moe_ffn_short(l, nt);
+            moe_ffn_short(l, nt);
             continue;
         }
         {   // FFN gate/up: parts of both, SwiGLU'd by the down input's quant_act

@@ -1,4 +1,4 @@
-"""One short verification leg on the synthetic Llama-2-7B Q4_K_M (bench.py's verify_short shape:
+"""One short verification leg on the synthetic Llama-2-7B Q4_K_M (SHORT_CFG: another config) (bench.py's verify_short shape:
 a 32-token prompt, then `n` claimed tokens in one MI_OUT_ALL pass), printing progress -- a small
 program for counter passes (rocprofv3 --pmc) of the short-batch kernels."""
 import os
@@ -12,7 +12,7 @@ from blama_amd import engine, synthetic  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 20
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 2
-cfg = synthetic.CONFIGS["llama2-7b-q4_k_m"]
+cfg = synthetic.CONFIGS[os.environ.get("SHORT_CFG", "llama2-7b-q4_k_m")]
 t0 = time.time()
 m = engine.Model(synthetic.build_gguf(cfg, seed=1))
 print(f"model loaded {time.time() - t0:.1f}s", flush=True)
