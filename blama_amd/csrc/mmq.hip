@@ -1252,9 +1252,10 @@ __device__ __forceinline__ void ms1_sb(const MsW<T>& w, const MsAct& A, int lane
 template <int T> struct Ms1D { static constexpr int DW = 2, DA = 2; };
 template <> struct Ms1D<T_Q6_K> { static constexpr int DW = 1, DA = 2; };
 
-template <int T, bool AB, bool G>
-__global__ __launch_bounds__(64) void mmqs1_t(const MsArgs M, const ActQ8 act_in) {
-    constexpr int DW = Ms1D<T>::DW, DA = Ms1D<T>::DA;
+// LEAN: one-deep rings, sized for two waves per SIMD (mmqs1_lean_t)
+template <int T, bool AB, bool G, bool LEAN>
+__device__ __forceinline__ void mmqs1_body(const MsArgs& M, const ActQ8& act_in) {
+    constexpr int DW = LEAN ? 1 : Ms1D<T>::DW, DA = LEAN ? 1 : Ms1D<T>::DA;
     const int lane = threadIdx.x & 63;
     const int col = lane & 31, h = lane >> 5;
     const int nb = act_in.K >> 8;
@@ -1321,6 +1322,10 @@ __global__ __launch_bounds__(64) void mmqs1_t(const MsArgs M, const ActQ8 act_in
         if (tok < ntk) M.part[((long long)kp * M.prows + r0 + tok) * M.pstride + prow] = y[r];
     }
 }
+template <int T, bool AB, bool G>
+__global__ __launch_bounds__(64) void mmqs1_t(const MsArgs M, const ActQ8 act) { mmqs1_body<T, AB, G, false>(M, act); }
+template <int T, bool AB, bool G>
+__global__ __launch_bounds__(64, 2) void mmqs1_lean_t(const MsArgs M, const ActQ8 act) { mmqs1_body<T, AB, G, true>(M, act); }
 
 // the sum of the K-parts in part order, with the consumer's epilogue: Q / K RoPE (ggml NORM, the
 // rope table of the batch), Q to q, K / V to the f16 caches (and the cell positions)
@@ -1523,6 +1528,15 @@ void launch_mmq32(const GemmParams& p, const ActQ8& act, const float2* rope, hip
     launch_mmq2(p, S, act, rope, s);
 }
 
+// The Q4_K / Q5_K mmqs1 launches on the one-deep-ring, two-waves-per-SIMD form (214-220 VGPRs
+// instead of 246-256 at one wave: 20-token verify 7B 3.61 -> 3.40 ms, Mixtral 18.2 -> 15.7 ms,
+// same box, scripts/r05_lean.sh); MI_MMQS1_LEAN=0: the two-deep rings at one wave per SIMD.  Q6_K
+// keeps its ring (the lean form at two waves spills).
+static bool mmqs1_lean() {
+    static const bool on = getenv("MI_MMQS1_LEAN") == nullptr || atoi(getenv("MI_MMQS1_LEAN")) != 0;
+    return on;
+}
+
 int mmqs_parts(int K) { return (K / 256 + mmq::MS_SBW - 1) / mmq::MS_SBW; }
 
 int launch_mmqs(const QMat* const* mats, const int* prow, int n, bool pair, int nff, const ActQ8& act, float* part,
@@ -1560,11 +1574,14 @@ int launch_mmqs(const QMat* const* mats, const int* prow, int n, bool pair, int 
     const int lds = mmq::MS_SBW * NT * 8192 + (KQ ? mmq::MS_SBW * NT * 1024 + mmq::MS_SBW * 256 : mmq::MS_SBW * 8 * 256);
     // one token tile, k-quants: the one-wave register form (MI_MMQS1=0: the LDS form)
     static const bool ms1_env = getenv("MI_MMQS1") == nullptr || atoi(getenv("MI_MMQS1")) != 0;
+    const bool lean = mmqs1_lean();
     if (ms1_env && NT == 1 && T != T_Q8_0) {
         decltype(&mmq::mmqs1_t<T_Q4_K, false, false>) f1 = nullptr;
         switch (T) {
-        case T_Q4_K: f1 = pair ? mmq::mmqs1_t<T_Q4_K, true, false> : mmq::mmqs1_t<T_Q4_K, false, false>; break;
-        case T_Q5_K: f1 = pair ? mmq::mmqs1_t<T_Q5_K, true, false> : mmq::mmqs1_t<T_Q5_K, false, false>; break;
+        case T_Q4_K: f1 = lean ? (pair ? mmq::mmqs1_lean_t<T_Q4_K, true, false> : mmq::mmqs1_lean_t<T_Q4_K, false, false>)
+                           : (pair ? mmq::mmqs1_t<T_Q4_K, true, false> : mmq::mmqs1_t<T_Q4_K, false, false>); break;
+        case T_Q5_K: f1 = lean ? (pair ? mmq::mmqs1_lean_t<T_Q5_K, true, false> : mmq::mmqs1_lean_t<T_Q5_K, false, false>)
+                           : (pair ? mmq::mmqs1_t<T_Q5_K, true, false> : mmq::mmqs1_t<T_Q5_K, false, false>); break;
         default: f1 = pair ? mmq::mmqs1_t<T_Q6_K, true, false> : mmq::mmqs1_t<T_Q6_K, false, false>; break;
         }
         hipLaunchKernelGGL(f1, dim3(M.nrt_tot * M.kp), dim3(64), 0, s, M, act);
@@ -1620,10 +1637,13 @@ int launch_mmqs_grouped(const QMat& A, bool pair, int nff, const ActQ8& act, flo
     M.grp = grp;
     M.grp_n = n_expert;
     M.grp_stride = A.sw_expert_stride;
+    const bool lean = mmqs1_lean();
     decltype(&mmq::mmqs1_t<T_Q4_K, false, true>) f1 = nullptr;
     switch (T) {
-    case T_Q4_K: f1 = pair ? mmq::mmqs1_t<T_Q4_K, true, true> : mmq::mmqs1_t<T_Q4_K, false, true>; break;
-    case T_Q5_K: f1 = pair ? mmq::mmqs1_t<T_Q5_K, true, true> : mmq::mmqs1_t<T_Q5_K, false, true>; break;
+    case T_Q4_K: f1 = lean ? (pair ? mmq::mmqs1_lean_t<T_Q4_K, true, true> : mmq::mmqs1_lean_t<T_Q4_K, false, true>)
+                       : (pair ? mmq::mmqs1_t<T_Q4_K, true, true> : mmq::mmqs1_t<T_Q4_K, false, true>); break;
+    case T_Q5_K: f1 = lean ? (pair ? mmq::mmqs1_lean_t<T_Q5_K, true, true> : mmq::mmqs1_lean_t<T_Q5_K, false, true>)
+                       : (pair ? mmq::mmqs1_t<T_Q5_K, true, true> : mmq::mmqs1_t<T_Q5_K, false, true>); break;
     default: f1 = pair ? mmq::mmqs1_t<T_Q6_K, true, true> : mmq::mmqs1_t<T_Q6_K, false, true>; break;
     }
     // an expert holds at most max_rows rows (one per token routed to it): ceil(max_rows / 32) tiles
