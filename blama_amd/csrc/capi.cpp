@@ -504,7 +504,16 @@ int32_t mi_prof_read(mi_ctx* c, float* us, int32_t n) {
 int64_t mi_prof_ffn_bytes(const mi_ctx* c) { return c ? c->impl->ffn_bytes() : -1; }
 int64_t mi_prof_bytes(const mi_ctx* c) { return c ? c->impl->prof_bytes : -1; }
 
-int32_t mi_decode_path(const mi_ctx* c) { return c ? (c->impl->sp_ok ? 1 : 0) : -1; }
+int32_t mi_decode_path(const mi_ctx* c) {
+    if (!c) return -1;
+    return c->impl->ps_usable() ? 2 : c->impl->sp_ok ? 1 : 0;
+}
+int32_t mi_decode_set_mode(mi_ctx* c, int32_t mode) {
+    if (!c || mode < 0 || mode > 1) return -1;
+    const int prev = c->impl->decode_mode;
+    c->impl->decode_mode = mode;
+    return prev;
+}
 int32_t mi_debug_stamps(mi_ctx* c, uint64_t* out, int32_t n_launch) {
     try {
         if (!c || !out) throw Error("null argument");

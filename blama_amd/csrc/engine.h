@@ -241,6 +241,17 @@ struct Ctx {
     char* sp_act[5] = {};               // QKV, WO, gate/up, down, head inputs
     bool sp_setup();
     void enqueue_step_sp(bool with_logits);
+    // persistent decode step (pstep.hip): every layer of a dense k-quant LLaMA token in one launch,
+    // for contexts within ATTN_SHORT cells, while this context is the only one on its device (its
+    // workgroups need every CU).  decode_mode: 0 auto (persistent when available), 1 launches only.
+    PsStep* ps = nullptr;
+    float* ps_xout = nullptr;           // the residual after the last layer (the head's input)
+    bool ps_off = false;                // a spin of the persistent step gave up: launches from now on
+    int decode_mode = 0;
+    hipGraphExec_t g_ps[2] = {nullptr, nullptr};   // [with_logits]
+    void ps_setup();
+    bool ps_usable() const;             // the next step may run persistent
+    void enqueue_step_ps(bool with_logits, bool timed);
     struct LayerBufs {
         const float* x_in;              // residual stream into the layer
         float *q, *po, *xa, *h, *h2, *xf;   // q, attention output, residual after WO, FFN (2nd expert), after down

@@ -1,6 +1,7 @@
 // Kernel parameter blocks and host-side launchers (implemented in kernels.hip).
 #pragma once
 #include "common.h"
+#include <vector>
 
 namespace mi {
 
@@ -293,6 +294,40 @@ void launch_moe_group(const int* sel, int n, int U, int E, int* grp, int* rows, 
                       hipStream_t s);
 void launch_moe_combine(const float* y, const int* pos, const float* w, float* x, int ntok, int n_embd,
                         hipStream_t s);
+
+// ---- the persistent decode step (pstep.hip): every layer of one dense LLaMA token in one launch
+// (a loader wave per CU streams the weights into an LDS ring; consumer waves hand activations
+// between CUs as tagged granules).  Matrices: Q4_K / Q5_K / Q6_K; contexts within ATTN_SHORT cells.
+struct PsOpDesc {
+    QMat A, B;                 // B: the gate/up partner (up)
+    int role;                  // 0 a Q|K|V group, 1 WO, 2 gate/up, 3 down
+    int row0;                  // a Q|K|V group: its first row within the layer's Q|K|V rows
+};
+struct PsLayerDesc {
+    PsOpDesc op[5];            // the Q|K|V groups, then WO, gate/up, down
+    int n_op;
+    const float* attn_norm;
+    const float* ffn_norm;
+    __half* kc;                // this layer's caches [n_ctx][kv_dim]
+    __half* vc;
+};
+struct PsConfig {
+    int n_layer, n_embd, n_ff, n_head, n_head_kv, head_dim, kv_dim, n_rot;
+    float eps, theta_scale, freq_scale, kq_scale;
+    const float* freq_factors;
+    const int* tokpos;         // {token, pos, cell, -}
+    int* cell_pos;
+    const unsigned* step;      // decode steps so far (the embedding launch increments it)
+    const float* xin;          // the embedding row
+    float* xout;               // the residual after the last layer
+    unsigned* err;             // host-mapped error word (a spin gave up: codes >= 0x100)
+};
+struct PsStep;
+// nullptr, with the reason in *why, when the model or device has no persistent form
+PsStep* ps_create(const PsConfig& c, const std::vector<PsLayerDesc>& layers, std::string* why);
+void ps_destroy(PsStep* s);
+void ps_launch(const PsStep* s, hipStream_t st);
+long long ps_bytes(const PsStep* s);   // quantised weight bytes one launch streams
 
 // ---- load-time repack of GGUF blocks into planes ----
 void launch_repack(const uint8_t* raw, int type, long long rows, int K, uint8_t* const planes[4],

@@ -85,6 +85,7 @@ _SIGS = {
     "mi_prof_read": (C.c_int32, [_P, C.POINTER(C.c_float), C.c_int32]),
     "mi_prof_ffn_bytes": (C.c_int64, [_P]),
     "mi_decode_path": (C.c_int32, [_P]),
+    "mi_decode_set_mode": (C.c_int32, [_P, C.c_int32]),
     "mi_prof_bytes": (C.c_int64, [_P]),
     "mi_debug_stamps": (C.c_int32, [_P, _P, C.c_int32]),
     "mi_op_gemv": (C.c_int32, [C.c_int32, C.c_int32, _P, C.c_int32, C.c_int32, _P, _P]),
@@ -315,6 +316,10 @@ class Context:
     @property
     def ffn_bytes(self) -> int:
         return lib().mi_prof_ffn_bytes(self.h)
+
+    def set_decode_mode(self, mode: int) -> int:
+        """0: the persistent decode step where available (default); 1: the launch form only."""
+        return int(lib().mi_decode_set_mode(self.h, mode))
 
     def decode_path(self) -> int:
         """1: decode steps within 512 cells run on the streaming GEMV (dgemv.hip); 0: gemv_kernel."""

@@ -147,9 +147,13 @@ int32_t mi_prof_read(mi_ctx* ctx, float* us, int32_t n);
 int64_t mi_prof_ffn_bytes(const mi_ctx* ctx);
 /* Algorithmic HBM bytes of the launch mi_prof_read last timed (the FFN gate/up launch). */
 int64_t mi_prof_bytes(const mi_ctx* ctx);
-/* Diagnostics: 1 when the context's decode steps (within 512 cells) run on the streaming GEMV
- * (dgemv.hip), 0 on the gemv_kernel graph; -1 for a null context. */
+/* Diagnostics: the form the context's next decode step (within 512 cells) takes: 2 the persistent
+ * launch (pstep.hip), 1 the streaming GEMV launches (dgemv.hip), 0 the gemv_kernel graph; -1 for
+ * a null context. */
 int32_t mi_decode_path(const mi_ctx* ctx);
+/* Decode step form: 0 (default) the persistent launch where the model and device allow it, 1 the
+ * launch form only.  Returns the previous mode, -1 on a bad argument. */
+int32_t mi_decode_set_mode(mi_ctx* ctx, int32_t mode);
 /* Diagnostics: copies the per-workgroup s_memrealtime stamps (100 MHz) of the
  * first n_launch launches of the last decode step, [launch][512][8] uint64, to
  * out.  Returns the number of launches copied; 0 unless the library is the
