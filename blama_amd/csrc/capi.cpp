@@ -508,6 +508,36 @@ int32_t mi_decode_path(const mi_ctx* c) {
     if (!c) return -1;
     return c->impl->ps_usable() ? 2 : c->impl->sp_ok ? 1 : 0;
 }
+const char* mi_decode_path_note(const mi_ctx* c) {
+    if (!c) return "null context";
+    const Ctx& x = *c->impl;
+    if (!x.ps_note.empty()) return x.ps_note.c_str();
+    if (x.ps_off) return "a hand-off of the persistent step timed out on this context";
+    if (x.decode_mode != 1) return "launch form (mi_decode_set_mode 0, the default)";
+    if (dev_chain_contexts(x.device) != 1) return "other contexts on the device";
+    return "";
+}
+int32_t mi_debug_ps_stamps(mi_ctx* c, int32_t layer, uint64_t* out, int32_t n) {
+    try {
+        if (!c) throw Error("null context");
+        Ctx& x = *c->impl;
+        if (!x.ps) return 0;
+        MI_HIP(hipSetDevice(x.device));
+        static std::map<const Ctx*, unsigned long long*> bufs;
+        unsigned long long*& b = bufs[&x];
+        if (!b) MI_HIP(hipMalloc(&b, 1024 * 16 * sizeof(unsigned long long)));
+        const int ncu = ps_arm_stamps(x.ps, layer >= 0 ? b : nullptr, layer);
+        x.invalidate_graphs();
+        if (out && n > 0) {
+            x.sync();
+            MI_HIP(hipMemcpy(out, b, (size_t)std::min(n, ncu) * 16 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+        }
+        return ncu;
+    } catch (const std::exception& e) {
+        set_last_error(e.what());
+        return -1;
+    }
+}
 int32_t mi_decode_set_mode(mi_ctx* c, int32_t mode) {
     if (!c || mode < 0 || mode > 1) return -1;
     const int prev = c->impl->decode_mode;
@@ -601,6 +631,62 @@ int32_t mi_op_gemv(int32_t device, int32_t type, const void* raw, int32_t rows, 
         launch_gemv(single_gemv(m, dx.as<float>(), dy.as<float>()), nullptr);
         MI_HIP(hipDeviceSynchronize());
         MI_HIP(hipMemcpy(y, dy.p, rows * sizeof(float), hipMemcpyDeviceToHost));
+        return 0;
+    }
+    MI_TRY(-1)
+}
+
+// The decode step's streaming GEMV (dgemv.hip) for one launch of a given role: x quantised on the
+// device by dv_quant_kernel (no norm), then dgemv_kernel.  role 0 (Q/K/V, no RoPE: every row a Q
+// row; a second matrix = a second segment of another type), 1 (residual add), 2 (SwiGLU of the pair
+// A = gate, B = up), 3 (store).
+int32_t mi_op_dgemv(int32_t device, int32_t role, int32_t type, const void* raw, int32_t rows, int32_t K, int32_t type2,
+                    const void* raw2, int32_t rows2, const float* x, const float* resid, float* y) {
+    try {
+        MI_HIP(hipSetDevice(device));
+        ensure_attrs(device);
+        if (role < 0 || role > 3) throw Error("op_dgemv: role");
+        std::vector<std::unique_ptr<DevBuf>> keep;
+        const QMat a = upload_qmat(type, raw, rows, K, keep);
+        QMat b{};
+        const bool two = raw2 && rows2 > 0;
+        if (two) b = upload_qmat(type2, raw2, rows2, K, keep);
+        if (role == 2 && (!two || type2 != type || rows2 != rows)) throw Error("op_dgemv: SwiGLU needs a pair");
+        if ((role == 1 || role == 3) && two) throw Error("op_dgemv: one matrix for this role");
+        const int out_rows = role == 0 ? rows + (two ? rows2 : 0) : rows;
+        DevBuf dx(K * sizeof(float)), dy(out_rows * sizeof(float)), dr(out_rows * sizeof(float)), dtp(16);
+        MI_HIP(hipMemcpy(dx.p, x, K * sizeof(float), hipMemcpyHostToDevice));
+        if (role == 1) MI_HIP(hipMemcpy(dr.p, resid, rows * sizeof(float), hipMemcpyHostToDevice));
+        MI_HIP(hipMemset(dtp.p, 0, 16));
+        int fmt = 0;
+        for (int t : {type, two ? type2 : type}) fmt |= t == T_Q8_0 ? 2 : 1;
+        DevBuf act(dv_act_bytes(K, fmt & 1, fmt >> 1));
+        launch_dv_quant(dx.as<float>(), ActOut{K, fmt & 1, fmt >> 1, act.as<char>(), nullptr, 1e-5f}, nullptr);
+        GemvParams p;
+        std::memset(&p, 0, sizeof(p));
+        p.K = K;
+        p.act_in = act.as<char>();
+        p.act_q8k = fmt & 1;
+        p.act_q80 = fmt >> 1;
+        p.tokpos = dtp.as<int>();
+        p.head_dim = 128;
+        p.nseg = role == 0 && two ? 2 : 1;
+        const int epi[4] = {EPI_QKV, EPI_ADD, EPI_SWIGLU, EPI_STORE};
+        for (int s = 0; s < p.nseg; ++s) {
+            GemvSeg& g = p.seg[s];
+            g.A = s == 0 ? a : b;
+            g.B = role == 2 ? b : g.A;
+            g.pair = role == 2 ? PAIR_AB : PAIR_ADJ;
+            g.epi = epi[role];
+            g.expA = g.expB = -1;
+            g.out = dy.as<float>() + (s == 0 ? 0 : rows);
+            g.nq = g.A.rows;   // Q/K/V: every row a Q row, n_rot 0 (no rotation)
+            g.resid = role == 1 ? dr.as<float>() : nullptr;
+        }
+        if (!dgemv_supported(p)) throw Error("op_dgemv: no compiled variant for this launch");
+        launch_dgemv(p, nullptr);
+        MI_HIP(hipDeviceSynchronize());
+        MI_HIP(hipMemcpy(y, dy.p, out_rows * sizeof(float), hipMemcpyDeviceToHost));
         return 0;
     }
     MI_TRY(-1)

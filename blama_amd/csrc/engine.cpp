@@ -563,6 +563,7 @@ GemvSeg seg_of(const QMat& A, int pair, int epi, float* out) {
     return g;
 }
 }  // namespace
+int dev_chain_contexts(int device) { return dev_chain(device).nctx.load(); }
 
 Ctx::Ctx(Model* model, uint32_t nctx, uint32_t nbatch, uint32_t nubatch) : m(model) {
     if (m->vocab_only) throw Error("cannot create a context on a vocab-only model");
@@ -1118,13 +1119,18 @@ void Ctx::enqueue_step_sp(bool with_logits) {
 // needs the streaming step's head buffers (sp_ok); MoE, GPT-2 and Q8_0 models keep the launches.
 void Ctx::ps_setup() {
     const HParams& hp = m->hp;
-    if (!sp_ok || hp.arch != ARCH_LLAMA || hp.n_expert > 0) return;
+    ps_note = !sp_ok ? "no streaming step (head buffers)" : hp.arch != ARCH_LLAMA ? "not a LLaMA graph"
+            : hp.n_expert > 0 ? "MoE" : "";
+    if (!ps_note.empty()) return;
     std::vector<PsLayerDesc> ld(hp.n_layer);
     for (int l = 0; l < hp.n_layer; ++l) {
         const Layer& L = m->layers[l];
         PsLayerDesc& d = ld[l];
         std::memset(&d, 0, sizeof(d));
-        if (L.n_qkv < 1 || L.n_qkv > 2) return;
+        if (L.n_qkv < 1 || L.n_qkv > 2) {
+            ps_note = "Q/K/V groups";
+            return;
+        }
         int row0 = 0;
         for (int g = 0; g < L.n_qkv; ++g) {
             d.op[d.n_op].A = L.qkv[g];
@@ -1170,10 +1176,11 @@ void Ctx::ps_setup() {
     c.err = d_attn_xerr;
     std::string why;
     ps = ps_create(c, ld, &why);
+    if (!ps) ps_note = why;
 }
 
 bool Ctx::ps_usable() const {
-    return ps && !ps_off && decode_mode == 0 && attn_fused && dev_chain(device).nctx.load() == 1;
+    return ps && !ps_off && decode_mode == 1 && n_cells + 1 <= ATTN_SHORT && dev_chain(device).nctx.load() == 1;
 }
 
 // One batch-1 decode step as the embedding, the persistent launch, then the output head on the

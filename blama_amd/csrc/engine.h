@@ -122,6 +122,8 @@ struct Model {
 };
 
 // ------------------------------------------------------------- context ----
+int dev_chain_contexts(int device);   // live contexts on the device
+
 struct Ctx {
     Model* m = nullptr;
     int device = 0;
@@ -243,11 +245,13 @@ struct Ctx {
     void enqueue_step_sp(bool with_logits);
     // persistent decode step (pstep.hip): every layer of a dense k-quant LLaMA token in one launch,
     // for contexts within ATTN_SHORT cells, while this context is the only one on its device (its
-    // workgroups need every CU).  decode_mode: 0 auto (persistent when available), 1 launches only.
+    // workgroups need every CU).  decode_mode: 0 the launch form (default), 1 the persistent step
+    // where available.
     PsStep* ps = nullptr;
     float* ps_xout = nullptr;           // the residual after the last layer (the head's input)
     bool ps_off = false;                // a spin of the persistent step gave up: launches from now on
     int decode_mode = 0;
+    std::string ps_note;                // why the persistent step is unavailable (empty: available)
     hipGraphExec_t g_ps[2] = {nullptr, nullptr};   // [with_logits]
     void ps_setup();
     bool ps_usable() const;             // the next step may run persistent

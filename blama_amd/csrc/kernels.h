@@ -328,6 +328,9 @@ PsStep* ps_create(const PsConfig& c, const std::vector<PsLayerDesc>& layers, std
 void ps_destroy(PsStep* s);
 void ps_launch(const PsStep* s, hipStream_t st);
 long long ps_bytes(const PsStep* s);   // quantised weight bytes one launch streams
+// diagnostics: s_memrealtime stamps of every CU at the phases of layer `layer` into dev [ncu][16]
+// (null: off); returns the CU count.  Graphs captured before keep the old arguments.
+int ps_arm_stamps(PsStep* s, unsigned long long* dev, int layer);
 
 // ---- load-time repack of GGUF blocks into planes ----
 void launch_repack(const uint8_t* raw, int type, long long rows, int K, uint8_t* const planes[4],

@@ -1076,16 +1076,46 @@ static AttnFn attn_fused_hg1(int hd, int hg) {
     }
 }
 
-bool attn_quant_supported(int n_head, int n_head_kv, int head_dim) {
-    if (n_head_kv <= 0 || n_head % n_head_kv) return false;
+// The quantising fused kernel for a head geometry -- the decode step's (launch_attn with
+// act_out) and a short batch's (launch_attn_multi with act_q8): a workgroup serves whole 256-blocks
+// of the output, hg groups of 4 waves, each group one kv head (R q heads) or, with few kv heads
+// (qsplit), one q head.  One picker for the support query and both launchers.
+struct AttnQuantPick {
+    AttnFn f;
+    int qsplit, hg, units;
+};
+static AttnQuantPick attn_quant_pick(int n_head, int n_head_kv, int head_dim) {
+    AttnQuantPick k{nullptr, 0, 1, 0};
+    if (n_head_kv <= 0 || n_head % n_head_kv) return k;
     const int r = n_head / n_head_kv;
-    const bool qs = r > 1 && n_head_kv < 16;
-    const int per = (qs ? 1 : r) * head_dim;
+    if (r != 1 && r != 2 && r != 4 && r != 8) return k;
+    const bool qs = r > 1 && n_head_kv < 16;   // few kv heads: a group per q head
+    const int per = (qs ? 1 : r) * head_dim;   // output elements of one group
     const int hg = per >= 256 ? 1 : 256 / per;
     const int units = qs ? n_head : n_head_kv;
-    if (units % hg || per * hg % 256 || (r != 1 && r != 2 && r != 4 && r != 8)) return false;
-    return (hg == 1 && !qs) ? (head_dim == 32 || head_dim == 64 || head_dim == 128 || head_dim == 256)
-                            : attn_fused_hg1(head_dim, hg) != nullptr;
+    if (units % hg || per * hg % 256) return k;
+    AttnFn f = nullptr;
+    if (hg == 1 && !qs) {
+        AttnFn fa = nullptr, fb = nullptr;
+        switch (r) {
+        case 1: attn_fns_r<1>(head_dim, fa, fb, f); break;
+        case 2: attn_fns_r<2>(head_dim, fa, fb, f); break;
+        case 4: attn_fns_r<4>(head_dim, fa, fb, f); break;
+        case 8: attn_fns_r<8>(head_dim, fa, fb, f); break;
+        default: break;
+        }
+    } else if (qs || r == 1) {
+        f = attn_fused_hg1(head_dim, hg);
+    }
+    k.f = f;
+    k.qsplit = qs ? r : 0;
+    k.hg = hg;
+    k.units = units;
+    return k;
+}
+
+bool attn_quant_supported(int n_head, int n_head_kv, int head_dim) {
+    return attn_quant_pick(n_head, n_head_kv, head_dim).f != nullptr;
 }
 
 void launch_attn(const AttnParams& p, hipStream_t s) {
@@ -1102,18 +1132,12 @@ void launch_attn(const AttnParams& p, hipStream_t s) {
     if (!fa) throw Error("attn: unsupported head_dim / GQA ratio (head_dim 32..256, ratio 1/2/4/8)");
     if (p.fused && p.act_out.act) {
         // the streaming decode step: the output also quantised, whole 256-blocks per workgroup
-        const bool qs = r > 1 && p.n_head_kv < 16;   // few kv heads: a group per q head
-        const int per = (qs ? 1 : r) * p.head_dim;   // output elements of one group
-        const int hg = per >= 256 ? 1 : 256 / per;
-        const int units = qs ? p.n_head : p.n_head_kv;
-        AttnFn f = nullptr;
-        if (hg == 1 && !qs) f = ff;
-        else if (qs || r == 1) f = attn_fused_hg1(p.head_dim, hg);
-        if (!f || units % hg || per * hg % 256 || p.act_out.K != p.n_head * p.head_dim)
+        const AttnQuantPick k = attn_quant_pick(p.n_head, p.n_head_kv, p.head_dim);
+        if (!k.f || p.act_out.K != p.n_head * p.head_dim)
             throw Error("attn: no quantising decode kernel for this head geometry");
         AttnParams q = p;
-        q.qsplit = qs ? r : 0;
-        hipLaunchKernelGGL(f, dim3(units / hg), dim3(256 * hg), 0, s, q);
+        q.qsplit = k.qsplit;
+        hipLaunchKernelGGL(k.f, dim3(k.units / k.hg), dim3(256 * k.hg), 0, s, q);
         MI_HIP(hipGetLastError());
         return;
     }
@@ -1167,27 +1191,11 @@ void launch_attn_multi(const AttnParams& p_in, int ntok, float* out, hipStream_t
     if (p.act_q8.q) {
         // each token's output also quantised (a short batch's WO input): the decode step's
         // quantising geometry, whole 256-blocks per workgroup, one grid row per token
-        const bool qs = r > 1 && p.n_head_kv < 16;
-        const int per = (qs ? 1 : r) * p.head_dim;
-        const int hg = per >= 256 ? 1 : 256 / per;
-        const int units = qs ? p.n_head : p.n_head_kv;
-        AttnFn f = nullptr;
-        if (hg == 1 && !qs) {
-            AttnFn fa = nullptr, fb = nullptr;
-            switch (r) {
-            case 1: attn_fns_r<1>(p.head_dim, fa, fb, f); break;
-            case 2: attn_fns_r<2>(p.head_dim, fa, fb, f); break;
-            case 4: attn_fns_r<4>(p.head_dim, fa, fb, f); break;
-            case 8: attn_fns_r<8>(p.head_dim, fa, fb, f); break;
-            default: break;
-            }
-        } else if (qs || r == 1) {
-            f = attn_fused_hg1(p.head_dim, hg);
-        }
-        if (!f || units % hg || per * hg % 256 || p.act_q8.K != p.n_head * p.head_dim || p.act_q8.ntok != ntok)
+        const AttnQuantPick k = attn_quant_pick(p.n_head, p.n_head_kv, p.head_dim);
+        if (!k.f || p.act_q8.K != p.n_head * p.head_dim || p.act_q8.ntok != ntok)
             throw Error("attn: no quantising batch kernel for this head geometry");
-        p.qsplit = qs ? r : 0;
-        hipLaunchKernelGGL(f, dim3(units / hg, ntok), dim3(256 * hg), 0, s, p);
+        p.qsplit = k.qsplit;
+        hipLaunchKernelGGL(k.f, dim3(k.units / k.hg, ntok), dim3(256 * k.hg), 0, s, p);
         MI_HIP(hipGetLastError());
         return;
     }

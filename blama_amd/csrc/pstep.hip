@@ -262,6 +262,8 @@ struct PsArgs {
     unsigned long long* g_xa;  // x after WO [n_embd]
     unsigned long long* g_h;   // FFN [n_ff]
     unsigned* err;             // host-mapped: a spin gave up (the step is invalid)
+    unsigned long long* stamps; // diagnostics: [ncu][16] s_memrealtime stamps of layer stamp_layer (null: off)
+    int stamp_layer;
     int slot_bytes;            // ring slot size
     int act_off;               // LDS offset of the activation / attention scratch region
     int ctl_off;               // LDS offset of the control block
@@ -273,6 +275,7 @@ struct Ctl {                   // LDS control block layout (offsets from ctl_off
     static constexpr int FULL = 0;        // int[PS_NSLOT]: fill seq + 1 of the slot's data
     static constexpr int FREE = 32;       // int[PS_NSLOT]: consumer releases of the slot
     static constexpr int SYNC = 64;       // int: consumer barrier counter
+    static constexpr int GATH = 68;       // int: consumer waves sweeping another CU's data (the loader thins)
     static constexpr int RED = 128;       // double[8]: per-wave norm partials
     static constexpr int RES = 256;       // float[PS_MAXRES]: residual rows of this CU
     static constexpr int MISC = 512;      // float[PS_NC][4]: attention maxima
@@ -312,11 +315,13 @@ __device__ __forceinline__ void ps_loader(const PsArgs& a, lchar* smem, int cu, 
     const int lane = threadIdx.x & 63;
     lint* full = reinterpret_cast<lint*>(smem + a.ctl_off + Ctl::FULL);
     lint* fre = reinterpret_cast<lint*>(smem + a.ctl_off + Ctl::FREE);
+    lint* gath = reinterpret_cast<lint*>(smem + a.ctl_off + Ctl::GATH);
     int seq = 0, prev_cnt = -1;   // fills issued; instructions of fill seq - 1 (-1: marked)
     Guard g;
     for (int l = 0; l < a.n_layer; ++l) {
         const PsLayer* Lp = a.layers + l;
         const int n_op = ld_const(&Lp->n_op);
+        if (a.stamps && l == a.stamp_layer && lane == 0) a.stamps[blockIdx.x * 16 + 13] = rt_now();
         for (int o = 0; o < n_op; ++o) {
             const PsOp op = ld_const(Lp->op + o);
             int u0, u1;
@@ -334,6 +339,13 @@ __device__ __forceinline__ void ps_loader(const PsArgs& a, lchar* smem, int cu, 
                     }
                     while (lds_ld_asm(fre + s) < use * PS_NC)
                         if (!g.ok(a.err, 0x101)) return;
+                }
+                if (prev_cnt >= 0 && lds_ld_asm(gath) > 0) {
+                    // consumers are sweeping other CUs' outputs: keep one fill in flight, so their
+                    // loads do not queue behind a refill burst (MI355X guide, gather-pass)
+                    vm_wait(0);
+                    lds_st_asm(full + (seq - 1) % PS_NSLOT, seq);
+                    prev_cnt = -1;
                 }
                 Region rg[2][4];
                 slot_regions(op, ua, ub, rg);
@@ -369,6 +381,7 @@ __device__ __forceinline__ void ps_loader(const PsArgs& a, lchar* smem, int cu, 
         vm_wait(0);
         lds_st_asm(full + (seq - 1) % PS_NSLOT, seq);
     }
+    if (a.stamps && lane == 0) a.stamps[blockIdx.x * 16 + 14] = rt_now();
 }
 
 // ---- consumer-wave barrier (the loader never joins: LDS counter) ----
@@ -441,16 +454,12 @@ __device__ __forceinline__ bool gather_vec(const unsigned long long* g, const fl
 // Two consumer barriers: every wave is done with the previous activation before it is overwritten,
 // and the new one is complete before any wave reads it.
 template <int MB>
-__device__ __forceinline__ bool build_act(const PsArgs& a, lchar* smem, CSync& cs, float (&v)[MB][4], int nb, const float* nw,
-                          int r0, int r1, int cw, int lane, unsigned code) {
+__device__ __forceinline__ bool build_act(const PsArgs& a, lchar* smem, CSync& cs, float (&v)[MB][4], const f32x4 (&w)[MB], int nb,
+                          const float* nw, int r0, int r1, int cw, int lane, unsigned code) {
     lane = fresh_lane();
     __attribute__((address_space(3))) double* lred =
         reinterpret_cast<__attribute__((address_space(3))) double*>(smem + a.ctl_off + Ctl::RED);
-    f32x4 w[MB];
     if (nw) {
-#pragma unroll
-        for (int i = 0; i < MB; ++i)
-            if (cw + PS_NC * i < nb) w[i] = gptr(reinterpret_cast<const f32x4*>(nw))[(cw + PS_NC * i) * 64 + lane];
         double s = 0.0;
 #pragma unroll
         for (int i = 0; i < MB; ++i)
@@ -527,6 +536,13 @@ __device__ __forceinline__ bool ps_op(const PsArgs& a, const PsLayer& L, const P
     unit_span(op.units, cu, ncu, u0, u1);
     i32x4 tp = {0, 0, 0, 0};
     if (ROLE == PS_R_QKV) tp = *gptr(reinterpret_cast<const i32x4*>(a.tokpos));
+    // the activation slices this lane's dots read (the same for every row): once per op
+    typename KQ::AR ar[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+        const int sb0 = 8 * c + sbl;
+        ar[c] = KQ::act(av, sb0 < nb ? sb0 : nb - 1, j);
+    }
     for (int ua = u0; ua < u1; ua += op.ups) {
         const int ub = min(u1, ua + op.ups);
         const int s = oc.seq % PS_NSLOT;
@@ -579,8 +595,7 @@ __device__ __forceinline__ bool ps_op(const PsArgs& a, const PsLayer& L, const P
 #pragma unroll
                 for (int c = 0; c < C; ++c) {
                     const int sb0 = 8 * c + sbl;
-                    const int sb = sb0 < nb ? sb0 : nb - 1;
-                    const float p = KQ::dot(w[r][c], KQ::act(av, sb, j), j);
+                    const float p = KQ::dot(w[r][c], ar[c], j);
                     acc += sb0 < nb ? p : 0.0f;
                 }
                 y[r] = wave_sum63(acc);
@@ -627,15 +642,9 @@ __device__ __forceinline__ bool ps_op(const PsArgs& a, const PsLayer& L, const P
     return true;
 }
 
-#ifndef PS_DBG
-#define PS_DBG 0
-#endif
 template <int T, int ROLE>
 __device__ __forceinline__ bool ps_op_c(const PsArgs& a, const PsLayer& L, const PsOp& op, lchar* smem, OpCtx& oc, int cu, int ncu,
                         int cw, int lane) {
-#if PS_DBG == 1
-    return ps_op<T, ROLE, 2>(a, L, op, smem, oc, cu, ncu, cw, lane);
-#endif
     switch (op.C) {
     case 1: return ps_op<T, ROLE, 1>(a, L, op, smem, oc, cu, ncu, cw, lane);
     case 2: return ps_op<T, ROLE, 2>(a, L, op, smem, oc, cu, ncu, cw, lane);
@@ -656,9 +665,6 @@ __device__ __forceinline__ bool ps_op_c(const PsArgs& a, const PsLayer& L, const
 template <int ROLE>
 __device__ __forceinline__ bool ps_op_t(const PsArgs& a, const PsLayer& L, const PsOp& op, lchar* smem, OpCtx& oc, int cu, int ncu,
                         int cw, int lane) {
-#if PS_DBG >= 1
-    return ps_op_c<T_Q4_K, ROLE>(a, L, op, smem, oc, cu, ncu, cw, lane);
-#endif
     switch (op.type) {
     case T_Q4_K: return ps_op_c<T_Q4_K, ROLE>(a, L, op, smem, oc, cu, ncu, cw, lane);
     case T_Q5_K: return ps_op_c<T_Q5_K, ROLE>(a, L, op, smem, oc, cu, ncu, cw, lane);
@@ -680,11 +686,28 @@ __device__ __forceinline__ bool ps_attention(const PsArgs& a, const PsLayer& L, 
     constexpr int LPC = HD / 8;            // lanes per cell (8 dims each)
     constexpr int CPW = 64 / LPC;          // cells per wave step
     constexpr int HPB = 256 / HD;          // q heads per output block
+    constexpr int KP = HPB >= 4 ? 1 : 8 / HPB;   // wave steps whose cache rows are requested up front
     lane = fresh_lane();
     const int Lh = lane % LPC, G = lane / LPC;
     const int r = a.n_head / a.n_head_kv;
     const i32x4 tp = *gptr(reinterpret_cast<const i32x4*>(a.tokpos));
     const int qpos = tp.y, ncell = min(tp.z + 1, ATTN_SHORT), cnew = tp.z;
+    // 0. the cached cells' K / V rows and positions of this wave's first KP steps, all requested
+    // before anything waits (under the weight stream every round trip costs microseconds)
+    u32x4 kc[KP][HPB], vc[KP][HPB];
+    int pc[KP];
+#pragma unroll
+    for (int k = 0; k < KP; ++k) {
+        const int c = cw * CPW + k * PS_NC * CPW + G;
+        const int cc = min(c, max(cnew - 1, 0));
+        pc[k] = gptr(a.cell_pos)[cc];
+#pragma unroll
+        for (int t = 0; t < HPB; ++t) {
+            const int hk = (blk * HPB + t) / r;
+            kc[k][t] = *gptr(reinterpret_cast<const u32x4*>(L.kc + (long long)cc * a.kv_dim + hk * HD + Lh * 8));
+            vc[k][t] = *gptr(reinterpret_cast<const u32x4*>(L.vc + (long long)cc * a.kv_dim + hk * HD + Lh * 8));
+        }
+    }
     // this step's q / k / v of the block's heads (granules; 8 consecutive dims per lane)
     float q[HPB][8], kn[HPB][8], vn[HPB][8];
     {
@@ -723,32 +746,37 @@ __device__ __forceinline__ bool ps_attention(const PsArgs& a, const PsLayer& L, 
         reinterpret_cast<__attribute__((address_space(3))) float*>(smem + a.ctl_off + Ctl::MISC);
     __attribute__((address_space(3))) double* dred =
         reinterpret_cast<__attribute__((address_space(3))) double*>(smem + a.ctl_off + Ctl::DRED);
+    // 8 f16 of a cache row -> floats
+    auto cvt8 = [](const u32x4& w, float (&f)[8]) {
+        const unsigned ww[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            f[2 * e] = h2f(ww[e]);
+            f[2 * e + 1] = h2f(ww[e] >> 16);
+        }
+    };
+    auto load_row = [&](const __half* cache, int c, int t) {
+        const int hk = (blk * HPB + t) / r;
+        return *gptr(reinterpret_cast<const u32x4*>(cache + (long long)c * a.kv_dim + hk * HD + Lh * 8));
+    };
     // 1. scaled KQ of every cell (LDS), per-head maxima
     float mx[HPB];
 #pragma unroll
     for (int t = 0; t < HPB; ++t) mx[t] = -INFINITY;
-    for (int cb = cw * CPW; cb < ncell; cb += PS_NC * CPW) {
-        const int c = cb + G;
+    const int nsteps = (ncell - cw * CPW + PS_NC * CPW - 1) / (PS_NC * CPW);
+    auto score_step = [&](int k, const u32x4 (&kw)[HPB], int pos_c) {
+        const int c = cw * CPW + k * PS_NC * CPW + G;
         const bool in = c < ncell;
-        const int cc = in ? c : ncell - 1;
-        const bool isnew = cc == cnew;
-        const int cpos = isnew ? qpos : gptr(a.cell_pos)[cc];
-        const bool valid = in && cpos <= qpos;
+        const bool isnew = !in || c == cnew;
+        const bool valid = in && (isnew ? qpos : pos_c) <= qpos;
 #pragma unroll
         for (int t = 0; t < HPB; ++t) {
-            const int hk = (blk * HPB + t) / r;
             float kf[8];
             if (isnew) {
 #pragma unroll
                 for (int e = 0; e < 8; ++e) kf[e] = kn[t][e];
             } else {
-                const u32x4 kk = *gptr(reinterpret_cast<const u32x4*>(L.kc + (long long)cc * a.kv_dim + hk * HD + Lh * 8));
-                const unsigned kw[4] = {kk.x, kk.y, kk.z, kk.w};
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    kf[2 * e] = h2f(kw[e]);
-                    kf[2 * e + 1] = h2f(kw[e] >> 16);
-                }
+                cvt8(kw[t], kf);
             }
             float d = 0.0f;
 #pragma unroll
@@ -759,6 +787,16 @@ __device__ __forceinline__ bool ps_attention(const PsArgs& a, const PsLayer& L, 
             mx[t] = fmaxf(mx[t], wv);
             if (Lh == 0 && in) sw[t * ATTN_SHORT + c] = wv;
         }
+    };
+#pragma unroll
+    for (int k = 0; k < KP; ++k)
+        if (k < nsteps) score_step(k, kc[k], pc[k]);
+    for (int k = KP; k < nsteps; ++k) {
+        const int c = min(cw * CPW + k * PS_NC * CPW + G, max(cnew - 1, 0));
+        u32x4 kw[HPB];
+#pragma unroll
+        for (int t = 0; t < HPB; ++t) kw[t] = load_row(L.kc, c, t);
+        score_step(k, kw, gptr(a.cell_pos)[c]);
     }
 #pragma unroll
     for (int t = 0; t < HPB; ++t) {
@@ -797,32 +835,34 @@ __device__ __forceinline__ bool ps_attention(const PsArgs& a, const PsLayer& L, 
     for (int t = 0; t < HPB; ++t)
 #pragma unroll
         for (int e = 0; e < 8; ++e) o[t][e] = 0.0f;
-    for (int cb = cw * CPW; cb < ncell; cb += PS_NC * CPW) {
-        const int c = cb + G;
+    auto pv_step = [&](int k, const u32x4 (&vw)[HPB]) {
+        const int c = cw * CPW + k * PS_NC * CPW + G;
         const bool in = c < ncell;
-        const int cc = in ? c : ncell - 1;
-        const bool isnew = cc == cnew;
+        const int cc = in ? c : cnew;
 #pragma unroll
         for (int t = 0; t < HPB; ++t) {
-            const int hk = (blk * HPB + t) / r;
             float vf[8];
-            if (isnew) {
+            if (cc == cnew) {
 #pragma unroll
                 for (int e = 0; e < 8; ++e) vf[e] = vn[t][e];
             } else {
-                const u32x4 vv = *gptr(reinterpret_cast<const u32x4*>(L.vc + (long long)cc * a.kv_dim + hk * HD + Lh * 8));
-                const unsigned vw[4] = {vv.x, vv.y, vv.z, vv.w};
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    vf[2 * e] = h2f(vw[e]);
-                    vf[2 * e + 1] = h2f(vw[e] >> 16);
-                }
+                cvt8(vw[t], vf);
             }
             const float p = expf(sw[t * ATTN_SHORT + cc] - M[t]) * inv[t];   // ggml_vec_soft_max_f32, f16 vec_dot_type
             const float pw = in ? __half2float(__float2half_rn(p)) : 0.0f;
 #pragma unroll
             for (int e = 0; e < 8; ++e) o[t][e] = fmaf(pw, vf[e], o[t][e]);
         }
+    };
+#pragma unroll
+    for (int k = 0; k < KP; ++k)
+        if (k < nsteps) pv_step(k, vc[k]);
+    for (int k = KP; k < nsteps; ++k) {
+        const int c = min(cw * CPW + k * PS_NC * CPW + G, max(cnew - 1, 0));
+        u32x4 vw[HPB];
+#pragma unroll
+        for (int t = 0; t < HPB; ++t) vw[t] = load_row(L.vc, c, t);
+        pv_step(k, vw);
     }
 #pragma unroll
     for (int t = 0; t < HPB; ++t)
@@ -858,6 +898,8 @@ __device__ __forceinline__ bool ps_attention(const PsArgs& a, const PsLayer& L, 
 // WO's activation: the quantised attention blocks (nb of them), consumer wave cw taking blocks cw + 7 i
 __device__ __forceinline__ bool gather_att(const PsArgs& a, lchar* smem, CSync& cs, int nb, unsigned tag, int cw, int lane) {
     lane = fresh_lane();
+    lint* gath = reinterpret_cast<lint*>(smem + a.ctl_off + Ctl::GATH);
+    if (lane == 0) __hip_atomic_fetch_add(gath, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     unsigned qv[PS_MB], bs[PS_MB], dv[PS_MB];
     unsigned pend = 0;
 #pragma unroll
@@ -882,6 +924,7 @@ __device__ __forceinline__ bool gather_att(const PsArgs& a, lchar* smem, CSync& 
         }
         if (pend && !g.ok(a.err, 0x140)) return false;
     }
+    if (lane == 0) __hip_atomic_fetch_add(gath, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     if (!cs.wait(a.err, 0x141)) return false;   // every wave is done with the previous activation
     const int K = nb * 256;
     lchar* act = smem + a.act_off;
@@ -900,17 +943,24 @@ __device__ __forceinline__ bool ps_layer_attention(const PsArgs& a, const PsLaye
                                    unsigned ta, int cw, int lane) {
     // every wave is done with QKV's activation before the scores overwrite it
     if (!cs.wait(a.err, 0x12F)) return false;
-#if PS_DBG >= 2
-    return true;
-#endif
+    lint* gath = reinterpret_cast<lint*>(smem + a.ctl_off + Ctl::GATH);
+    if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(gath, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    bool ok = false, known = true;
     switch (a.head_dim) {
-    case 64: return ps_attention<64>(a, L, smem, cs, blk, tq, ta, cw, lane);
-    case 128: return ps_attention<128>(a, L, smem, cs, blk, tq, ta, cw, lane);
-    case 256: return ps_attention<256>(a, L, smem, cs, blk, tq, ta, cw, lane);
-    default: break;
+    case 64: ok = ps_attention<64>(a, L, smem, cs, blk, tq, ta, cw, lane); break;
+    case 128: ok = ps_attention<128>(a, L, smem, cs, blk, tq, ta, cw, lane); break;
+    case 256: ok = ps_attention<256>(a, L, smem, cs, blk, tq, ta, cw, lane); break;
+    default: known = false; break;
     }
+    if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(gath, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (known) return ok;
     __hip_atomic_store(a.err, 0x1F2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     return false;
+}
+
+__device__ __forceinline__ void ps_stamp(const PsArgs& a, int l, int k, int cw, int lane) {
+    if (a.stamps && l == a.stamp_layer && cw == 0 && lane == 0)
+        a.stamps[blockIdx.x * 16 + k] = rt_now();
 }
 
 __device__ __forceinline__ unsigned ps_tag(unsigned step, int n_layer, int l, int e) {
@@ -920,16 +970,30 @@ __device__ __forceinline__ unsigned ps_tag(unsigned step, int n_layer, int l, in
 // gather a vector edge and build the next activation from it, sized by the blocks per wave
 template <int MB>
 __device__ __forceinline__ bool edge_mb(const PsArgs& a, lchar* smem, CSync& cs, const unsigned long long* g, const float* x,
-                                        int nb, unsigned tag, const float* nw, int r0, int r1, int cw, int lane, unsigned code) {
+                                        int nb, unsigned tag, const float* nw, int r0, int r1, int cw, int lane, unsigned code,
+                                        int l, int st) {
     float v[MB][4];
-    if (!gather_vec<MB>(g, x, nb, tag, cw, lane, v, a.err, code)) return false;
-    return build_act<MB>(a, smem, cs, v, nb, nw, r0, r1, cw, lane, code + 2);
+    f32x4 w[MB];   // the norm weight, requested before the gather waits
+    if (nw) {
+        const int ln = fresh_lane();
+#pragma unroll
+        for (int i = 0; i < MB; ++i)
+            if (cw + PS_NC * i < nb) w[i] = gptr(reinterpret_cast<const f32x4*>(nw))[(cw + PS_NC * i) * 64 + ln];
+    }
+    lint* gath = reinterpret_cast<lint*>(smem + a.ctl_off + Ctl::GATH);
+    if (lane == 0) __hip_atomic_fetch_add(gath, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const bool ok = gather_vec<MB>(g, x, nb, tag, cw, lane, v, a.err, code);
+    if (lane == 0) __hip_atomic_fetch_add(gath, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (!ok) return false;
+    ps_stamp(a, l, st, cw, lane);
+    return build_act<MB>(a, smem, cs, v, w, nb, nw, r0, r1, cw, lane, code + 2);
 }
 __device__ __forceinline__ bool edge(const PsArgs& a, lchar* smem, CSync& cs, const unsigned long long* g, const float* x, int nb,
-                                     unsigned tag, const float* nw, int r0, int r1, int cw, int lane, unsigned code) {
-    if (nb <= 3 * PS_NC) return edge_mb<3>(a, smem, cs, g, x, nb, tag, nw, r0, r1, cw, lane, code);
-    if (nb <= 5 * PS_NC) return edge_mb<5>(a, smem, cs, g, x, nb, tag, nw, r0, r1, cw, lane, code);
-    return edge_mb<PS_MB>(a, smem, cs, g, x, nb, tag, nw, r0, r1, cw, lane, code);
+                                     unsigned tag, const float* nw, int r0, int r1, int cw, int lane, unsigned code, int l,
+                                     int st) {
+    if (nb <= 3 * PS_NC) return edge_mb<3>(a, smem, cs, g, x, nb, tag, nw, r0, r1, cw, lane, code, l, st);
+    if (nb <= 5 * PS_NC) return edge_mb<5>(a, smem, cs, g, x, nb, tag, nw, r0, r1, cw, lane, code, l, st);
+    return edge_mb<PS_MB>(a, smem, cs, g, x, nb, tag, nw, r0, r1, cw, lane, code, l, st);
 }
 
 __device__ __forceinline__ void ps_consumer(const PsArgs& a, lchar* smem, int cu, int ncu, int cw, int lane) {
@@ -955,32 +1019,42 @@ __device__ __forceinline__ void ps_consumer(const PsArgs& a, lchar* smem, int cu
         unit_span(a.n_embd, cu, ncu, r0, r1);
         oc.res0 = r0;
         // E_X: the layer input, rms_norm * attn_norm -> Q8_K
+        ps_stamp(a, l, 0, cw, lane);
         if (!edge(a, smem, cs, l == 0 ? nullptr : a.g_x, a.xin, nbe, ps_tag(step, a.n_layer, l - 1, E_X), L.attn_norm, r0, r1,
-                  cw, lane, 0x150))
+                  cw, lane, 0x150, l, 1))
             return;
+        ps_stamp(a, l, 2, cw, lane);
         // Q / K / V groups
         oc.tag_out = ps_tag(step, a.n_layer, l, E_QKV);
         const int nq = L.n_op - 3;
         for (int o = 0; o < nq; ++o)
             if (!ps_op_t<PS_R_QKV>(a, L, ld_const(ops + o), smem, oc, cu, ncu, cw, lane)) return;
+        ps_stamp(a, l, 3, cw, lane);
         // attention (CUs 0 .. nbe-1)
         if (cu < nbe) {
             if (!ps_layer_attention(a, L, smem, cs, cu, oc.tag_out, ps_tag(step, a.n_layer, l, E_ATT), cw, lane)) return;
         }
+        ps_stamp(a, l, 4, cw, lane);
         if (!gather_att(a, smem, cs, nbe, ps_tag(step, a.n_layer, l, E_ATT), cw, lane)) return;
+        ps_stamp(a, l, 5, cw, lane);
         // WO + residual
         oc.tag_out = ps_tag(step, a.n_layer, l, E_XA);
         if (!ps_op_t<PS_R_WO>(a, L, ld_const(ops + nq), smem, oc, cu, ncu, cw, lane)) return;
+        ps_stamp(a, l, 6, cw, lane);
         // E_XA: rms_norm * ffn_norm -> Q8_K; the residual of down
-        if (!edge(a, smem, cs, a.g_xa, nullptr, nbe, oc.tag_out, L.ffn_norm, r0, r1, cw, lane, 0x160)) return;
+        if (!edge(a, smem, cs, a.g_xa, nullptr, nbe, oc.tag_out, L.ffn_norm, r0, r1, cw, lane, 0x160, l, 7)) return;
+        ps_stamp(a, l, 8, cw, lane);
         // gate / up + SwiGLU
         oc.tag_out = ps_tag(step, a.n_layer, l, E_H);
         if (!ps_op_t<PS_R_GU>(a, L, ld_const(ops + nq + 1), smem, oc, cu, ncu, cw, lane)) return;
+        ps_stamp(a, l, 9, cw, lane);
         // E_H: h -> Q8_K
-        if (!edge(a, smem, cs, a.g_h, nullptr, nbf, oc.tag_out, nullptr, 0, 0, cw, lane, 0x170)) return;
+        if (!edge(a, smem, cs, a.g_h, nullptr, nbf, oc.tag_out, nullptr, 0, 0, cw, lane, 0x170, l, 10)) return;
+        ps_stamp(a, l, 11, cw, lane);
         // down + residual
         oc.tag_out = ps_tag(step, a.n_layer, l, E_X);
         if (!ps_op_t<PS_R_DN>(a, L, ld_const(ops + nq + 2), smem, oc, cu, ncu, cw, lane)) return;
+        ps_stamp(a, l, 12, cw, lane);
     }
 }
 
@@ -992,15 +1066,10 @@ __global__ __launch_bounds__(PS_NW * 64) void ps_step_kernel(const PsArgs a) {
     const int cu = blockIdx.x, ncu = gridDim.x;
     // the control block starts zeroed (LDS is not), then the roles split for good
     if (threadIdx.x < 64) reinterpret_cast<lint*>(smem + a.ctl_off)[threadIdx.x] = 0;
+    if (a.stamps && threadIdx.x == 0) a.stamps[blockIdx.x * 16 + 15] = rt_now();
     __syncthreads();
-#if PS_DBG == 3
-    if (wave == 0) ps_loader(a, smem, cu, ncu);
-#elif PS_DBG == 4
-    if (wave != 0) ps_consumer(a, smem, cu, ncu, wave - 1, lane);
-#else
     if (wave == 0) ps_loader(a, smem, cu, ncu);
     else ps_consumer(a, smem, cu, ncu, wave - 1, lane);
-#endif
 }
 
 }  // namespace
@@ -1068,7 +1137,7 @@ PsStep* ps_create(const PsConfig& c, const std::vector<PsLayerDesc>& layers, std
             if (t != T_Q4_K && t != T_Q5_K && t != T_Q6_K) { delete s; return fail("matrix type"); }
             const bool gu = od.role == PS_R_GU;
             if (gu && (od.B.type != t || od.B.rows != od.A.rows || od.B.K != od.A.K)) { delete s; return fail("gate/up pair"); }
-            if (od.A.n_exp > 1 || od.A.expert_stride[0]) { delete s; return fail("MoE"); }
+            if (od.A.n_exp > 1) { delete s; return fail("MoE"); }
             for (int p = 0; p < 4; ++p) {
                 op.a[p] = od.A.p[p];
                 op.b[p] = gu ? od.B.p[p] : od.A.p[p];
@@ -1158,5 +1227,12 @@ void ps_launch(const PsStep* s, hipStream_t st) {
 }
 
 long long ps_bytes(const PsStep* s) { return s ? s->bytes : 0; }
+
+int ps_arm_stamps(PsStep* s, unsigned long long* dev, int layer) {
+    if (!s) return 0;
+    s->args.stamps = dev;
+    s->args.stamp_layer = layer;
+    return s->ncu;
+}
 
 }  // namespace mi

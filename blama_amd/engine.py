@@ -86,6 +86,10 @@ _SIGS = {
     "mi_prof_ffn_bytes": (C.c_int64, [_P]),
     "mi_decode_path": (C.c_int32, [_P]),
     "mi_decode_set_mode": (C.c_int32, [_P, C.c_int32]),
+    "mi_op_dgemv": (C.c_int32, [C.c_int32, C.c_int32, C.c_int32, C.c_void_p, C.c_int32, C.c_int32, C.c_int32,
+                                C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "mi_decode_path_note": (C.c_char_p, [_P]),
+    "mi_debug_ps_stamps": (C.c_int32, [_P, C.c_int32, C.POINTER(C.c_uint64), C.c_int32]),
     "mi_prof_bytes": (C.c_int64, [_P]),
     "mi_debug_stamps": (C.c_int32, [_P, _P, C.c_int32]),
     "mi_op_gemv": (C.c_int32, [C.c_int32, C.c_int32, _P, C.c_int32, C.c_int32, _P, _P]),
@@ -318,8 +322,19 @@ class Context:
         return lib().mi_prof_ffn_bytes(self.h)
 
     def set_decode_mode(self, mode: int) -> int:
-        """0: the persistent decode step where available (default); 1: the launch form only."""
+        """0: the launch form (default); 1: the persistent decode step where available."""
         return int(lib().mi_decode_set_mode(self.h, mode))
+
+    def ps_stamps(self, layer: int, read: bool = False):
+        """Diagnostics: arm the persistent step's per-CU phase stamps for `layer`; with read=True
+        return the last step's stamps [n_cu][16] (100 MHz ticks)."""
+        buf = np.zeros((1024, 16), np.uint64)
+        n = lib().mi_debug_ps_stamps(self.h, layer, buf.ctypes.data_as(C.POINTER(C.c_uint64)) if read else None, 1024)
+        _check(n, "ps_stamps")
+        return buf[:n] if read else n
+
+    def decode_path_note(self) -> str:
+        return (lib().mi_decode_path_note(self.h) or b"").decode()
 
     def decode_path(self) -> int:
         """1: decode steps within 512 cells run on the streaming GEMV (dgemv.hip); 0: gemv_kernel."""
@@ -337,6 +352,23 @@ def op_gemv(type_: int, raw: np.ndarray, rows: int, K: int, x: np.ndarray, devic
     x = np.ascontiguousarray(x, np.float32)
     y = np.empty(rows, np.float32)
     _check(lib().mi_op_gemv(device, type_, _ptr(raw), rows, K, _ptr(x), _ptr(y)), "op_gemv")
+    return y
+
+
+def op_dgemv(role: int, type_: int, raw: np.ndarray, rows: int, K: int, x: np.ndarray, type2: int = -1,
+             raw2=None, rows2: int = 0, resid=None, device: int = 0) -> np.ndarray:
+    """mi_op_dgemv: the decode step's streaming GEMV launch of `role` (0 Q/K/V without RoPE, 1 residual
+    add, 2 SwiGLU pair, 3 store)."""
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    out_rows = rows + (rows2 if role == 0 and raw2 is not None else 0)
+    y = np.empty(out_rows, np.float32)
+    r = None if resid is None else np.ascontiguousarray(resid, dtype=np.float32)
+    raw = np.ascontiguousarray(raw)
+    raw2 = None if raw2 is None else np.ascontiguousarray(raw2)
+    rc = lib().mi_op_dgemv(device, role, type_, raw.ctypes.data, rows, K, type2,
+                           raw2.ctypes.data if raw2 is not None else None, rows2 if raw2 is not None else 0,
+                           _ptr(x), _ptr(r) if r is not None else None, _ptr(y))
+    _check(rc, "op_dgemv")
     return y
 
 

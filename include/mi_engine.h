@@ -151,9 +151,16 @@ int64_t mi_prof_bytes(const mi_ctx* ctx);
  * launch (pstep.hip), 1 the streaming GEMV launches (dgemv.hip), 0 the gemv_kernel graph; -1 for
  * a null context. */
 int32_t mi_decode_path(const mi_ctx* ctx);
-/* Decode step form: 0 (default) the persistent launch where the model and device allow it, 1 the
- * launch form only.  Returns the previous mode, -1 on a bad argument. */
+/* Decode step form: 0 (default) the launch form, 1 the persistent launch where the model and
+ * device allow it.  Returns the previous mode, -1 on a bad argument. */
 int32_t mi_decode_set_mode(mi_ctx* ctx, int32_t mode);
+/* Diagnostics: why the next step does not take the persistent launch ("" when it does, apart from
+ * the cell limit). */
+const char* mi_decode_path_note(const mi_ctx* ctx);
+/* Diagnostics: arms per-CU s_memrealtime stamps (100 MHz) of the persistent step's phases in layer
+ * `layer` (< 0: disarm) for the following steps, and copies the last stamps, [n_cu][16] uint64,
+ * into out when out is set.  Returns the CU count (0 without a persistent step, -1 on error). */
+int32_t mi_debug_ps_stamps(mi_ctx* ctx, int32_t layer, uint64_t* out, int32_t n_cu);
 /* Diagnostics: copies the per-workgroup s_memrealtime stamps (100 MHz) of the
  * first n_launch launches of the last decode step, [launch][512][8] uint64, to
  * out.  Returns the number of launches copied; 0 unless the library is the
@@ -192,6 +199,12 @@ int32_t mi_op_attention_batch(int32_t device, int32_t n_head, int32_t n_head_kv,
                               const uint16_t* v_f16, const int32_t* cell_pos, const int32_t* tok_cell,
                               const int32_t* tok_pos, float* out);
 /* Median device time (us) of `iters` launches of the GEMV above (micro-benchmark). */
+/* The decode step's streaming GEMV (dgemv.hip), one launch: x quantised on the device (Q8_K /
+ * Q8_0 as the matrices need), then role 0 Q/K/V rows without RoPE (a second matrix of another type
+ * = a second segment; y = [A x | B x]), 1 y = A x + resid, 2 y = silu(A x) * (B x) (gate/up pair),
+ * 3 y = A x.  type2/raw2/rows2: the second matrix (raw2 NULL: none). */
+int32_t mi_op_dgemv(int32_t device, int32_t role, int32_t type, const void* raw_blocks, int32_t rows, int32_t K,
+                    int32_t type2, const void* raw_blocks2, int32_t rows2, const float* x, const float* resid, float* y);
 int32_t mi_op_gemv_bench(int32_t device, int32_t type, const void* raw_blocks, int32_t rows, int32_t K,
                          int32_t iters, float* median_us);
 

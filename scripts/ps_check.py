@@ -10,27 +10,26 @@ sys.path.insert(0, ".")
 from blama_amd import engine, synthetic  # noqa: E402
 
 
-def run(model, cfg, mode, steps, timed):
+def run(model, cfg, mode, steps, timed, nprompt=8, nobs=12):
     ctx = engine.Context(model, n_ctx=512)
-    prev = ctx.set_decode_mode(mode)
-    assert prev == 0
+    ctx.set_decode_mode(mode)
     rng = np.random.default_rng(5)
-    prompt = rng.integers(0, cfg.n_vocab, 8).astype(np.int32)
+    prompt = rng.integers(0, cfg.n_vocab, nprompt).astype(np.int32)
     ctx.decode(prompt)
     toks = rng.integers(0, cfg.n_vocab, steps).astype(np.int32)
-    path = ctx.decode_path()
+    path = (ctx.decode_path(), ctx.decode_path_note())
     outs = []
-    for t in toks[:12]:
+    for t in toks[:nobs]:
         ctx.decode([int(t)])
         outs.append(ctx.logits())
     rate = None
     if timed:
         ctx.synchronize()
         t0 = time.perf_counter()
-        for t in toks[12:]:
+        for t in toks[nobs:]:
             ctx.decode([int(t)])
         ctx.synchronize()
-        rate = (len(toks) - 12) / (time.perf_counter() - t0)
+        rate = (len(toks) - nobs) / (time.perf_counter() - t0)
     ctx.close()
     return np.array(outs), path, rate
 
@@ -45,12 +44,14 @@ def main():
         cfg = synthetic.CONFIGS[name]
         model = engine.Model(synthetic.build_gguf(cfg, seed=0))
         timed = cfg.n_embd >= 2048
-        a, pa, ra = run(model, cfg, 0, steps, timed)
-        b, pb, rb = run(model, cfg, 1, steps, timed)
+        nprompt = int(next((x.split("=")[1] for x in sys.argv if x.startswith("--prompt=")), 8))
+        nobs = int(next((x.split("=")[1] for x in sys.argv if x.startswith("--obs=")), 12))
+        a, pa, ra = run(model, cfg, 1, steps, timed, nprompt, nobs)
+        b, pb, rb = run(model, cfg, 0, steps, timed, nprompt, nobs)
         rms = float(np.sqrt(np.mean(b.astype(np.float64) ** 2)))
         err = np.abs(a - b).max(axis=1) / rms
         top_eq = [int(np.argmax(x) == np.argmax(y)) for x, y in zip(a, b)]
-        print(f"{name}: path persistent={pa} launches={pb}; max|d|/rms per step {np.round(err, 6).tolist()}; "
+        print(f"{name} prompt {nprompt}: path persistent={pa} launches={pb}; max|d|/rms per step {np.round(err, 6).tolist()}; "
               f"top1 equal {sum(top_eq)}/{len(top_eq)}; tok/s persistent {ra} launches {rb}", flush=True)
         model.close()
 
