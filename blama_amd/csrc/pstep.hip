@@ -49,7 +49,8 @@ typedef __attribute__((address_space(3))) char lchar;
 
 constexpr int PS_NW = 8;           // waves per workgroup: 0 loader, 1..7 consumers
 constexpr int PS_NC = PS_NW - 1;
-constexpr int PS_NSLOT = 5;        // LDS ring slots
+constexpr int PS_NSLOT = 8;        // LDS ring slots at most (PsArgs::nslot; FULL / FREE words)
+constexpr int PS_DEPTH = 3;        // slot fills the loader keeps in flight
 constexpr int PS_MU = 2;           // units per consumer wave per slot (ups <= PS_NC * PS_MU)
 constexpr int PS_MAXRES = 64;      // residual rows per CU (WO / down units)
 constexpr int PS_MB = 8;           // activation blocks per consumer wave (K <= 7 * 8 * 256 = 14336)
@@ -265,6 +266,7 @@ struct PsArgs {
     unsigned long long* stamps; // diagnostics: [ncu][16] s_memrealtime stamps of layer stamp_layer (null: off)
     int stamp_layer;
     int slot_bytes;            // ring slot size
+    int nslot;                 // ring slots
     int act_off;               // LDS offset of the activation / attention scratch region
     int ctl_off;               // LDS offset of the control block
 };
@@ -273,6 +275,7 @@ namespace {
 
 struct Ctl {                   // LDS control block layout (offsets from ctl_off)
     static constexpr int FULL = 0;        // int[PS_NSLOT]: fill seq + 1 of the slot's data
+    static_assert(PS_NSLOT * 4 <= 32, "FULL / FREE words");
     static constexpr int FREE = 32;       // int[PS_NSLOT]: consumer releases of the slot
     static constexpr int SYNC = 64;       // int: consumer barrier counter
     static constexpr int GATH = 68;       // int: consumer waves sweeping another CU's data (the loader thins)
@@ -313,10 +316,19 @@ __device__ __forceinline__ int slot_regions(const PsOp& op, int ua, int ub, Regi
 // ---- the loader (wave 0) ----
 __device__ __forceinline__ void ps_loader(const PsArgs& a, lchar* smem, int cu, int ncu) {
     const int lane = threadIdx.x & 63;
+    const int nslot = a.nslot;
     lint* full = reinterpret_cast<lint*>(smem + a.ctl_off + Ctl::FULL);
     lint* fre = reinterpret_cast<lint*>(smem + a.ctl_off + Ctl::FREE);
-    lint* gath = reinterpret_cast<lint*>(smem + a.ctl_off + Ctl::GATH);
-    int seq = 0, prev_cnt = -1;   // fills issued; instructions of fill seq - 1 (-1: marked)
+    // fills in flight (up to PS_DEPTH): fill seq - nin .. seq - 1, c0 the oldest's DMA count
+    int seq = 0, nin = 0, c0 = 0, c1 = 0, c2 = 0;
+    auto mark_oldest = [&](int younger) {   // wait for the oldest in-flight fill, publish it
+        vm_wait(younger);
+        const int f = seq - nin;
+        lds_st_asm(full + f % nslot, f + 1);
+        c0 = c1;
+        c1 = c2;
+        --nin;
+    };
     Guard g;
     for (int l = 0; l < a.n_layer; ++l) {
         const PsLayer* Lp = a.layers + l;
@@ -328,24 +340,13 @@ __device__ __forceinline__ void ps_loader(const PsArgs& a, lchar* smem, int cu, 
             unit_span(op.units, cu, ncu, u0, u1);
             for (int ua = u0; ua < u1; ua += op.ups) {
                 const int ub = min(u1, ua + op.ups);
-                const int s = seq % PS_NSLOT, use = seq / PS_NSLOT;
-                if (use > 0) {
-                    // the slot's previous data must be released by every consumer; first let the
-                    // consumers have the fill still in flight
-                    if (prev_cnt >= 0 && lds_ld_asm(fre + s) < use * PS_NC) {
-                        vm_wait(0);
-                        lds_st_asm(full + (seq - 1) % PS_NSLOT, seq);
-                        prev_cnt = -1;
-                    }
+                const int s = seq % nslot, use = seq / nslot;
+                if (use > 0 && lds_ld_asm(fre + s) < use * PS_NC) {
+                    // the slot's previous data is still being read: publish what is in flight
+                    // first, then wait for the release
+                    while (nin > 0) mark_oldest(nin == 3 ? c1 + c2 : nin == 2 ? c1 : 0);
                     while (lds_ld_asm(fre + s) < use * PS_NC)
                         if (!g.ok(a.err, 0x101)) return;
-                }
-                if (prev_cnt >= 0 && lds_ld_asm(gath) > 0) {
-                    // consumers are sweeping other CUs' outputs: keep one fill in flight, so their
-                    // loads do not queue behind a refill burst (MI355X guide, gather-pass)
-                    vm_wait(0);
-                    lds_st_asm(full + (seq - 1) % PS_NSLOT, seq);
-                    prev_cnt = -1;
                 }
                 Region rg[2][4];
                 slot_regions(op, ua, ub, rg);
@@ -368,19 +369,16 @@ __device__ __forceinline__ void ps_loader(const PsArgs& a, lchar* smem, int cu, 
                         }
                     }
                 }
-                if (prev_cnt >= 0) {   // fill seq - 1 has landed once only this fill is outstanding
-                    vm_wait(cnt);
-                    lds_st_asm(full + (seq - 1) % PS_NSLOT, seq);
-                }
-                prev_cnt = cnt;
+                if (nin == 0) c0 = cnt;
+                else if (nin == 1) c1 = cnt;
+                else c2 = cnt;
+                ++nin;
                 ++seq;
+                if (nin == PS_DEPTH) mark_oldest(c1 + c2);   // PS_DEPTH 3: the two younger stay in flight
             }
         }
     }
-    if (prev_cnt >= 0) {
-        vm_wait(0);
-        lds_st_asm(full + (seq - 1) % PS_NSLOT, seq);
-    }
+    while (nin > 0) mark_oldest(nin == 3 ? c1 + c2 : nin == 2 ? c1 : 0);
     if (a.stamps && lane == 0) a.stamps[blockIdx.x * 16 + 14] = rt_now();
 }
 
@@ -545,7 +543,7 @@ __device__ __forceinline__ bool ps_op(const PsArgs& a, const PsLayer& L, const P
     }
     for (int ua = u0; ua < u1; ua += op.ups) {
         const int ub = min(u1, ua + op.ups);
-        const int s = oc.seq % PS_NSLOT;
+        const int s = oc.seq % a.nslot;
         {
             Guard g;
             while (__hip_atomic_load(full + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != oc.seq + 1)
@@ -1115,7 +1113,8 @@ PsStep* ps_create(const PsConfig& c, const std::vector<PsLayerDesc>& layers, std
     const int act_region = std::max(((int)act_layout(std::max(c.n_embd, c.n_ff), 1, 0).slot_bytes + 15) / 16 * 16,
                                     hpb * ATTN_SHORT * 4 + PS_NC * 256 * 4);
     const int lds_max = 160 * 1024;
-    const int slot = ((lds_max - act_region - PS_CTL) / PS_NSLOT) & ~1023;
+    const int nslot = 6;
+    const int slot = ((lds_max - act_region - PS_CTL) / nslot) & ~1023;
     if (slot < 8192) return fail("LDS");
     auto* s = new PsStep();
     std::vector<PsLayer> hl(c.n_layer);
@@ -1198,7 +1197,8 @@ PsStep* ps_create(const PsConfig& c, const std::vector<PsLayerDesc>& layers, std
     a.g_h = a.g_xa + c.n_embd;
     a.err = c.err;
     a.slot_bytes = slot;
-    a.act_off = PS_NSLOT * slot;
+    a.nslot = nslot;
+    a.act_off = nslot * slot;
     a.ctl_off = a.act_off + act_region;
     s->lds = (size_t)a.ctl_off + PS_CTL;
     s->ncu = ncu;
