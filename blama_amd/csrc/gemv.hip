@@ -67,7 +67,6 @@ struct GvArgs {
                                   // 4: waves [0, npro) build the activation (staged by LDS-DMA)
                                   // while the others stream, then stream themselves
     int npro;                     // order 4: prologue waves
-    int touch;                    // order 4: wave npro prefetches the workgroup's share into L2
     int stage_off;                // order 4: LDS byte offset of the staged activation arrays
     int flag_off;                 // order 4: LDS byte offset of the [2][GV_NW] flag words
     int pre;                      // ring items issued before the prologue (the rest after it)
@@ -430,7 +429,6 @@ __device__ __forceinline__ void gv_body(const GvArgs& a, char* lds, Wait&& wait 
             rope[2 * i + 1] = sinf(th);
         }
     };
-    unsigned touch_sink = 0;   // order 4 + touch: the VGPR the L2 prefetch loads write
     if (order4) {
         // ---- prologue waves (order 4) ----------------------------------------------------------
         // A wave that has issued its weight ring cannot run the prologue: its later instructions
@@ -482,36 +480,6 @@ __device__ __forceinline__ void gv_body(const GvArgs& a, char* lds, Wait&& wait 
         };
         const unsigned pmask = (1u << npro) - 1u;
         if (!pw) {
-            if (a.touch && wave == npro) {
-                // L2 prefetch of the workgroup's whole share (every row of its units, one dword
-                // per 128-byte line), ahead of this wave's ring: the later ring requests of every
-                // wave then hit L2.  The touch loads are invisible to the compiler (one pinned
-                // VGPR, written in order); they precede every load this wave waits for, so its
-                // vmcnt waits cover them.
-                const int M = S.units > wg ? (S.units - wg + S.nblk - 1) / S.nblk : 0;
-#pragma unroll
-                for (int pl = 0; pl < 4; ++pl) {
-                    constexpr int bpa[4] = {PlaneBytes<T>::b[0], PlaneBytes<T>::b[1], PlaneBytes<T>::b[2], PlaneBytes<T>::b[3]};
-                    if (bpa[pl] == 0) continue;
-                    const long long rowb = (long long)nb * bpa[pl];
-                    const int Lp = (int)((rowb + 127) / 128);
-                    const long long ex = (long long)S.rows * rowb;
-#pragma unroll
-                    for (int r = 0; r < RW; ++r) {
-                        const bool isB = ab && r == 1;
-                        const uint8_t* base = isB ? S.b[pl] + eB * ex : S.a[pl] + eA * ex;
-                        const __amdgpu_buffer_rsrc_t rs = buf_rsrc(rfl_ptr(base));
-                        for (int i = lane; i < M * Lp; i += 64) {
-                            const int m = i / Lp, l = i - m * Lp;
-                            const long long u = wg + (long long)m * S.nblk;
-                            long long row = ab ? u : u * RW + r;
-                            if (row >= S.rows) row = S.rows - 1;
-                            const unsigned off = (unsigned)(row * rowb + (long long)l * 128);
-                            asm volatile("buffer_load_dword %0, %1, %2, 0 offen" : "+v"(touch_sink) : "v"(off), "s"(rs) : "memory");
-                        }
-                    }
-                }
-            }
             if (rope_wave) {   // before its ring: the table is on the critical path of the epilogue
                 rope_table(readfirstlane_i(tp.y), ff0, ff1);
                 __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the table is written
@@ -867,7 +835,6 @@ __device__ __forceinline__ void gv_body(const GvArgs& a, char* lds, Wait&& wait 
             }
         }
     }
-    asm volatile("" ::"v"(touch_sink));   // pinned to the end (no other value may take the VGPR)
     GV_STAMP(4)
 #ifdef MI_STAMPS   // 5: the workgroup's last wave to finish
     if (a.stamps && lane == 0) atomicMax(a.stamps + blockIdx.x * 8 + 5, (unsigned long long)__builtin_amdgcn_s_memrealtime());
@@ -977,10 +944,7 @@ size_t gv_lds_total(const GvArgs& a, int nb, int pro) {
 }
 
 // cap on workgroups: the weight ring keeps D items x RW rows in flight per wave
-int gv_grid_cap() {
-    static const int cap = getenv("MI_GEMV_GRID") ? std::max(1, atoi(getenv("MI_GEMV_GRID"))) : 256;
-    return cap;
-}
+int gv_grid_cap() { return 256; }
 
 }  // namespace
 
@@ -1116,22 +1080,17 @@ static void gv_prepare(const GemvParams& p, int cap, GvArgs& a, int& grid_out, G
     a.kv_dim = p.kv_dim;
     a.stamps = p.stamps;
     // default: prologue waves (order 4; +2 % decode over order 0 on two boxes)
-    static const int order = getenv("MI_GEMV_ORDER") ? atoi(getenv("MI_GEMV_ORDER")) : 4;
-    static const int pre = getenv("MI_GEMV_PRE") ? atoi(getenv("MI_GEMV_PRE")) : 8;
-    a.order = order;
-    a.pre = pre;
+    a.order = 4;
+    a.pre = 8;
     // order 4 (prologue waves): not for the GPT-2 launches (LayerNorm) nor a WO launch that adds
     // the splits of a long-context attention; too wide to stage -> order 0
     if (a.order == 4 && (key.tag == 2 || p.pro == PRO_LAYERNORM || (p.pro == PRO_ATTN && p.attn_nsplit != 1))) a.order = 0;
     {
-        static const int npro_env = getenv("MI_GEMV_NPRO") ? atoi(getenv("MI_GEMV_NPRO")) : 0;
         const int nb = p.K / 256;
-        // (default 8 from K = 4096 up: 556 vs 548 tok/s against ceil(nb/4) = 4 on the 7B, same box;
-        // 2 prologue waves: 455.  Narrower K keeps ceil(nb/4), the r04 rule it was measured with)
-        a.npro = npro_env > 0 ? npro_env : (nb >= 16 ? 8 : (nb + 3) / 4);
+        // 8 from K = 4096 up: 556 vs 548 tok/s against ceil(nb/4) = 4 on the 7B, same box; 2 prologue
+        // waves: 455.  Narrower K keeps ceil(nb/4), the r04 rule it was measured with
+        a.npro = nb >= 16 ? 8 : (nb + 3) / 4;
         a.npro = std::max(1, std::min(a.npro, std::min(GV_NW - 2, nb)));
-        static const int touch_env = getenv("MI_GEMV_TOUCH") ? atoi(getenv("MI_GEMV_TOUCH")) : 0;
-        a.touch = touch_env;
     }
     a.stage_off = (int)((gv_lds_bytes(p.K / 256, a.nslots, p.n_rot) + 15) & ~(size_t)15);
     a.flag_off = a.stage_off + gv_stage_arrays(p.pro, a.nslots) * (p.K / 256) * 1024;

@@ -1027,6 +1027,175 @@ __global__ __launch_bounds__(256 * HG) void attn_fused_kernel(const AttnParams P
 #endif
 }
 
+// The streaming decode step's attention (one token, contexts within ATTN_SHORT cells, the output
+// quantised into P.act_out): attn_fused_kernel's arithmetic for one q head per group (R = 1: a kv
+// head per group, or a q head of a GQA kv head with qsplit), with NWV waves per group -- twice the
+// fused kernel's 4, so each wave walks half the cells -- and the score reductions on DPP (the
+// fused kernel's ds_bpermute shuffles were one LDS round trip each).  f16(q) . k over the f16
+// cache, scale, causal mask by cell position, the exact softmax (global max; the double sum of
+// expf(w - max); p = f16(e * (1/sum))), sum_c f16(p_c) v_c; then whole 256-blocks of the output
+// (HG groups) quantised as the WO launch's activation.
+template <int CTRL, int RMASK>
+__device__ __forceinline__ float dppf(float v, float old) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(v), CTRL, RMASK, 0xf, false));
+}
+// max over the wave of any floats (-inf identity), every lane
+__device__ __forceinline__ float wave_max_any(float v) {
+    const float ni = -INFINITY;
+    v = fmaxf(v, dppf<0x111, 0xf>(v, ni));
+    v = fmaxf(v, dppf<0x112, 0xf>(v, ni));
+    v = fmaxf(v, dppf<0x114, 0xf>(v, ni));
+    v = fmaxf(v, dppf<0x118, 0xf>(v, ni));
+    v = fmaxf(v, dppf<0x142, 0xa>(v, ni));
+    v = fmaxf(v, dppf<0x143, 0xc>(v, ni));
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+template <int LPC, int HG, int NWV>
+__global__ __launch_bounds__(64 * NWV * HG) void attn_dec_kernel(const AttnParams P) {
+    static_assert(LPC == 8 || LPC == 16, "head_dim 64 or 128");
+    constexpr int HD = LPC * 8, CPW = 64 / LPC, NT = 64 * NWV, STEP = NWV * CPW;
+    constexpr int U = 2;   // cell steps per wave whose cache rows are requested at entry
+    __shared__ float sw[HG][ATTN_SHORT];
+    __shared__ float redm[HG][NWV];
+    __shared__ double dred[HG][NWV];
+    __shared__ float red_o[HG][NWV][HD];
+    const int grp = (int)threadIdx.x / NT;
+    const int tid = (int)threadIdx.x % NT, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int unit = (int)blockIdx.x * HG + grp;   // this group's q head
+    const int g = P.qsplit ? unit / P.qsplit : unit;   // its kv head
+    const int L = lane % LPC, G = lane / LPC;
+    const int tp2 = P.tokpos[2], qpos = P.tokpos[1];
+    const int ncell = min(tp2 + 1, ATTN_SHORT);
+    // the first U steps' K / V rows and positions, requested before anything waits
+    u32x4 k0[U], v0[U];
+    int cp0[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int c = min(wave * CPW + u * STEP + G, P.n_ctx - 1);
+        k0[u] = *gptr(reinterpret_cast<const u32x4*>(P.kcache + (long long)c * P.kv_dim + (long long)g * HD + L * 8));
+        v0[u] = *gptr(reinterpret_cast<const u32x4*>(P.vcache + (long long)c * P.kv_dim + (long long)g * HD + L * 8));
+        cp0[u] = gptr(P.cell_pos)[c];
+    }
+    float q[8];
+    {
+        const f32x4 a = gptr(reinterpret_cast<const f32x4*>(P.q + (long long)unit * HD + L * 8))[0];
+        const f32x4 b = gptr(reinterpret_cast<const f32x4*>(P.q + (long long)unit * HD + L * 8))[1];
+        const float t[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) q[e] = __half2float(__float2half_rn(t[e]));
+    }
+    auto cvt8 = [](const u32x4& w, float (&f)[8]) {
+        const unsigned ww[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            f[2 * e] = h2f(ww[e]);
+            f[2 * e + 1] = h2f(ww[e] >> 16);
+        }
+    };
+    // 1. scaled KQ of every cell into LDS (lane L == 0 of each cell's group), the wave's maximum
+    float mx = -INFINITY;
+    auto score = [&](int c, const u32x4& kk, int cp) {
+        float kf[8];
+        cvt8(kk, kf);
+        float d = 0.0f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) d = fmaf(q[e], kf[e], d);
+        d += dppf<0xB1, 0xf>(d, 0.0f);    // quad_perm [1,0,3,2]
+        d += dppf<0x4E, 0xf>(d, 0.0f);    // quad_perm [2,3,0,1]: every lane its quad's sum
+        d += dppf<0x141, 0xf>(d, 0.0f);   // row_half_mirror: the 8-lane group's sum
+        if (LPC == 16) d += dppf<0x140, 0xf>(d, 0.0f);   // row_mirror: the 16-lane row's
+        const bool valid = c < ncell && cp <= qpos;
+        const float w = valid ? d * P.scale : -INFINITY;
+        mx = fmaxf(mx, w);
+        if (L == 0 && c < ncell) sw[grp][c] = w;
+    };
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int c = wave * CPW + u * STEP + G;
+        if (wave * CPW + u * STEP < ncell) score(c, k0[u], cp0[u]);
+    }
+    for (int cb = wave * CPW + U * STEP; cb < ncell; cb += STEP) {
+        const int c = min(cb + G, ncell - 1);
+        const u32x4 kk = *gptr(reinterpret_cast<const u32x4*>(P.kcache + (long long)c * P.kv_dim + (long long)g * HD + L * 8));
+        const int cp = gptr(P.cell_pos)[c];
+        score(cb + G, kk, cp);
+    }
+    const float wm = wave_max_any(mx);
+    if (lane == 0) redm[grp][wave] = wm;
+    __syncthreads();
+    float M = redm[grp][0];
+#pragma unroll
+    for (int w = 1; w < NWV; ++w) M = fmaxf(M, redm[grp][w]);
+    // 2. sum over every cell of expf(w - M) in double, fixed order (a cell per thread, waves in order)
+    {
+        double acc = 0.0;
+        for (int c = tid; c < ncell; c += NT) acc += (double)expf(sw[grp][c] - M);
+        acc = wave_sum63_d(acc);
+        if (lane == 63) dred[grp][wave] = acc;
+    }
+    __syncthreads();
+    double tot = 0.0;
+#pragma unroll
+    for (int w = 0; w < NWV; ++w) tot += dred[grp][w];
+    const float inv = (float)(1.0 / tot);
+    // 3. sum_c f16(p_c) v_c over the wave's cells, then the wave's cell groups, then the waves in order
+    float o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = 0.0f;
+    auto pv = [&](int c, const u32x4& vv) {
+        float vf[8];
+        cvt8(vv, vf);
+        const bool in = c < ncell;
+        const float p = expf(sw[grp][in ? c : 0] - M) * inv;   // ggml_vec_soft_max_f32, f16 vec_dot_type
+        const float pw = in ? __half2float(__float2half_rn(p)) : 0.0f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = fmaf(pw, vf[e], o[e]);
+    };
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int c = wave * CPW + u * STEP + G;
+        if (wave * CPW + u * STEP < ncell) pv(c, v0[u]);
+    }
+    for (int cb = wave * CPW + U * STEP; cb < ncell; cb += STEP) {
+        const int c = min(cb + G, ncell - 1);
+        const u32x4 vv = *gptr(reinterpret_cast<const u32x4*>(P.vcache + (long long)c * P.kv_dim + (long long)g * HD + L * 8));
+        pv(cb + G, vv);
+    }
+#pragma unroll
+    for (int off = LPC; off < 64; off <<= 1)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] += __shfl_xor(o[e], off, 64);
+    if (G == 0) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) red_o[grp][wave][L * 8 + e] = o[e];
+    }
+    __syncthreads();
+    for (int d = tid; d < HD; d += NT) {
+        float s = red_o[grp][0][d];
+#pragma unroll
+        for (int w = 1; w < NWV; ++w) s += red_o[grp][w][d];
+        P.part_o[(long long)unit * HD + d] = s;
+    }
+    // the WO launch's quantised activation: the workgroup's HG heads are whole 256-blocks, one
+    // wave per block; element e of the workgroup's span is head e / HD, dim e % HD
+    constexpr int NE = HG * HD;
+    const int gw = (int)threadIdx.x >> 6;
+    const int e0 = (int)blockIdx.x * NE;
+    for (int b = gw; b < NE / 256; b += HG * NWV) {
+        float v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int e = b * 256 + lane * 4 + k, gg = e / HD, d = e % HD;
+            float s = red_o[gg][0][d];
+#pragma unroll
+            for (int w = 1; w < NWV; ++w) s += red_o[gg][w][d];
+            v[k] = s;
+        }
+        dv_quant_block(P.act_out, e0 / 256 + b, v, lane);
+    }
+}
+
 typedef void (*AttnFn)(const AttnParams);
 // Can `need` workgroups of attn_long_kernel (256 threads, `lds` dynamic LDS) be resident on the
 // current device at once?  The splits of a head spin on each other, so they all must be.
@@ -1137,7 +1306,25 @@ void launch_attn(const AttnParams& p, hipStream_t s) {
             throw Error("attn: no quantising decode kernel for this head geometry");
         AttnParams q = p;
         q.qsplit = k.qsplit;
-        hipLaunchKernelGGL(k.f, dim3(k.units / k.hg), dim3(256 * k.hg), 0, s, q);
+        // one q head per group (R = 1) of head_dim 64 / 128: the decode kernel with 16 waves per
+        // workgroup (attn_dec_kernel); otherwise the fused kernel
+        AttnFn fd = nullptr;
+        int nwv = 4;
+        if (k.hg > 1 || k.qsplit || r == 1) {
+            switch (p.head_dim * 8 + k.hg) {
+            case 128 * 8 + 1: fd = attn_dec_kernel<16, 1, 16>; nwv = 16; break;
+            case 128 * 8 + 2: fd = attn_dec_kernel<16, 2, 8>; nwv = 8; break;
+            case 64 * 8 + 1: fd = attn_dec_kernel<8, 1, 16>; nwv = 16; break;
+            case 64 * 8 + 2: fd = attn_dec_kernel<8, 2, 8>; nwv = 8; break;
+            case 64 * 8 + 4: fd = attn_dec_kernel<8, 4, 4>; nwv = 4; break;
+            default: break;
+            }
+        }
+        if (fd) {
+            hipLaunchKernelGGL(fd, dim3(k.units / k.hg), dim3(64 * nwv * k.hg), 0, s, q);
+        } else {
+            hipLaunchKernelGGL(k.f, dim3(k.units / k.hg), dim3(256 * k.hg), 0, s, q);
+        }
         MI_HIP(hipGetLastError());
         return;
     }
