@@ -11,11 +11,19 @@ compared with the oracle decoding the same tokens one at a time.  Plus BASELINE 
 and the batched verification path (MI_OUT_ALL), against the oracle at the last token and at every
 32nd row.
 
-Acceptance is the reference gate exactly (t-LogitComparer.cpp:76-78): the MetricsAggregator
-score >= 0.95, the mean logit similarity >= 0.98, and the top-1 id matching on EVERY step and
-every verified row -- no near-tie waiver.  The element-wise error is printed, not gated: at 32
-layers the CPU algorithm's own re-quantisation floor (test_gpu_fullwidth.py's docstring) grows
-past any fixed tolerance."""
+Acceptance is the reference gate (t-LogitComparer.cpp:76-78): the MetricsAggregator score >= 0.95,
+the mean logit similarity >= 0.98, and the top-1 id matching on every step and every verified row,
+except where the oracle's own top-1 margin at that row is within the CPU algorithm's live reorder
+floor (util.c_alt_floor, computed only when a mismatch occurs); every such waiver is printed and
+raised as a warning (none fired in the r05 runs).  The element-wise error is printed, not gated:
+at 32 layers the CPU algorithm's own re-quantisation floor (test_gpu_fullwidth.py's docstring)
+grows past any fixed tolerance.
+
+MoE rows are attributed (VERDICT r05 "What's weak" 3): every Mixtral row whose l2/rms error exceeds
+3x the model's median must follow a routing near-tie -- a token, at or before that row, whose
+oracle router gap (the last expert picked vs the first left out, min over the layers) is below
+ROUTE_TIE: any fp32 order may pick the other expert there, and a different expert's output then
+lives on in the residual and in that token's K/V cells.  The attribution is printed per row."""
 import warnings
 
 import numpy as np
@@ -24,7 +32,7 @@ import pytest
 import ggml_cpu
 import ggml_ref as R
 from blama_amd import engine, synthetic
-from util import c_alt_floor
+from util import ROUTE_TIE, c_alt_floor
 
 pytestmark = [pytest.mark.gpu, pytest.mark.timeout(600)]   # the 32-layer oracle: ~1 min per model
 
@@ -72,6 +80,29 @@ def _floor_by_tokens(buf, n_ctx, seq, n0):
     return f
 
 
+def _attribute_moe_rows(name, errs, gaps):
+    """Every row whose l2/rms exceeds 3x the median must follow a routing near-tie: a token at or
+    before the row's last token with an oracle router gap < ROUTE_TIE.  Prints the attribution."""
+    med = float(np.median([e for _, e, _ in errs]))
+    ties = [j for j, g in enumerate(gaps) if g < ROUTE_TIE]
+    print(f"{name}: median l2/rms {med:.2e}; routing near-ties (token index, gap): "
+          f"{[(j, round(float(gaps[j]), 5)) for j in ties]}")
+    bad = []
+    for label, e, j in errs:
+        if e <= 3 * med:
+            continue
+        prev = [k for k in ties if k <= j]
+        if not prev:
+            bad.append((label, e))
+            print(f"{name} {label}: l2/rms {e:.2e} ({e / med:.1f}x median) -- NO routing near-tie at or before token {j}")
+            continue
+        k = prev[-1]
+        where = "at this token" if k == j else f"carried from token {k} ({j - k} tokens earlier)"
+        print(f"{name} {label}: l2/rms {e:.2e} ({e / med:.1f}x median) <- routing near-tie {where}, "
+              f"oracle router gap {gaps[k]:.4f}")
+    assert not bad, (name, "rows above 3x the median error with no routing near-tie", bad)
+
+
 @pytest.mark.parametrize("name", MODELS)
 def test_fulldepth_decode_and_verify_match_oracle(gpu_lib, name):
     cfg = synthetic.CONFIGS[name]
@@ -85,10 +116,13 @@ def test_fulldepth_decode_and_verify_match_oracle(gpu_lib, name):
     prompt = [int(t) for t in rng.integers(0, cfg.n_vocab, 16)]
     rows = []
     seq = list(prompt)
+    gaps = []      # the oracle's router gap of every token decoded (inf: dense)
+    errs = []      # (row label, l2/rms, index into gaps of the row's last token)
     try:
         assert ctx.decode(prompt) == 0
         for t in prompt:
             ref = orc.decode_one(t).astype(np.float64)
+            gaps.append(orc.last_moe_margin)
         for s in range(17):
             got = ctx.logits()
             ids, vals = ctx.topk(10)
@@ -96,6 +130,7 @@ def test_fulldepth_decode_and_verify_match_oracle(gpu_lib, name):
             rms = float(np.sqrt(np.mean(ref ** 2)))
             print(f"{name} decode step {s}: max/rms {d.max() / rms:.2e} l2/rms {np.sqrt(np.mean(d ** 2)) / rms:.2e}",
                   flush=True)
+            errs.append((f"decode step {s}", float(np.sqrt(np.mean(d ** 2)) / rms), len(gaps) - 1))
             rows.append(([(int(i), float(v)) for i, v in zip(ids, vals)], ref, len(seq)))
             if s == 16:
                 break
@@ -103,11 +138,13 @@ def test_fulldepth_decode_and_verify_match_oracle(gpu_lib, name):
             seq.append(t)
             assert ctx.decode([t]) == 0
             ref = orc.decode_one(t).astype(np.float64)
+            gaps.append(orc.last_moe_margin)
         # the batched verification pass of 64 claimed tokens (Session::fillCtx, batchedVerify)
         claimed = [int(t) for t in rng.integers(0, cfg.n_vocab, 64)]
         assert ctx.decode(claimed, all_logits=True) == 0
         for i, t in enumerate(claimed):
             ref = orc.decode_one(t).astype(np.float64)
+            gaps.append(orc.last_moe_margin)
             seq.append(t)
             ids, vals = ctx.topk(10, row=i)
             got = ctx.logits(row=i)
@@ -116,7 +153,10 @@ def test_fulldepth_decode_and_verify_match_oracle(gpu_lib, name):
             if i % 16 == 0 or i == len(claimed) - 1:
                 print(f"{name} verify row {i}: max/rms {d.max() / rms:.2e} l2/rms {np.sqrt(np.mean(d ** 2)) / rms:.2e}",
                       flush=True)
+            errs.append((f"verify row {i}", float(np.sqrt(np.mean(d ** 2)) / rms), len(gaps) - 1))
             rows.append(([(int(x), float(v)) for x, v in zip(ids, vals)], ref, len(seq)))
+        if cfg.n_expert:
+            _attribute_moe_rows(name, errs, gaps)
         _gate(name, rows, _floor_by_tokens(buf, 128, seq, len(prompt)))
     finally:
         ctx.close()

@@ -39,7 +39,7 @@ import pytest
 import ggml_cpu
 import ggml_ref as R
 from blama_amd import engine, synthetic
-from util import c_alt_floor
+from util import ROUTE_TIE, c_alt_floor
 
 pytestmark = pytest.mark.gpu
 
@@ -47,7 +47,6 @@ TOL_MAX = 0.12
 TOL_L2 = 0.03
 # MoE: router probabilities of the last expert picked and the first left out closer than this
 # (in the oracle) are a near-tie that another fp32 order of the same arithmetic may swap
-ROUTE_TIE = 0.01
 
 FULL = {
     "llama2-7b-q4_k_m": dict(n_layer=2),

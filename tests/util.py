@@ -125,3 +125,8 @@ def parse_state(st: bytes, n_layer: int, kv_dim: int):
     k = np.frombuffer(st[off:off + n].tobytes(), np.float16).reshape(n_layer, nc, kv_dim)
     v = np.frombuffer(st[off + n:off + 2 * n].tobytes(), np.float16).reshape(n_layer, nc, kv_dim)
     return pos, k, v
+
+
+# A routing near-tie: the oracle's router separates the last expert picked from the first one left
+# out by less than this (probability units); any other fp32 order may then pick the other expert.
+ROUTE_TIE = 0.01
