@@ -859,7 +859,7 @@ int32_t mi_op_gemm(int32_t device, int32_t type, const void* raw, const void* ra
         // up to MMQS_MAX tokens: the short-batch GEMM (K-part sums, added by part_sum) as the
         // engine's verification batches take it; MI_MMQS_MAX=0: the tiled GEMM for every count
         const char* ms = getenv("MI_MMQS_MAX");
-        const bool short_b = ntok <= (ms ? atoi(ms) : MMQS_MAX);
+        const bool short_b = ntok <= (ms ? std::min(MMQS_MAX, std::max(0, atoi(ms))) : MMQS_MAX);   // as Ctx::Ctx clamps it
         if (short_b) {
             const int pst = pair ? 2 * rows : rows;
             DevBuf part((size_t)mmqs_parts(K) * ntok * pst * sizeof(float));

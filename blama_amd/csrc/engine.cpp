@@ -636,7 +636,7 @@ Ctx::Ctx(Model* model, uint32_t nctx, uint32_t nbatch, uint32_t nubatch) : m(mod
             // no room for the copy: prompt batches fall back to the v_dot4 GEMM
             mmq_ok = m->ensure_mmq_copies();
             out_mmq = mmq_ok && mmq32_supported(m->output.type);
-            attn_mfma = attn_mfma_supported(hp.head_dim) && getenv("MI_ATTN_VALU") == nullptr;
+            attn_mfma = attn_mfma_supported(hp.head_dim);
             MI_HIP(hipMalloc(&ub_q, (size_t)UB_MAX * kmax));
             MI_HIP(hipMalloc(&ub_dT, (size_t)UB_MAX * (kmax / 32) * sizeof(float)));   // Q8_0: per 32
             MI_HIP(hipMalloc(&ub_bsb, (size_t)UB_MAX * (kmax / 256) * 16));
@@ -661,12 +661,11 @@ Ctx::Ctx(Model* model, uint32_t nctx, uint32_t nbatch, uint32_t nubatch) : m(mod
             }
             MI_HIP(hipMalloc(&ub_rope, (size_t)UB_MAX * std::max(1, hp.n_rot / 2) * sizeof(float2)));
             // split-K partials of the residual GEMMs (WO, FFN down) of dense models
-            static const bool ksplit_env = getenv("MI_MMQ_KSPLIT") == nullptr || atoi(getenv("MI_MMQ_KSPLIT")) != 0;
-            if (ksplit_env && mmq2_active())
+            if (mmq2_active())
                 MI_HIP(hipMalloc(&ub_part, (size_t)2 * UB_MAX * hp.n_embd * sizeof(float)));
             mmqs_max = getenv("MI_MMQS_MAX") ? std::min(MMQS_MAX, std::max(0, atoi(getenv("MI_MMQS_MAX")))) : MMQS_MAX;
             // MoE: short batches when every expert matrix has the grouped form (k-quants)
-            moe_short = hp.n_expert > 0 && getenv("MI_MOE_SHORT_OFF") == nullptr;
+            moe_short = hp.n_expert > 0;
             for (const Layer& L : m->layers)
                 moe_short = moe_short && mmqs_grouped_supported(L.gate.type) && L.up.type == L.gate.type &&
                             mmqs_grouped_supported(L.down.type);
@@ -739,7 +738,7 @@ Ctx::~Ctx() {
                     (void*)xb, (void*)qb, (void*)attnb, (void*)hb, (void*)tokpos_b, (void*)ub_q, (void*)ub_dT, (void*)ub_bsb, (void*)ub_rope, (void*)ub_part, (void*)ub_spart,
                     (void*)ub_q0, (void*)ub_dT0, (void*)yb, (void*)sel_b, (void*)selw_b, (void*)moe_rows, (void*)moe_pos,
                     (void*)moe_rowsel, (void*)moe_grp, (void*)moe_q, (void*)moe_dT, (void*)moe_bsb,
-                    (void*)logits_all, (void*)grows_ids, (void*)grows_out, (void*)sp_mem, (void*)ps_xout})
+                    (void*)logits_all, (void*)grows_ids, (void*)grows_out, (void*)sp_mem, (void*)sp_gx, (void*)sp_gh, (void*)ps_xout})
         if (p) hipFree(p);
     for (void* p : {(void*)h_tokpos, (void*)h_topk_ids, (void*)h_topk_vals, (void*)h_logits, (void*)h_gather, (void*)h_grows,
                     (void*)h_tokpos_b, (void*)h_attn_xerr})
@@ -986,6 +985,11 @@ bool Ctx::sp_setup() {
     MI_HIP(hipSetDevice(device));
     MI_HIP(hipMalloc(&sp_mem, 4 * act_n + act_f));
     MI_HIP(hipMemset(sp_mem, 0, 4 * act_n + act_f));
+    MI_HIP(hipMalloc(&sp_gx, (size_t)hp.n_embd * 8));
+    MI_HIP(hipMemset(sp_gx, 0, (size_t)hp.n_embd * 8));
+    MI_HIP(hipMalloc(&sp_gh, (size_t)hp.n_ff * 8));
+    MI_HIP(hipMemset(sp_gh, 0, (size_t)hp.n_ff * 8));
+    sp_fuse = hp.n_embd <= 8192 ? (getenv("MI_DV_FUSE") ? atoi(getenv("MI_DV_FUSE")) : 1) : 0;
     sp_act[0] = sp_mem;
     sp_act[1] = sp_mem + act_n;
     sp_act[2] = sp_mem + 2 * act_n;
@@ -1006,6 +1010,22 @@ void Ctx::enqueue_step_sp(bool with_logits) {
     const float kq_scale = 1.0f / std::sqrt((float)hp.head_dim);
     auto act = [&](int role, int fmt, int K, const float* norm_w) {
         return ActOut{K, fmt & 1, fmt >> 1, sp_act[role], norm_w, hp.eps};
+    };
+    // the in-launch activation of a residual / SwiGLU launch: edge e (1 WO, 2 gate/up, 3 down) of
+    // layer l; tag = step * (3 n_layer + 1) + 3 l + e, unique per step, layer and edge
+    const int fuse_m = sp_fuse;   // 1 every edge, 2 h only, 3 the normed x edges only
+    auto fused = [&](int e) { return fuse_m == 1 || (fuse_m == 2 && e == 2) || (fuse_m == 3 && e != 2); };
+    auto qout = [&](const ActOut& t, unsigned long long* g, int l, int e) {
+        DvQuantOut o;
+        std::memset(&o, 0, sizeof(o));
+        if (!fused(e)) return o;
+        o.t = t;
+        o.gran = g;
+        o.step = step_ctr;
+        o.tag_mul = 3u * (unsigned)hp.n_layer + 1u;
+        o.tag_add = 3u * (unsigned)l + (unsigned)e;
+        o.err = d_attn_xerr;
+        return o;
     };
     if (on()) {
         EmbedParams ep{m->tok_embd, tokpos, x, hp.n_embd, m->pos_embd, 0, step_ctr};
@@ -1063,9 +1083,10 @@ void Ctx::enqueue_step_sp(bool with_logits) {
             p.nseg = 1;
             p.seg[0] = seg_of(L.wo, PAIR_ADJ, EPI_ADD, x);
             p.seg[0].resid = x;
+            p.qout = qout(act(2, b.fC, hp.n_embd, L.ffn_norm), sp_gx, l, 1);
             if (on()) {
                 launch_dgemv(p, stream);
-                launch_dv_quant(x, act(2, b.fC, hp.n_embd, L.ffn_norm), stream);
+                if (!fused(1)) launch_dv_quant(x, act(2, b.fC, hp.n_embd, L.ffn_norm), stream);
             }
         }
         {   // FFN gate/up + SwiGLU, then h quantised
@@ -1076,11 +1097,12 @@ void Ctx::enqueue_step_sp(bool with_logits) {
             p.nseg = 1;
             p.seg[0] = seg_of(L.gate, PAIR_AB, EPI_SWIGLU, h);
             p.seg[0].B = L.up;
+            p.qout = qout(act(3, b.fD, hp.n_ff, nullptr), sp_gh, l, 2);
             if (l == prof_layer) seg = 1;
             const bool timed = l == prof_layer && seg_filter == 1;
             if (on()) launch_dgemv(p, stream, timed ? prof_ev[0] : nullptr, timed ? prof_ev[1] : nullptr);
             if (l == prof_layer) seg = 2;
-            if (on()) launch_dv_quant(h, act(3, b.fD, hp.n_ff, nullptr), stream);
+            if (on() && !fused(2)) launch_dv_quant(h, act(3, b.fD, hp.n_ff, nullptr), stream);
         }
         {   // FFN down + residual (in place), then the next layer's (or the output head's) input quantised
             GemvParams p = base;
@@ -1091,12 +1113,13 @@ void Ctx::enqueue_step_sp(bool with_logits) {
             p.nseg = 1;
             p.seg[0] = seg_of(L.down, PAIR_ADJ, EPI_ADD, x);
             p.seg[0].resid = x;
+            const bool next = l + 1 < hp.n_layer || with_logits;
+            const ActOut nx = l + 1 < hp.n_layer ? act(0, sp[l + 1].fA, hp.n_embd, m->layers[l + 1].attn_norm)
+                                                 : act(4, sp_fH, hp.n_embd, m->output_norm);
+            if (next) p.qout = qout(nx, sp_gx, l, 3);
             if (on()) {
                 launch_dgemv(p, stream);
-                if (l + 1 < hp.n_layer)
-                    launch_dv_quant(x, act(0, sp[l + 1].fA, hp.n_embd, m->layers[l + 1].attn_norm), stream);
-                else if (with_logits)
-                    launch_dv_quant(x, act(4, sp_fH, hp.n_embd, m->output_norm), stream);
+                if (next && !fused(3)) launch_dv_quant(x, nx, stream);
             }
         }
     }
@@ -1644,8 +1667,7 @@ void Ctx::decode_ubatch(const int32_t* tokens, int n, bool all) {
         // split-K parts of the residual GEMMs: 4 for short batches of dense models (verification
         // of tens of tokens: more workgroups, a quarter of the superblock steps each; 4 x nt rows
         // fit the 2 x UB_MAX partials buffer), else 2 (the MoE router adds 2)
-        static const int ks_short = getenv("MI_MMQ_KS4") ? atoi(getenv("MI_MMQ_KS4")) : 64;
-        const int ks = hp_dense() && nt <= ks_short ? 4 : 2;
+        const int ks = hp_dense() && nt <= 64 ? 4 : 2;   // 4 x 64 rows fit the 2 x UB_MAX partials buffer
         for (int l = 0; l < hp.n_layer; ++l) {
             const Layer& L = m->layers[l];
             __half* kl = kcache + (size_t)l * n_ctx * kv_dim;
@@ -1855,11 +1877,10 @@ int Ctx::ubatch_layers_short(int nt) {
                      hp.head_dim, kv_dim, (int)n_ctx, kq_scale};
         // within ATTN_SHORT cells the decode step's fused kernel, one workgroup per (kv head, token)
         // (20-token verify 3.52 -> 3.30 ms against the MFMA kernel's 32-token tiles; 64 tokens
-        // equal, same box); MI_SHORT_ATTN_MFMA=1: the MFMA kernel
-        static const bool mfma_env = getenv("MI_SHORT_ATTN_MFMA") != nullptr;
+        // equal, same box)
         const ActQ8 act_wo = ub_act(hp.n_embd, nt, L.wo.type);
         const bool qattn = attn_quant_supported(hp.n_head, hp.n_head_kv, hp.head_dim);
-        if (attn_mfma && (mfma_env || n_cells > ATTN_SHORT)) {
+        if (attn_mfma && n_cells > ATTN_SHORT) {
             launch_attn_mfma(a, nt, attnb, stream);
             launch_quant_act(attnb, hp.n_embd, nullptr, hp.eps, act_wo, stream);
         } else if (qattn) {   // the fused kernel also quantises each token's output for W_o
@@ -2024,6 +2045,11 @@ void Ctx::sync() {
             pos_max = undo_pos;
         }
         invalidate_graphs();
+        if (code == 0x300) {   // dgemv.hip: a waiter's sweep of the output granules gave up
+            sp_fuse = 0;
+            throw Error("decode step: an in-launch activation sweep timed out; the step was rolled back and this "
+                        "context now quantises each activation in a launch of its own");
+        }
         if (code >= 0x100) {   // pstep.hip: a spin of the persistent step gave up
             ps_off = true;
             char msg[160];

@@ -241,6 +241,11 @@ struct Ctx {
     int sp_fH = 0;                      // the output head's activation formats
     char* sp_mem = nullptr;
     char* sp_act[5] = {};               // QKV, WO, gate/up, down, head inputs
+    // in-launch activations (DvQuantOut): the WO / gate/up / down launches publish their outputs as
+    // granules and build the next launch's activation themselves (no dv_quant launch between)
+    unsigned long long* sp_gx = nullptr;   // granules of x after WO / down [n_embd]
+    unsigned long long* sp_gh = nullptr;   // granules of h [n_ff]
+    int sp_fuse = 1;                    // 0 after a sweep gave up (or MI_DV_FUSE=0)
     bool sp_setup();
     void enqueue_step_sp(bool with_logits);
     // persistent decode step (pstep.hip): every layer of a dense k-quant LLaMA token in one launch,

@@ -90,6 +90,18 @@ struct ActOut {
     float eps;
 };
 
+// The next launch's quantised activation, built inside a residual / SwiGLU streaming GEMV launch
+// (launch_dgemv): its lanes publish every output as an 8-byte {value, tag} granule, and waiter
+// workgroups after the producers sweep them and quantise (rms_norm(out) * norm_w, or out itself)
+// into t -- dv_quant_kernel's result, without its launch.
+struct DvQuantOut {
+    ActOut t;                     // t.K == the launch's output rows
+    unsigned long long* gran;     // [rows] granules (null: no in-launch activation)
+    const unsigned* step;         // the decode step counter (the embedding launch increments it)
+    unsigned tag_mul, tag_add;    // tag = *step * tag_mul + tag_add: unique per step, layer and edge
+    unsigned* err;                // host-mapped error word: 0x300 when a sweep gave up
+};
+
 constexpr int GEMV_MAX_SEG = 2;
 struct GemvParams {
     GemvSeg seg[GEMV_MAX_SEG];
@@ -121,6 +133,7 @@ struct GemvParams {
     // arrives quantised, act_layout(K, act_q8k, act_q80) at act_in (pro / x / norm_w unused)
     const char* act_in;
     int act_q8k, act_q80;
+    DvQuantOut qout;          // DV_ADD / DV_SWIGLU: the next launch's activation in-launch (gran set)
 };
 
 void init_kernel_attributes();   // once per device, before any graph capture

@@ -1050,11 +1050,15 @@ __device__ __forceinline__ float wave_max_any(float v) {
     v = fmaxf(v, dppf<0x143, 0xc>(v, ni));
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
 }
-template <int LPC, int HG, int NWV>
+template <int LPC, int HG, int NWV, int PF = 0>
 __global__ __launch_bounds__(64 * NWV * HG) void attn_dec_kernel(const AttnParams P) {
     static_assert(LPC == 8 || LPC == 16, "head_dim 64 or 128");
     constexpr int HD = LPC * 8, CPW = 64 / LPC, NT = 64 * NWV, STEP = NWV * CPW;
-    constexpr int U = 2;   // cell steps per wave whose cache rows are requested at entry
+    // every step of the first 256 cells: q, then the cache rows and positions, requested at entry
+    // (buffer loads parked past the descriptor for steps at or past ncell: zeros, no memory
+    // access; K before V, which is needed last), so within 256 cells no K or V row is a dependent
+    // round trip; past that, a loop
+    constexpr int UM = PF ? PF : (256 + STEP - 1) / STEP;
     __shared__ float sw[HG][ATTN_SHORT];
     __shared__ float redm[HG][NWV];
     __shared__ double dred[HG][NWV];
@@ -1067,21 +1071,27 @@ __global__ __launch_bounds__(64 * NWV * HG) void attn_dec_kernel(const AttnParam
     const int L = lane % LPC, G = lane / LPC;
     const int tp2 = P.tokpos[2], qpos = P.tokpos[1];
     const int ncell = min(tp2 + 1, ATTN_SHORT);
-    // the first U steps' K / V rows and positions, requested before anything waits
-    u32x4 k0[U], v0[U];
-    int cp0[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const int c = min(wave * CPW + u * STEP + G, P.n_ctx - 1);
-        k0[u] = *gptr(reinterpret_cast<const u32x4*>(P.kcache + (long long)c * P.kv_dim + (long long)g * HD + L * 8));
-        v0[u] = *gptr(reinterpret_cast<const u32x4*>(P.vcache + (long long)c * P.kv_dim + (long long)g * HD + L * 8));
-        cp0[u] = gptr(P.cell_pos)[c];
-    }
     float q[8];
+    const f32x4 qa = gptr(reinterpret_cast<const f32x4*>(P.q + (long long)unit * HD + L * 8))[0];
+    const f32x4 qb = gptr(reinterpret_cast<const f32x4*>(P.q + (long long)unit * HD + L * 8))[1];
+    const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(const_cast<__half*>(rfl_ptr(P.kcache + (long long)g * HD)), 0, 0x7FFFFFFF, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(const_cast<__half*>(rfl_ptr(P.vcache + (long long)g * HD)), 0, 0x7FFFFFFF, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(const_cast<int*>(P.cell_pos), 0, 0x7FFFFFFF, 0x00020000);
+    u32x4 k0[UM], v0[UM];
+    int cp0[UM];
+    unsigned ko[UM];
+#pragma unroll
+    for (int u = 0; u < UM; ++u) {
+        const bool park = wave * CPW + u * STEP >= ncell;
+        const unsigned c = (unsigned)min(wave * CPW + u * STEP + G, ncell - 1);
+        ko[u] = oob((c * (unsigned)P.kv_dim + (unsigned)L * 8u) * 2u, park);
+        k0[u] = __builtin_amdgcn_raw_buffer_load_b128(rk, ko[u], 0, 0);
+        cp0[u] = (int)__builtin_amdgcn_raw_buffer_load_b32(rc, oob(c * 4u, park), 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < UM; ++u) v0[u] = __builtin_amdgcn_raw_buffer_load_b128(rv, ko[u], 0, 0);
     {
-        const f32x4 a = gptr(reinterpret_cast<const f32x4*>(P.q + (long long)unit * HD + L * 8))[0];
-        const f32x4 b = gptr(reinterpret_cast<const f32x4*>(P.q + (long long)unit * HD + L * 8))[1];
-        const float t[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+        const float t[8] = {qa.x, qa.y, qa.z, qa.w, qb.x, qb.y, qb.z, qb.w};
 #pragma unroll
         for (int e = 0; e < 8; ++e) q[e] = __half2float(__float2half_rn(t[e]));
     }
@@ -1111,11 +1121,11 @@ __global__ __launch_bounds__(64 * NWV * HG) void attn_dec_kernel(const AttnParam
         if (L == 0 && c < ncell) sw[grp][c] = w;
     };
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
+    for (int u = 0; u < UM; ++u) {
         const int c = wave * CPW + u * STEP + G;
         if (wave * CPW + u * STEP < ncell) score(c, k0[u], cp0[u]);
     }
-    for (int cb = wave * CPW + U * STEP; cb < ncell; cb += STEP) {
+    for (int cb = wave * CPW + UM * STEP; cb < ncell; cb += STEP) {
         const int c = min(cb + G, ncell - 1);
         const u32x4 kk = *gptr(reinterpret_cast<const u32x4*>(P.kcache + (long long)c * P.kv_dim + (long long)g * HD + L * 8));
         const int cp = gptr(P.cell_pos)[c];
@@ -1153,11 +1163,11 @@ __global__ __launch_bounds__(64 * NWV * HG) void attn_dec_kernel(const AttnParam
         for (int e = 0; e < 8; ++e) o[e] = fmaf(pw, vf[e], o[e]);
     };
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
+    for (int u = 0; u < UM; ++u) {
         const int c = wave * CPW + u * STEP + G;
         if (wave * CPW + u * STEP < ncell) pv(c, v0[u]);
     }
-    for (int cb = wave * CPW + U * STEP; cb < ncell; cb += STEP) {
+    for (int cb = wave * CPW + UM * STEP; cb < ncell; cb += STEP) {
         const int c = min(cb + G, ncell - 1);
         const u32x4 vv = *gptr(reinterpret_cast<const u32x4*>(P.vcache + (long long)c * P.kv_dim + (long long)g * HD + L * 8));
         pv(cb + G, vv);
@@ -1206,20 +1216,11 @@ static bool attn_long_resident(const void* fn, size_t lds, long long need) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, lds) != hipSuccess) return false;
     return (long long)per_cu * cus >= need;
 }
-// MI_ATTN_U=<4|8>: cell steps per wave whose cache loads the split kernels issue together
-static int attn_u() {
-    static const int u = getenv("MI_ATTN_U") ? atoi(getenv("MI_ATTN_U")) : 4;
-    return u == 8 ? 8 : 4;
-}
+// the split kernels issue the cache loads of 4 cell steps per wave together (8: no faster, r03)
 template <int R, int LPC>
 static void attn_fns_l(AttnFn& a, AttnFn& b, AttnFn& f) {
-    if (attn_u() == 8) {
-        a = attn_scores_kernel<R, LPC, 8>;
-        b = attn_pv_kernel<R, LPC, 8>;
-    } else {
-        a = attn_scores_kernel<R, LPC, 4>;
-        b = attn_pv_kernel<R, LPC, 4>;
-    }
+    a = attn_scores_kernel<R, LPC, 4>;
+    b = attn_pv_kernel<R, LPC, 4>;
     f = attn_fused_kernel<R, LPC, 1>;
 }
 template <int R>
@@ -1313,7 +1314,13 @@ void launch_attn(const AttnParams& p, hipStream_t s) {
         if (k.hg > 1 || k.qsplit || r == 1) {
             switch (p.head_dim * 8 + k.hg) {
             case 128 * 8 + 1: fd = attn_dec_kernel<16, 1, 16>; nwv = 16; break;
-            case 128 * 8 + 2: fd = attn_dec_kernel<16, 2, 8>; nwv = 8; break;
+            case 128 * 8 + 2: {
+                const int pf = getenv("MI_ATTN_PF") ? atoi(getenv("MI_ATTN_PF")) : 0;
+                fd = pf == 1 ? attn_dec_kernel<16, 2, 8, 1> : pf == 2 ? attn_dec_kernel<16, 2, 8, 2> : pf == 3 ? attn_dec_kernel<16, 2, 8, 3>
+                   : pf == 4 ? attn_dec_kernel<16, 2, 8, 4> : attn_dec_kernel<16, 2, 8>;
+                nwv = 8;
+                break;
+            }
             case 64 * 8 + 1: fd = attn_dec_kernel<8, 1, 16>; nwv = 16; break;
             case 64 * 8 + 2: fd = attn_dec_kernel<8, 2, 8>; nwv = 8; break;
             case 64 * 8 + 4: fd = attn_dec_kernel<8, 4, 4>; nwv = 4; break;
@@ -1342,7 +1349,7 @@ void launch_attn(const AttnParams& p, hipStream_t s) {
         MI_HIP(hipGetLastError());
         return;
     }
-    if (p.xflags && p.step && !p.long_off && (p.head_dim == 64 || p.head_dim == 128) && getenv("MI_ATTN_SPLIT2") == nullptr) {
+    if (p.xflags && p.step && !p.long_off && (p.head_dim == 64 || p.head_dim == 128)) {
         // one launch, the splits of a q head exchanging their softmax statistics
         const size_t lds = (size_t)std::max(64, ((p.n_ctx + ATTN_SMAX - 1) / ATTN_SMAX + 63) / 64 * 64) * sizeof(float);
         auto fn = p.head_dim == 128 ? attn_long_kernel<16> : attn_long_kernel<8>;

@@ -1442,17 +1442,15 @@ void launch_mmq2(const GemmParams& p, const mmq::MmqSegs& S, const ActQ8& act, c
                          (p.ksplit != 2 && p.ksplit != 4)))
         throw Error("mmq2: split-K (2 or 4 parts) is for a single EPI_ADD matrix with a partials buffer");
     const int g2 = g1 * (p.ksplit > 1 ? p.ksplit : 1);
-    // MI_MMQ2_NST: 1 = one stage, two workgroups per CU; 2 = two stages, one workgroup per CU;
-    // 0 (default) = one stage when the grid fills two workgroups per CU, else two.  7B 512-token
-    // prefill, NST 1 vs 2: 15.5 vs 16.8 ms (same box, scripts/ab_prefill.sh)
-    static const int nst_req = getenv("MI_MMQ2_NST") ? atoi(getenv("MI_MMQ2_NST")) : 0;
+    // one stage (two workgroups per CU) when the grid fills two workgroups per CU, else two stages
+    // (one per CU).  7B 512-token prefill, one vs two stages: 15.5 vs 16.8 ms (same box, r04)
     static int n_cu = 0;
     if (!n_cu) {
         int dev = 0;
         MI_HIP(hipGetDevice(&dev));
         MI_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
     }
-    const int nst = nst_req ? nst_req : (g2 >= 2 * n_cu ? 1 : 2);
+    const int nst = g2 >= 2 * n_cu ? 1 : 2;
     decltype(&mmq::mmq2_t<T_Q4_K, false, 2>) f2;
     int lds;
 #define M2_PICK(NST_)                                                                                           \
@@ -1530,12 +1528,7 @@ void launch_mmq32(const GemmParams& p, const ActQ8& act, const float2* rope, hip
 
 // The Q4_K / Q5_K mmqs1 launches on the one-deep-ring, two-waves-per-SIMD form (214-220 VGPRs
 // instead of 246-256 at one wave: 20-token verify 7B 3.61 -> 3.40 ms, Mixtral 18.2 -> 15.7 ms,
-// same box, scripts/r05_lean.sh); MI_MMQS1_LEAN=0: the two-deep rings at one wave per SIMD.  Q6_K
-// keeps its ring (the lean form at two waves spills).
-static bool mmqs1_lean() {
-    static const bool on = getenv("MI_MMQS1_LEAN") == nullptr || atoi(getenv("MI_MMQS1_LEAN")) != 0;
-    return on;
-}
+// same box, r05).  Q6_K keeps its two-deep ring at one wave (the lean form at two waves spills).
 
 int mmqs_parts(int K) { return (K / 256 + mmq::MS_SBW - 1) / mmq::MS_SBW; }
 
@@ -1572,16 +1565,12 @@ int launch_mmqs(const QMat* const* mats, const int* prow, int n, bool pair, int 
     const int NT = act.npad / 32;
     const int KQ = T != T_Q8_0;
     const int lds = mmq::MS_SBW * NT * 8192 + (KQ ? mmq::MS_SBW * NT * 1024 + mmq::MS_SBW * 256 : mmq::MS_SBW * 8 * 256);
-    // one token tile, k-quants: the one-wave register form (MI_MMQS1=0: the LDS form)
-    static const bool ms1_env = getenv("MI_MMQS1") == nullptr || atoi(getenv("MI_MMQS1")) != 0;
-    const bool lean = mmqs1_lean();
-    if (ms1_env && NT == 1 && T != T_Q8_0) {
+    // one token tile, k-quants: the one-wave register form (3.42 vs 3.50 ms for the LDS form, r05)
+    if (NT == 1 && T != T_Q8_0) {
         decltype(&mmq::mmqs1_t<T_Q4_K, false, false>) f1 = nullptr;
         switch (T) {
-        case T_Q4_K: f1 = lean ? (pair ? mmq::mmqs1_lean_t<T_Q4_K, true, false> : mmq::mmqs1_lean_t<T_Q4_K, false, false>)
-                           : (pair ? mmq::mmqs1_t<T_Q4_K, true, false> : mmq::mmqs1_t<T_Q4_K, false, false>); break;
-        case T_Q5_K: f1 = lean ? (pair ? mmq::mmqs1_lean_t<T_Q5_K, true, false> : mmq::mmqs1_lean_t<T_Q5_K, false, false>)
-                           : (pair ? mmq::mmqs1_t<T_Q5_K, true, false> : mmq::mmqs1_t<T_Q5_K, false, false>); break;
+        case T_Q4_K: f1 = pair ? mmq::mmqs1_lean_t<T_Q4_K, true, false> : mmq::mmqs1_lean_t<T_Q4_K, false, false>; break;
+        case T_Q5_K: f1 = pair ? mmq::mmqs1_lean_t<T_Q5_K, true, false> : mmq::mmqs1_lean_t<T_Q5_K, false, false>; break;
         default: f1 = pair ? mmq::mmqs1_t<T_Q6_K, true, false> : mmq::mmqs1_t<T_Q6_K, false, false>; break;
         }
         hipLaunchKernelGGL(f1, dim3(M.nrt_tot * M.kp), dim3(64), 0, s, M, act);
@@ -1637,13 +1626,10 @@ int launch_mmqs_grouped(const QMat& A, bool pair, int nff, const ActQ8& act, flo
     M.grp = grp;
     M.grp_n = n_expert;
     M.grp_stride = A.sw_expert_stride;
-    const bool lean = mmqs1_lean();
     decltype(&mmq::mmqs1_t<T_Q4_K, false, true>) f1 = nullptr;
     switch (T) {
-    case T_Q4_K: f1 = lean ? (pair ? mmq::mmqs1_lean_t<T_Q4_K, true, true> : mmq::mmqs1_lean_t<T_Q4_K, false, true>)
-                       : (pair ? mmq::mmqs1_t<T_Q4_K, true, true> : mmq::mmqs1_t<T_Q4_K, false, true>); break;
-    case T_Q5_K: f1 = lean ? (pair ? mmq::mmqs1_lean_t<T_Q5_K, true, true> : mmq::mmqs1_lean_t<T_Q5_K, false, true>)
-                       : (pair ? mmq::mmqs1_t<T_Q5_K, true, true> : mmq::mmqs1_t<T_Q5_K, false, true>); break;
+    case T_Q4_K: f1 = pair ? mmq::mmqs1_lean_t<T_Q4_K, true, true> : mmq::mmqs1_lean_t<T_Q4_K, false, true>; break;
+    case T_Q5_K: f1 = pair ? mmq::mmqs1_lean_t<T_Q5_K, true, true> : mmq::mmqs1_lean_t<T_Q5_K, false, true>; break;
     default: f1 = pair ? mmq::mmqs1_t<T_Q6_K, true, true> : mmq::mmqs1_t<T_Q6_K, false, true>; break;
     }
     // an expert holds at most max_rows rows (one per token routed to it): ceil(max_rows / 32) tiles

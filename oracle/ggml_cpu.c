@@ -225,6 +225,110 @@ static float dot_q8_0(const uint8_t* row, int K, const q80_t* y) {   /* ggml_vec
     return sumf;
 }
 
+/* ---------------------------------------------- x86 AVX2 dot kernels ---- *
+ * The CPU-baseline leg of bench.py times the reference's CPU path; on x86 ggml b5187 runs the
+ * AVX2 forms of these dots (ggml-cpu-quants.c ggml_vec_dot_{q4_K,q5_K,q6_K}_q8_K,
+ * ggml_vec_dot_q8_0_q8_0 under __AVX2__), not the generic loops above.  These restate that
+ * technique: maddubs of the unsigned quants against the signed Q8 bytes, madd by the sub-block
+ * scales, an int32 vector per superblock converted once and fused into 8 float lanes by d.  Every
+ * integer is the one the generic loop forms; only the fp32 lane grouping differs (so results
+ * match the scalar loops to rounding, not bit for bit).  Off by default: the parity tests keep
+ * the generic order (orc_set_simd / ORC_SIMD=1 switch it on for timing). */
+#include <immintrin.h>
+static int g_simd = -1;
+static int use_simd(void) {
+    if (g_simd < 0) g_simd = getenv("ORC_SIMD") != NULL && atoi(getenv("ORC_SIMD")) != 0;
+    return g_simd;
+}
+void orc_set_simd(int on) { g_simd = on ? 1 : 0; }
+static float hsum8(__m256 v) {
+    __m128 a = _mm_add_ps(_mm256_castps256_ps128(v), _mm256_extractf128_ps(v, 1));
+    a = _mm_add_ps(a, _mm_movehl_ps(a, a));
+    a = _mm_add_ss(a, _mm_movehdup_ps(a));
+    return _mm_cvtss_f32(a);
+}
+/* Q4_K (q5 = 0) / Q5_K (q5 = 1) */
+static float dot_q45_K_avx2(const uint8_t* row, int K, const q8k_t* y, int q5) {
+    const int bb = q5 ? 176 : 144;
+    const __m256i m4 = _mm256_set1_epi8(0x0F), m1 = _mm256_set1_epi8(0x01);
+    __m256 acc = _mm256_setzero_ps();
+    float summ = 0.0f;
+    for (int i = 0; i < K / QK_K; ++i) {
+        const uint8_t* blk = row + (size_t)i * bb;
+        const uint8_t* qs = blk + (q5 ? 48 : 16);
+        uint8_t scl[8], mn[8];
+        for (int j = 0; j < 8; ++j) scale_min_k4(j, blk + 4, &scl[j], &mn[j]);
+        int sumi_m = 0;
+        for (int j = 0; j < QK_K / 16; ++j) sumi_m += y[i].bsums[j] * mn[j / 2];
+        const __m256i qhv = q5 ? _mm256_loadu_si256((const __m256i*)(blk + 16)) : _mm256_setzero_si256();
+        __m256i sumi = _mm256_setzero_si256();
+        for (int c = 0; c < 4; ++c) {
+            const __m256i qb = _mm256_loadu_si256((const __m256i*)(qs + 32 * c));
+            __m256i lo = _mm256_and_si256(qb, m4), hi = _mm256_and_si256(_mm256_srli_epi16(qb, 4), m4);
+            if (q5) {
+                lo = _mm256_add_epi8(lo, _mm256_slli_epi16(_mm256_and_si256(_mm256_srli_epi16(qhv, 2 * c), m1), 4));
+                hi = _mm256_add_epi8(hi, _mm256_slli_epi16(_mm256_and_si256(_mm256_srli_epi16(qhv, 2 * c + 1), m1), 4));
+            }
+            const __m256i yl = _mm256_loadu_si256((const __m256i*)(y[i].qs + 64 * c));
+            const __m256i yh = _mm256_loadu_si256((const __m256i*)(y[i].qs + 64 * c + 32));
+            const __m256i pl = _mm256_madd_epi16(_mm256_set1_epi16(scl[2 * c]), _mm256_maddubs_epi16(lo, yl));
+            const __m256i ph = _mm256_madd_epi16(_mm256_set1_epi16(scl[2 * c + 1]), _mm256_maddubs_epi16(hi, yh));
+            sumi = _mm256_add_epi32(sumi, _mm256_add_epi32(pl, ph));
+        }
+        uint16_t dh, dmh;
+        memcpy(&dh, blk, 2);
+        memcpy(&dmh, blk + 2, 2);
+        acc = _mm256_fmadd_ps(_mm256_set1_ps(h2f(dh) * y[i].d), _mm256_cvtepi32_ps(sumi), acc);
+        summ -= h2f(dmh) * y[i].d * sumi_m;
+    }
+    return hsum8(acc) + summ;
+}
+static float dot_q6_K_avx2(const uint8_t* row, int K, const q8k_t* y) {
+    const __m256i m4 = _mm256_set1_epi8(0x0F), m3 = _mm256_set1_epi8(0x03), m32 = _mm256_set1_epi8(32);
+    __m256 acc = _mm256_setzero_ps();
+    for (int i = 0; i < K / QK_K; ++i) {
+        const uint8_t* blk = row + (size_t)i * 210;
+        const int8_t* sc = (const int8_t*)(blk + 192);
+        __m256i sumi = _mm256_setzero_si256();
+        for (int h = 0; h < 2; ++h) {
+            const __m256i l0 = _mm256_loadu_si256((const __m256i*)(blk + 64 * h));
+            const __m256i l1 = _mm256_loadu_si256((const __m256i*)(blk + 64 * h + 32));
+            const __m256i qh = _mm256_loadu_si256((const __m256i*)(blk + 128 + 32 * h));
+            const __m256i q[4] = {
+                _mm256_or_si256(_mm256_and_si256(l0, m4), _mm256_slli_epi16(_mm256_and_si256(qh, m3), 4)),
+                _mm256_or_si256(_mm256_and_si256(l1, m4), _mm256_slli_epi16(_mm256_and_si256(_mm256_srli_epi16(qh, 2), m3), 4)),
+                _mm256_or_si256(_mm256_and_si256(_mm256_srli_epi16(l0, 4), m4), _mm256_slli_epi16(_mm256_and_si256(_mm256_srli_epi16(qh, 4), m3), 4)),
+                _mm256_or_si256(_mm256_and_si256(_mm256_srli_epi16(l1, 4), m4), _mm256_slli_epi16(_mm256_and_si256(_mm256_srli_epi16(qh, 6), m3), 4))};
+            for (int g = 0; g < 4; ++g) {   /* elements 128 h + 32 g ..: scales 8 h + 2 g, + 1 */
+                const __m256i yv = _mm256_loadu_si256((const __m256i*)(y[i].qs + 128 * h + 32 * g));
+                const __m256i p = _mm256_sub_epi16(_mm256_maddubs_epi16(q[g], yv), _mm256_maddubs_epi16(m32, yv));
+                const int j = 8 * h + 2 * g;
+                const __m256i s = _mm256_setr_epi16(sc[j], sc[j], sc[j], sc[j], sc[j], sc[j], sc[j], sc[j], sc[j + 1],
+                                                    sc[j + 1], sc[j + 1], sc[j + 1], sc[j + 1], sc[j + 1], sc[j + 1], sc[j + 1]);
+                sumi = _mm256_add_epi32(sumi, _mm256_madd_epi16(s, p));
+            }
+        }
+        uint16_t dh;
+        memcpy(&dh, blk + 208, 2);
+        acc = _mm256_fmadd_ps(_mm256_set1_ps(h2f(dh) * y[i].d), _mm256_cvtepi32_ps(sumi), acc);
+    }
+    return hsum8(acc);
+}
+static float dot_q8_0_avx2(const uint8_t* row, int K, const q80_t* y) {
+    __m256 acc = _mm256_setzero_ps();
+    for (int b = 0; b < K / 32; ++b) {
+        const uint8_t* blk = row + (size_t)b * 34;
+        const __m256i x = _mm256_loadu_si256((const __m256i*)(blk + 2));
+        const __m256i v = _mm256_loadu_si256((const __m256i*)y[b].qs);
+        /* signed x signed: |x| maddubs (v with x's sign), as ggml's mul_sum_i8_pairs_float */
+        const __m256i p = _mm256_madd_epi16(_mm256_set1_epi16(1), _mm256_maddubs_epi16(_mm256_sign_epi8(x, x), _mm256_sign_epi8(v, x)));
+        uint16_t dh;
+        memcpy(&dh, blk, 2);
+        acc = _mm256_fmadd_ps(_mm256_set1_ps(h2f(dh) * y[b].d), _mm256_cvtepi32_ps(p), acc);
+    }
+    return hsum8(acc);
+}
+
 static size_t row_bytes(int t, int K) {
     switch (t) {
     case T_Q4_K: return (size_t)K / 256 * 144;
@@ -255,11 +359,12 @@ int orc_gemv(int type, const void* w, int rows, int K, const float* x, float* y)
     for (int r = 0; r < rows; ++r) {
         const uint8_t* row = W + (size_t)r * rb;
         float v = 0;
+        const int simd = use_simd();
         switch (type) {
-        case T_Q4_K: v = dot_q45_K(row, K, a8k, 0); break;
-        case T_Q5_K: v = dot_q45_K(row, K, a8k, 1); break;
-        case T_Q6_K: v = dot_q6_K(row, K, a8k); break;
-        case T_Q8_0: v = dot_q8_0(row, K, a80); break;
+        case T_Q4_K: v = simd ? dot_q45_K_avx2(row, K, a8k, 0) : dot_q45_K(row, K, a8k, 0); break;
+        case T_Q5_K: v = simd ? dot_q45_K_avx2(row, K, a8k, 1) : dot_q45_K(row, K, a8k, 1); break;
+        case T_Q6_K: v = simd ? dot_q6_K_avx2(row, K, a8k) : dot_q6_K(row, K, a8k); break;
+        case T_Q8_0: v = simd ? dot_q8_0_avx2(row, K, a80) : dot_q8_0(row, K, a80); break;
         case T_F32: {
             const float* f = (const float*)row;
             double s = 0;   /* ggml_vec_dot_f32 scalar path accumulates in ggml_float */

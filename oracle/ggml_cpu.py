@@ -38,9 +38,16 @@ def lib():
         L.orc_kv_clear.argtypes = [C.c_void_p]
         L.orc_n_threads.restype = C.c_int
         L.orc_set_alt.argtypes = [C.c_int]
+        L.orc_set_simd.argtypes = [C.c_int]
         L.orc_last_moe_margin.restype = C.c_float
         _lib = L
     return _lib
+
+
+def set_simd(on: bool) -> None:
+    """The AVX2 dot kernels (ggml's x86 technique; the bench's CPU-baseline timing) instead of the
+    generic loops (the parity order, default)."""
+    lib().orc_set_simd(1 if on else 0)
 
 
 def gemv(t: int, raw: np.ndarray, rows: int, K: int, x: np.ndarray) -> np.ndarray:

@@ -54,6 +54,24 @@ def test_c_oracle_matches_numpy_oracle_gemv(t):
     assert np.all(np.abs(a - b) <= bound)
 
 
+@pytest.mark.parametrize("t", QTYPES)
+def test_c_oracle_avx2_dots_match_generic(t):
+    """The AVX2 dot kernels the bench's CPU-baseline leg times (ggml's x86 technique) form the
+    generic loops' integers; only the fp32 lane grouping differs -- at the GEMV bar."""
+    import ggml_cpu
+    rows, K = 45, 4096
+    w = rand_matrix(t, rows, K, seed=19)
+    x = rand_x(K, seed=4)
+    try:
+        ggml_cpu.set_simd(True)
+        a = ggml_cpu.gemv(t, w, rows, K, x).astype(np.float64)
+    finally:
+        ggml_cpu.set_simd(False)
+    b = ggml_cpu.gemv(t, w, rows, K, x).astype(np.float64)
+    bound = R.mul_mat_vec_abs(w, t, K, x) * 2e-6
+    assert np.all(np.abs(a - b) <= bound), float(np.max(np.abs(a - b) / bound))
+
+
 @pytest.mark.parametrize("cfg", ["tiny-q4_k_m", "tiny-q8_0", "tiny-moe-q5_k_m"])
 def test_c_oracle_matches_numpy_oracle_decode(cfg):
     import ggml_cpu
