@@ -506,43 +506,7 @@ int64_t mi_prof_bytes(const mi_ctx* c) { return c ? c->impl->prof_bytes : -1; }
 
 int32_t mi_decode_path(const mi_ctx* c) {
     if (!c) return -1;
-    return c->impl->ps_usable() ? 2 : c->impl->sp_ok ? 1 : 0;
-}
-const char* mi_decode_path_note(const mi_ctx* c) {
-    if (!c) return "null context";
-    const Ctx& x = *c->impl;
-    if (!x.ps_note.empty()) return x.ps_note.c_str();
-    if (x.ps_off) return "a hand-off of the persistent step timed out on this context";
-    if (x.decode_mode != 1) return "launch form (mi_decode_set_mode 0, the default)";
-    if (dev_chain_contexts(x.device) != 1) return "other contexts on the device";
-    return "";
-}
-int32_t mi_debug_ps_stamps(mi_ctx* c, int32_t layer, uint64_t* out, int32_t n) {
-    try {
-        if (!c) throw Error("null context");
-        Ctx& x = *c->impl;
-        if (!x.ps) return 0;
-        MI_HIP(hipSetDevice(x.device));
-        static std::map<const Ctx*, unsigned long long*> bufs;
-        unsigned long long*& b = bufs[&x];
-        if (!b) MI_HIP(hipMalloc(&b, 1024 * 16 * sizeof(unsigned long long)));
-        const int ncu = ps_arm_stamps(x.ps, layer >= 0 ? b : nullptr, layer);
-        x.invalidate_graphs();
-        if (out && n > 0) {
-            x.sync();
-            MI_HIP(hipMemcpy(out, b, (size_t)std::min(n, ncu) * 16 * sizeof(uint64_t), hipMemcpyDeviceToHost));
-        }
-        return ncu;
-    } catch (const std::exception& e) {
-        set_last_error(e.what());
-        return -1;
-    }
-}
-int32_t mi_decode_set_mode(mi_ctx* c, int32_t mode) {
-    if (!c || mode < 0 || mode > 1) return -1;
-    const int prev = c->impl->decode_mode;
-    c->impl->decode_mode = mode;
-    return prev;
+    return c->impl->sp_ok ? 1 : 0;
 }
 int32_t mi_debug_stamps(mi_ctx* c, uint64_t* out, int32_t n_launch) {
     try {

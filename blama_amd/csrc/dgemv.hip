@@ -46,8 +46,6 @@ struct DvSeg {
 
 struct DvArgs {
     DvSeg seg[2];
-    DvQuantOut qo;              // DV_ADD / DV_SWIGLU: the next launch's activation, built in-launch
-    int nblk;                   // producer workgroups (the waiters follow them)
     const char* act;            // this launch's activation, act_layout(K, q8k, q80)
     int act_bytes, K, q8k, q80;
     const float* resid;         // DV_ADD
@@ -59,12 +57,6 @@ struct DvArgs {
     float theta_scale, freq_scale;
     int n_rot, head_dim, kv_dim;
 };
-
-// one 8-byte {value, tag} granule, written through to the coherent copy (sc1)
-__device__ __forceinline__ void put_gran(unsigned long long* g, unsigned tag, float v) {
-    __hip_atomic_store((__attribute__((address_space(1))) unsigned long long*)(g),
-                       ((unsigned long long)tag << 32) | __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 __device__ __forceinline__ void dv_lds_barrier() {
     __builtin_amdgcn_s_waitcnt((0xF) | (0x3 << 14) | (0x7 << 4));   // lgkmcnt(0); vmcnt untouched
@@ -110,9 +102,6 @@ __device__ __forceinline__ void dv_body(const DvArgs& a, char* lds) {
     const bool isk = ROLE == DV_QKV && !isq && r0 < S.nq + S.nk;
     const int i0 = (ROLE == DV_QKV && (isq || isk)) ? (isq ? r0 : r0 - S.nq) % a.head_dim : 0;
     const bool roped = (isq || isk) && i0 < a.n_rot;
-    // the output granules' tag (the in-launch activation): this step's (layer, edge) epoch
-    unsigned tag = 0;
-    if ((ADD || ROLE == DV_SWIGLU) && a.qo.gran) tag = *gptr(a.qo.step) * a.qo.tag_mul + a.qo.tag_add;
     float ff = 1.0f;
     if (ROLE == DV_QKV && a.freq_factors) {
         const uint8_t* fb = reinterpret_cast<const uint8_t*>(rfl_ptr(a.freq_factors));
@@ -190,118 +179,11 @@ __device__ __forceinline__ void dv_body(const DvArgs& a, char* lds) {
             if (r0 + 1 < S.rows) vr[rv + 1] = __float2half_rn(o1);
         }
     } else if (ROLE == DV_SWIGLU) {
-        const float o = silu_f(y[0]) * y[RW - 1];
-        S.out[u] = o;
-        if (a.qo.gran) put_gran(a.qo.gran + u, tag, o);
+        S.out[u] = silu_f(y[0]) * y[RW - 1];
     } else if (ADD) {
-        const float o = y[0] + res;
-        S.out[u] = o;
-        if (a.qo.gran) put_gran(a.qo.gran + u, tag, o);
+        S.out[u] = y[0] + res;
     } else {
         S.out[u] = y[0];
-    }
-}
-
-// ---- the waiters: the workgroups after the producers (dispatched last, so every producer is
-// resident or done by the time they run -- they wait on nothing but the producers' stores).
-// They sweep the output granules until every tag is this step's, then build the next launch's
-// activation with dv_quant_kernel's arithmetic and summation order (bit-identical to it):
-//   norm_w set (after WO / FFN down): ONE workgroup; the sum of squares of the whole vector in
-//     dv_quant_kernel's order (thread t < 256 of 4 waves: pieces t, t + 256, ..; DPP; waves in
-//     order), then wave w quantises blocks w, w + 8, ..
-//   plain (after gate/up: h): wave w of waiter g quantises block 8 g + w as soon as its 256 rows
-//     have landed, on its own.
-// A sweep that outlasts DV_SPIN_TIMEOUT writes 0x300 to the error word and gives up (the host
-// rolls the step back and falls back to separate quantisation launches).
-constexpr unsigned long long DV_SPIN_TIMEOUT = 25000000ull;   // 0.25 s of the 100 MHz clock
-constexpr int DV_WP = 4;   // 16-B pieces per waiter thread: K <= 8192 under the norm
-
-// lanes whose pieces are all tagged `tag`: v = their values
-__device__ __forceinline__ bool dv_sweep(const unsigned long long* g, unsigned piece, unsigned tag, f32x4& v) {
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned long long*>(g), 0, 0x7FFFFFFF, 0x00020000);
-    const u32x4 q0 = __builtin_amdgcn_raw_buffer_load_b128(r, piece * 32u, 0, 16);        // sc1: the coherent copy
-    const u32x4 q1 = __builtin_amdgcn_raw_buffer_load_b128(r, piece * 32u + 16u, 0, 16);
-    if (q0.y != tag || q0.w != tag || q1.y != tag || q1.w != tag) return false;
-    v = f32x4{__uint_as_float(q0.x), __uint_as_float(q0.z), __uint_as_float(q1.x), __uint_as_float(q1.z)};
-    return true;
-}
-__device__ __forceinline__ bool dv_spin_ok(unsigned long long& t0, unsigned* err) {
-    __builtin_amdgcn_s_sleep(2);
-    const unsigned long long t = __builtin_amdgcn_s_memrealtime();
-    if (t0 == 0) t0 = t;
-    if (t - t0 < DV_SPIN_TIMEOUT) return true;
-    if (err) __hip_atomic_store(err, 0x300u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    return false;
-}
-
-__device__ __forceinline__ void dv_waiter(const DvArgs& a, char* lds) {
-    const DvQuantOut& Q = a.qo;
-    const ActOut& t = Q.t;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int nb = t.K >> 8, np = t.K >> 2;
-    const unsigned tag = *gptr(Q.step) * Q.tag_mul + Q.tag_add;
-    unsigned long long t0 = 0;
-    if (!t.norm_w) {
-        const int b = ((int)blockIdx.x - a.nblk) * DV_NW + wave;
-        if (b >= nb) return;
-        f32x4 v;
-        bool got = false;
-        for (;;) {
-            if (!got) got = dv_sweep(Q.gran, (unsigned)(b * 64 + lane), tag, v);
-            if (__all(got)) break;
-            if (!dv_spin_ok(t0, Q.err)) return;
-        }
-        const float q[4] = {v.x, v.y, v.z, v.w};
-        dv_quant_block(t, b, q, lane);
-        return;
-    }
-    // norm: every piece into LDS (xs[np] f32x4), then dv_quant_kernel's order
-    f32x4* xs = reinterpret_cast<f32x4*>(lds);
-    double* red = reinterpret_cast<double*>(lds + np * 16);
-    unsigned pend = 0;
-#pragma unroll
-    for (int i = 0; i < DV_WP; ++i)
-        if (tid + i * DV_NW * 64 < np) pend |= 1u << i;
-    for (;;) {
-#pragma unroll
-        for (int i = 0; i < DV_WP; ++i)
-            if (pend & (1u << i)) {
-                const int pc = tid + i * DV_NW * 64;
-                f32x4 v;
-                if (dv_sweep(Q.gran, (unsigned)pc, tag, v)) {
-                    xs[pc] = v;
-                    pend &= ~(1u << i);
-                }
-            }
-        if (__all(pend == 0)) break;
-        if (!dv_spin_ok(t0, Q.err)) {   // the whole workgroup leaves (no barrier is pending)
-            pend = 0xFFFFFFFFu;
-            break;
-        }
-    }
-    if (__syncthreads_or(pend != 0)) return;
-    if (wave < 4) {   // dv_quant_kernel: thread t sums pieces t, t + 256, .. in double, then the wave
-        double sq = 0.0;
-        for (int pc = tid; pc < np; pc += 256) {
-            const f32x4 y = xs[pc];
-            sq += (double)(y.x * y.x);
-            sq += (double)(y.y * y.y);
-            sq += (double)(y.z * y.z);
-            sq += (double)(y.w * y.w);
-        }
-        sq = wave_sum63_d(sq);
-        if (lane == 63) red[wave] = sq;
-    }
-    __syncthreads();
-    double tot = 0.0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) tot += red[k];
-    const float scale = 1.0f / sqrtf((float)(tot / (double)t.K) + t.eps);
-    for (int b = wave; b < nb; b += DV_NW) {
-        const f32x4 v = xs[b * 64 + lane];
-        const f32x4 wn = gptr(reinterpret_cast<const f32x4*>(t.norm_w))[b * 64 + lane];
-        const float q[4] = {(v.x * scale) * wn.x, (v.y * scale) * wn.y, (v.z * scale) * wn.z, (v.w * scale) * wn.w};
-        dv_quant_block(t, b, q, lane);
     }
 }
 
@@ -309,10 +191,6 @@ __device__ __forceinline__ void dv_waiter(const DvArgs& a, char* lds) {
 template <int T0, int T1, int RW, int C, int ROLE>
 __global__ __launch_bounds__(DV_NW * 64) void dgemv_kernel(const DvArgs a) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
-    if ((ROLE == DV_ADD || ROLE == DV_SWIGLU) && (int)blockIdx.x >= a.nblk) {
-        dv_waiter(a, lds);
-        return;
-    }
     if (T1 < 0 || (int)blockIdx.x < a.seg[1].blk0) dv_body<T0, 0, RW, C, ROLE>(a, lds);
     else dv_body<(T1 < 0 ? T0 : T1), 1, RW, C, ROLE>(a, lds);
 }
@@ -493,23 +371,6 @@ void launch_dgemv(const GemvParams& p, hipStream_t s, hipEvent_t ev_start, hipEv
         blk += o.nblk;
     }
     if (p.nseg == 1) a.seg[1].blk0 = blk;
-    a.nblk = blk;
-    int nwait = 0;
-    size_t smem_w = 0;
-    if (p.qout.gran) {   // the next launch's activation, built by waiter workgroups of this one
-        const ActOut& t = p.qout.t;
-        if (role != DV_ADD && role != DV_SWIGLU) throw Error("dgemv: an in-launch activation needs a residual or SwiGLU launch");
-        if (t.K != g0.A.rows || t.K % 256 || !t.act || (!t.q8k && !t.q80) || !p.qout.step)
-            throw Error("dgemv: in-launch activation shape");
-        if (t.norm_w) {
-            if (t.K > DV_WP * DV_NW * 64 * 4) throw Error("dgemv: in-launch RMSNorm past 8192 elements");
-            nwait = 1;
-            smem_w = (size_t)t.K * 4 + 4 * sizeof(double);
-        } else {
-            nwait = (t.K / 256 + DV_NW - 1) / DV_NW;
-        }
-        a.qo = p.qout;
-    }
     a.act = p.act_in;
     a.K = p.K;
     a.q8k = p.act_q8k;
@@ -529,11 +390,11 @@ void launch_dgemv(const GemvParams& p, hipStream_t s, hipEvent_t ev_start, hipEv
     if (role == DV_ADD && !g0.resid) throw Error("dgemv: residual epilogue without resid");
     if (role == DV_QKV && !p.tokpos) throw Error("dgemv: QKV epilogue needs tokpos");
     const DvFn fn = dv_fn(role, g0.A.type, p.nseg == 2 ? p.seg[1].A.type : -1, dv_chunks(p.K));
-    const size_t smem = std::max((dv_act_bytes(p.K, p.act_q8k, p.act_q80) + 15) / 16 * 16, smem_w);
+    const size_t smem = (dv_act_bytes(p.K, p.act_q8k, p.act_q80) + 15) / 16 * 16;
     if (ev_start || ev_stop)
-        hipExtLaunchKernelGGL(fn, dim3(blk + nwait), dim3(DV_NW * 64), smem, s, ev_start, ev_stop, 0, a);
+        hipExtLaunchKernelGGL(fn, dim3(blk), dim3(DV_NW * 64), smem, s, ev_start, ev_stop, 0, a);
     else
-        hipLaunchKernelGGL(fn, dim3(blk + nwait), dim3(DV_NW * 64), smem, s, a);
+        hipLaunchKernelGGL(fn, dim3(blk), dim3(DV_NW * 64), smem, s, a);
     MI_HIP(hipGetLastError());
 }
 

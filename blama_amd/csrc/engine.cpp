@@ -718,7 +718,6 @@ Ctx::Ctx(Model* model, uint32_t nctx, uint32_t nbatch, uint32_t nubatch) : m(mod
     MI_HIP(hipHostMalloc(&h_gather, 4096 * sizeof(float)));
     h_cell_pos.assign(n_ctx, 0);
     sp_ok = sp_setup();
-    ps_setup();
     dev_chain(device).nctx++;
 }
 
@@ -727,8 +726,6 @@ Ctx::~Ctx() {
     hipSetDevice(device);
     if (stream) hipStreamSynchronize(stream);
     invalidate_graphs();
-    ps_destroy(ps);
-    ps = nullptr;
     for (auto e : prof_ev) if (e) hipEventDestroy(e);
     for (void* p : {(void*)kcache, (void*)vcache, (void*)kv_scratch, (void*)cell_pos, (void*)tokpos, (void*)x,
                     (void*)q, (void*)attn, (void*)h, (void*)h2, (void*)logits, (void*)cand, (void*)topk_ids,
@@ -738,7 +735,7 @@ Ctx::~Ctx() {
                     (void*)xb, (void*)qb, (void*)attnb, (void*)hb, (void*)tokpos_b, (void*)ub_q, (void*)ub_dT, (void*)ub_bsb, (void*)ub_rope, (void*)ub_part, (void*)ub_spart,
                     (void*)ub_q0, (void*)ub_dT0, (void*)yb, (void*)sel_b, (void*)selw_b, (void*)moe_rows, (void*)moe_pos,
                     (void*)moe_rowsel, (void*)moe_grp, (void*)moe_q, (void*)moe_dT, (void*)moe_bsb,
-                    (void*)logits_all, (void*)grows_ids, (void*)grows_out, (void*)sp_mem, (void*)sp_gx, (void*)sp_gh, (void*)ps_xout})
+                    (void*)logits_all, (void*)grows_ids, (void*)grows_out, (void*)sp_mem})
         if (p) hipFree(p);
     for (void* p : {(void*)h_tokpos, (void*)h_topk_ids, (void*)h_topk_vals, (void*)h_logits, (void*)h_gather, (void*)h_grows,
                     (void*)h_tokpos_b, (void*)h_attn_xerr})
@@ -747,10 +744,6 @@ Ctx::~Ctx() {
 }
 
 void Ctx::invalidate_graphs() {
-    for (hipGraphExec_t* g : {&g_ps[0], &g_ps[1]}) {
-        if (*g) hipGraphExecDestroy(*g);
-        *g = nullptr;
-    }
     for (int m = 0; m < 2; ++m) {
         for (hipGraphExec_t* g : {&g_full[m], &g_nolog[m], &g_seg[m][0], &g_seg[m][1], &g_seg[m][2]}) {
             if (*g) hipGraphExecDestroy(*g);
@@ -985,11 +978,6 @@ bool Ctx::sp_setup() {
     MI_HIP(hipSetDevice(device));
     MI_HIP(hipMalloc(&sp_mem, 4 * act_n + act_f));
     MI_HIP(hipMemset(sp_mem, 0, 4 * act_n + act_f));
-    MI_HIP(hipMalloc(&sp_gx, (size_t)hp.n_embd * 8));
-    MI_HIP(hipMemset(sp_gx, 0, (size_t)hp.n_embd * 8));
-    MI_HIP(hipMalloc(&sp_gh, (size_t)hp.n_ff * 8));
-    MI_HIP(hipMemset(sp_gh, 0, (size_t)hp.n_ff * 8));
-    sp_fuse = hp.n_embd <= 8192 ? (getenv("MI_DV_FUSE") ? atoi(getenv("MI_DV_FUSE")) : 1) : 0;
     sp_act[0] = sp_mem;
     sp_act[1] = sp_mem + act_n;
     sp_act[2] = sp_mem + 2 * act_n;
@@ -1010,22 +998,6 @@ void Ctx::enqueue_step_sp(bool with_logits) {
     const float kq_scale = 1.0f / std::sqrt((float)hp.head_dim);
     auto act = [&](int role, int fmt, int K, const float* norm_w) {
         return ActOut{K, fmt & 1, fmt >> 1, sp_act[role], norm_w, hp.eps};
-    };
-    // the in-launch activation of a residual / SwiGLU launch: edge e (1 WO, 2 gate/up, 3 down) of
-    // layer l; tag = step * (3 n_layer + 1) + 3 l + e, unique per step, layer and edge
-    const int fuse_m = sp_fuse;   // 1 every edge, 2 h only, 3 the normed x edges only
-    auto fused = [&](int e) { return fuse_m == 1 || (fuse_m == 2 && e == 2) || (fuse_m == 3 && e != 2); };
-    auto qout = [&](const ActOut& t, unsigned long long* g, int l, int e) {
-        DvQuantOut o;
-        std::memset(&o, 0, sizeof(o));
-        if (!fused(e)) return o;
-        o.t = t;
-        o.gran = g;
-        o.step = step_ctr;
-        o.tag_mul = 3u * (unsigned)hp.n_layer + 1u;
-        o.tag_add = 3u * (unsigned)l + (unsigned)e;
-        o.err = d_attn_xerr;
-        return o;
     };
     if (on()) {
         EmbedParams ep{m->tok_embd, tokpos, x, hp.n_embd, m->pos_embd, 0, step_ctr};
@@ -1083,10 +1055,9 @@ void Ctx::enqueue_step_sp(bool with_logits) {
             p.nseg = 1;
             p.seg[0] = seg_of(L.wo, PAIR_ADJ, EPI_ADD, x);
             p.seg[0].resid = x;
-            p.qout = qout(act(2, b.fC, hp.n_embd, L.ffn_norm), sp_gx, l, 1);
             if (on()) {
                 launch_dgemv(p, stream);
-                if (!fused(1)) launch_dv_quant(x, act(2, b.fC, hp.n_embd, L.ffn_norm), stream);
+                launch_dv_quant(x, act(2, b.fC, hp.n_embd, L.ffn_norm), stream);
             }
         }
         {   // FFN gate/up + SwiGLU, then h quantised
@@ -1097,12 +1068,11 @@ void Ctx::enqueue_step_sp(bool with_logits) {
             p.nseg = 1;
             p.seg[0] = seg_of(L.gate, PAIR_AB, EPI_SWIGLU, h);
             p.seg[0].B = L.up;
-            p.qout = qout(act(3, b.fD, hp.n_ff, nullptr), sp_gh, l, 2);
             if (l == prof_layer) seg = 1;
             const bool timed = l == prof_layer && seg_filter == 1;
             if (on()) launch_dgemv(p, stream, timed ? prof_ev[0] : nullptr, timed ? prof_ev[1] : nullptr);
             if (l == prof_layer) seg = 2;
-            if (on() && !fused(2)) launch_dv_quant(h, act(3, b.fD, hp.n_ff, nullptr), stream);
+            if (on()) launch_dv_quant(h, act(3, b.fD, hp.n_ff, nullptr), stream);
         }
         {   // FFN down + residual (in place), then the next layer's (or the output head's) input quantised
             GemvParams p = base;
@@ -1116,10 +1086,9 @@ void Ctx::enqueue_step_sp(bool with_logits) {
             const bool next = l + 1 < hp.n_layer || with_logits;
             const ActOut nx = l + 1 < hp.n_layer ? act(0, sp[l + 1].fA, hp.n_embd, m->layers[l + 1].attn_norm)
                                                  : act(4, sp_fH, hp.n_embd, m->output_norm);
-            if (next) p.qout = qout(nx, sp_gx, l, 3);
             if (on()) {
                 launch_dgemv(p, stream);
-                if (next && !fused(3)) launch_dv_quant(x, nx, stream);
+                if (next) launch_dv_quant(x, nx, stream);
             }
         }
     }
@@ -1136,99 +1105,6 @@ void Ctx::enqueue_step_sp(bool with_logits) {
         TopkParams tp{logits, hp.n_vocab, cand, topk_ids, topk_vals, d_h_topk_ids, d_h_topk_vals};
         launch_topk(tp, stream);
     }
-}
-
-// The persistent step's plan (pstep.hip): every layer's Q|K|V groups, WO, gate/up and down.  It
-// needs the streaming step's head buffers (sp_ok); MoE, GPT-2 and Q8_0 models keep the launches.
-void Ctx::ps_setup() {
-    const HParams& hp = m->hp;
-    ps_note = !sp_ok ? "no streaming step (head buffers)" : hp.arch != ARCH_LLAMA ? "not a LLaMA graph"
-            : hp.n_expert > 0 ? "MoE" : "";
-    if (!ps_note.empty()) return;
-    std::vector<PsLayerDesc> ld(hp.n_layer);
-    for (int l = 0; l < hp.n_layer; ++l) {
-        const Layer& L = m->layers[l];
-        PsLayerDesc& d = ld[l];
-        std::memset(&d, 0, sizeof(d));
-        if (L.n_qkv < 1 || L.n_qkv > 2) {
-            ps_note = "Q/K/V groups";
-            return;
-        }
-        int row0 = 0;
-        for (int g = 0; g < L.n_qkv; ++g) {
-            d.op[d.n_op].A = L.qkv[g];
-            d.op[d.n_op].role = 0;
-            d.op[d.n_op].row0 = row0;
-            row0 += L.qkv[g].rows;
-            d.n_op++;
-        }
-        d.op[d.n_op].A = L.wo;
-        d.op[d.n_op++].role = 1;
-        d.op[d.n_op].A = L.gate;
-        d.op[d.n_op].B = L.up;
-        d.op[d.n_op++].role = 2;
-        d.op[d.n_op].A = L.down;
-        d.op[d.n_op++].role = 3;
-        d.attn_norm = L.attn_norm;
-        d.ffn_norm = L.ffn_norm;
-        d.kc = kcache + (size_t)l * n_ctx * kv_dim;
-        d.vc = vcache + (size_t)l * n_ctx * kv_dim;
-    }
-    MI_HIP(hipSetDevice(device));
-    MI_HIP(hipMalloc(&ps_xout, hp.n_embd * sizeof(float)));
-    PsConfig c;
-    std::memset(&c, 0, sizeof(c));
-    c.n_layer = hp.n_layer;
-    c.n_embd = hp.n_embd;
-    c.n_ff = hp.n_ff;
-    c.n_head = hp.n_head;
-    c.n_head_kv = hp.n_head_kv;
-    c.head_dim = hp.head_dim;
-    c.kv_dim = kv_dim;
-    c.n_rot = hp.n_rot;
-    c.eps = hp.eps;
-    c.theta_scale = std::pow(hp.rope_base, -2.0f / (float)hp.n_rot);
-    c.freq_scale = hp.freq_scale;
-    c.kq_scale = 1.0f / std::sqrt((float)hp.head_dim);
-    c.freq_factors = m->rope_freqs;
-    c.tokpos = tokpos;
-    c.cell_pos = cell_pos;
-    c.step = step_ctr;
-    c.xin = x;
-    c.xout = ps_xout;
-    c.err = d_attn_xerr;
-    std::string why;
-    ps = ps_create(c, ld, &why);
-    if (!ps) ps_note = why;
-}
-
-bool Ctx::ps_usable() const {
-    return ps && !ps_off && decode_mode == 1 && n_cells + 1 <= ATTN_SHORT && dev_chain(device).nctx.load() == 1;
-}
-
-// One batch-1 decode step as the embedding, the persistent launch, then the output head on the
-// streaming GEMV (rms_norm(x) * output_norm quantised, the head, the top-k).  timed: the persistent
-// launch carries the profiling event pair (eager enqueue).
-void Ctx::enqueue_step_ps(bool with_logits, bool timed) {
-    const HParams& hp = m->hp;
-    EmbedParams ep{m->tok_embd, tokpos, x, hp.n_embd, m->pos_embd, 0, step_ctr};
-    launch_embed(ep, stream);
-    if (timed) MI_HIP(hipEventRecord(prof_ev[0], stream));
-    ps_launch(ps, stream);
-    if (timed) MI_HIP(hipEventRecord(prof_ev[1], stream));
-    if (!with_logits) return;
-    launch_dv_quant(ps_xout, ActOut{hp.n_embd, sp_fH & 1, sp_fH >> 1, sp_act[4], m->output_norm, hp.eps}, stream);
-    GemvParams p;
-    std::memset(&p, 0, sizeof(p));
-    p.K = hp.n_embd;
-    p.act_in = sp_act[4];
-    p.act_q8k = sp_fH & 1;
-    p.act_q80 = sp_fH >> 1;
-    p.nseg = 1;
-    p.seg[0] = seg_of(m->output, PAIR_ADJ, EPI_STORE, logits);
-    launch_dgemv(p, stream);
-    TopkParams tp{logits, hp.n_vocab, cand, topk_ids, topk_vals, d_h_topk_ids, d_h_topk_vals};
-    launch_topk(tp, stream);
 }
 
 // One decode step for the token in tokpos (batch 1): the llm_build_llama graph.
@@ -1966,34 +1842,7 @@ int Ctx::decode(const int32_t* tokens, int n, bool all) {
         hp[2] = cell;
         hp[3] = 0;
         MI_HIP(hipMemcpyAsync(tokpos, hp, 4 * sizeof(int), hipMemcpyHostToDevice, stream));
-        if (ps_usable()) {
-            if (last && prof_layer >= 0) {   // the persistent launch timed by events (eager)
-                for (int k = 0; k < 2; ++k)
-                    if (!prof_ev[k]) MI_HIP(hipEventCreate(&prof_ev[k]));
-                enqueue_step_ps(true, true);
-                prof_pending = true;
-                prof_bytes = ps_bytes(ps);
-            } else if (!use_graphs) {
-                enqueue_step_ps(last, false);
-            } else {
-                hipGraphExec_t& g = g_ps[last ? 1 : 0];
-                if (!g) {
-                    hipGraph_t gr = nullptr;
-                    MI_HIP(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
-                    try {
-                        enqueue_step_ps(last, false);
-                    } catch (...) {
-                        hipStreamEndCapture(stream, &gr);
-                        if (gr) hipGraphDestroy(gr);
-                        throw;
-                    }
-                    MI_HIP(hipStreamEndCapture(stream, &gr));
-                    MI_HIP(hipGraphInstantiate(&g, gr, nullptr, nullptr, 0));
-                    MI_HIP(hipGraphDestroy(gr));
-                }
-                MI_HIP(hipGraphLaunch(g, stream));
-            }
-        } else if (last && prof_layer >= 0 && prof_layer < m->hp.n_layer) {
+        if (last && prof_layer >= 0 && prof_layer < m->hp.n_layer) {
             for (int k = 0; k < 2; ++k)
                 if (!prof_ev[k]) MI_HIP(hipEventCreate(&prof_ev[k]));
             // graph up to the profiled launch, the launch itself eagerly with
@@ -2035,7 +1884,6 @@ void Ctx::sync() {
     const bool was_unsynced = unsynced;
     unsynced = false;
     if (h_attn_xerr && *h_attn_xerr) {   // an attention exchange gave up: the step's logits are invalid
-        const unsigned code = *h_attn_xerr;
         *h_attn_xerr = 0;
         logits_valid = false;
         // the cells decoded since the last good sync hold KV rows built from a wrong attention
@@ -2045,18 +1893,6 @@ void Ctx::sync() {
             pos_max = undo_pos;
         }
         invalidate_graphs();
-        if (code == 0x300) {   // dgemv.hip: a waiter's sweep of the output granules gave up
-            sp_fuse = 0;
-            throw Error("decode step: an in-launch activation sweep timed out; the step was rolled back and this "
-                        "context now quantises each activation in a launch of its own");
-        }
-        if (code >= 0x100) {   // pstep.hip: a spin of the persistent step gave up
-            ps_off = true;
-            char msg[160];
-            snprintf(msg, sizeof msg, "persistent decode step: a hand-off timed out (code 0x%x); the step was rolled "
-                     "back and this context now decodes on the launch form", code);
-            throw Error(msg);
-        }
         attn_long_off = true;
         throw Error("long-context attention: the splits of a head were not co-resident (exchange timed out); "
                     "the step was rolled back and this context now uses the two-launch kernels");

@@ -227,9 +227,6 @@ struct Ctx {
 
     static constexpr int kTokRing = 8192;
 
-    // persistent decode step (gemv.hip decode_step_kernel) for contexts within ATTN_SHORT cells:
-    // stage tables without / with the output head, built on first use; per-layer activation
-    // buffers (q, attention, residual after WO, FFN, residual after down) written once per step
     // streaming decode step (dgemv.hip) for dense LLaMA contexts within ATTN_SHORT cells: every GEMV
     // reads its activation quantised -- WO's from the attention kernel, the others' from a
     // dv_quant launch (rms_norm'd x, or h) -- from sp_act[role]
@@ -241,26 +238,8 @@ struct Ctx {
     int sp_fH = 0;                      // the output head's activation formats
     char* sp_mem = nullptr;
     char* sp_act[5] = {};               // QKV, WO, gate/up, down, head inputs
-    // in-launch activations (DvQuantOut): the WO / gate/up / down launches publish their outputs as
-    // granules and build the next launch's activation themselves (no dv_quant launch between)
-    unsigned long long* sp_gx = nullptr;   // granules of x after WO / down [n_embd]
-    unsigned long long* sp_gh = nullptr;   // granules of h [n_ff]
-    int sp_fuse = 1;                    // 0 after a sweep gave up (or MI_DV_FUSE=0)
     bool sp_setup();
     void enqueue_step_sp(bool with_logits);
-    // persistent decode step (pstep.hip): every layer of a dense k-quant LLaMA token in one launch,
-    // for contexts within ATTN_SHORT cells, while this context is the only one on its device (its
-    // workgroups need every CU).  decode_mode: 0 the launch form (default), 1 the persistent step
-    // where available.
-    PsStep* ps = nullptr;
-    float* ps_xout = nullptr;           // the residual after the last layer (the head's input)
-    bool ps_off = false;                // a spin of the persistent step gave up: launches from now on
-    int decode_mode = 0;
-    std::string ps_note;                // why the persistent step is unavailable (empty: available)
-    hipGraphExec_t g_ps[2] = {nullptr, nullptr};   // [with_logits]
-    void ps_setup();
-    bool ps_usable() const;             // the next step may run persistent
-    void enqueue_step_ps(bool with_logits, bool timed);
     struct LayerBufs {
         const float* x_in;              // residual stream into the layer
         float *q, *po, *xa, *h, *h2, *xf;   // q, attention output, residual after WO, FFN (2nd expert), after down

@@ -90,18 +90,6 @@ struct ActOut {
     float eps;
 };
 
-// The next launch's quantised activation, built inside a residual / SwiGLU streaming GEMV launch
-// (launch_dgemv): its lanes publish every output as an 8-byte {value, tag} granule, and waiter
-// workgroups after the producers sweep them and quantise (rms_norm(out) * norm_w, or out itself)
-// into t -- dv_quant_kernel's result, without its launch.
-struct DvQuantOut {
-    ActOut t;                     // t.K == the launch's output rows
-    unsigned long long* gran;     // [rows] granules (null: no in-launch activation)
-    const unsigned* step;         // the decode step counter (the embedding launch increments it)
-    unsigned tag_mul, tag_add;    // tag = *step * tag_mul + tag_add: unique per step, layer and edge
-    unsigned* err;                // host-mapped error word: 0x300 when a sweep gave up
-};
-
 constexpr int GEMV_MAX_SEG = 2;
 struct GemvParams {
     GemvSeg seg[GEMV_MAX_SEG];
@@ -133,7 +121,6 @@ struct GemvParams {
     // arrives quantised, act_layout(K, act_q8k, act_q80) at act_in (pro / x / norm_w unused)
     const char* act_in;
     int act_q8k, act_q80;
-    DvQuantOut qout;          // DV_ADD / DV_SWIGLU: the next launch's activation in-launch (gran set)
 };
 
 void init_kernel_attributes();   // once per device, before any graph capture
@@ -307,43 +294,6 @@ void launch_moe_group(const int* sel, int n, int U, int E, int* grp, int* rows, 
                       hipStream_t s);
 void launch_moe_combine(const float* y, const int* pos, const float* w, float* x, int ntok, int n_embd,
                         hipStream_t s);
-
-// ---- the persistent decode step (pstep.hip): every layer of one dense LLaMA token in one launch
-// (a loader wave per CU streams the weights into an LDS ring; consumer waves hand activations
-// between CUs as tagged granules).  Matrices: Q4_K / Q5_K / Q6_K; contexts within ATTN_SHORT cells.
-struct PsOpDesc {
-    QMat A, B;                 // B: the gate/up partner (up)
-    int role;                  // 0 a Q|K|V group, 1 WO, 2 gate/up, 3 down
-    int row0;                  // a Q|K|V group: its first row within the layer's Q|K|V rows
-};
-struct PsLayerDesc {
-    PsOpDesc op[5];            // the Q|K|V groups, then WO, gate/up, down
-    int n_op;
-    const float* attn_norm;
-    const float* ffn_norm;
-    __half* kc;                // this layer's caches [n_ctx][kv_dim]
-    __half* vc;
-};
-struct PsConfig {
-    int n_layer, n_embd, n_ff, n_head, n_head_kv, head_dim, kv_dim, n_rot;
-    float eps, theta_scale, freq_scale, kq_scale;
-    const float* freq_factors;
-    const int* tokpos;         // {token, pos, cell, -}
-    int* cell_pos;
-    const unsigned* step;      // decode steps so far (the embedding launch increments it)
-    const float* xin;          // the embedding row
-    float* xout;               // the residual after the last layer
-    unsigned* err;             // host-mapped error word (a spin gave up: codes >= 0x100)
-};
-struct PsStep;
-// nullptr, with the reason in *why, when the model or device has no persistent form
-PsStep* ps_create(const PsConfig& c, const std::vector<PsLayerDesc>& layers, std::string* why);
-void ps_destroy(PsStep* s);
-void ps_launch(const PsStep* s, hipStream_t st);
-long long ps_bytes(const PsStep* s);   // quantised weight bytes one launch streams
-// diagnostics: s_memrealtime stamps of every CU at the phases of layer `layer` into dev [ncu][16]
-// (null: off); returns the CU count.  Graphs captured before keep the old arguments.
-int ps_arm_stamps(PsStep* s, unsigned long long* dev, int layer);
 
 // ---- load-time repack of GGUF blocks into planes ----
 void launch_repack(const uint8_t* raw, int type, long long rows, int K, uint8_t* const planes[4],

@@ -1050,15 +1050,16 @@ __device__ __forceinline__ float wave_max_any(float v) {
     v = fmaxf(v, dppf<0x143, 0xc>(v, ni));
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
 }
-template <int LPC, int HG, int NWV, int PF = 0>
+template <int LPC, int HG, int NWV>
 __global__ __launch_bounds__(64 * NWV * HG) void attn_dec_kernel(const AttnParams P) {
     static_assert(LPC == 8 || LPC == 16, "head_dim 64 or 128");
     constexpr int HD = LPC * 8, CPW = 64 / LPC, NT = 64 * NWV, STEP = NWV * CPW;
-    // every step of the first 256 cells: q, then the cache rows and positions, requested at entry
+    // the steps of the first 128 cells: q, then the cache rows and positions, requested at entry
     // (buffer loads parked past the descriptor for steps at or past ncell: zeros, no memory
-    // access; K before V, which is needed last), so within 256 cells no K or V row is a dependent
-    // round trip; past that, a loop
-    constexpr int UM = PF ? PF : (256 + STEP - 1) / STEP;
+    // access; K before V, which is needed last); past that, a loop.  The depth barely matters:
+    // 1, 2, 3 and 4 steps (32-128 cells at 8 waves) measured within 0.8 % of each other, the
+    // first 256 cells at entry 1-2 % slower (profiles/r06_fuse_ab.txt)
+    constexpr int UM = (128 + STEP - 1) / STEP;
     __shared__ float sw[HG][ATTN_SHORT];
     __shared__ float redm[HG][NWV];
     __shared__ double dred[HG][NWV];
@@ -1314,13 +1315,7 @@ void launch_attn(const AttnParams& p, hipStream_t s) {
         if (k.hg > 1 || k.qsplit || r == 1) {
             switch (p.head_dim * 8 + k.hg) {
             case 128 * 8 + 1: fd = attn_dec_kernel<16, 1, 16>; nwv = 16; break;
-            case 128 * 8 + 2: {
-                const int pf = getenv("MI_ATTN_PF") ? atoi(getenv("MI_ATTN_PF")) : 0;
-                fd = pf == 1 ? attn_dec_kernel<16, 2, 8, 1> : pf == 2 ? attn_dec_kernel<16, 2, 8, 2> : pf == 3 ? attn_dec_kernel<16, 2, 8, 3>
-                   : pf == 4 ? attn_dec_kernel<16, 2, 8, 4> : attn_dec_kernel<16, 2, 8>;
-                nwv = 8;
-                break;
-            }
+            case 128 * 8 + 2: fd = attn_dec_kernel<16, 2, 8>; nwv = 8; break;
             case 64 * 8 + 1: fd = attn_dec_kernel<8, 1, 16>; nwv = 16; break;
             case 64 * 8 + 2: fd = attn_dec_kernel<8, 2, 8>; nwv = 8; break;
             case 64 * 8 + 4: fd = attn_dec_kernel<8, 4, 4>; nwv = 4; break;

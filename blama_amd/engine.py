@@ -85,11 +85,8 @@ _SIGS = {
     "mi_prof_read": (C.c_int32, [_P, C.POINTER(C.c_float), C.c_int32]),
     "mi_prof_ffn_bytes": (C.c_int64, [_P]),
     "mi_decode_path": (C.c_int32, [_P]),
-    "mi_decode_set_mode": (C.c_int32, [_P, C.c_int32]),
     "mi_op_dgemv": (C.c_int32, [C.c_int32, C.c_int32, C.c_int32, C.c_void_p, C.c_int32, C.c_int32, C.c_int32,
                                 C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p]),
-    "mi_decode_path_note": (C.c_char_p, [_P]),
-    "mi_debug_ps_stamps": (C.c_int32, [_P, C.c_int32, C.POINTER(C.c_uint64), C.c_int32]),
     "mi_prof_bytes": (C.c_int64, [_P]),
     "mi_debug_stamps": (C.c_int32, [_P, _P, C.c_int32]),
     "mi_op_gemv": (C.c_int32, [C.c_int32, C.c_int32, _P, C.c_int32, C.c_int32, _P, _P]),
@@ -320,21 +317,6 @@ class Context:
     @property
     def ffn_bytes(self) -> int:
         return lib().mi_prof_ffn_bytes(self.h)
-
-    def set_decode_mode(self, mode: int) -> int:
-        """0: the launch form (default); 1: the persistent decode step where available."""
-        return int(lib().mi_decode_set_mode(self.h, mode))
-
-    def ps_stamps(self, layer: int, read: bool = False):
-        """Diagnostics: arm the persistent step's per-CU phase stamps for `layer`; with read=True
-        return the last step's stamps [n_cu][16] (100 MHz ticks)."""
-        buf = np.zeros((1024, 16), np.uint64)
-        n = lib().mi_debug_ps_stamps(self.h, layer, buf.ctypes.data_as(C.POINTER(C.c_uint64)) if read else None, 1024)
-        _check(n, "ps_stamps")
-        return buf[:n] if read else n
-
-    def decode_path_note(self) -> str:
-        return (lib().mi_decode_path_note(self.h) or b"").decode()
 
     def decode_path(self) -> int:
         """1: decode steps within 512 cells run on the streaming GEMV (dgemv.hip); 0: gemv_kernel."""

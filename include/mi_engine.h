@@ -147,20 +147,9 @@ int32_t mi_prof_read(mi_ctx* ctx, float* us, int32_t n);
 int64_t mi_prof_ffn_bytes(const mi_ctx* ctx);
 /* Algorithmic HBM bytes of the launch mi_prof_read last timed (the FFN gate/up launch). */
 int64_t mi_prof_bytes(const mi_ctx* ctx);
-/* Diagnostics: the form the context's next decode step (within 512 cells) takes: 2 the persistent
- * launch (pstep.hip), 1 the streaming GEMV launches (dgemv.hip), 0 the gemv_kernel graph; -1 for
- * a null context. */
+/* Diagnostics: the form the context's next decode step within 512 cells takes: 1 the streaming GEMV
+ * launches (dgemv.hip), 0 the gemv_kernel graph (MoE, GPT-2); -1 for a null context. */
 int32_t mi_decode_path(const mi_ctx* ctx);
-/* Decode step form: 0 (default) the launch form, 1 the persistent launch where the model and
- * device allow it.  Returns the previous mode, -1 on a bad argument. */
-int32_t mi_decode_set_mode(mi_ctx* ctx, int32_t mode);
-/* Diagnostics: why the next step does not take the persistent launch ("" when it does, apart from
- * the cell limit). */
-const char* mi_decode_path_note(const mi_ctx* ctx);
-/* Diagnostics: arms per-CU s_memrealtime stamps (100 MHz) of the persistent step's phases in layer
- * `layer` (< 0: disarm) for the following steps, and copies the last stamps, [n_cu][16] uint64,
- * into out when out is set.  Returns the CU count (0 without a persistent step, -1 on error). */
-int32_t mi_debug_ps_stamps(mi_ctx* ctx, int32_t layer, uint64_t* out, int32_t n_cu);
 /* Diagnostics: copies the per-workgroup s_memrealtime stamps (100 MHz) of the
  * first n_launch launches of the last decode step, [launch][512][8] uint64, to
  * out.  Returns the number of launches copied; 0 unless the library is the

@@ -269,32 +269,3 @@ def test_prefill_512_tokens_matches_oracle(gpu_lib):
     ref = oracle_from_gguf(buf, n_ctx=520).decode(prompt)
     assert _logits_close(a.logits(), ref)
     assert [int(i) for i in a.topk(10)[0]] == [i for i, _ in R.topk(ref, 10)]
-
-
-@pytest.mark.parametrize("name", ["tiny-q4_k_m", "tiny-q8_0", "tiny-q6_k"])
-def test_in_launch_activation_bit_identical(gpu_lib, monkeypatch, name):
-    """The streaming step's WO / gate/up / down launches build the next launch's quantised
-    activation themselves (dgemv.hip dv_waiter: output granules swept by waiter workgroups, then
-    dv_quant_kernel's arithmetic in its summation order).  Logits and the KV cache must be
-    bit-identical to the same step with a dv_quant launch between every pair (MI_DV_FUSE=0), step
-    after step, with and without the output head (the decode graph without logits)."""
-    cfg = synthetic.CONFIGS[name]
-    buf = synthetic.build_gguf(cfg, seed=33)
-    m = engine.Model(buf)
-    prompt = [int(t) for t in np.random.default_rng(5).integers(0, cfg.n_vocab, 5)]
-    monkeypatch.setenv("MI_NO_BATCH", "1")        # token-by-token decode graphs
-    a = engine.Context(m, n_ctx=64)
-    monkeypatch.setenv("MI_DV_FUSE", "0")
-    b = engine.Context(m, n_ctx=64)
-    try:
-        assert a.decode(prompt) == 0 and b.decode(prompt) == 0
-        assert np.array_equal(a.logits().view(np.uint32), b.logits().view(np.uint32))
-        for t in [7, 9, 11, 400 % cfg.n_vocab, 3]:
-            a.decode([t])
-            b.decode([t])
-            assert np.array_equal(a.logits().view(np.uint32), b.logits().view(np.uint32)), t
-        assert a.state_get() == b.state_get()
-    finally:
-        a.close()
-        b.close()
-        m.close()
