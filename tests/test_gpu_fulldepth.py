@@ -87,19 +87,23 @@ def _attribute_moe_rows(name, errs, gaps):
     ties = [j for j, g in enumerate(gaps) if g < ROUTE_TIE]
     print(f"{name}: median l2/rms {med:.2e}; routing near-ties (token index, gap): "
           f"{[(j, round(float(gaps[j]), 5)) for j in ties]}")
-    bad = []
+    bad, lines = [], []
     for label, e, j in errs:
         if e <= 3 * med:
             continue
         prev = [k for k in ties if k <= j]
         if not prev:
             bad.append((label, e))
-            print(f"{name} {label}: l2/rms {e:.2e} ({e / med:.1f}x median) -- NO routing near-tie at or before token {j}")
+            lines.append(f"{label}: l2/rms {e:.2e} ({e / med:.1f}x median) -- NO routing near-tie at or before token {j}")
             continue
         k = prev[-1]
         where = "at this token" if k == j else f"carried from token {k} ({j - k} tokens earlier)"
-        print(f"{name} {label}: l2/rms {e:.2e} ({e / med:.1f}x median) <- routing near-tie {where}, "
-              f"oracle router gap {gaps[k]:.4f}")
+        lines.append(f"{label}: l2/rms {e:.2e} ({e / med:.1f}x median) <- routing near-tie {where}, "
+                     f"oracle router gap {gaps[k]:.4f}")
+    for ln in lines:
+        print(f"{name} {ln}")
+    if lines:   # in pytest's warnings summary, so the attribution is in every run's log
+        warnings.warn(f"MoE row attribution, {name} (median l2/rms {med:.2e}): " + "; ".join(lines))
     assert not bad, (name, "rows above 3x the median error with no routing near-tie", bad)
 
 
