@@ -441,10 +441,13 @@ struct MmqSegs {
     int n;
 };
 
-template <int T> struct M2 {
+// the pre-scaled Q4_K / Q5_K tile (QMat::ps): P0 [8][64][16] | P1 [8][64][16] | header [32][16]
+constexpr int MMQ_PS_TB = 16384 + 512;
+template <int T, bool PS = false> struct M2 {
     static constexpr int RT = 2;                                        // row tiles per block
     static constexpr int NW = 4 * RT;                                    // waves: one 32x32 tile each
-    static constexpr int SLOT = (mmq32_tile_bytes_d(T) + 1023) / 1024 * 1024;
+    static constexpr int TB = PS ? MMQ_PS_TB : mmq32_tile_bytes_d(T);   // bytes of a tile-superblock
+    static constexpr int SLOT = (TB + 1023) / 1024 * 1024;
     static constexpr int A_OFF = RT * SLOT;
     static constexpr int BSB_OFF = A_OFF + 4 * 8192;
     static constexpr int DT_OFF = BSB_OFF + 2048;
@@ -453,7 +456,7 @@ template <int T> struct M2 {
     static constexpr int NI = STAGE / 1024;                             // 1 KiB LDS-DMA pieces
     static constexpr int NIW = (NI + NW - 1) / NW;                      // per wave (some repeat)
     static constexpr int NPL = 2;                                       // K-quant operand planes
-    static constexpr int PLANES = (T == T_Q4_K || T == T_Q5_K) ? RT * NPL * 8 * 1024 : 0;
+    static constexpr int PLANES = ((T == T_Q4_K || T == T_Q5_K) && !PS) ? RT * NPL * 8 * 1024 : 0;
     static constexpr int lds(int nst) { return nst * STAGE + PLANES; }
 };
 
@@ -484,12 +487,90 @@ __device__ __forceinline__ unsigned bmul(unsigned x, unsigned s) {
 template <typename V>
 __device__ __forceinline__ V lds_ld(const lchar* p) { return *reinterpret_cast<const __attribute__((address_space(3))) V*>(p); }
 
+// The two int8 operand planes of the scaled weights sc_j * q of sub-blocks 2w, 2w + 1 of one row
+// (lane) of a Q4_K / Q5_K tile, every byte <= 127:
+//   Q4_K (sc = 8 sh + sl, q <= 15):  P0 = q * sl, P1 = q * sh,  sc q = P0 + 8 P1
+//   Q5_K (q = lo4 + 16 hb <= 31):    p = sc * q <= 1953 (16-bit products),
+//                                    P0 = p & 127, P1 = p >> 7,  sc q = P0 + 128 P1
+// hd: the row's header, wq: its qs piece w, qh (Q5_K): its high bits.  o0 / o1: P0 / P1 of
+// sub-block 2w, o2 / o3: of sub-block 2w + 1.  Shared by mmq2_t's in-LDS decode and
+// prescale_kernel, so the two GEMM forms multiply the same operands.
+template <int T>
+__device__ __forceinline__ void q45_planes(const u32x4 hd, const u32x4 wq, const u32x4 qh, int w, u32x4& o0, u32x4& o1,
+                                           u32x4& o2, u32x4& o3) {
+    const unsigned Y = hd.y, W = hd.w;
+    // get_scale_min_k4 for j = 2w, 2w + 1
+    int s0, s1;
+    if (w < 2) {
+        s0 = (Y >> (16 * w)) & 63;
+        s1 = (Y >> (16 * w + 8)) & 63;
+    } else {
+        const int k = 2 * w - 4;
+        s0 = ((W >> (8 * k)) & 0xF) | (((Y >> (8 * k + 6)) & 3) << 4);
+        s1 = ((W >> (8 * k + 8)) & 0xF) | (((Y >> (8 * k + 14)) & 3) << 4);
+    }
+    const unsigned q[4] = {wq.x, wq.y, wq.z, wq.w};
+    unsigned* p0 = reinterpret_cast<unsigned*>(&o0);
+    unsigned* p1 = reinterpret_cast<unsigned*>(&o1);
+    unsigned* p2 = reinterpret_cast<unsigned*>(&o2);
+    unsigned* p3 = reinterpret_cast<unsigned*>(&o3);
+    if (T == T_Q4_K) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const unsigned lo = q[i] & 0x0F0F0F0Fu, hi = (q[i] >> 4) & 0x0F0F0F0Fu;
+            p0[i] = bmul(lo, s0 & 7);
+            p1[i] = bmul(lo, s0 >> 3);
+            p2[i] = bmul(hi, s1 & 7);
+            p3[i] = bmul(hi, s1 >> 3);
+        }
+    } else {
+        const unsigned b[4] = {qh.x, qh.y, qh.z, qh.w};
+        // 4 elements q (bytes) times s as 16-bit products, split into lo7 / hi bytes
+        auto split = [](unsigned q5, unsigned sc, unsigned& lo, unsigned& hi) {
+            const unsigned m02 = wmul16(q5 & 0x00FF00FFu, sc), m13 = wmul16((q5 >> 8) & 0x00FF00FFu, sc);
+            lo = (m02 & 0x007F007Fu) | ((m13 & 0x007F007Fu) << 8);
+            hi = ((m02 >> 7) & 0x001F001Fu) | (((m13 >> 7) & 0x001F001Fu) << 8);
+        };
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const unsigned q5a = (q[i] & 0x0F0F0F0Fu) | (((b[i] >> (2 * w)) & 0x01010101u) << 4);
+            const unsigned q5b = ((q[i] >> 4) & 0x0F0F0F0Fu) | (((b[i] >> (2 * w + 1)) & 0x01010101u) << 4);
+            split(q5a, s0, p0[i], p1[i]);
+            split(q5b, s1, p2[i], p3[i]);
+        }
+    }
+}
+
+// QMat::ps from QMat::sw: one workgroup per tile-superblock, wave w writes the planes of piece w
+// (sub-blocks 2w, 2w + 1) for every lane's row, at the offsets mmq2_t's decode writes its LDS
+// planes; the header follows at 16384
+template <int T>
+__global__ __launch_bounds__(256) void prescale_kernel(const uint8_t* sw, uint8_t* dst) {
+    constexpr int TB = mmq32_tile_bytes_d(T), HD = T == T_Q5_K ? 5120 : 4096;
+    const long long tile = blockIdx.x;
+    const uint8_t* src = sw + tile * TB;
+    uint8_t* o = dst + tile * MMQ_PS_TB;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, col = lane & 31;
+    const u32x4 hd = *gp(reinterpret_cast<const u32x4*>(src + HD + col * 16));
+    const u32x4 wq = *gp(reinterpret_cast<const u32x4*>(src + w * 1024 + lane * 16));
+    const u32x4 qh = T == T_Q5_K ? *gp(reinterpret_cast<const u32x4*>(src + 4096 + lane * 16)) : u32x4{0, 0, 0, 0};
+    u32x4 o0, o1, o2, o3;
+    q45_planes<T>(hd, wq, qh, w, o0, o1, o2, o3);
+    *reinterpret_cast<u32x4*>(o + (0 * 8 + 2 * w) * 1024 + lane * 16) = o0;
+    *reinterpret_cast<u32x4*>(o + (1 * 8 + 2 * w) * 1024 + lane * 16) = o1;
+    *reinterpret_cast<u32x4*>(o + (0 * 8 + 2 * w + 1) * 1024 + lane * 16) = o2;
+    *reinterpret_cast<u32x4*>(o + (1 * 8 + 2 * w + 1) * 1024 + lane * 16) = o3;
+    if (threadIdx.x < 32) *reinterpret_cast<u32x4*>(o + 16384 + threadIdx.x * 16) = *gp(reinterpret_cast<const u32x4*>(src + HD + threadIdx.x * 16));
+}
+
 // NST 2: two stages (copy of sb + 1 during sb), one workgroup per CU.  NST 1: one stage, copy and
 // compute in turn, sized (LDS, <= 128 VGPRs) for two workgroups per CU that overlap each other.
-template <int T, bool AB, int NST>
-__global__ __launch_bounds__(64 * M2<T>::NW) __attribute__((amdgpu_waves_per_eu(NST == 1 ? 4 : 2)))
+// PS (Q4_K / Q5_K): the segments' copies are pre-scaled (QMat::ps): no decode step, the operand
+// planes come with the tile (the Q6_K form's shape: one barrier per superblock instead of two).
+template <int T, bool AB, int NST, bool PS = false>
+__global__ __launch_bounds__((64 * M2<T, PS>::NW)) __attribute__((amdgpu_waves_per_eu(NST == 1 ? 4 : 2)))
 void mmq2_t(const GemmParams P, const ActQ8 act, const float2* rope, const MmqSegs S) {
-    using C = M2<T>;
+    using C = M2<T, PS>;
     constexpr int RT = C::RT;
     constexpr int NPL = C::NPL;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -507,7 +588,7 @@ void mmq2_t(const GemmParams P, const ActQ8 act, const float2* rope, const MmqSe
     for (int i = 0; i < MMQ_SEGS; ++i)
         if (i < S.n) nrb += ((AB ? (S.rows[i] + 15) / 16 : (S.rows[i] + 31) / 32) + RT - 1) / RT;
     const int ntb = (act.npad + 127) / 128;           // token blocks
-    const int TB = mmq32_tile_bytes_d(T);
+    const int TB = C::TB;
     // split-K: part kh of the grid's ksplit parts takes superblocks [nb kh / ks, nb (kh + 1) / ks)
     const int ks = P.ksplit > 1 ? P.ksplit : 1;
     const int nbid = (int)gridDim.x / ks;
@@ -673,64 +754,26 @@ void mmq2_t(const GemmParams P, const ActQ8 act, const float2* rope, const MmqSe
             //     (no integer multiply per result); wave w decodes piece w (sub-blocks 2w, 2w + 1)
             //     for every lane's row.
             const lchar* wt = stg + wr * C::SLOT;
-            lchar* pl = (lchar*)(smem + NST * C::STAGE) + wr * (NPL * 8 * 1024) + lane * 16;
-            {
-                const u32x4 hd = lds_ld<u32x4>(wt + (T == T_Q5_K ? 5120 : 4096) + col * 16);
-                const unsigned Y = hd.y, W = hd.w;
-                // get_scale_min_k4 for j = 2w, 2w + 1 (w is wave-uniform: a scalar branch)
-                int s0, s1;
-                if (w < 2) {
-                    s0 = (Y >> (16 * w)) & 63;
-                    s1 = (Y >> (16 * w + 8)) & 63;
-                } else {
-                    const int k = 2 * w - 4;
-                    s0 = ((W >> (8 * k)) & 0xF) | (((Y >> (8 * k + 6)) & 3) << 4);
-                    s1 = ((W >> (8 * k + 8)) & 0xF) | (((Y >> (8 * k + 14)) & 3) << 4);
-                }
+            // PS: the planes are in the tile (P0 at 0, P1 at 8 KiB, the header at 16 KiB)
+            lchar* pl = PS ? (lchar*)wt + lane * 16 : (lchar*)(smem + NST * C::STAGE) + wr * (NPL * 8 * 1024) + lane * 16;
+            constexpr int HDO = PS ? 16384 : (T == T_Q5_K ? 5120 : 4096);
+            if (!PS) {
+                const u32x4 hd = lds_ld<u32x4>(wt + HDO + col * 16);
                 const u32x4 wq = lds_ld<u32x4>(wt + w * 1024 + lane * 16);
-                const unsigned q[4] = {wq.x, wq.y, wq.z, wq.w};
+                const u32x4 qh = T == T_Q5_K ? lds_ld<u32x4>(wt + 4096 + lane * 16) : u32x4{0, 0, 0, 0};
                 u32x4 o0, o1, o2, o3;   // P0/P1 of sub-block 2w, P0/P1 of sub-block 2w + 1
-                unsigned* p0 = reinterpret_cast<unsigned*>(&o0);
-                unsigned* p1 = reinterpret_cast<unsigned*>(&o1);
-                unsigned* p2 = reinterpret_cast<unsigned*>(&o2);
-                unsigned* p3 = reinterpret_cast<unsigned*>(&o3);
-                if (T == T_Q4_K) {
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const unsigned lo = q[i] & 0x0F0F0F0Fu, hi = (q[i] >> 4) & 0x0F0F0F0Fu;
-                        p0[i] = bmul(lo, s0 & 7);
-                        p1[i] = bmul(lo, s0 >> 3);
-                        p2[i] = bmul(hi, s1 & 7);
-                        p3[i] = bmul(hi, s1 >> 3);
-                    }
-                } else {
-                    const u32x4 qh = lds_ld<u32x4>(wt + 4096 + lane * 16);
-                    const unsigned b[4] = {qh.x, qh.y, qh.z, qh.w};
-                    // 4 elements q (bytes) times s as 16-bit products, split into lo7 / hi bytes
-                    auto split = [](unsigned q5, unsigned sc, unsigned& lo, unsigned& hi) {
-                        const unsigned m02 = wmul16(q5 & 0x00FF00FFu, sc), m13 = wmul16((q5 >> 8) & 0x00FF00FFu, sc);
-                        lo = (m02 & 0x007F007Fu) | ((m13 & 0x007F007Fu) << 8);
-                        hi = ((m02 >> 7) & 0x001F001Fu) | (((m13 >> 7) & 0x001F001Fu) << 8);
-                    };
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const unsigned q5a = (q[i] & 0x0F0F0F0Fu) | (((b[i] >> (2 * w)) & 0x01010101u) << 4);
-                        const unsigned q5b = ((q[i] >> 4) & 0x0F0F0F0Fu) | (((b[i] >> (2 * w + 1)) & 0x01010101u) << 4);
-                        split(q5a, s0, p0[i], p1[i]);
-                        split(q5b, s1, p2[i], p3[i]);
-                    }
-                }
+                q45_planes<T>(hd, wq, qh, w, o0, o1, o2, o3);
                 *reinterpret_cast<__attribute__((address_space(3))) u32x4*>(pl + (0 * 8 + 2 * w) * 1024) = o0;
                 *reinterpret_cast<__attribute__((address_space(3))) u32x4*>(pl + (1 * 8 + 2 * w) * 1024) = o1;
                 *reinterpret_cast<__attribute__((address_space(3))) u32x4*>(pl + (0 * 8 + 2 * w + 1) * 1024) = o2;
                 *reinterpret_cast<__attribute__((address_space(3))) u32x4*>(pl + (1 * 8 + 2 * w + 1) * 1024) = o3;
+                __builtin_amdgcn_s_waitcnt((0xF) | (0x3 << 14) | (0x7 << 4));   // lgkmcnt(0): planes written
+                __builtin_amdgcn_s_barrier();
             }
-            __builtin_amdgcn_s_waitcnt((0xF) | (0x3 << 14) | (0x7 << 4));   // lgkmcnt(0): planes written
-            __builtin_amdgcn_s_barrier();
             // (2) the MFMAs: token tile w x row tile wr, the planes accumulated over the sub-blocks
             if (busy) {
                 constexpr int r = 0;
-                const u32x4 hd = lds_ld<u32x4>(wt + (T == T_Q5_K ? 5120 : 4096) + col * 16);
+                const u32x4 hd = lds_ld<u32x4>(wt + HDO + col * 16);
                 v16i acc0 = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, acc1 = acc0;
                 const lchar* plr = (const lchar*)pl;
                 // every operand of the superblock read first (at 2 waves per SIMD the LDS latency
@@ -1374,7 +1417,7 @@ __global__ __launch_bounds__(256) void part_sum_kernel(const float* part, int kp
     out[(long long)t * ostride + r] = acc;
 }
 
-template <int T, int NST> constexpr int m2_lds() { return M2<T>::lds(NST); }
+template <int T, int NST, bool PS = false> constexpr int m2_lds() { return M2<T, PS>::lds(NST); }
 
 }  // namespace mmq
 
@@ -1417,6 +1460,21 @@ size_t mmq32_copy_bytes(const QMat& A, bool pair) {
     return (size_t)nrt * A.nb * mmq32_tile_bytes(A.type);
 }
 
+size_t mmq32_ps_bytes(const QMat& A, bool pair) {
+    if (A.type != T_Q4_K && A.type != T_Q5_K) return 0;
+    const long long nrt = pair ? (A.rows + 15) / 16 : (A.rows + 31) / 32;
+    return (size_t)nrt * A.nb * mmq::MMQ_PS_TB;
+}
+
+void launch_mmq32_prescale(const QMat& A, bool pair, uint8_t* dst, hipStream_t s) {
+    if (A.type != T_Q4_K && A.type != T_Q5_K) throw Error("mmq32 prescale: Q4_K / Q5_K only");
+    if (!A.sw) throw Error("mmq32 prescale: no MFMA-order copy");
+    const long long nrt = pair ? (A.rows + 15) / 16 : (A.rows + 31) / 32;
+    auto f = A.type == T_Q4_K ? mmq::prescale_kernel<T_Q4_K> : mmq::prescale_kernel<T_Q5_K>;
+    hipLaunchKernelGGL(f, dim3((unsigned)(nrt * A.nb)), dim3(256), 0, s, A.sw, dst);
+    MI_HIP(hipGetLastError());
+}
+
 void launch_mmq32_swizzle(const QMat& A, const QMat* B, uint8_t* dst, hipStream_t s) {
     if (!mmq32_supported(A.type)) throw Error("mmq32 swizzle: Q4_K / Q5_K / Q6_K / Q8_0 only");
     if (B && (B->type != A.type || B->rows != A.rows || B->K != A.K)) throw Error("mmq32 swizzle: bad pair");
@@ -1427,8 +1485,16 @@ void launch_mmq32_swizzle(const QMat& A, const QMat* B, uint8_t* dst, hipStream_
 
 namespace {
 bool mmq2_enabled() { return true; }
-// one mmq2 launch over the segments S (all of p.A's type; one segment unless launch_mmq32_multi)
-void launch_mmq2(const GemmParams& p, const mmq::MmqSegs& S, const ActQ8& act, const float2* rope, hipStream_t s) {
+// MI_MMQ_PS=0: the tiled GEMM decodes its Q4_K / Q5_K operand planes in LDS even where a
+// pre-scaled copy exists (the A/B control; both forms multiply the same operands)
+bool mmq_ps_enabled() {
+    const char* e = getenv("MI_MMQ_PS");   // (read per launch: the op tests switch it in-process)
+    return e == nullptr || atoi(e) != 0;
+}
+// one mmq2 launch over the segments S (all of p.A's type; one segment unless launch_mmq32_multi);
+// ps: S.sw are pre-scaled copies (QMat::ps)
+void launch_mmq2(const GemmParams& p, const mmq::MmqSegs& S, const ActQ8& act, const float2* rope, hipStream_t s,
+                 bool ps = false) {
     const bool ab = p.pair == PAIR_AB;
     const int T = p.A.type;
     const int RT = mmq::M2<T_Q4_K>::RT;
@@ -1460,14 +1526,25 @@ void launch_mmq2(const GemmParams& p, const mmq::MmqSegs& S, const ActQ8& act, c
     case T_Q6_K: f2 = ab ? mmq::mmq2_t<T_Q6_K, true, NST_> : mmq::mmq2_t<T_Q6_K, false, NST_>; lds = mmq::m2_lds<T_Q6_K, NST_>(); break; \
     default: f2 = ab ? mmq::mmq2_t<T_Q8_0, true, NST_> : mmq::mmq2_t<T_Q8_0, false, NST_>; lds = mmq::m2_lds<T_Q8_0, NST_>(); break; \
     }
-    if (nst == 1) { M2_PICK(1) } else { M2_PICK(2) }
+#define M2_PICK_PS(NST_)                                                                                        \
+    switch (T) {                                                                                                \
+    case T_Q4_K: f2 = ab ? mmq::mmq2_t<T_Q4_K, true, NST_, true> : mmq::mmq2_t<T_Q4_K, false, NST_, true>; lds = mmq::m2_lds<T_Q4_K, NST_, true>(); break; \
+    default: f2 = ab ? mmq::mmq2_t<T_Q5_K, true, NST_, true> : mmq::mmq2_t<T_Q5_K, false, NST_, true>; lds = mmq::m2_lds<T_Q5_K, NST_, true>(); break; \
+    }
+    if (ps && T != T_Q4_K && T != T_Q5_K) throw Error("mmq2: pre-scaled copies are Q4_K / Q5_K");
+    if (ps) {
+        if (nst == 1) { M2_PICK_PS(1) } else { M2_PICK_PS(2) }
+    } else {
+        if (nst == 1) { M2_PICK(1) } else { M2_PICK(2) }
+    }
 #undef M2_PICK
-    static bool attr_done[2][4][2] = {};
+#undef M2_PICK_PS
+    static bool attr_done[2][2][4][2] = {};
     const int ti = T == T_Q4_K ? 0 : T == T_Q5_K ? 1 : T == T_Q6_K ? 2 : 3;
     const int ni = nst == 1 ? 0 : 1;
-    if (!attr_done[ni][ti][ab]) {
+    if (!attr_done[ps][ni][ti][ab]) {
         MI_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(f2), hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-        attr_done[ni][ti][ab] = true;
+        attr_done[ps][ni][ti][ab] = true;
     }
     hipLaunchKernelGGL(f2, dim3(g2), dim3(64 * NWv), (size_t)lds, s, p, act, rope, S);
     MI_HIP(hipGetLastError());
@@ -1496,12 +1573,14 @@ void launch_mmq32_multi(const GemmParams* ps, int n, const ActQ8& act, const flo
     if (act.ntok < 1 || act.npad % 32 || act.npad > UB_MAX) throw Error("mmq32: bad token count");
     mmq::MmqSegs S{};
     S.n = n;
+    bool pre = mmq_ps_enabled();
+    for (int i = 0; i < n; ++i) pre = pre && ps[i].A.ps;
     for (int i = 0; i < n; ++i) {
-        S.sw[i] = ps[i].A.sw;
+        S.sw[i] = pre ? ps[i].A.ps : ps[i].A.sw;
         S.rows[i] = ps[i].A.rows;
         S.epi[i] = ps[i].epi;
     }
-    launch_mmq2(ps[0], S, act, rope, s);
+    launch_mmq2(ps[0], S, act, rope, s, pre);
 }
 
 bool mmq2_active() { return mmq2_enabled(); }
@@ -1520,10 +1599,11 @@ void launch_mmq32(const GemmParams& p, const ActQ8& act, const float2* rope, hip
     if (!p.A.sw) throw Error("mmq32: the matrix has no MFMA-order copy");
     mmq::MmqSegs S{};
     S.n = 1;
-    S.sw[0] = p.A.sw;
+    const bool pre = mmq_ps_enabled() && p.A.ps && !p.grp;
+    S.sw[0] = pre ? p.A.ps : p.A.sw;
     S.rows[0] = p.A.rows;
     S.epi[0] = p.epi;
-    launch_mmq2(p, S, act, rope, s);
+    launch_mmq2(p, S, act, rope, s, pre);
 }
 
 // The Q4_K / Q5_K mmqs1 launches on the one-deep-ring, two-waves-per-SIMD form (214-220 VGPRs

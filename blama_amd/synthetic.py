@@ -65,6 +65,10 @@ CONFIGS = {
     "tiny1-q4_k_m": LlamaConfig("tiny1", 512, 256, 1, 4, 2, 512, 256, 10000.0, 1e-5, "Q4_K_M"),
     "tiny-moe-q5_k_m": LlamaConfig("tiny-moe", 512, 256, 2, 4, 2, 512, 256, 1e6, 1e-5,
                                     "Q5_K_M", n_expert=4, n_expert_used=2),
+    # GQA ratio 2 with 16 kv heads of 64: the quantising decode attention has no
+    # kernel for two kv heads per 256-block, so decode takes the gemv_kernel step and short
+    # batches the plain fused attention + quant_act -- both must still run
+    "tiny-gqa16-q4_k_m": LlamaConfig("tiny-gqa16", 512, 2048, 2, 32, 16, 512, 256, 10000.0, 1e-5, "Q4_K_M"),
     # the reference's own KAT model shape (gpt2-117m-q6_k, t-integration.cpp:25): 12 x 768,
     # 12 heads of 64, n_ff 3072, V 50257, 1024 positions, every matrix Q6_K, tied output head
     "gpt2-117m-q6_k": LlamaConfig("GPT-2-117M", 50257, 768, 12, 12, 12, 3072, 1024, 10000.0, 1e-5,

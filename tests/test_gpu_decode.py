@@ -269,3 +269,42 @@ def test_prefill_512_tokens_matches_oracle(gpu_lib):
     ref = oracle_from_gguf(buf, n_ctx=520).decode(prompt)
     assert _logits_close(a.logits(), ref)
     assert [int(i) for i in a.topk(10)[0]] == [i for i, _ in R.topk(ref, 10)]
+
+
+def test_gqa16_layout_decode_and_short_batch(gpu_lib):
+    """32 q heads over 16 kv heads of 64: decode against the oracle, and a short
+    verification batch (MI_OUT_ALL, the split-K streaming GEMMs) row by row against the same
+    tokens decoded one at a time."""
+    cfg = synthetic.CONFIGS["tiny-gqa16-q4_k_m"]
+    buf = synthetic.build_gguf(cfg, seed=12)
+    m = engine.Model(buf)
+    a = engine.Context(m, n_ctx=64)
+    b = engine.Context(m, n_ctx=64)
+    orc = oracle_from_gguf(buf, n_ctx=64)
+    try:
+        prompt = [3, 77, 120, 9]
+        assert a.decode(prompt) == 0
+        ref = orc.decode(prompt)
+        assert _logits_close(a.logits(), ref)
+        for t in [5, 300, 41]:
+            a.decode([t])
+            ref = orc.decode_one(t)
+            assert _logits_close(a.logits(), ref), t
+            assert [int(i) for i in a.topk(10)[0]] == [i for i, _ in R.topk(ref, 10)]
+        claimed = [int(t) for t in np.random.default_rng(3).integers(0, cfg.n_vocab, 20)]
+        assert b.decode(prompt + [5, 300, 41]) == 0
+        assert b.decode(claimed, all_logits=True) == 0
+        # the batch's GEMMs sum in another fp32 order, which can flip a Q8_K rounding of a later
+        # activation (test_gpu_fullwidth.py's docstring): rows within 2e-2 rms of the per-token
+        # path, the same top-1 unless the two ids are within twice the row's largest difference
+        for i, t in enumerate(claimed):
+            a.decode([t])
+            x, y = b.logits(row=i).astype(np.float64), a.logits().astype(np.float64)
+            d = float(np.max(np.abs(x - y)))
+            assert d <= 2e-2 * float(np.sqrt(np.mean(y ** 2))), (i, d)
+            ix, iy = int(np.argmax(x)), int(np.argmax(y))
+            assert ix == iy or y[iy] - y[ix] <= 2 * d, (i, ix, iy)
+    finally:
+        a.close()
+        b.close()
+        m.close()
