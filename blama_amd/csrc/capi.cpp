@@ -812,11 +812,6 @@ int32_t mi_op_gemm(int32_t device, int32_t type, const void* raw, const void* ra
         DevBuf sw(mmq32_copy_bytes(A, pair));
         launch_mmq32_swizzle(A, pair ? &B : nullptr, sw.as<uint8_t>(), nullptr);
         A.sw = sw.as<uint8_t>();
-        DevBuf psb(std::max<size_t>(16, mmq32_ps_bytes(A, pair)));   // the engine's pre-scaled copy (Q4_K / Q5_K)
-        if (mmq32_ps_bytes(A, pair)) {
-            launch_mmq32_prescale(A, pair, psb.as<uint8_t>(), nullptr);
-            A.ps = psb.as<uint8_t>();
-        }
         const int npad = (ntok + 31) / 32 * 32;
         DevBuf dx((size_t)ntok * K * sizeof(float)), dy((size_t)ntok * rows * sizeof(float));
         DevBuf dq((size_t)npad * K), ddT((size_t)npad * (K / 32) * sizeof(float)), dbs((size_t)npad * (K / 256) * 16);

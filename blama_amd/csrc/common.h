@@ -61,10 +61,6 @@ struct QMat {                // device view of one (expert of a) quantised matri
     // 16 gate + 16 up rows per tile.
     const uint8_t* sw;
     long long sw_expert_stride;  // bytes between the experts' MFMA-order copies (MoE)
-    // Q4_K / Q5_K of dense models: the same tiles with the two int8 operand planes of the scaled
-    // weights already decoded (mmq.hip prescale_kernel): [row tile][superblock][P0 8 KiB | P1
-    // 8 KiB | header 512 B], read by the tiled GEMM instead of decoding every superblock in LDS
-    const uint8_t* ps;
     int n_exp;                   // experts stacked in the planes (MoE *_exps tensors), else 1
 };
 

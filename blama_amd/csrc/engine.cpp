@@ -145,7 +145,6 @@ Model::~Model() {
     if (arena || mmq_arena || gelu_tab) hipSetDevice(device);
     if (arena) hipFree(arena);
     if (mmq_arena) hipFree(mmq_arena);
-    if (mmq_ps_arena) hipFree(mmq_ps_arena);
     if (gelu_tab) hipFree(gelu_tab);
 }
 
@@ -216,26 +215,6 @@ bool Model::ensure_mmq_copies() {
         }
         A.sw = mmq_arena + offs[i];
         A.sw_expert_stride = (long long)one;
-    }
-    // the pre-scaled copies of the dense Q4_K / Q5_K projections (MoE experts keep the decode:
-    // their copies would triple an already ~30 GB set)
-    size_t ps_total = 0;
-    std::vector<size_t> ps_offs;
-    for (auto& t : todo) {
-        ps_offs.push_back(ps_total);
-        if (t.first->n_exp <= 1) ps_total = (ps_total + mmq32_ps_bytes(*t.first, t.second != nullptr) + 255) & ~size_t(255);
-    }
-    if (ps_total && hipMalloc(&mmq_ps_arena, ps_total) == hipSuccess) {
-        for (size_t i = 0; i < todo.size(); ++i) {
-            QMat& A = *todo[i].first;
-            if (A.n_exp > 1 || !mmq32_ps_bytes(A, todo[i].second != nullptr)) continue;
-            launch_mmq32_prescale(A, todo[i].second != nullptr, mmq_ps_arena + ps_offs[i], nullptr);
-            A.ps = mmq_ps_arena + ps_offs[i];
-        }
-        mmq_bytes += ps_total;
-    } else {
-        (void)hipGetLastError();   // no room: the tiled GEMM decodes the planes itself
-        mmq_ps_arena = nullptr;
     }
     MI_HIP(hipDeviceSynchronize());
     return true;

@@ -98,9 +98,6 @@ struct Model {
     // their own after the arena broadcast): one more weight-sized allocation, HBM for speed
     uint8_t* mmq_arena = nullptr;
     size_t mmq_bytes = 0;
-    // the pre-scaled operand-plane copies (QMat::ps) of the dense Q4_K / Q5_K matrices: ~3.7x their
-    // MFMA-order copies (7B Q4_K_M: +9.7 GB), built with them; null if it does not fit
-    uint8_t* mmq_ps_arena = nullptr;
     std::mutex mmq_mu;
     // false when the copy does not fit (the batch path then uses the v_dot4 GEMM).  The copies are
     // taken from the arena once: writes to the arena (mi_model_arena, mi_model_replicate) must

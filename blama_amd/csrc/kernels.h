@@ -351,10 +351,6 @@ int mmq32_tile_bytes(int type);
 size_t mmq32_copy_bytes(const QMat& A, bool pair);
 // Builds the MFMA-order copy of A (and B for a pair) into dst from the planes.
 void launch_mmq32_swizzle(const QMat& A, const QMat* B, uint8_t* dst, hipStream_t s);
-// The pre-scaled operand-plane copy (QMat::ps) of a Q4_K / Q5_K MFMA-order copy: its bytes, and
-// its construction from A.sw (the planes are the tiled GEMM's own decode, bit for bit).
-size_t mmq32_ps_bytes(const QMat& A, bool pair);
-void launch_mmq32_prescale(const QMat& A, bool pair, uint8_t* dst, hipStream_t s);
 // GemmParams: A (B = up for PAIR_AB / EPI_SWIGLU), epi, K, out/out_stride, resid, tokpos [ntok][4],
 // RoPE fields (rope table from launch_rope_table), caches; the tokens are act's.
 void launch_mmq32(const GemmParams& p, const ActQ8& act, const float2* rope, hipStream_t s);

@@ -441,12 +441,10 @@ struct MmqSegs {
     int n;
 };
 
-// the pre-scaled Q4_K / Q5_K tile (QMat::ps): P0 [8][64][16] | P1 [8][64][16] | header [32][16]
-constexpr int MMQ_PS_TB = 16384 + 512;
-template <int T, bool PS = false> struct M2 {
+template <int T> struct M2 {
     static constexpr int RT = 2;                                        // row tiles per block
     static constexpr int NW = 4 * RT;                                    // waves: one 32x32 tile each
-    static constexpr int TB = PS ? MMQ_PS_TB : mmq32_tile_bytes_d(T);   // bytes of a tile-superblock
+    static constexpr int TB = mmq32_tile_bytes_d(T);                    // bytes of a tile-superblock
     static constexpr int SLOT = (TB + 1023) / 1024 * 1024;
     static constexpr int A_OFF = RT * SLOT;
     static constexpr int BSB_OFF = A_OFF + 4 * 8192;
@@ -456,7 +454,7 @@ template <int T, bool PS = false> struct M2 {
     static constexpr int NI = STAGE / 1024;                             // 1 KiB LDS-DMA pieces
     static constexpr int NIW = (NI + NW - 1) / NW;                      // per wave (some repeat)
     static constexpr int NPL = 2;                                       // K-quant operand planes
-    static constexpr int PLANES = ((T == T_Q4_K || T == T_Q5_K) && !PS) ? RT * NPL * 8 * 1024 : 0;
+    static constexpr int PLANES = (T == T_Q4_K || T == T_Q5_K) ? RT * NPL * 8 * 1024 : 0;
     static constexpr int lds(int nst) { return nst * STAGE + PLANES; }
 };
 
@@ -493,8 +491,8 @@ __device__ __forceinline__ V lds_ld(const lchar* p) { return *reinterpret_cast<c
 //   Q5_K (q = lo4 + 16 hb <= 31):    p = sc * q <= 1953 (16-bit products),
 //                                    P0 = p & 127, P1 = p >> 7,  sc q = P0 + 128 P1
 // hd: the row's header, wq: its qs piece w, qh (Q5_K): its high bits.  o0 / o1: P0 / P1 of
-// sub-block 2w, o2 / o3: of sub-block 2w + 1.  Shared by mmq2_t's in-LDS decode and
-// prescale_kernel, so the two GEMM forms multiply the same operands.
+// sub-block 2w, o2 / o3: of sub-block 2w + 1.  (r06: a copy holding these planes pre-decoded,
+// 3.7x the tile bytes, measured slower -- the L2->LDS copies bound this GEMM)
 template <int T>
 __device__ __forceinline__ void q45_planes(const u32x4 hd, const u32x4 wq, const u32x4 qh, int w, u32x4& o0, u32x4& o1,
                                            u32x4& o2, u32x4& o3) {
@@ -541,36 +539,12 @@ __device__ __forceinline__ void q45_planes(const u32x4 hd, const u32x4 wq, const
     }
 }
 
-// QMat::ps from QMat::sw: one workgroup per tile-superblock, wave w writes the planes of piece w
-// (sub-blocks 2w, 2w + 1) for every lane's row, at the offsets mmq2_t's decode writes its LDS
-// planes; the header follows at 16384
-template <int T>
-__global__ __launch_bounds__(256) void prescale_kernel(const uint8_t* sw, uint8_t* dst) {
-    constexpr int TB = mmq32_tile_bytes_d(T), HD = T == T_Q5_K ? 5120 : 4096;
-    const long long tile = blockIdx.x;
-    const uint8_t* src = sw + tile * TB;
-    uint8_t* o = dst + tile * MMQ_PS_TB;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, col = lane & 31;
-    const u32x4 hd = *gp(reinterpret_cast<const u32x4*>(src + HD + col * 16));
-    const u32x4 wq = *gp(reinterpret_cast<const u32x4*>(src + w * 1024 + lane * 16));
-    const u32x4 qh = T == T_Q5_K ? *gp(reinterpret_cast<const u32x4*>(src + 4096 + lane * 16)) : u32x4{0, 0, 0, 0};
-    u32x4 o0, o1, o2, o3;
-    q45_planes<T>(hd, wq, qh, w, o0, o1, o2, o3);
-    *reinterpret_cast<u32x4*>(o + (0 * 8 + 2 * w) * 1024 + lane * 16) = o0;
-    *reinterpret_cast<u32x4*>(o + (1 * 8 + 2 * w) * 1024 + lane * 16) = o1;
-    *reinterpret_cast<u32x4*>(o + (0 * 8 + 2 * w + 1) * 1024 + lane * 16) = o2;
-    *reinterpret_cast<u32x4*>(o + (1 * 8 + 2 * w + 1) * 1024 + lane * 16) = o3;
-    if (threadIdx.x < 32) *reinterpret_cast<u32x4*>(o + 16384 + threadIdx.x * 16) = *gp(reinterpret_cast<const u32x4*>(src + HD + threadIdx.x * 16));
-}
-
 // NST 2: two stages (copy of sb + 1 during sb), one workgroup per CU.  NST 1: one stage, copy and
 // compute in turn, sized (LDS, <= 128 VGPRs) for two workgroups per CU that overlap each other.
-// PS (Q4_K / Q5_K): the segments' copies are pre-scaled (QMat::ps): no decode step, the operand
-// planes come with the tile (the Q6_K form's shape: one barrier per superblock instead of two).
-template <int T, bool AB, int NST, bool PS = false>
-__global__ __launch_bounds__((64 * M2<T, PS>::NW)) __attribute__((amdgpu_waves_per_eu(NST == 1 ? 4 : 2)))
+template <int T, bool AB, int NST>
+__global__ __launch_bounds__(64 * M2<T>::NW) __attribute__((amdgpu_waves_per_eu(NST == 1 ? 4 : 2)))
 void mmq2_t(const GemmParams P, const ActQ8 act, const float2* rope, const MmqSegs S) {
-    using C = M2<T, PS>;
+    using C = M2<T>;
     constexpr int RT = C::RT;
     constexpr int NPL = C::NPL;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -754,10 +728,9 @@ void mmq2_t(const GemmParams P, const ActQ8 act, const float2* rope, const MmqSe
             //     (no integer multiply per result); wave w decodes piece w (sub-blocks 2w, 2w + 1)
             //     for every lane's row.
             const lchar* wt = stg + wr * C::SLOT;
-            // PS: the planes are in the tile (P0 at 0, P1 at 8 KiB, the header at 16 KiB)
-            lchar* pl = PS ? (lchar*)wt + lane * 16 : (lchar*)(smem + NST * C::STAGE) + wr * (NPL * 8 * 1024) + lane * 16;
-            constexpr int HDO = PS ? 16384 : (T == T_Q5_K ? 5120 : 4096);
-            if (!PS) {
+            lchar* pl = (lchar*)(smem + NST * C::STAGE) + wr * (NPL * 8 * 1024) + lane * 16;
+            constexpr int HDO = T == T_Q5_K ? 5120 : 4096;
+            {
                 const u32x4 hd = lds_ld<u32x4>(wt + HDO + col * 16);
                 const u32x4 wq = lds_ld<u32x4>(wt + w * 1024 + lane * 16);
                 const u32x4 qh = T == T_Q5_K ? lds_ld<u32x4>(wt + 4096 + lane * 16) : u32x4{0, 0, 0, 0};
@@ -1417,7 +1390,7 @@ __global__ __launch_bounds__(256) void part_sum_kernel(const float* part, int kp
     out[(long long)t * ostride + r] = acc;
 }
 
-template <int T, int NST, bool PS = false> constexpr int m2_lds() { return M2<T, PS>::lds(NST); }
+template <int T, int NST> constexpr int m2_lds() { return M2<T>::lds(NST); }
 
 }  // namespace mmq
 
@@ -1460,20 +1433,6 @@ size_t mmq32_copy_bytes(const QMat& A, bool pair) {
     return (size_t)nrt * A.nb * mmq32_tile_bytes(A.type);
 }
 
-size_t mmq32_ps_bytes(const QMat& A, bool pair) {
-    if (A.type != T_Q4_K && A.type != T_Q5_K) return 0;
-    const long long nrt = pair ? (A.rows + 15) / 16 : (A.rows + 31) / 32;
-    return (size_t)nrt * A.nb * mmq::MMQ_PS_TB;
-}
-
-void launch_mmq32_prescale(const QMat& A, bool pair, uint8_t* dst, hipStream_t s) {
-    if (A.type != T_Q4_K && A.type != T_Q5_K) throw Error("mmq32 prescale: Q4_K / Q5_K only");
-    if (!A.sw) throw Error("mmq32 prescale: no MFMA-order copy");
-    const long long nrt = pair ? (A.rows + 15) / 16 : (A.rows + 31) / 32;
-    auto f = A.type == T_Q4_K ? mmq::prescale_kernel<T_Q4_K> : mmq::prescale_kernel<T_Q5_K>;
-    hipLaunchKernelGGL(f, dim3((unsigned)(nrt * A.nb)), dim3(256), 0, s, A.sw, dst);
-    MI_HIP(hipGetLastError());
-}
 
 void launch_mmq32_swizzle(const QMat& A, const QMat* B, uint8_t* dst, hipStream_t s) {
     if (!mmq32_supported(A.type)) throw Error("mmq32 swizzle: Q4_K / Q5_K / Q6_K / Q8_0 only");
@@ -1485,16 +1444,8 @@ void launch_mmq32_swizzle(const QMat& A, const QMat* B, uint8_t* dst, hipStream_
 
 namespace {
 bool mmq2_enabled() { return true; }
-// MI_MMQ_PS=0: the tiled GEMM decodes its Q4_K / Q5_K operand planes in LDS even where a
-// pre-scaled copy exists (the A/B control; both forms multiply the same operands)
-bool mmq_ps_enabled() {
-    const char* e = getenv("MI_MMQ_PS");   // (read per launch: the op tests switch it in-process)
-    return e == nullptr || atoi(e) != 0;
-}
-// one mmq2 launch over the segments S (all of p.A's type; one segment unless launch_mmq32_multi);
-// ps: S.sw are pre-scaled copies (QMat::ps)
-void launch_mmq2(const GemmParams& p, const mmq::MmqSegs& S, const ActQ8& act, const float2* rope, hipStream_t s,
-                 bool ps = false) {
+// one mmq2 launch over the segments S (all of p.A's type; one segment unless launch_mmq32_multi)
+void launch_mmq2(const GemmParams& p, const mmq::MmqSegs& S, const ActQ8& act, const float2* rope, hipStream_t s) {
     const bool ab = p.pair == PAIR_AB;
     const int T = p.A.type;
     const int RT = mmq::M2<T_Q4_K>::RT;
@@ -1526,25 +1477,14 @@ void launch_mmq2(const GemmParams& p, const mmq::MmqSegs& S, const ActQ8& act, c
     case T_Q6_K: f2 = ab ? mmq::mmq2_t<T_Q6_K, true, NST_> : mmq::mmq2_t<T_Q6_K, false, NST_>; lds = mmq::m2_lds<T_Q6_K, NST_>(); break; \
     default: f2 = ab ? mmq::mmq2_t<T_Q8_0, true, NST_> : mmq::mmq2_t<T_Q8_0, false, NST_>; lds = mmq::m2_lds<T_Q8_0, NST_>(); break; \
     }
-#define M2_PICK_PS(NST_)                                                                                        \
-    switch (T) {                                                                                                \
-    case T_Q4_K: f2 = ab ? mmq::mmq2_t<T_Q4_K, true, NST_, true> : mmq::mmq2_t<T_Q4_K, false, NST_, true>; lds = mmq::m2_lds<T_Q4_K, NST_, true>(); break; \
-    default: f2 = ab ? mmq::mmq2_t<T_Q5_K, true, NST_, true> : mmq::mmq2_t<T_Q5_K, false, NST_, true>; lds = mmq::m2_lds<T_Q5_K, NST_, true>(); break; \
-    }
-    if (ps && T != T_Q4_K && T != T_Q5_K) throw Error("mmq2: pre-scaled copies are Q4_K / Q5_K");
-    if (ps) {
-        if (nst == 1) { M2_PICK_PS(1) } else { M2_PICK_PS(2) }
-    } else {
-        if (nst == 1) { M2_PICK(1) } else { M2_PICK(2) }
-    }
+    if (nst == 1) { M2_PICK(1) } else { M2_PICK(2) }
 #undef M2_PICK
-#undef M2_PICK_PS
-    static bool attr_done[2][2][4][2] = {};
+    static bool attr_done[2][4][2] = {};
     const int ti = T == T_Q4_K ? 0 : T == T_Q5_K ? 1 : T == T_Q6_K ? 2 : 3;
     const int ni = nst == 1 ? 0 : 1;
-    if (!attr_done[ps][ni][ti][ab]) {
+    if (!attr_done[ni][ti][ab]) {
         MI_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(f2), hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-        attr_done[ps][ni][ti][ab] = true;
+        attr_done[ni][ti][ab] = true;
     }
     hipLaunchKernelGGL(f2, dim3(g2), dim3(64 * NWv), (size_t)lds, s, p, act, rope, S);
     MI_HIP(hipGetLastError());
@@ -1573,14 +1513,12 @@ void launch_mmq32_multi(const GemmParams* ps, int n, const ActQ8& act, const flo
     if (act.ntok < 1 || act.npad % 32 || act.npad > UB_MAX) throw Error("mmq32: bad token count");
     mmq::MmqSegs S{};
     S.n = n;
-    bool pre = mmq_ps_enabled();
-    for (int i = 0; i < n; ++i) pre = pre && ps[i].A.ps;
     for (int i = 0; i < n; ++i) {
-        S.sw[i] = pre ? ps[i].A.ps : ps[i].A.sw;
+        S.sw[i] = ps[i].A.sw;
         S.rows[i] = ps[i].A.rows;
         S.epi[i] = ps[i].epi;
     }
-    launch_mmq2(ps[0], S, act, rope, s, pre);
+    launch_mmq2(ps[0], S, act, rope, s);
 }
 
 bool mmq2_active() { return mmq2_enabled(); }
@@ -1599,11 +1537,10 @@ void launch_mmq32(const GemmParams& p, const ActQ8& act, const float2* rope, hip
     if (!p.A.sw) throw Error("mmq32: the matrix has no MFMA-order copy");
     mmq::MmqSegs S{};
     S.n = 1;
-    const bool pre = mmq_ps_enabled() && p.A.ps && !p.grp;
-    S.sw[0] = pre ? p.A.ps : p.A.sw;
+    S.sw[0] = p.A.sw;
     S.rows[0] = p.A.rows;
     S.epi[0] = p.epi;
-    launch_mmq2(p, S, act, rope, s, pre);
+    launch_mmq2(p, S, act, rope, s);
 }
 
 // The Q4_K / Q5_K mmqs1 launches on the one-deep-ring, two-waves-per-SIMD form (214-220 VGPRs

@@ -162,23 +162,6 @@ def test_mmqs_matches_oracle(gpu_lib, t, rows, K, ntoks, pair):
         _check_gemm(t, rows, K, ntok, pair, seed=3 * rows + K + ntok)
 
 
-@pytest.mark.parametrize("t,rows,K,ntok,pair", [(R.Q4_K, 11008, 4096, 512, True), (R.Q4_K, 4096, 11008, 128, False),
-                                                 (R.Q5_K, 1000, 4096, 70, True), (R.Q5_K, 4096, 4096, 33, False)])
-def test_mmq32_prescaled_copy_bit_identical(gpu_lib, monkeypatch, t, rows, K, ntok, pair):
-    """The tiled GEMM on the pre-scaled operand-plane copy (QMat::ps, prescale_kernel: the planes
-    decoded once at load) against the same GEMM decoding the planes from the MFMA-order copy in
-    LDS every superblock (MI_MMQ_PS=0): the same operands, the same MFMAs, the same fp32 updates
-    in the same order -- bit-identical outputs."""
-    monkeypatch.setenv("MI_MMQS_MAX", "0")
-    raw = rand_matrix(t, rows, K, seed=rows + 5)
-    up = rand_matrix(t, rows, K, seed=rows + 6) if pair else None
-    X = np.stack([rand_x(K, seed=77 + i) for i in range(ntok)])
-    a = engine.op_gemm(t, raw, rows, K, X, raw_up=up)
-    monkeypatch.setenv("MI_MMQ_PS", "0")
-    b = engine.op_gemm(t, raw, rows, K, X, raw_up=up)
-    assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), (R.TYPE_NAME[t], rows, K, ntok, pair)
-
-
 def test_mmq32_rows_not_multiple_of_tile(gpu_lib, monkeypatch):
     """Row counts that leave a partial 32-row (pair: 16-row) tile (the tiled GEMM at every count)."""
     monkeypatch.setenv("MI_MMQS_MAX", "0")
