@@ -894,10 +894,10 @@ int act_fmt(std::initializer_list<int> types) {
 }  // namespace
 
 // The streaming decode step's buffers (dense LLaMA; DESIGN.md §4 "dgemv"), and whether every
-// launch of the step has a compiled variant.  MI_DECODE_OLD=1 keeps the gemv_kernel graph.
+// launch of the step has a compiled variant (MoE and GPT-2 keep the gemv_kernel graph).
 bool Ctx::sp_setup() {
     const HParams& hp = m->hp;
-    if (hp.arch != ARCH_LLAMA || hp.n_expert > 0 || getenv("MI_DECODE_OLD")) return false;
+    if (hp.arch != ARCH_LLAMA || hp.n_expert > 0) return false;
     if (hp.n_embd % 256 || hp.n_ff % 256 || hp.n_head * hp.head_dim != hp.n_embd) return false;
     if (!attn_quant_supported(hp.n_head, hp.n_head_kv, hp.head_dim)) return false;
     const int nl = hp.n_layer;
