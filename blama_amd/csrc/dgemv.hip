@@ -260,7 +260,8 @@ int dv_chunks(int K) {
 // workgroup in the same order: thread-strided 16-B pieces, the wave's DPP tree, the 4 waves in
 // order -- so all blocks see one scale, and the result is bit-reproducible); without it, one wave
 // reads its block.  ggml_compute_forward_rms_norm_f32 + ggml_mul, then quantize_row_q8_K /
-// quantize_row_q8_0 (x86 form).
+// quantize_row_q8_0 (x86 form).  (r06: one wave per block standing in for the four, no LDS or
+// barrier, bit-identical, measured 635-637 vs 644-647 tok/s: not kept, profiles/r06_dvq_ab.txt.)
 constexpr int DQ_NORM_W = 4;   // waves per workgroup with the norm
 __global__ __launch_bounds__(DQ_NORM_W * 64) void dv_quant_kernel(const float* x, const ActOut t) {
     __shared__ double red[DQ_NORM_W];

@@ -1182,12 +1182,7 @@ __global__ __launch_bounds__(64 * NWV * HG) void attn_dec_kernel(const AttnParam
         for (int e = 0; e < 8; ++e) red_o[grp][wave][L * 8 + e] = o[e];
     }
     __syncthreads();
-    for (int d = tid; d < HD; d += NT) {
-        float s = red_o[grp][0][d];
-#pragma unroll
-        for (int w = 1; w < NWV; ++w) s += red_o[grp][w][d];
-        P.part_o[(long long)unit * HD + d] = s;
-    }
+    // (no fp32 copy of the output: the streaming WO launch reads only the quantised one)
     // the WO launch's quantised activation: the workgroup's HG heads are whole 256-blocks, one
     // wave per block; element e of the workgroup's span is head e / HD, dim e % HD
     constexpr int NE = HG * HD;
