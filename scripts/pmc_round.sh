@@ -17,5 +17,7 @@ cp $CSV $OUT/counter_collection.csv
 python3 scripts/pmc_traffic.py $CSV "dgemv_kernel<12, -1, 2, 2, 2>" $OUT/${RND}_pmc_ffn.json
 python3 scripts/pmc_traffic.py $CSV "dgemv_kernel<12, -1, 1, 2, 1>" $OUT/${RND}_pmc_wo.json
 python3 scripts/pmc_traffic.py $CSV "dv_quant_kernel" $OUT/${RND}_pmc_dv_quant.json
-python3 scripts/pmc_traffic.py $CSV "attn_fused_kernel<" $OUT/${RND}_pmc_attn_fused.json
+python3 scripts/pmc_traffic.py $CSV "attn_dec_kernel<" $OUT/${RND}_pmc_attn_dec.json
+python3 scripts/pmc_traffic.py $CSV "dgemv_kernel<14, -1, 1, 6, 1>" $OUT/${RND}_pmc_down_q6k.json
+python3 scripts/pmc_traffic.py $CSV "dgemv_kernel<12, -1, 1, 6, 1>" $OUT/${RND}_pmc_down_q4k.json
 true
