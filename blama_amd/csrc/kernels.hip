@@ -1070,11 +1070,13 @@ __global__ __launch_bounds__(64 * NWV * HG) void attn_dec_kernel(const AttnParam
     const int unit = (int)blockIdx.x * HG + grp;   // this group's q head
     const int g = P.qsplit ? unit / P.qsplit : unit;   // its kv head
     const int L = lane % LPC, G = lane / LPC;
-    const int tp2 = P.tokpos[2], qpos = P.tokpos[1];
+    const int tok = blockIdx.y;   // query token of a short batch (launch_attn_multi); 0 for a decode step
+    const int tp2 = P.tokpos[4 * tok + 2], qpos = P.tokpos[4 * tok + 1];
     const int ncell = min(tp2 + 1, ATTN_SHORT);
     float q[8];
-    const f32x4 qa = gptr(reinterpret_cast<const f32x4*>(P.q + (long long)unit * HD + L * 8))[0];
-    const f32x4 qb = gptr(reinterpret_cast<const f32x4*>(P.q + (long long)unit * HD + L * 8))[1];
+    const float* qrow = P.q + (long long)tok * P.n_head * HD;
+    const f32x4 qa = gptr(reinterpret_cast<const f32x4*>(qrow + (long long)unit * HD + L * 8))[0];
+    const f32x4 qb = gptr(reinterpret_cast<const f32x4*>(qrow + (long long)unit * HD + L * 8))[1];
     const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(const_cast<__half*>(rfl_ptr(P.kcache + (long long)g * HD)), 0, 0x7FFFFFFF, 0x00020000);
     const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(const_cast<__half*>(rfl_ptr(P.vcache + (long long)g * HD)), 0, 0x7FFFFFFF, 0x00020000);
     const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(const_cast<int*>(P.cell_pos), 0, 0x7FFFFFFF, 0x00020000);
@@ -1198,7 +1200,8 @@ __global__ __launch_bounds__(64 * NWV * HG) void attn_dec_kernel(const AttnParam
             for (int w = 1; w < NWV; ++w) s += red_o[gg][w][d];
             v[k] = s;
         }
-        dv_quant_block(P.act_out, e0 / 256 + b, v, lane);
+        if (P.act_q8.q) quant_actq8_block(P.act_q8, tok, e0 / 256 + b, v, lane);   // a short batch's WO input
+        else dv_quant_block(P.act_out, e0 / 256 + b, v, lane);
     }
 }
 
@@ -1229,6 +1232,11 @@ static void attn_fns_r(int hd, AttnFn& a, AttnFn& b, AttnFn& f) {
     default: a = b = f = nullptr; break;
     }
 }
+
+// one q head per group (R = 1) of head_dim 64 / 128 for a quantising pick: the decode kernel with
+// 8-16 waves per group (attn_dec_kernel), nwv its waves per group; null: the fused kernel serves it
+struct AttnQuantPick;
+static AttnFn attn_dec_pick(const AttnQuantPick& k, int r, int head_dim, int& nwv);
 
 // the R = 1 fused kernel with hg groups of 4 waves (the streaming decode step's quantising form)
 static AttnFn attn_fused_hg1(int hd, int hg) {
@@ -1280,6 +1288,19 @@ static AttnQuantPick attn_quant_pick(int n_head, int n_head_kv, int head_dim) {
     return k;
 }
 
+static AttnFn attn_dec_pick(const AttnQuantPick& k, int r, int head_dim, int& nwv) {
+    nwv = 4;
+    if (!(k.hg > 1 || k.qsplit || r == 1)) return nullptr;
+    switch (head_dim * 8 + k.hg) {
+    case 128 * 8 + 1: nwv = 16; return attn_dec_kernel<16, 1, 16>;
+    case 128 * 8 + 2: nwv = 8; return attn_dec_kernel<16, 2, 8>;
+    case 64 * 8 + 1: nwv = 16; return attn_dec_kernel<8, 1, 16>;
+    case 64 * 8 + 2: nwv = 8; return attn_dec_kernel<8, 2, 8>;
+    case 64 * 8 + 4: nwv = 4; return attn_dec_kernel<8, 4, 4>;
+    default: return nullptr;
+    }
+}
+
 bool attn_quant_supported(int n_head, int n_head_kv, int head_dim) {
     return attn_quant_pick(n_head, n_head_kv, head_dim).f != nullptr;
 }
@@ -1303,20 +1324,8 @@ void launch_attn(const AttnParams& p, hipStream_t s) {
             throw Error("attn: no quantising decode kernel for this head geometry");
         AttnParams q = p;
         q.qsplit = k.qsplit;
-        // one q head per group (R = 1) of head_dim 64 / 128: the decode kernel with 16 waves per
-        // workgroup (attn_dec_kernel); otherwise the fused kernel
-        AttnFn fd = nullptr;
         int nwv = 4;
-        if (k.hg > 1 || k.qsplit || r == 1) {
-            switch (p.head_dim * 8 + k.hg) {
-            case 128 * 8 + 1: fd = attn_dec_kernel<16, 1, 16>; nwv = 16; break;
-            case 128 * 8 + 2: fd = attn_dec_kernel<16, 2, 8>; nwv = 8; break;
-            case 64 * 8 + 1: fd = attn_dec_kernel<8, 1, 16>; nwv = 16; break;
-            case 64 * 8 + 2: fd = attn_dec_kernel<8, 2, 8>; nwv = 8; break;
-            case 64 * 8 + 4: fd = attn_dec_kernel<8, 4, 4>; nwv = 4; break;
-            default: break;
-            }
-        }
+        const AttnFn fd = attn_dec_pick(k, r, p.head_dim, nwv);
         if (fd) {
             hipLaunchKernelGGL(fd, dim3(k.units / k.hg), dim3(64 * nwv * k.hg), 0, s, q);
         } else {
@@ -1379,7 +1388,12 @@ void launch_attn_multi(const AttnParams& p_in, int ntok, float* out, hipStream_t
         if (!k.f || p.act_q8.K != p.n_head * p.head_dim || p.act_q8.ntok != ntok)
             throw Error("attn: no quantising batch kernel for this head geometry");
         p.qsplit = k.qsplit;
-        hipLaunchKernelGGL(k.f, dim3(k.units / k.hg, ntok), dim3(256 * k.hg), 0, s, p);
+        // the decode kernel, one grid row per token, where it serves the geometry (20 / 64 claimed
+        // tokens 3.38 / 5.15 -> 3.36 / 5.09 ms against the fused kernel, profiles/r06_short_attn_ab.txt)
+        int nwv = 4;
+        const AttnFn fd = attn_dec_pick(k, r, p.head_dim, nwv);
+        if (fd) hipLaunchKernelGGL(fd, dim3(k.units / k.hg, ntok), dim3(64 * nwv * k.hg), 0, s, p);
+        else hipLaunchKernelGGL(k.f, dim3(k.units / k.hg, ntok), dim3(256 * k.hg), 0, s, p);
         MI_HIP(hipGetLastError());
         return;
     }
