@@ -986,8 +986,9 @@ bool Ctx::sp_setup() {
     return true;
 }
 
-// One batch-1 decode step on the streaming kernels: the embedding, per layer dv_quant(rms_norm(x) *
-// attn_norm) -> QKV -> attention (its output also quantised) -> WO + residual -> dv_quant(rms_norm
+// One batch-1 decode step on the streaming kernels (any context length): the embedding, per layer
+// dv_quant(rms_norm(x) * attn_norm) -> QKV -> attention (its output also quantised; past ATTN_SHORT
+// cells the split attention + attn_combine_quant) -> WO + residual -> dv_quant(rms_norm
 // * ffn_norm) -> gate/up -> dv_quant(h) -> down + residual, then the output head and the top-k.
 // Profiling segments as enqueue_step's (the gate/up launch of prof_layer carries the event pair).
 void Ctx::enqueue_step_sp(bool with_logits) {
@@ -1040,12 +1041,32 @@ void Ctx::enqueue_step_sp(bool with_logits) {
                 if (on()) launch_dgemv(p, stream);
             }
         }
-        {   // attention (fused, <= ATTN_SHORT cells), its output also quantised for WO
+        {   // attention, its output quantised for WO: <= ATTN_SHORT cells one fused launch (which
+            // quantises); past that the split launch(es) of the r04 step, then the splits summed in
+            // split order and quantised (attn_combine_quant_kernel)
             AttnParams a{q, kl, vl, tokpos, cell_pos, attn_scores, attn_smax, part_o, hp.n_head, hp.n_head_kv,
                          hp.head_dim, kv_dim, (int)n_ctx, kq_scale};
-            a.fused = 1;
-            a.act_out = act(1, b.fB, hp.n_embd, nullptr);
-            if (on()) launch_attn(a, stream);
+            if (attn_fused) {
+                a.fused = 1;
+                a.act_out = act(1, b.fB, hp.n_embd, nullptr);
+                if (on()) launch_attn(a, stream);
+            } else {
+                a.fused = 0;
+                a.xflags = attn_xflags;
+                a.xmax = attn_xmax;
+                a.xsum = attn_xsum;
+                a.step = step_ctr;
+                a.layer = l;
+                a.n_layer = hp.n_layer;
+                a.xerr = d_attn_xerr;
+                a.long_share = dev_chain(device).nctx.load();
+                a.long_off = attn_long_off ? 1 : 0;
+                if (on()) {
+                    launch_attn(a, stream);
+                    launch_attn_combine_quant(AttnPartials{part_o, hp.n_head, hp.head_dim}, tokpos,
+                                              act(1, b.fB, hp.n_embd, nullptr), stream);
+                }
+            }
         }
         {   // output projection + residual (in place), then rms_norm(x) * ffn_norm quantised
             GemvParams p = base;
@@ -1112,7 +1133,7 @@ void Ctx::enqueue_step_sp(bool with_logits) {
 // (0: up to layer prof_layer's FFN gate/up, 1: that launch, 2: the rest).
 void Ctx::enqueue_step(bool with_logits) {
     const HParams& hp = m->hp;
-    if (attn_fused && sp_ok) {
+    if (sp_ok) {   // dense LLaMA at any context (past 512 cells: 474-481 vs 429-435 tok/s at 3968, r06)
         enqueue_step_sp(with_logits);
         return;
     }

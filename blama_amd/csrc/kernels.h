@@ -239,6 +239,9 @@ void launch_attn(const AttnParams& p, hipStream_t s);
 bool attn_quant_supported(int n_head, int n_head_kv, int head_dim);
 // Combine the partials into out[n_head*hd] (tests / the eager debug path).
 void launch_attn_combine(const AttnPartials& a, const int* tokpos, float* out, hipStream_t s);
+// The same sum of the splits (split order, as gemv.hip's PRO_ATTN prologue), quantised into t
+// (t.K == n_head * head_dim): the streaming WO launch's activation past ATTN_SHORT cells.
+void launch_attn_combine_quant(const AttnPartials& a, const int* tokpos, const ActOut& t, hipStream_t s);
 
 // ---- top-k over logits (sorted by logit desc, id asc), k <= 64 ----
 // Stage 1: every 1024-logit block -> its sorted top 64 (wave bitonic sorts +

@@ -1422,6 +1422,39 @@ __global__ void attn_combine_kernel(const AttnPartials A, const int* tokpos, flo
     }
 }
 
+// one wave per 256-block of the output: its 4 elements per lane summed over the splits in split
+// order (split 0 first, then += 1, 2, ..), then dv_quant_block
+__global__ __launch_bounds__(64) void attn_combine_quant_kernel(const AttnPartials A, const int* tokpos, const ActOut t) {
+    int chunk, nsplit;
+    attn_split(tokpos[2] + 1, chunk, nsplit);
+    const int b = blockIdx.x, lane = threadIdx.x;
+    const long long stride = (long long)A.n_head * A.head_dim;
+    const f32x4* o = reinterpret_cast<const f32x4*>(A.o);
+    f32x4 v = o[b * 64 + lane];
+    for (int s0 = 1; s0 < nsplit; s0 += 4) {   // four splits' loads in flight, added in order
+        f32x4 t4[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (s0 + j < nsplit) t4[j] = o[(s0 + j) * stride / 4 + b * 64 + lane];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (s0 + j < nsplit) {
+                v.x += t4[j].x;
+                v.y += t4[j].y;
+                v.z += t4[j].z;
+                v.w += t4[j].w;
+            }
+    }
+    const float q[4] = {v.x, v.y, v.z, v.w};
+    dv_quant_block(t, b, q, lane);
+}
+
+void launch_attn_combine_quant(const AttnPartials& a, const int* tokpos, const ActOut& t, hipStream_t s) {
+    if (t.K != a.n_head * a.head_dim || t.K % 256 || !t.act || t.norm_w) throw Error("attn combine: bad activation");
+    hipLaunchKernelGGL(attn_combine_quant_kernel, dim3(t.K / 256), dim3(64), 0, s, a, tokpos, t);
+    MI_HIP(hipGetLastError());
+}
+
 void launch_attn_combine(const AttnPartials& a, const int* tokpos, float* out, hipStream_t s) {
     hipLaunchKernelGGL(attn_combine_kernel, dim3(a.n_head), dim3(128), 0, s, a, tokpos, out);
     MI_HIP(hipGetLastError());
