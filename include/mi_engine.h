@@ -147,7 +147,7 @@ int32_t mi_prof_read(mi_ctx* ctx, float* us, int32_t n);
 int64_t mi_prof_ffn_bytes(const mi_ctx* ctx);
 /* Algorithmic HBM bytes of the launch mi_prof_read last timed (the FFN gate/up launch). */
 int64_t mi_prof_bytes(const mi_ctx* ctx);
-/* Diagnostics: the form the context's next decode step within 512 cells takes: 1 the streaming GEMV
+/* Diagnostics: the form the context's decode steps take: 1 the streaming GEMV
  * launches (dgemv.hip), 0 the gemv_kernel graph (MoE, GPT-2); -1 for a null context. */
 int32_t mi_decode_path(const mi_ctx* ctx);
 /* Diagnostics: copies the per-workgroup s_memrealtime stamps (100 MHz) of the
