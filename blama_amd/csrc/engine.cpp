@@ -897,7 +897,8 @@ int act_fmt(std::initializer_list<int> types) {
 // launch of the step has a compiled variant (MoE and GPT-2 keep the gemv_kernel graph).
 bool Ctx::sp_setup() {
     const HParams& hp = m->hp;
-    if (hp.arch != ARCH_LLAMA || hp.n_expert > 0) return false;
+    if (hp.arch != ARCH_LLAMA) return false;
+    const bool moe = hp.n_expert > 0;   // MoE: the attention half streams, the experts keep gemv_kernel
     if (hp.n_embd % 256 || hp.n_ff % 256 || hp.n_head * hp.head_dim != hp.n_embd) return false;
     if (!attn_quant_supported(hp.n_head, hp.n_head_kv, hp.head_dim)) return false;
     const int nl = hp.n_layer;
@@ -938,6 +939,7 @@ bool Ctx::sp_setup() {
         w.act_q8k = sp[l].fB & 1;
         w.act_q80 = sp[l].fB >> 1;
         ok = ok && dgemv_supported(w);
+        if (moe) continue;
         GemvParams gu = p;
         gu.nseg = 1;
         gu.seg[0] = seg_of(L.gate, PAIR_AB, EPI_SWIGLU, h);
@@ -993,6 +995,7 @@ bool Ctx::sp_setup() {
 // Profiling segments as enqueue_step's (the gate/up launch of prof_layer carries the event pair).
 void Ctx::enqueue_step_sp(bool with_logits) {
     const HParams& hp = m->hp;
+    const bool moe = hp.n_expert > 0;
     int seg = 0;
     auto on = [&]() { return seg_filter < 0 || seg_filter == seg; };
     const float theta_scale = std::pow(hp.rope_base, -2.0f / (float)hp.n_rot);
@@ -1078,8 +1081,52 @@ void Ctx::enqueue_step_sp(bool with_logits) {
             p.seg[0].resid = x;
             if (on()) {
                 launch_dgemv(p, stream);
-                launch_dv_quant(x, act(2, b.fC, hp.n_embd, L.ffn_norm), stream);
+                if (!moe) launch_dv_quant(x, act(2, b.fC, hp.n_embd, L.ffn_norm), stream);
             }
+        }
+        if (moe) {   // the routed experts on the r04 step's kernels (layer_ops' MoE FFN), x in place
+            GemvParams gb = base;
+            gb.eps = hp.eps;
+            RouterParams rp{x, L.ffn_norm, hp.eps, L.router, hp.n_embd, hp.n_expert, hp.n_expert_used, sel, selw, 0};
+            if (on()) launch_router(rp, stream);
+            GemvParams p = gb;
+            p.pro = PRO_RMSNORM;
+            p.x[0] = x;
+            p.norm_w = L.ffn_norm;
+            p.sel = sel;
+            p.selw = selw;
+            p.nseg = 2;
+            for (int k = 0; k < 2; ++k) {
+                p.seg[k] = seg_of(L.gate, PAIR_AB, EPI_SWIGLU, k == 0 ? h : h2);
+                p.seg[k].B = L.up;
+                p.seg[k].expA = p.seg[k].expB = k;
+            }
+            if (l == prof_layer) seg = 1;
+            const bool timed = l == prof_layer && seg_filter == 1;
+            if (on()) launch_gemv(p, stream, timed ? prof_ev[0] : nullptr, timed ? prof_ev[1] : nullptr);
+            if (l == prof_layer) seg = 2;
+            GemvParams d = gb;
+            d.pro = PRO_PLAIN;
+            d.x[0] = h;
+            d.x[1] = h2;
+            d.nslots = 2;
+            d.K = hp.n_ff;
+            d.sel = sel;
+            d.selw = selw;
+            d.nseg = 1;
+            d.seg[0] = seg_of(L.down, PAIR_AB, EPI_MOE_DOWN, x);
+            d.seg[0].expA = 0;
+            d.seg[0].expB = 1;
+            d.seg[0].actB = 1;
+            d.seg[0].resid = x;
+            if (on()) {
+                launch_gemv(d, stream);
+                if (l + 1 < hp.n_layer)
+                    launch_dv_quant(x, act(0, sp[l + 1].fA, hp.n_embd, m->layers[l + 1].attn_norm), stream);
+                else if (with_logits)
+                    launch_dv_quant(x, act(4, sp_fH, hp.n_embd, m->output_norm), stream);
+            }
+            continue;
         }
         {   // FFN gate/up + SwiGLU, then h quantised
             GemvParams p = base;
