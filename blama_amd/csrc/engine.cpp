@@ -894,7 +894,7 @@ int act_fmt(std::initializer_list<int> types) {
 }  // namespace
 
 // The streaming decode step's buffers (dense LLaMA; DESIGN.md §4 "dgemv"), and whether every
-// launch of the step has a compiled variant (MoE and GPT-2 keep the gemv_kernel graph).
+// launch of the step has a compiled variant (GPT-2 keeps the gemv_kernel graph; MoE experts run on it).
 bool Ctx::sp_setup() {
     const HParams& hp = m->hp;
     if (hp.arch != ARCH_LLAMA) return false;

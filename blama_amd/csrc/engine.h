@@ -233,7 +233,7 @@ struct Ctx {
     struct SpLayer {
         int fA, fB, fC, fD;             // activation formats of QKV, WO, gate/up, down: bit 0 Q8_K, bit 1 Q8_0
     };
-    bool sp_ok = false;                 // false: the gemv_kernel graph (MoE, GPT-2)
+    bool sp_ok = false;                 // false: the gemv_kernel graph (GPT-2)
     std::vector<SpLayer> sp;
     int sp_fH = 0;                      // the output head's activation formats
     char* sp_mem = nullptr;

@@ -148,7 +148,8 @@ int64_t mi_prof_ffn_bytes(const mi_ctx* ctx);
 /* Algorithmic HBM bytes of the launch mi_prof_read last timed (the FFN gate/up launch). */
 int64_t mi_prof_bytes(const mi_ctx* ctx);
 /* Diagnostics: the form the context's decode steps take: 1 the streaming GEMV
- * launches (dgemv.hip), 0 the gemv_kernel graph (MoE, GPT-2); -1 for a null context. */
+ * launches (dgemv.hip; MoE: the attention half, the experts on gemv_kernel), 0 the gemv_kernel graph
+ * (GPT-2); -1 for a null context. */
 int32_t mi_decode_path(const mi_ctx* ctx);
 /* Diagnostics: copies the per-workgroup s_memrealtime stamps (100 MHz) of the
  * first n_launch launches of the last decode step, [launch][512][8] uint64, to
