@@ -603,13 +603,16 @@ int32_t mi_op_gemv(int32_t device, int32_t type, const void* raw, int32_t rows, 
 // The decode step's streaming GEMV (dgemv.hip) for one launch of a given role: x quantised on the
 // device by dv_quant_kernel (no norm), then dgemv_kernel.  role 0 (Q/K/V, no RoPE: every row a Q
 // row; a second matrix = a second segment of another type), 1 (residual add), 2 (SwiGLU of the pair
-// A = gate, B = up), 3 (store).
+// A = gate, B = up), 3 (store), 4 (residual add with x quantised inside the launch, by every
+// workgroup: the small models' FFN down).
 int32_t mi_op_dgemv(int32_t device, int32_t role, int32_t type, const void* raw, int32_t rows, int32_t K, int32_t type2,
                     const void* raw2, int32_t rows2, const float* x, const float* resid, float* y) {
     try {
         MI_HIP(hipSetDevice(device));
         ensure_attrs(device);
-        if (role < 0 || role > 3) throw Error("op_dgemv: role");
+        if (role < 0 || role > 4) throw Error("op_dgemv: role");
+        const bool addq = role == 4;
+        if (addq) role = 1;
         std::vector<std::unique_ptr<DevBuf>> keep;
         const QMat a = upload_qmat(type, raw, rows, K, keep);
         QMat b{};
@@ -629,7 +632,8 @@ int32_t mi_op_dgemv(int32_t device, int32_t role, int32_t type, const void* raw,
         GemvParams p;
         std::memset(&p, 0, sizeof(p));
         p.K = K;
-        p.act_in = act.as<char>();
+        p.act_in = addq ? nullptr : act.as<char>();
+        p.x[0] = addq ? dx.as<float>() : nullptr;
         p.act_q8k = fmt & 1;
         p.act_q80 = fmt >> 1;
         p.tokpos = dtp.as<int>();

@@ -15,8 +15,9 @@
 //    alternatives (scripts/exp_fgemv.cpp, profiles/r05_exp_fgemv*.txt): publishing
 //    the activation inside the producing launch by arrival tickets cost 6-10 us per launch; an
 //    rms-norm prologue in every QKV / gate/up workgroup as much as the separate launch; the FFN
-//    down launch quantising h itself in every workgroup (no launch before it) 1-1.5 % slower per
-//    token; an Infinity-Cache prefetch of the next layer's weights from a side stream slowed the
+//    down launch quantising h itself in every workgroup (no launch before it, DV_ADDQ) 1-1.5 %
+//    slower per 7B token but 4-5 % faster for TinyLlama, so the step uses it for small models
+//    (profiles/r06_hq_ab.txt); an Infinity-Cache prefetch of the next layer's weights from a side stream slowed the
 //    chain 1.7-2.6x.
 //    Every sum is taken in a fixed order: results are bit-reproducible.
 #include "qdot.h"
@@ -33,7 +34,8 @@ namespace {
 constexpr int DV_NW = 8;       // waves per workgroup
 constexpr int DV_ACT_LD = 5;   // 16-B activation loads per lane: act bytes <= 5 x 8 KiB
 
-enum DvRole { DV_QKV = 0, DV_ADD = 1, DV_SWIGLU = 2, DV_STORE = 3 };
+// DV_ADDQ: DV_ADD whose workgroups quantise the fp32 activation (hraw, no norm) into LDS themselves
+enum DvRole { DV_QKV = 0, DV_ADD = 1, DV_SWIGLU = 2, DV_STORE = 3, DV_ADDQ = 4 };
 
 
 struct DvSeg {
@@ -49,6 +51,7 @@ struct DvArgs {
     const char* act;            // this launch's activation, act_layout(K, q8k, q80)
     int act_bytes, K, q8k, q80;
     const float* resid;         // DV_ADD
+    const float* hraw;          // DV_ADDQ: the fp32 activation (K floats)
     const int* tokpos;          // DV_QKV: {token, pos, cell, -}
     int* cell_pos;
     __half* kcache;
@@ -78,13 +81,22 @@ __device__ __forceinline__ void dv_body(const DvArgs& a, char* lds) {
     const int u = wg * DV_NW + wave;
     const bool uv = u < S.units;
     const int uc = uv ? u : S.units - 1;
-    constexpr bool ADD = ROLE == DV_ADD;
+    constexpr bool ADD = ROLE == DV_ADD || ROLE == DV_ADDQ;
+    constexpr bool RAWQ = ROLE == DV_ADDQ;
     constexpr int NLD = DV_ACT_LD;
     const ActLayout L = act_layout(a.K, a.q8k, a.q80);
     // ---- 1. the activation and the epilogue's inputs, requested before any weight (loads retire
     // in order: the compiler's wait for them is then a count that leaves the weights in flight)
-    u32x4 av[NLD];
-    {
+    u32x4 av[RAWQ ? 1 : NLD];
+    f32x4 hv[RAWQ ? C : 1];   // DV_ADDQ: blocks wave, wave + 8, .. (nb <= 8 C), 4 floats per lane
+    if constexpr (RAWQ) {
+        const __amdgpu_buffer_rsrc_t hr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.hraw), 0, a.K * 4, 0x00020000);
+#pragma unroll
+        for (int k = 0; k < C; ++k) {
+            const int b = wave + DV_NW * k;
+            hv[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(hr, oob((b * 64 + lane) * 16, b >= nb), 0, 0));
+        }
+    } else {
         const __amdgpu_buffer_rsrc_t ar = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(a.act), 0, a.act_bytes, 0x00020000);
 #pragma unroll
         for (int k = 0; k < NLD; ++k) av[k] = __builtin_amdgcn_raw_buffer_load_b128(ar, (k * DV_NW * 64 + tid) * 16, 0, 0);
@@ -127,10 +139,22 @@ __device__ __forceinline__ void dv_body(const DvArgs& a, char* lds) {
     }
 
     // ---- 3. the activation into LDS (the waits the compiler puts here leave the weights in flight)
+    if constexpr (RAWQ) {   // dv_quant_kernel's arithmetic without the norm, block by block into LDS
+        const ActOut t{a.K, a.q8k, a.q80, lds, nullptr, 0.0f};
 #pragma unroll
-    for (int k = 0; k < NLD; ++k) {
-        const int o = (k * DV_NW * 64 + tid) * 16;
-        if (o < a.act_bytes) *reinterpret_cast<u32x4*>(lds + o) = av[k];
+        for (int k = 0; k < C; ++k) {
+            const int b = wave + DV_NW * k;
+            if (b < nb) {
+                const float q[4] = {hv[k].x, hv[k].y, hv[k].z, hv[k].w};
+                dv_quant_block(t, b, q, lane);
+            }
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < NLD; ++k) {
+            const int o = (k * DV_NW * 64 + tid) * 16;
+            if (o < a.act_bytes) *reinterpret_cast<u32x4*>(lds + o) = av[k];
+        }
     }
     dv_lds_barrier();
 
@@ -207,7 +231,7 @@ DvFn dv_fn_c(int c) {
     case 4: return dgemv_kernel<T0, T1, RW, 4, ROLE>;
     default: break;
     }
-    if constexpr (ROLE == DV_ADD) {
+    if constexpr (ROLE == DV_ADD || ROLE == DV_ADDQ) {
         switch (c) {
         case 3: return dgemv_kernel<T0, T1, RW, 3, ROLE>;
         case 6: return dgemv_kernel<T0, T1, RW, 6, ROLE>;
@@ -244,6 +268,7 @@ DvFn dv_fn(int role, int t0, int t1, int c) {
     switch (role) {
     case DV_QKV: return dv_fn_role<DV_QKV>(t0, t1, c);
     case DV_ADD: return dv_fn_role<DV_ADD>(t0, t1, c);
+    case DV_ADDQ: return dv_fn_role<DV_ADDQ>(t0, t1, c);
     case DV_SWIGLU: return dv_fn_role<DV_SWIGLU>(t0, t1, c);
     case DV_STORE: return dv_fn_role<DV_STORE>(t0, t1, c);
     default: return nullptr;
@@ -326,7 +351,8 @@ void launch_dv_quant(const float* x, const ActOut& t, hipStream_t s) {
 namespace {
 int dv_role(const GemvParams& p) {
     const GemvSeg& g = p.seg[0];
-    return g.epi == EPI_QKV ? DV_QKV : g.epi == EPI_ADD ? DV_ADD : g.epi == EPI_SWIGLU ? DV_SWIGLU
+    // (an ADD launch given the fp32 activation x[0] instead of a quantised one: DV_ADDQ)
+    return g.epi == EPI_QKV ? DV_QKV : g.epi == EPI_ADD ? (!p.act_in && p.x[0] ? DV_ADDQ : DV_ADD) : g.epi == EPI_SWIGLU ? DV_SWIGLU
          : g.epi == EPI_STORE ? DV_STORE : -1;
 }
 }  // namespace
@@ -343,7 +369,7 @@ bool dgemv_supported(const GemvParams& p) {
 }
 
 void launch_dgemv(const GemvParams& p, hipStream_t s, hipEvent_t ev_start, hipEvent_t ev_stop) {
-    if (!p.act_in) throw Error("dgemv: no quantised activation");
+    if (!p.act_in && !(p.seg[0].epi == EPI_ADD && p.x[0])) throw Error("dgemv: no activation");
     if (!dgemv_supported(p)) throw Error("dgemv: unsupported launch shape");
     const GemvSeg& g0 = p.seg[0];
     const int role = dv_role(p);
@@ -388,7 +414,9 @@ void launch_dgemv(const GemvParams& p, hipStream_t s, hipEvent_t ev_start, hipEv
     a.n_rot = p.n_rot;
     a.head_dim = p.head_dim > 0 ? p.head_dim : 1;
     a.kv_dim = p.kv_dim;
-    if (role == DV_ADD && !g0.resid) throw Error("dgemv: residual epilogue without resid");
+    a.hraw = p.x[0];
+    if (role == DV_ADDQ && p.K > DV_NW * 256 * dv_chunks(p.K)) throw Error("dgemv: activation too long to quantise in-launch");
+    if ((role == DV_ADD || role == DV_ADDQ) && !g0.resid) throw Error("dgemv: residual epilogue without resid");
     if (role == DV_QKV && !p.tokpos) throw Error("dgemv: QKV epilogue needs tokpos");
     const DvFn fn = dv_fn(role, g0.A.type, p.nseg == 2 ? p.seg[1].A.type : -1, dv_chunks(p.K));
     const size_t smem = (dv_act_bytes(p.K, p.act_q8k, p.act_q80) + 15) / 16 * 16;

@@ -991,10 +991,16 @@ bool Ctx::sp_setup() {
 // One batch-1 decode step on the streaming kernels (any context length): the embedding, per layer
 // dv_quant(rms_norm(x) * attn_norm) -> QKV -> attention (its output also quantised; past ATTN_SHORT
 // cells the split attention + attn_combine_quant) -> WO + residual -> dv_quant(rms_norm
-// * ffn_norm) -> gate/up -> dv_quant(h) -> down + residual, then the output head and the top-k.
+// * ffn_norm) -> gate/up -> dv_quant(h) (small models: inside the down launch) -> down + residual,
+// then the output head and the top-k.
 // Profiling segments as enqueue_step's (the gate/up launch of prof_layer carries the event pair).
 void Ctx::enqueue_step_sp(bool with_logits) {
+    // The FFN down launch quantises h in every workgroup itself (no dv_quant launch before it) when
+    // that redundant work -- n_ff elements in each of n_embd / 8 workgroups -- is small: one launch
+    // fewer per layer wins for TinyLlama (1398-1409 vs 1341-1342 tok/s), loses 1 % for 7B
+    // (profiles/r06_hq_ab.txt).
     const HParams& hp = m->hp;
+    const bool hq_down = (long long)hp.n_ff * hp.n_embd <= (1LL << 24);
     const bool moe = hp.n_expert > 0;
     int seg = 0;
     auto on = [&]() { return seg_filter < 0 || seg_filter == seg; };
@@ -1140,11 +1146,12 @@ void Ctx::enqueue_step_sp(bool with_logits) {
             const bool timed = l == prof_layer && seg_filter == 1;
             if (on()) launch_dgemv(p, stream, timed ? prof_ev[0] : nullptr, timed ? prof_ev[1] : nullptr);
             if (l == prof_layer) seg = 2;
-            if (on()) launch_dv_quant(h, act(3, b.fD, hp.n_ff, nullptr), stream);
+            if (on() && !hq_down) launch_dv_quant(h, act(3, b.fD, hp.n_ff, nullptr), stream);
         }
         {   // FFN down + residual (in place), then the next layer's (or the output head's) input quantised
             GemvParams p = base;
-            p.act_in = sp_act[3];
+            p.act_in = hq_down ? nullptr : sp_act[3];
+            p.x[0] = h;
             p.K = hp.n_ff;
             p.act_q8k = b.fD & 1;
             p.act_q80 = b.fD >> 1;

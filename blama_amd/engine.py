@@ -340,7 +340,7 @@ def op_gemv(type_: int, raw: np.ndarray, rows: int, K: int, x: np.ndarray, devic
 def op_dgemv(role: int, type_: int, raw: np.ndarray, rows: int, K: int, x: np.ndarray, type2: int = -1,
              raw2=None, rows2: int = 0, resid=None, device: int = 0) -> np.ndarray:
     """mi_op_dgemv: the decode step's streaming GEMV launch of `role` (0 Q/K/V without RoPE, 1 residual
-    add, 2 SwiGLU pair, 3 store)."""
+    add, 2 SwiGLU pair, 3 store, 4 residual add with x quantised inside the launch)."""
     x = np.ascontiguousarray(x, dtype=np.float32)
     out_rows = rows + (rows2 if role == 0 and raw2 is not None else 0)
     y = np.empty(out_rows, np.float32)

@@ -192,7 +192,8 @@ int32_t mi_op_attention_batch(int32_t device, int32_t n_head, int32_t n_head_kv,
 /* The decode step's streaming GEMV (dgemv.hip), one launch: x quantised on the device (Q8_K /
  * Q8_0 as the matrices need), then role 0 Q/K/V rows without RoPE (a second matrix of another type
  * = a second segment; y = [A x | B x]), 1 y = A x + resid, 2 y = silu(A x) * (B x) (gate/up pair),
- * 3 y = A x.  type2/raw2/rows2: the second matrix (raw2 NULL: none). */
+ * 3 y = A x, 4 as 1 with x quantised inside the launch by every workgroup (the FFN down launch
+ * of small models).  type2/raw2/rows2: the second matrix (raw2 NULL: none). */
 int32_t mi_op_dgemv(int32_t device, int32_t role, int32_t type, const void* raw_blocks, int32_t rows, int32_t K,
                     int32_t type2, const void* raw_blocks2, int32_t rows2, const float* x, const float* resid, float* y);
 int32_t mi_op_gemv_bench(int32_t device, int32_t type, const void* raw_blocks, int32_t rows, int32_t K,

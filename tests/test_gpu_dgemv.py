@@ -2,7 +2,9 @@
 against the CPU restatement (oracle/ggml_ref.py): every instantiation the step's dispatcher
 (dv_fn) can return -- role {Q/K/V, residual add, SwiGLU pair, store} x chunks per row
 C in {1, 2, 3, 4, 6, 7} (K = 256 ... 14336) x weight type, and the mixed-type Q/K/V launches
-(Q4_K + Q6_K, Q4_K + Q8_0, Q5_K + Q6_K) -- at the BASELINE models' real widths.
+(Q4_K + Q6_K, Q4_K + Q8_0, Q5_K + Q6_K) -- at the BASELINE models' real widths; and the residual
+add whose workgroups quantise x themselves (DV_ADDQ, the small models' FFN down) bit-identical to
+the one fed by dv_quant_kernel.
 
 The activation is quantised on the device by dv_quant_kernel (bit-exact with quantize_row_q8_K /
 the x86 quantize_row_q8_0, test_gpu_ops.py), so every per-block integer dot equals the CPU's; only
@@ -18,7 +20,7 @@ from util import rand_matrix, rand_x
 pytestmark = pytest.mark.gpu
 
 GEMV_TOL = 2e-5
-ROLE_QKV, ROLE_ADD, ROLE_SWIGLU, ROLE_STORE = 0, 1, 2, 3
+ROLE_QKV, ROLE_ADD, ROLE_SWIGLU, ROLE_STORE, ROLE_ADDQ = 0, 1, 2, 3, 4
 
 
 def _ref(t, w, K, x, sel=None):
@@ -54,6 +56,18 @@ def test_dgemv_residual_add(gpu_lib, t, rows, K):
     bound = absb * GEMV_TOL + (np.abs(ref) + np.abs(r)) * 1.2e-7 + 1e-30
     err = np.abs(got - (ref + r))
     assert np.all(err <= bound), (R.TYPE_NAME[t], rows, K, float((err / bound).max()))
+
+
+# DV_ADDQ runs dv_quant_kernel's no-norm arithmetic per 256-block in each workgroup: same bits
+@pytest.mark.parametrize("t", [R.Q4_K, R.Q5_K, R.Q6_K, R.Q8_0])
+@pytest.mark.parametrize("rows,K", [(64, 256), (2048, 5632), (512, 8192), (4096, 11008), (1024, 14336)])
+def test_dgemv_residual_add_inlaunch_quant(gpu_lib, t, rows, K):
+    w = rand_matrix(t, rows, K, seed=rows + K + t + 7)
+    x = rand_x(K, seed=K + 5)
+    res = rand_x(rows, seed=rows + 2)
+    y1 = engine.op_dgemv(ROLE_ADD, t, w, rows, K, x, resid=res)
+    y4 = engine.op_dgemv(ROLE_ADDQ, t, w, rows, K, x, resid=res)
+    assert np.array_equal(y1.view(np.uint32), y4.view(np.uint32)), (R.TYPE_NAME[t], rows, K)
 
 
 @pytest.mark.parametrize("t", [R.Q4_K, R.Q5_K, R.Q6_K, R.Q8_0])
