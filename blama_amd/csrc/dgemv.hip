@@ -14,10 +14,11 @@
 //    each workgroup loads those few KB ahead of its weights and copies them into LDS.  Measured
 //    alternatives (scripts/exp_fgemv.cpp, profiles/r05_exp_fgemv*.txt): publishing
 //    the activation inside the producing launch by arrival tickets cost 6-10 us per launch; an
-//    rms-norm prologue in every QKV / gate/up workgroup as much as the separate launch; the FFN
-//    down launch quantising h itself in every workgroup (no launch before it, DV_ADDQ) 1-1.5 %
-//    slower per 7B token but 4-5 % faster for TinyLlama, so the step uses it for small models
-//    (profiles/r06_hq_ab.txt); an Infinity-Cache prefetch of the next layer's weights from a side stream slowed the
+//    rms-norm prologue in every QKV / gate/up workgroup (DV_QKVN / DV_SWIGLUN) 8-9 % slower for 7B
+//    and Llama-3-8B but 17 % faster for TinyLlama; the FFN down launch quantising h itself in
+//    every workgroup (DV_ADDQ) 1-1.5 % slower per 7B token but 4-5 % faster for TinyLlama -- so
+//    the step quantises in-launch for small models only (n_ff * n_embd <= 2^24; bit-identical to
+//    the dv_quant launches; profiles/r06_hq_ab.txt, r06_nq_ab.txt); an Infinity-Cache prefetch of the next layer's weights from a side stream slowed the
 //    chain 1.7-2.6x.
 //    Every sum is taken in a fixed order: results are bit-reproducible.
 #include "qdot.h"
@@ -34,8 +35,10 @@ namespace {
 constexpr int DV_NW = 8;       // waves per workgroup
 constexpr int DV_ACT_LD = 5;   // 16-B activation loads per lane: act bytes <= 5 x 8 KiB
 
-// DV_ADDQ: DV_ADD whose workgroups quantise the fp32 activation (hraw, no norm) into LDS themselves
-enum DvRole { DV_QKV = 0, DV_ADD = 1, DV_SWIGLU = 2, DV_STORE = 3, DV_ADDQ = 4 };
+// DV_ADDQ: DV_ADD whose workgroups quantise the fp32 activation (hraw, no norm) into LDS themselves;
+// DV_QKVN / DV_SWIGLUN: DV_QKV / DV_SWIGLU whose workgroups build rms_norm(hraw) * norm_w so
+enum DvRole { DV_QKV = 0, DV_ADD = 1, DV_SWIGLU = 2, DV_STORE = 3, DV_ADDQ = 4, DV_QKVN = 5, DV_SWIGLUN = 6 };
+constexpr int dv_base(int r) { return r == DV_ADDQ ? DV_ADD : r == DV_QKVN ? DV_QKV : r == DV_SWIGLUN ? DV_SWIGLU : r; }
 
 
 struct DvSeg {
@@ -51,7 +54,10 @@ struct DvArgs {
     const char* act;            // this launch's activation, act_layout(K, q8k, q80)
     int act_bytes, K, q8k, q80;
     const float* resid;         // DV_ADD
-    const float* hraw;          // DV_ADDQ: the fp32 activation (K floats)
+    const float* hraw;          // DV_ADDQ / _QKVN / _SWIGLUN: the fp32 activation (K floats)
+    const float* norm_w;        // DV_QKVN / DV_SWIGLUN
+    float eps;
+    int red_off;                // DV_QKVN / DV_SWIGLUN: LDS offset of the 4 waves' sums of squares
     const int* tokpos;          // DV_QKV: {token, pos, cell, -}
     int* cell_pos;
     __half* kcache;
@@ -68,8 +74,9 @@ __device__ __forceinline__ void dv_lds_barrier() {
 
 // One workgroup's work for segment SI of type T.  RW: rows per unit (2: DV_QKV RoPE pairs /
 // DV_SWIGLU gate-up pairs); C: 8-superblock chunks per row (ceil(K / 2048)).
-template <int T, int SI, int RW, int C, int ROLE>
+template <int T, int SI, int RW, int C, int ROLE0>
 __device__ __forceinline__ void dv_body(const DvArgs& a, char* lds) {
+    constexpr int ROLE = dv_base(ROLE0);
     using K = Kq<T>;
     const DvSeg& S = a.seg[SI];
     const int tid = threadIdx.x;
@@ -81,15 +88,30 @@ __device__ __forceinline__ void dv_body(const DvArgs& a, char* lds) {
     const int u = wg * DV_NW + wave;
     const bool uv = u < S.units;
     const int uc = uv ? u : S.units - 1;
-    constexpr bool ADD = ROLE == DV_ADD || ROLE == DV_ADDQ;
-    constexpr bool RAWQ = ROLE == DV_ADDQ;
+    constexpr bool ADD = ROLE == DV_ADD;
+    constexpr bool RAWQ = ROLE0 == DV_ADDQ;
+    constexpr bool NORMQ = ROLE0 == DV_QKVN || ROLE0 == DV_SWIGLUN;
+    constexpr int NP = NORMQ ? 2 * C : 1;   // NORMQ: pieces tid + 256 k of waves 0-3 (dv_quant_kernel's)
+    const int n4 = a.K >> 2;
     constexpr int NLD = DV_ACT_LD;
     const ActLayout L = act_layout(a.K, a.q8k, a.q80);
     // ---- 1. the activation and the epilogue's inputs, requested before any weight (loads retire
     // in order: the compiler's wait for them is then a count that leaves the weights in flight)
-    u32x4 av[RAWQ ? 1 : NLD];
+    u32x4 av[RAWQ || NORMQ ? 1 : NLD];
     f32x4 hv[RAWQ ? C : 1];   // DV_ADDQ: blocks wave, wave + 8, .. (nb <= 8 C), 4 floats per lane
-    if constexpr (RAWQ) {
+    f32x4 xv[NP], nv[NP];
+    if constexpr (NORMQ) {
+        if (wave < 4) {
+            const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.hraw), 0, a.K * 4, 0x00020000);
+            const __amdgpu_buffer_rsrc_t nr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.norm_w), 0, a.K * 4, 0x00020000);
+#pragma unroll
+            for (int k = 0; k < NP; ++k) {
+                const int i = tid + 256 * k;
+                xv[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, oob(i * 16, i >= n4), 0, 0));
+                nv[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(nr, oob(i * 16, i >= n4), 0, 0));
+            }
+        }
+    } else if constexpr (RAWQ) {
         const __amdgpu_buffer_rsrc_t hr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.hraw), 0, a.K * 4, 0x00020000);
 #pragma unroll
         for (int k = 0; k < C; ++k) {
@@ -139,7 +161,39 @@ __device__ __forceinline__ void dv_body(const DvArgs& a, char* lds) {
     }
 
     // ---- 3. the activation into LDS (the waits the compiler puts here leave the weights in flight)
-    if constexpr (RAWQ) {   // dv_quant_kernel's arithmetic without the norm, block by block into LDS
+    if constexpr (NORMQ) {   // dv_quant_kernel with the norm: the same sums in the same order, waves 0-3
+        double* red = reinterpret_cast<double*>(lds + a.red_off);
+        if (wave < 4) {
+            double sq = 0.0;
+#pragma unroll
+            for (int k = 0; k < NP; ++k)
+                if (tid + 256 * k < n4) {
+                    sq += (double)(xv[k].x * xv[k].x);
+                    sq += (double)(xv[k].y * xv[k].y);
+                    sq += (double)(xv[k].z * xv[k].z);
+                    sq += (double)(xv[k].w * xv[k].w);
+                }
+            sq = wave_sum63_d(sq);
+            if (lane == 63) red[wave] = sq;
+        }
+        dv_lds_barrier();
+        if (wave < 4) {
+            double tot = 0.0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) tot += red[k];
+            const float scale = 1.0f / sqrtf((float)(tot / (double)a.K) + a.eps);
+            const ActOut t{a.K, a.q8k, a.q80, lds, nullptr, 0.0f};
+#pragma unroll
+            for (int k = 0; k < NP; ++k) {
+                const int b = wave + 4 * k;   // piece tid + 256 k = block b's lane piece
+                if (b < nb) {
+                    const float q[4] = {(xv[k].x * scale) * nv[k].x, (xv[k].y * scale) * nv[k].y,
+                                        (xv[k].z * scale) * nv[k].z, (xv[k].w * scale) * nv[k].w};
+                    dv_quant_block(t, b, q, lane);
+                }
+            }
+        }
+    } else if constexpr (RAWQ) {   // dv_quant_kernel's arithmetic without the norm, block by block into LDS
         const ActOut t{a.K, a.q8k, a.q80, lds, nullptr, 0.0f};
 #pragma unroll
         for (int k = 0; k < C; ++k) {
@@ -231,7 +285,7 @@ DvFn dv_fn_c(int c) {
     case 4: return dgemv_kernel<T0, T1, RW, 4, ROLE>;
     default: break;
     }
-    if constexpr (ROLE == DV_ADD || ROLE == DV_ADDQ) {
+    if constexpr (dv_base(ROLE) == DV_ADD) {
         switch (c) {
         case 3: return dgemv_kernel<T0, T1, RW, 3, ROLE>;
         case 6: return dgemv_kernel<T0, T1, RW, 6, ROLE>;
@@ -243,9 +297,9 @@ DvFn dv_fn_c(int c) {
 }
 template <int T0, int ROLE>
 DvFn dv_fn_t1(int t1, int c) {
-    constexpr int RW = (ROLE == DV_QKV || ROLE == DV_SWIGLU) ? 2 : 1;
+    constexpr int RW = (dv_base(ROLE) == DV_QKV || dv_base(ROLE) == DV_SWIGLU) ? 2 : 1;
     if (t1 < 0) return dv_fn_c<T0, -1, RW, ROLE>(c);
-    if constexpr (ROLE == DV_QKV) {   // mixed-type Q/K/V launches only
+    if constexpr (dv_base(ROLE) == DV_QKV) {   // mixed-type Q/K/V launches only
         switch (t1) {
         case T_Q6_K: return dv_fn_c<T0, T_Q6_K, RW, ROLE>(c);
         case T_Q8_0: return dv_fn_c<T0, T_Q8_0, RW, ROLE>(c);
@@ -269,6 +323,8 @@ DvFn dv_fn(int role, int t0, int t1, int c) {
     case DV_QKV: return dv_fn_role<DV_QKV>(t0, t1, c);
     case DV_ADD: return dv_fn_role<DV_ADD>(t0, t1, c);
     case DV_ADDQ: return dv_fn_role<DV_ADDQ>(t0, t1, c);
+    case DV_QKVN: return c <= 4 ? dv_fn_role<DV_QKVN>(t0, t1, c) : nullptr;
+    case DV_SWIGLUN: return c <= 4 ? dv_fn_role<DV_SWIGLUN>(t0, t1, c) : nullptr;
     case DV_SWIGLU: return dv_fn_role<DV_SWIGLU>(t0, t1, c);
     case DV_STORE: return dv_fn_role<DV_STORE>(t0, t1, c);
     default: return nullptr;
@@ -351,9 +407,12 @@ void launch_dv_quant(const float* x, const ActOut& t, hipStream_t s) {
 namespace {
 int dv_role(const GemvParams& p) {
     const GemvSeg& g = p.seg[0];
-    // (an ADD launch given the fp32 activation x[0] instead of a quantised one: DV_ADDQ)
-    return g.epi == EPI_QKV ? DV_QKV : g.epi == EPI_ADD ? (!p.act_in && p.x[0] ? DV_ADDQ : DV_ADD) : g.epi == EPI_SWIGLU ? DV_SWIGLU
-         : g.epi == EPI_STORE ? DV_STORE : -1;
+    // (a launch given the fp32 activation x[0] instead of a quantised one: ADD without a norm,
+    // Q/K/V and SwiGLU with rms_norm * norm_w, quantised in every workgroup)
+    const bool raw = !p.act_in && p.x[0];
+    if (raw && (g.epi == EPI_ADD) == (p.norm_w != nullptr)) return -1;
+    return g.epi == EPI_QKV ? (raw ? DV_QKVN : DV_QKV) : g.epi == EPI_ADD ? (raw ? DV_ADDQ : DV_ADD)
+         : g.epi == EPI_SWIGLU ? (raw ? DV_SWIGLUN : DV_SWIGLU) : g.epi == EPI_STORE && !raw ? DV_STORE : -1;
 }
 }  // namespace
 
@@ -364,15 +423,17 @@ bool dgemv_supported(const GemvParams& p) {
     const GemvSeg& g = p.seg[0];
     const int role = dv_role(p);
     if (role < 0 || g.bias || g.expA >= 0 || g.expB >= 0) return false;
-    if (p.nseg == 2 && (role != DV_QKV || p.seg[1].epi != EPI_QKV)) return false;
+    if (p.nseg == 2 && (dv_base(role) != DV_QKV || p.seg[1].epi != EPI_QKV)) return false;
+    if ((role == DV_QKVN || role == DV_SWIGLUN) && p.K > 4 * 256 * 2 * dv_chunks(p.K)) return false;
     return dv_fn(role, g.A.type, p.nseg == 2 ? p.seg[1].A.type : -1, dv_chunks(p.K)) != nullptr;
 }
 
 void launch_dgemv(const GemvParams& p, hipStream_t s, hipEvent_t ev_start, hipEvent_t ev_stop) {
-    if (!p.act_in && !(p.seg[0].epi == EPI_ADD && p.x[0])) throw Error("dgemv: no activation");
+    if (!p.act_in && !p.x[0]) throw Error("dgemv: no activation");
     if (!dgemv_supported(p)) throw Error("dgemv: unsupported launch shape");
     const GemvSeg& g0 = p.seg[0];
-    const int role = dv_role(p);
+    const int role0 = dv_role(p);
+    const int role = dv_base(role0);
     const int rw = (role == DV_QKV || role == DV_SWIGLU) ? 2 : 1;
     DvArgs a;
     std::memset(&a, 0, sizeof(a));
@@ -415,11 +476,15 @@ void launch_dgemv(const GemvParams& p, hipStream_t s, hipEvent_t ev_start, hipEv
     a.head_dim = p.head_dim > 0 ? p.head_dim : 1;
     a.kv_dim = p.kv_dim;
     a.hraw = p.x[0];
-    if (role == DV_ADDQ && p.K > DV_NW * 256 * dv_chunks(p.K)) throw Error("dgemv: activation too long to quantise in-launch");
-    if ((role == DV_ADD || role == DV_ADDQ) && !g0.resid) throw Error("dgemv: residual epilogue without resid");
+    a.norm_w = p.norm_w;
+    a.eps = p.eps;
+    const size_t actb = (dv_act_bytes(p.K, p.act_q8k, p.act_q80) + 15) / 16 * 16;
+    a.red_off = (int)actb;
+    if (role0 == DV_ADDQ && p.K > DV_NW * 256 * dv_chunks(p.K)) throw Error("dgemv: activation too long to quantise in-launch");
+    if (role == DV_ADD && !g0.resid) throw Error("dgemv: residual epilogue without resid");
     if (role == DV_QKV && !p.tokpos) throw Error("dgemv: QKV epilogue needs tokpos");
-    const DvFn fn = dv_fn(role, g0.A.type, p.nseg == 2 ? p.seg[1].A.type : -1, dv_chunks(p.K));
-    const size_t smem = (dv_act_bytes(p.K, p.act_q8k, p.act_q80) + 15) / 16 * 16;
+    const DvFn fn = dv_fn(role0, g0.A.type, p.nseg == 2 ? p.seg[1].A.type : -1, dv_chunks(p.K));
+    const size_t smem = actb + (role0 == DV_QKVN || role0 == DV_SWIGLUN ? 4 * sizeof(double) : 0);
     if (ev_start || ev_stop)
         hipExtLaunchKernelGGL(fn, dim3(blk), dim3(DV_NW * 64), smem, s, ev_start, ev_stop, 0, a);
     else

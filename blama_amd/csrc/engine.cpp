@@ -1001,6 +1001,11 @@ void Ctx::enqueue_step_sp(bool with_logits) {
     // (profiles/r06_hq_ab.txt).
     const HParams& hp = m->hp;
     const bool hq_down = (long long)hp.n_ff * hp.n_embd <= (1LL << 24);
+    // The same rule for the normed inputs of Q/K/V and gate/up (dense models): their workgroups
+    // build rms_norm(x) * norm_w and quantise it themselves, bit-identical to dv_quant_kernel. That
+    // removes two more launches per layer: TinyLlama 1407-1412 -> 1639-1653 tok/s, but 7B 637-643 ->
+    // 579-589 and Llama-3-8B 511 -> 470-480 (profiles/r06_nq_ab.txt).
+    const bool nq_in = hq_down && hp.n_expert == 0 && hp.n_embd <= 8192;
     const bool moe = hp.n_expert > 0;
     int seg = 0;
     auto on = [&]() { return seg_filter < 0 || seg_filter == seg; };
@@ -1012,7 +1017,7 @@ void Ctx::enqueue_step_sp(bool with_logits) {
     if (on()) {
         EmbedParams ep{m->tok_embd, tokpos, x, hp.n_embd, m->pos_embd, 0, step_ctr};
         launch_embed(ep, stream);
-        launch_dv_quant(x, act(0, sp[0].fA, hp.n_embd, m->layers[0].attn_norm), stream);
+        if (!nq_in) launch_dv_quant(x, act(0, sp[0].fA, hp.n_embd, m->layers[0].attn_norm), stream);
     }
     for (int l = 0; l < hp.n_layer; ++l) {
         const Layer& L = m->layers[l];
@@ -1029,7 +1034,10 @@ void Ctx::enqueue_step_sp(bool with_logits) {
         base.K = hp.n_embd;
         {   // Q/K/V + RoPE + KV append
             GemvParams p = base;
-            p.act_in = sp_act[0];
+            p.act_in = nq_in ? nullptr : sp_act[0];
+            p.x[0] = nq_in ? x : nullptr;
+            p.norm_w = nq_in ? L.attn_norm : nullptr;
+            p.eps = hp.eps;
             p.act_q8k = b.fA & 1;
             p.act_q80 = b.fA >> 1;
             p.theta_scale = theta_scale;
@@ -1087,7 +1095,7 @@ void Ctx::enqueue_step_sp(bool with_logits) {
             p.seg[0].resid = x;
             if (on()) {
                 launch_dgemv(p, stream);
-                if (!moe) launch_dv_quant(x, act(2, b.fC, hp.n_embd, L.ffn_norm), stream);
+                if (!moe && !nq_in) launch_dv_quant(x, act(2, b.fC, hp.n_embd, L.ffn_norm), stream);
             }
         }
         if (moe) {   // the routed experts on the r04 step's kernels (layer_ops' MoE FFN), x in place
@@ -1136,7 +1144,10 @@ void Ctx::enqueue_step_sp(bool with_logits) {
         }
         {   // FFN gate/up + SwiGLU, then h quantised
             GemvParams p = base;
-            p.act_in = sp_act[2];
+            p.act_in = nq_in ? nullptr : sp_act[2];
+            p.x[0] = nq_in ? x : nullptr;
+            p.norm_w = nq_in ? L.ffn_norm : nullptr;
+            p.eps = hp.eps;
             p.act_q8k = b.fC & 1;
             p.act_q80 = b.fC >> 1;
             p.nseg = 1;
@@ -1158,7 +1169,7 @@ void Ctx::enqueue_step_sp(bool with_logits) {
             p.nseg = 1;
             p.seg[0] = seg_of(L.down, PAIR_ADJ, EPI_ADD, x);
             p.seg[0].resid = x;
-            const bool next = l + 1 < hp.n_layer || with_logits;
+            const bool next = (l + 1 < hp.n_layer && !nq_in) || (l + 1 == hp.n_layer && with_logits);
             const ActOut nx = l + 1 < hp.n_layer ? act(0, sp[l + 1].fA, hp.n_embd, m->layers[l + 1].attn_norm)
                                                  : act(4, sp_fH, hp.n_embd, m->output_norm);
             if (on()) {

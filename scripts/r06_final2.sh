@@ -1,5 +1,5 @@
 #!/bin/bash
-# r06 round-end check after the small-model in-launch h quantisation: GPU parity suite, smoke, the
+# r06 round-end check after the small-model in-launch quantisations: GPU parity suite, smoke, the
 # default bench line, the TinyLlama decode line.
 OUT=gpurun_out/${1:-r06_final2}; mkdir -p $OUT; export TMPDIR=/tmp
 timeout -k 10 800 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
