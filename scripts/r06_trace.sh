@@ -1,7 +1,7 @@
 #!/bin/bash
-# eager kernel trace of the decode bench (the decode kernels' durations)
+# eager kernel trace of the decode bench (the decode kernels' durations); CFG=<config> for another model
 OUT=gpurun_out/${1:-r06_trace}; mkdir -p $OUT; export TMPDIR=/tmp
-MI_NO_GRAPH=1 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python -u bench.py --no-cpu --steps 48 --warmup 8 --prefill 0 > $OUT/trace_bench.json 2> $OUT/prof.err || { tail -3 $OUT/prof.err; exit 1; }
+MI_NO_GRAPH=1 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python -u bench.py ${CFG:+--config $CFG} --no-cpu --steps 48 --warmup 8 --prefill 0 > $OUT/trace_bench.json 2> $OUT/prof.err || { tail -3 $OUT/prof.err; exit 1; }
 find $OUT/prof -name '*kernel_stats.csv' -exec cp {} $OUT/kernel_stats.csv \;
 rm -rf $OUT/prof
 python3 - <<PY
